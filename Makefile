@@ -1,0 +1,27 @@
+# Top-level build: the product library (libtips_hip.so, gfx950 only) and the oracle checkers.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+LIB      := tips_amd/lib/libtips_hip.so
+SRCS     := tips_amd/csrc/kernels.hip tips_amd/csrc/runtime.cc tips_amd/csrc/bootstrap.cc
+HDRS     := tips_amd/csrc/kernels.h include/tips_hip.h
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-result
+
+all: $(LIB) oracle
+
+$(LIB): $(SRCS) $(HDRS)
+	@mkdir -p tips_amd/lib
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
+
+oracle:
+	$(MAKE) -C oracle
+
+tools: tools/sum_sweep
+
+tools/sum_sweep: tools/sum_sweep.cc $(LIB)
+	$(HIPCC) -O2 -std=c++17 -o $@ $< -Itips_amd -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../tips_amd/lib'
+
+clean:
+	rm -f $(LIB) tools/sum_sweep
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle tools clean

@@ -1,0 +1,158 @@
+/*
+ * tips_hip.h — C-ABI of libtips_hip.so, the MI355X-native gradient-bucket
+ * reduction path behind TiPS's collective-allreduce API.
+ *
+ * Plain C: pointers, sizes, ints. No torch / TF / HIP types in any signature
+ * (streams travel as `void*` = hipStream_t, NULL = the legacy default stream).
+ * No exception crosses this boundary: every data-path call returns an int
+ * status (TIPS_OK = 0, negative = error) and tips_last_error() returns the
+ * message of the calling thread's last failure.
+ *
+ * Which reference interface each entry point replaces is cited per symbol.
+ * Reference = Superjomn/TiPS.
+ */
+#ifndef TIPS_HIP_H_
+#define TIPS_HIP_H_
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* dtype codes: values 0-3 are message::DataType (tips/core/message/
+ * collective_messages.fbs:17-23: TF_FLOAT32=0, TF_FLOAT64=1, TF_INT32=2,
+ * TF_INT64=3). 4 and 5 are new in this build (the reference has no 16-bit
+ * allreduce). */
+enum tips_dtype {
+  TIPS_FLOAT32 = 0,
+  TIPS_FLOAT64 = 1,
+  TIPS_INT32 = 2,
+  TIPS_INT64 = 3,
+  TIPS_FLOAT16 = 4,
+  TIPS_BFLOAT16 = 5,
+};
+
+/* reduction codes = CollectiveOpKind (tips/core/collective/utils.h:21-25).
+ * The reference only ever issues SUM (coordinator.cc:256-274); so does this
+ * build: MAX/MIN return TIPS_ERR_UNSUPPORTED. */
+enum tips_op {
+  TIPS_OP_SUM = 0,
+  TIPS_OP_MAX = 1,
+  TIPS_OP_MIN = 2,
+};
+
+/* status codes (the reference returns tensorflow::Status, utils.h:66) */
+enum tips_status {
+  TIPS_OK = 0,
+  TIPS_ERR_INVALID_ARG = -1,
+  TIPS_ERR_NOT_INITIALIZED = -2,
+  TIPS_ERR_HIP = -3,
+  TIPS_ERR_RCCL = -4,
+  TIPS_ERR_UNSUPPORTED = -5,
+  TIPS_ERR_BOOTSTRAP = -6,
+  TIPS_ERR_MISMATCH = -7,
+};
+
+/* allreduce algorithms (tips_set_algorithm). */
+enum tips_algorithm {
+  TIPS_ALGO_AUTO = -1,  /* ring for p <= 2, direct otherwise */
+  TIPS_ALGO_RING = 0,   /* RCCL send/recv ring, RS + AG, sub-chunk pipelined */
+  TIPS_ALGO_DIRECT = 1, /* all-pairs RS over every xGMI link + p-input sum kernel + AG */
+  TIPS_ALGO_RCCL = 2,   /* ncclAllReduce, kept as a comparison point only */
+};
+
+/* ---- lifecycle: same names and types as tips/core/operations.h:7-21 ---- */
+
+/* Replaces tips_init (operations.cc:12-22). Collective over all ranks.
+ * Reads RANK / WORLD_SIZE / LOCAL_RANK (torchrun) or OMPI_COMM_WORLD_* /
+ * PMI_* (mpirun); WORLD_SIZE unset = one rank. For size > 1 the RCCL unique
+ * id is exchanged over TCP: rank 0 listens on MASTER_ADDR:TIPS_BOOTSTRAP_PORT
+ * (default MASTER_PORT + 17). Errors are reported by tips_last_error() and
+ * tips_is_initialize() stays false (the reference CHECK-fails instead). */
+void tips_init(void);
+/* Replaces tips_shutdown (operations.cc:24-44). Safe to call twice. */
+void tips_shutdown(void);
+/* Replaces tips_is_initialize (operations.cc:46). */
+bool tips_is_initialize(void);
+/* Replace tips_size / tips_rank (operations.cc:48,50). -1 before init. */
+int tips_size(void);
+int tips_rank(void);
+
+/* ---- lifecycle extensions (no reference counterpart) ---- */
+
+/* Bytes of an RCCL unique id (128). */
+int tips_unique_id_bytes(void);
+/* Writes a fresh unique id into out[0..cap). Call on rank 0 only; returns bytes or <0. */
+int tips_get_unique_id(void* out, int64_t cap);
+/* Initialise with an id distributed by the caller (e.g. through a
+ * torch.distributed store). device < 0: LOCAL_RANK % device count. */
+int tips_init_rank(int rank, int size, int device, const void* unique_id, int64_t id_bytes);
+/* The TCP exchange tips_init uses for the unique id, exposed for callers
+ * that bootstrap themselves (and for CPU tests): rank 0's buf[0..bytes) is
+ * delivered into every other rank's buf. Rank 0 listens on port; others
+ * connect to host:port, retrying for up to timeout_s seconds. */
+int tips_bootstrap_broadcast(int rank, int size, const char* host, int port, void* buf, int64_t bytes, int timeout_s);
+/* Message of the calling thread's last failed call ("" if none). */
+const char* tips_last_error(void);
+/* Library version string. */
+const char* tips_version(void);
+
+/* ---- data path ---- */
+
+/* dst[i] = a[i] + b[i] on the device: the per-chunk MPI_SUM local reduce
+ * that MPI_Allreduce runs at every reduce-scatter step (reached from
+ * AllreduceCpu<T>, tips/core/collective/utils.h:60-65). In-place (dst == a
+ * or dst == b) allowed. count in elements (int64: lifts the reference's
+ * int limit, utils.h:62). Device pointers only. Stream-ordered, async. */
+int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int dtype, void* stream);
+
+/* dst[i] = ((srcs[0][i] + srcs[1][i]) + srcs[2][i]) + ... (rank-order fold),
+ * 1 <= nsrc <= 16. f16/bf16 partials are kept in fp32 and rounded once. */
+int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, void* stream);
+
+/* Replaces AllreduceCpu<T> (tips/core/collective/utils.h:52-67) and the
+ * MPIAllreduce op's data path (tips/tensorflow/ops.cc:86-115):
+ * out = SUM over ranks of in, out-of-place (in == out allowed).
+ * Device pointers: stream-ordered, returns after enqueue.
+ * Host pointers (both): staged through HBM, returns when out is written.
+ * op must be TIPS_OP_SUM. */
+int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream);
+
+/* Tensor fusion (no reference counterpart): allreduce n device
+ * tensors in place, packed into buckets of at most the fusion threshold
+ * (TIPS_FUSION_THRESHOLD bytes, default 64 MiB). One dtype for all. */
+int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
+
+/* Select the allreduce algorithm (enum tips_algorithm). Returns the previous one. */
+int tips_set_algorithm(int algo);
+/* The algorithm AUTO resolves to for a given rank count. */
+int tips_resolve_algorithm(int nranks);
+
+/* ---- single-GPU harnesses (tests and benchmarks) ---- */
+
+/* Runs the device ring schedule for p virtual ranks on this one GPU:
+ * ins[r] / outs[r] are device buffers of rank r; the peer transfers are
+ * device-to-device copies in the same order the RCCL ring issues them, and
+ * the sums are the same tips_bucket_sum launches. Lets the ring's chunk
+ * arithmetic be checked bit-exact against oracle_ring on one device. */
+int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
+/* The same for the direct algorithm (checked against oracle_fold, wide_acc=1). */
+int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
+
+/* Explicit variant of the 2-input sum kernel, for the gfx950 tuning sweep
+ * (tools/sum_sweep.cc): mode 0 = grid-stride over `blocks` workgroups,
+ * mode 1 = one tile per workgroup; unroll = 16-B vectors per lane in flight
+ * (1/2/4/8); nt = non-temporal loads and stores. tips_bucket_sum uses the
+ * default chosen from that sweep. */
+int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
+                     int blocks, void* stream);
+
+/* Chunk partition the ring uses (element offsets), for tests. */
+int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TIPS_HIP_H_ */

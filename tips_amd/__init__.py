@@ -1,0 +1,87 @@
+"""tips_amd — MI355X-native gradient-bucket reduction behind TiPS's allreduce API.
+
+Drop-in surface of `tips.tensorflow` for the collective-allreduce path
+(reference tips/tensorflow/__init__.py:20-103,189-227, ops.py, basics.py,
+compression.py), over numpy arrays and torch tensors instead of TF tensors
+(TensorFlow is not in this image). Everything below reaches the GPU through
+libtips_hip.so (include/tips_hip.h); there is no CPU fallback.
+"""
+from .basics import TipsBasics, init, is_initialized, rank, shutdown, size
+from .compression import Compression, Compressor, FP16Compressor, NoneCompressor
+from .ops import allreduce_op, bucket_sum, fused_allreduce_, rank_op, set_algorithm, size_op
+from ._lib import TipsError, TipsLibraryError
+from . import tensors as _tensors
+
+Average = 'Average'
+Sum = 'Sum'
+
+__all__ = [
+    "allreduce", "allreduce_grads", "allreduce_op", "bucket_sum", "fused_allreduce_", "init", "shutdown",
+    "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
+    "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
+]
+
+
+def allreduce(tensor,
+              average=None,
+              device_dense='',
+              device_sparse='',
+              compression=Compression.none,
+              op=None,
+              prescale_factor=1.0,
+              postscale_factor=1.0,
+              name=None):
+    """Sum `tensor` over all ranks — mirrors tips.tensorflow.allreduce (__init__.py:20-91).
+
+    Same arguments as the reference. As in the reference, `op`,
+    `prescale_factor` and `postscale_factor` do not reach the reduction (they
+    are commented out at the C++ boundary, __init__.py:82-87), so the result
+    is the plain SUM for op=Average too — parity with the
+    reference, not a recommendation. `average`, `device_dense` and
+    `device_sparse` are accepted for signature compatibility. Sparse
+    (IndexedSlices-style) tensors take the reference's allgather branch,
+    which is out of scope here: they raise.
+    """
+    if _tensors.is_torch(tensor) and tensor.is_sparse:
+        raise NotImplementedError("sparse allreduce (allgather branch) is not part of this path")
+    tensor_compressed, ctx = compression.compress(tensor)
+    summed_tensor_compressed = allreduce_op(tensor_compressed, name=name)
+    return compression.decompress(summed_tensor_compressed, ctx)
+
+
+def _allreduce_cond(tensor, *args, **kwargs):
+    """size() > 1 ? allreduce(tensor) : tensor  (__init__.py:94-103)."""
+    if size() > 1:
+        return allreduce(tensor, *args, **kwargs)
+    return tensor
+
+
+def allreduce_grads(grads, compression=Compression.none, op=None, fused=True):
+    """Allreduce a list of gradients (None entries pass through).
+
+    Mirrors the per-gradient loop of _make_cached_allreduce_grads_fn
+    (__init__.py:203-222), including the size()==1 identity of
+    _allreduce_cond. With fused=True, device tensors are summed through the
+    fusion buckets (one allreduce per <=64 MiB bucket instead of one per
+    gradient); outputs are new tensors, inputs are left unchanged.
+    """
+    if size() <= 1:
+        return list(grads)
+    out = list(grads)
+    if fused:
+        groups = {}
+        for i, g in enumerate(grads):
+            if g is not None and _tensors.is_device(g):
+                groups.setdefault(g.dtype, []).append(i)
+        for idx in groups.values():
+            clones = []
+            for i in idx:
+                c, ctx = compression.compress(grads[i])
+                clones.append((i, c.contiguous().clone(), ctx))
+            fused_allreduce_([c for _, c, _ in clones])
+            for i, c, ctx in clones:
+                out[i] = compression.decompress(c, ctx)
+    for i, g in enumerate(grads):
+        if g is not None and (not fused or not _tensors.is_device(g)):
+            out[i] = allreduce(g, compression=compression, op=op)
+    return out

@@ -1,0 +1,133 @@
+"""ctypes binding of libtips_hip.so (the C-ABI declared in include/tips_hip.h).
+
+This is the only way the Python surface reaches the device: there is no CPU
+fallback. If the shared library is missing the first call raises
+``TipsLibraryError`` — the product path fails loudly rather than silently
+computing on the host (the oracle under ``oracle/`` is test infrastructure and
+is never imported from here).
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TIPS_HIP_LIB", os.path.join(_HERE, "lib", "libtips_hip.so"))
+
+# dtype codes (include/tips_hip.h enum tips_dtype; 0-3 = collective_messages.fbs:17-23)
+FLOAT32, FLOAT64, INT32, INT64, FLOAT16, BFLOAT16 = 0, 1, 2, 3, 4, 5
+OP_SUM, OP_MAX, OP_MIN = 0, 1, 2
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL = -1, 0, 1, 2
+
+STATUS_NAMES = {
+    0: "TIPS_OK",
+    -1: "TIPS_ERR_INVALID_ARG",
+    -2: "TIPS_ERR_NOT_INITIALIZED",
+    -3: "TIPS_ERR_HIP",
+    -4: "TIPS_ERR_RCCL",
+    -5: "TIPS_ERR_UNSUPPORTED",
+    -6: "TIPS_ERR_BOOTSTRAP",
+    -7: "TIPS_ERR_MISMATCH",
+}
+
+
+class TipsLibraryError(RuntimeError):
+    """libtips_hip.so could not be loaded (not built, or built for another arch)."""
+
+
+class TipsError(RuntimeError):
+    """A C-ABI call returned a negative status; carries tips_last_error()."""
+
+    def __init__(self, func, code, message):
+        self.func = func
+        self.code = code
+        super().__init__("%s -> %s (%d): %s" % (func, STATUS_NAMES.get(code, "?"), code, message))
+
+
+_lock = threading.Lock()
+_lib = None
+
+_c_void_pp = ctypes.POINTER(ctypes.c_void_p)
+_c_i64_p = ctypes.POINTER(ctypes.c_int64)
+
+# (name, restype, argtypes) — must match include/tips_hip.h
+_SIGNATURES = [
+    ("tips_init", None, []),
+    ("tips_shutdown", None, []),
+    ("tips_is_initialize", ctypes.c_bool, []),
+    ("tips_size", ctypes.c_int, []),
+    ("tips_rank", ctypes.c_int, []),
+    ("tips_unique_id_bytes", ctypes.c_int, []),
+    ("tips_get_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    ("tips_init_rank", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64]),
+    ("tips_last_error", ctypes.c_char_p, []),
+    ("tips_version", ctypes.c_char_p, []),
+    ("tips_bucket_sum", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_multi_sum", ctypes.c_int,
+     [ctypes.c_void_p, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_allreduce", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),
+    ("tips_resolve_algorithm", ctypes.c_int, [ctypes.c_int]),
+    ("tips_ring_simulate", ctypes.c_int,
+     [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_direct_simulate", ctypes.c_int,
+     [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_sum_variant", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+      ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_chunk_bounds", ctypes.c_int,
+     [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p]),
+    ("tips_bootstrap_broadcast", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
+]
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises TipsLibraryError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise TipsLibraryError(
+                    "libtips_hip.so not found at %s — build it with `make` (or __graft_entry__.build()); "
+                    "there is no CPU fallback" % LIB_PATH)
+            try:
+                handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            except OSError as e:
+                raise TipsLibraryError("cannot load %s: %s" % (LIB_PATH, e)) from e
+            for name, res, args in _SIGNATURES:
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def last_error():
+    return lib().tips_last_error().decode(errors="replace")
+
+
+def check(func, code):
+    """Raise TipsError for a negative status returned by C-ABI function `func`."""
+    if code < 0:
+        raise TipsError(func, code, last_error())
+    return code
+
+
+def call(name, *args):
+    """Call C-ABI function `name` and raise on a negative status."""
+    return check(name, getattr(lib(), name)(*args))
+
+
+def ptr_array(ptrs):
+    arr = (ctypes.c_void_p * len(ptrs))(*[ctypes.c_void_p(int(p)) for p in ptrs])
+    return ctypes.cast(arr, _c_void_pp), arr
+
+
+def i64_array(vals):
+    arr = (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+    return ctypes.cast(arr, _c_i64_p), arr

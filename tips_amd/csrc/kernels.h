@@ -1,0 +1,34 @@
+// kernels.h — launchers for the gfx950 kernels of the bucket-reduction path.
+// Internal to libtips_hip.so (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tips {
+
+int dtype_size(int dtype);  // 0 for unknown dtypes
+
+// dst = a + b, elementwise (the per-chunk MPI_SUM step).
+hipError_t launch_sum2(void* dst, const void* a, const void* b, int64_t n, int dtype, hipStream_t s);
+
+// dst = rank-order fold of srcs[0..nsrc), nsrc <= kMaxSrcs.
+constexpr int kMaxSrcs = 16;
+hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t s);
+
+// Batched byte copy for fusion pack/unpack: one workgroup per tile.
+struct CopyTile {
+  const char* src;
+  char* dst;
+  int64_t bytes;  // <= kCopyTileBytes
+};
+constexpr int64_t kCopyTileBytes = 64 * 1024;
+hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t s);
+
+// Tuning/sweep entry: explicit variant of the 2-input sum.
+//   mode 0 = grid-stride over (blocks) workgroups, mode 1 = one tile per workgroup
+//   unroll = 16-B vectors per lane in flight (1, 2, 4, 8), nt = non-temporal loads/stores
+hipError_t launch_sum2_variant(void* dst, const void* a, const void* b, int64_t n, int dtype, int mode, int unroll,
+                               int nt, int blocks, hipStream_t s);
+
+}  // namespace tips

@@ -1,0 +1,501 @@
+// kernels.hip — gfx950 (CDNA4) kernels of the gradient-bucket reduction path.
+//
+// What they replace: the local MPI_SUM reduction libmpi runs on every
+// received chunk inside MPI_Allreduce, reached from AllreduceCpu<T>
+// (reference tips/core/collective/utils.h:60-65, op from utils.cc:6-16).
+//
+// Design: the add is memory-bound — 1 flop per 12 B for
+// f32 — so there is no MFMA and no LDS round trip; every lane moves 16 B per
+// load/store (global_load_dwordx4 / global_store_dwordx4: one wave touches
+// 1 KiB contiguous), UNROLL independent 16-B vectors per operand are issued
+// before the first add so each lane keeps 2*UNROLL loads in flight, and the
+// grid either covers the bucket one tile per workgroup (mode 1) or
+// grid-strides over a CU-multiple of workgroups (mode 0). Elements that do
+// not fill a 16-B vector (the "tail", < 8 elements) are done scalar by
+// workgroup 0. Integer adds wrap (two's complement, as MPI_SUM on MPI_INT /
+// MPI_LONG_LONG); f16 adds are v_pk_add_f16 (correctly rounded, = fp32 add
+// rounded to half); bf16 adds in fp32 and rounds to nearest-even.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace tips {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+enum { kF32 = 0, kF64 = 1, kI32 = 2, kI64 = 3, kF16 = 4, kBF16 = 5 };
+constexpr int kBlock = 256;  // 4 waves of 64
+
+int dtype_size(int dtype) {
+  switch (dtype) {
+    case kF32: return 4;
+    case kF64: return 8;
+    case kI32: return 4;
+    case kI64: return 8;
+    case kF16: return 2;
+    case kBF16: return 2;
+    default: return 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 16-byte loads / stores
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 helpers: exact same rounding as oracle_float_to_bf16 (oracle/oracle.c)
+
+__device__ __forceinline__ unsigned bf16_round_bits(unsigned x) {
+  return ((x & 0x7fffffffu) > 0x7f800000u) ? ((x >> 16) | 0x40u) : ((x + 0x7fffu + ((x >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ u32x4 bf16_pack(f32x4 lo, f32x4 hi) {
+  u32x4 l = __builtin_bit_cast(u32x4, lo), h = __builtin_bit_cast(u32x4, hi);
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = bf16_round_bits(l[i]) | (bf16_round_bits(h[i]) << 16);
+  return r;
+}
+
+__device__ __forceinline__ f32x4 bf16_lo(u32x4 v) { return __builtin_bit_cast(f32x4, v << 16u); }
+__device__ __forceinline__ f32x4 bf16_hi(u32x4 v) { return __builtin_bit_cast(f32x4, v & 0xffff0000u); }
+
+// ---------------------------------------------------------------------------
+// 16-byte vector add per dtype (storage-precision result: one MPI_SUM step)
+
+template <int DT>
+__device__ __forceinline__ u32x4 add16(u32x4 a, u32x4 b);
+
+template <>
+__device__ __forceinline__ u32x4 add16<kF32>(u32x4 a, u32x4 b) {
+  return __builtin_bit_cast(u32x4, __builtin_bit_cast(f32x4, a) + __builtin_bit_cast(f32x4, b));
+}
+template <>
+__device__ __forceinline__ u32x4 add16<kF64>(u32x4 a, u32x4 b) {
+  return __builtin_bit_cast(u32x4, __builtin_bit_cast(f64x2, a) + __builtin_bit_cast(f64x2, b));
+}
+template <>
+__device__ __forceinline__ u32x4 add16<kI32>(u32x4 a, u32x4 b) {
+  return a + b;
+}
+template <>
+__device__ __forceinline__ u32x4 add16<kI64>(u32x4 a, u32x4 b) {
+  return __builtin_bit_cast(u32x4, __builtin_bit_cast(u64x2, a) + __builtin_bit_cast(u64x2, b));
+}
+template <>
+__device__ __forceinline__ u32x4 add16<kF16>(u32x4 a, u32x4 b) {
+  return __builtin_bit_cast(u32x4, __builtin_bit_cast(f16x8, a) + __builtin_bit_cast(f16x8, b));
+}
+template <>
+__device__ __forceinline__ u32x4 add16<kBF16>(u32x4 a, u32x4 b) {
+  return bf16_pack(bf16_lo(a) + bf16_lo(b), bf16_hi(a) + bf16_hi(b));
+}
+
+// Scalar element add for the tail (same arithmetic as add16, one element).
+template <int DT>
+__device__ __forceinline__ void add_elem(void* dst, const void* a, const void* b, int64_t i);
+
+template <>
+__device__ __forceinline__ void add_elem<kF32>(void* d, const void* a, const void* b, int64_t i) {
+  ((float*)d)[i] = ((const float*)a)[i] + ((const float*)b)[i];
+}
+template <>
+__device__ __forceinline__ void add_elem<kF64>(void* d, const void* a, const void* b, int64_t i) {
+  ((double*)d)[i] = ((const double*)a)[i] + ((const double*)b)[i];
+}
+template <>
+__device__ __forceinline__ void add_elem<kI32>(void* d, const void* a, const void* b, int64_t i) {
+  ((unsigned*)d)[i] = ((const unsigned*)a)[i] + ((const unsigned*)b)[i];
+}
+template <>
+__device__ __forceinline__ void add_elem<kI64>(void* d, const void* a, const void* b, int64_t i) {
+  ((unsigned long long*)d)[i] = ((const unsigned long long*)a)[i] + ((const unsigned long long*)b)[i];
+}
+template <>
+__device__ __forceinline__ void add_elem<kF16>(void* d, const void* a, const void* b, int64_t i) {
+  ((_Float16*)d)[i] = ((const _Float16*)a)[i] + ((const _Float16*)b)[i];
+}
+template <>
+__device__ __forceinline__ void add_elem<kBF16>(void* d, const void* a, const void* b, int64_t i) {
+  unsigned x = (unsigned)((const unsigned short*)a)[i] << 16, y = (unsigned)((const unsigned short*)b)[i] << 16;
+  float s = __builtin_bit_cast(float, x) + __builtin_bit_cast(float, y);
+  ((unsigned short*)d)[i] = (unsigned short)bf16_round_bits(__builtin_bit_cast(unsigned, s));
+}
+
+// ---------------------------------------------------------------------------
+// 2-input sum: dst = a + b
+
+template <int DT, int MODE, int UNROLL, bool NT>
+__global__ __launch_bounds__(kBlock) void sum2_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
+                                                     const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
+                                                     int64_t n) {
+  constexpr int64_t kTile = (int64_t)kBlock * UNROLL;  // vectors per workgroup-iteration
+  const int tid = threadIdx.x;
+  int64_t t = blockIdx.x;
+  const int64_t tstride = (MODE == 0) ? (int64_t)gridDim.x : 0;
+  do {
+    const int64_t base = t * kTile + tid;
+    if (base + (UNROLL - 1) * kBlock < nvec) {
+      u32x4 x[UNROLL], y[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) x[u] = ld16<NT>(a + base + u * kBlock);
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) y[u] = ld16<NT>(b + base + u * kBlock);
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) st16<NT>(dst + base + u * kBlock, add16<DT>(x[u], y[u]));
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) {
+        const int64_t i = base + u * kBlock;
+        if (i < nvec) st16<NT>(dst + i, add16<DT>(ld16<NT>(a + i), ld16<NT>(b + i)));
+      }
+    }
+    t += tstride;
+  } while (MODE == 0 && t * kTile < nvec);
+  if (blockIdx.x == 0 && tail_begin + tid < n) add_elem<DT>(dst, a, b, tail_begin + tid);
+}
+
+// Unaligned fallback (any pointer not 16-B aligned): one element per lane.
+template <int DT>
+__global__ __launch_bounds__(kBlock) void sum2_scalar_kernel(void* dst, const void* a, const void* b, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    add_elem<DT>(dst, a, b, i);
+}
+
+// ---------------------------------------------------------------------------
+// Multi-input sum: dst = ((s0 + s1) + s2) + ...  (rank-order fold)
+// f16/bf16 accumulate in fp32 and round once; others accumulate in storage type.
+
+template <int DT>
+struct Wide;
+template <>
+struct Wide<kF32> {
+  using A = f32x4;
+  static __device__ A load(u32x4 v) { return __builtin_bit_cast(f32x4, v); }
+  static __device__ u32x4 store(A a) { return __builtin_bit_cast(u32x4, a); }
+};
+template <>
+struct Wide<kF64> {
+  using A = f64x2;
+  static __device__ A load(u32x4 v) { return __builtin_bit_cast(f64x2, v); }
+  static __device__ u32x4 store(A a) { return __builtin_bit_cast(u32x4, a); }
+};
+template <>
+struct Wide<kI32> {
+  using A = u32x4;
+  static __device__ A load(u32x4 v) { return v; }
+  static __device__ u32x4 store(A a) { return a; }
+};
+template <>
+struct Wide<kI64> {
+  using A = u64x2;
+  static __device__ A load(u32x4 v) { return __builtin_bit_cast(u64x2, v); }
+  static __device__ u32x4 store(A a) { return __builtin_bit_cast(u32x4, a); }
+};
+template <>
+struct Wide<kF16> {
+  using A = f32x8;
+  static __device__ A load(u32x4 v) { return __builtin_convertvector(__builtin_bit_cast(f16x8, v), f32x8); }
+  static __device__ u32x4 store(A a) { return __builtin_bit_cast(u32x4, __builtin_convertvector(a, f16x8)); }
+};
+template <>
+struct Wide<kBF16> {
+  using A = f32x8;
+  static __device__ A load(u32x4 v) {
+    f32x4 lo = bf16_lo(v), hi = bf16_hi(v);
+    return A{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+  static __device__ u32x4 store(A a) {
+    return bf16_pack(f32x4{a[0], a[1], a[2], a[3]}, f32x4{a[4], a[5], a[6], a[7]});
+  }
+};
+
+template <int DT>
+struct ScalarOf;
+template <>
+struct ScalarOf<kF32> {
+  using T = float;
+};
+template <>
+struct ScalarOf<kF64> {
+  using T = double;
+};
+template <>
+struct ScalarOf<kI32> {
+  using T = unsigned;
+};
+template <>
+struct ScalarOf<kI64> {
+  using T = unsigned long long;
+};
+template <>
+struct ScalarOf<kF16> {
+  using T = _Float16;
+};
+template <>
+struct ScalarOf<kBF16> {
+  using T = unsigned short;
+};
+
+template <int DT>
+__device__ __forceinline__ void fold_elem(void* dst, const void* const* srcs, int nsrc, int64_t i) {
+  if constexpr (DT == kF16) {
+    float acc = (float)((const _Float16*)srcs[0])[i];
+    for (int j = 1; j < nsrc; j++) acc += (float)((const _Float16*)srcs[j])[i];
+    ((_Float16*)dst)[i] = (_Float16)acc;
+  } else if constexpr (DT == kBF16) {
+    float acc = __builtin_bit_cast(float, (unsigned)((const unsigned short*)srcs[0])[i] << 16);
+    for (int j = 1; j < nsrc; j++) acc += __builtin_bit_cast(float, (unsigned)((const unsigned short*)srcs[j])[i] << 16);
+    ((unsigned short*)dst)[i] = (unsigned short)bf16_round_bits(__builtin_bit_cast(unsigned, acc));
+  } else {
+    // storage-type fold in a register (dst may alias one of srcs: in-place)
+    using T = typename ScalarOf<DT>::T;
+    T acc = ((const T*)srcs[0])[i];
+    for (int j = 1; j < nsrc; j++) acc = acc + ((const T*)srcs[j])[i];
+    ((T*)dst)[i] = acc;
+  }
+}
+
+struct SrcList {
+  const u32x4* p[kMaxSrcs];
+};
+
+template <int DT, int NSRC, int UNROLL>
+__global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
+                                                          int64_t tail_begin, int64_t n) {
+  using W = Wide<DT>;
+  constexpr int64_t kTile = (int64_t)kBlock * UNROLL;
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile + tid;
+#pragma unroll
+  for (int u = 0; u < UNROLL; u++) {
+    const int64_t i = base + u * kBlock;
+    if (i < nvec) {
+      u32x4 v[NSRC];
+#pragma unroll
+      for (int j = 0; j < NSRC; j++) v[j] = srcs.p[j][i];
+      typename W::A acc = W::load(v[0]);
+#pragma unroll
+      for (int j = 1; j < NSRC; j++) acc = acc + W::load(v[j]);
+      dst[i] = W::store(acc);
+    }
+  }
+  if (blockIdx.x == 0 && NSRC > 1 && tail_begin + tid < n) {
+    const void* s[NSRC];
+#pragma unroll
+    for (int j = 0; j < NSRC; j++) s[j] = srcs.p[j];
+    fold_elem<DT>(dst, s, NSRC, tail_begin + tid);
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(kBlock) void multi_sum_scalar_kernel(void* dst, SrcList srcs, int nsrc, int64_t n) {
+  const void* s[kMaxSrcs];
+  for (int j = 0; j < nsrc; j++) s[j] = srcs.p[j];
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    fold_elem<DT>(dst, s, nsrc, i);
+}
+
+// ---------------------------------------------------------------------------
+// Batched copy (fusion pack / unpack)
+
+__global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __restrict__ tiles) {
+  const CopyTile t = tiles[blockIdx.x];
+  const int tid = threadIdx.x;
+  if (((reinterpret_cast<uintptr_t>(t.src) | reinterpret_cast<uintptr_t>(t.dst) | (uintptr_t)t.bytes) & 15) == 0) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(t.src);
+    u32x4* d = reinterpret_cast<u32x4*>(t.dst);
+    const int64_t nv = t.bytes >> 4;
+    constexpr int U = 4;
+    for (int64_t i = tid; i < nv; i += kBlock * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (i + u * kBlock < nv) v[u] = s[i + u * kBlock];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (i + u * kBlock < nv) d[i + u * kBlock] = v[u];
+    }
+  } else if (((reinterpret_cast<uintptr_t>(t.src) | reinterpret_cast<uintptr_t>(t.dst) | (uintptr_t)t.bytes) & 3) == 0) {
+    const unsigned* s = reinterpret_cast<const unsigned*>(t.src);
+    unsigned* d = reinterpret_cast<unsigned*>(t.dst);
+    for (int64_t i = tid; i < (t.bytes >> 2); i += kBlock) d[i] = s[i];
+  } else {
+    for (int64_t i = tid; i < t.bytes; i += kBlock) t.dst[i] = t.src[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+
+namespace {
+
+constexpr int kNumCUs = 256;
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int DT, int MODE, int UNROLL, bool NT>
+hipError_t run_sum2(void* dst, const void* a, const void* b, int64_t n, int blocks, hipStream_t s) {
+  const int64_t ve = 16 / (int64_t)dtype_size(DT);
+  const int64_t nvec = n / ve;
+  const int64_t tiles = (nvec + (int64_t)kBlock * UNROLL - 1) / ((int64_t)kBlock * UNROLL);
+  int64_t grid = (MODE == 1) ? tiles : (blocks > 0 ? blocks : kNumCUs * 8);
+  if (grid > tiles) grid = tiles;
+  if (grid < 1) grid = 1;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((sum2_kernel<DT, MODE, UNROLL, NT>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst,
+                     (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);
+  return hipGetLastError();
+}
+
+template <int DT>
+hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int mode, int unroll, int nt, int blocks,
+                         hipStream_t s) {
+  if (!(aligned16(dst) && aligned16(a) && aligned16(b))) {
+    int64_t grid = (n + kBlock - 1) / kBlock;
+    if (grid > kNumCUs * 16) grid = kNumCUs * 16;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((sum2_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, a, b, n);
+    return hipGetLastError();
+  }
+#define TIPS_SUM2_CASE(M, U, NTV) \
+  if (mode == M && unroll == U && (nt != 0) == NTV) return run_sum2<DT, M, U, NTV>(dst, a, b, n, blocks, s);
+  TIPS_SUM2_CASE(1, 1, false)
+  TIPS_SUM2_CASE(1, 2, false)
+  TIPS_SUM2_CASE(1, 4, false)
+  TIPS_SUM2_CASE(1, 8, false)
+  TIPS_SUM2_CASE(1, 1, true)
+  TIPS_SUM2_CASE(1, 2, true)
+  TIPS_SUM2_CASE(1, 4, true)
+  TIPS_SUM2_CASE(1, 8, true)
+  TIPS_SUM2_CASE(0, 1, false)
+  TIPS_SUM2_CASE(0, 2, false)
+  TIPS_SUM2_CASE(0, 4, false)
+  TIPS_SUM2_CASE(0, 8, false)
+  TIPS_SUM2_CASE(0, 1, true)
+  TIPS_SUM2_CASE(0, 2, true)
+  TIPS_SUM2_CASE(0, 4, true)
+  TIPS_SUM2_CASE(0, 8, true)
+#undef TIPS_SUM2_CASE
+  return hipErrorInvalidValue;
+}
+
+// Default variant for the product path (chosen from the gfx950 sweep,
+// profiles/ + DESIGN.md §Kernels).
+constexpr int kDefMode = 1, kDefUnroll = 4, kDefNT = 1;
+
+template <int DT, int NSRC>
+hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
+  constexpr int U = NSRC <= 4 ? 2 : 1;
+  const int64_t ve = 16 / (int64_t)dtype_size(DT);
+  const int64_t nvec = n / ve;
+  int64_t grid = (nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((multi_sum_kernel<DT, NSRC, U>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst, sl, nvec,
+                     nvec * ve, n);
+  return hipGetLastError();
+}
+
+template <int DT>
+hipError_t multi_dispatch(void* dst, const void* const* srcs, int nsrc, int64_t n, hipStream_t s) {
+  SrcList sl{};
+  bool al = aligned16(dst);
+  for (int j = 0; j < nsrc; j++) {
+    sl.p[j] = (const u32x4*)srcs[j];
+    al = al && aligned16(srcs[j]);
+  }
+  if (!al) {
+    int64_t grid = (n + kBlock - 1) / kBlock;
+    if (grid > kNumCUs * 16) grid = kNumCUs * 16;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((multi_sum_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, sl, nsrc, n);
+    return hipGetLastError();
+  }
+  switch (nsrc) {
+    case 1: return run_multi<DT, 1>(dst, sl, n, s);
+    case 2: return run_multi<DT, 2>(dst, sl, n, s);
+    case 3: return run_multi<DT, 3>(dst, sl, n, s);
+    case 4: return run_multi<DT, 4>(dst, sl, n, s);
+    case 5: return run_multi<DT, 5>(dst, sl, n, s);
+    case 6: return run_multi<DT, 6>(dst, sl, n, s);
+    case 7: return run_multi<DT, 7>(dst, sl, n, s);
+    case 8: return run_multi<DT, 8>(dst, sl, n, s);
+    case 9: return run_multi<DT, 9>(dst, sl, n, s);
+    case 10: return run_multi<DT, 10>(dst, sl, n, s);
+    case 11: return run_multi<DT, 11>(dst, sl, n, s);
+    case 12: return run_multi<DT, 12>(dst, sl, n, s);
+    case 13: return run_multi<DT, 13>(dst, sl, n, s);
+    case 14: return run_multi<DT, 14>(dst, sl, n, s);
+    case 15: return run_multi<DT, 15>(dst, sl, n, s);
+    case 16: return run_multi<DT, 16>(dst, sl, n, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_sum2_variant(void* dst, const void* a, const void* b, int64_t n, int dtype, int mode, int unroll,
+                               int nt, int blocks, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  switch (dtype) {
+    case kF32: return sum2_dispatch<kF32>(dst, a, b, n, mode, unroll, nt, blocks, s);
+    case kF64: return sum2_dispatch<kF64>(dst, a, b, n, mode, unroll, nt, blocks, s);
+    case kI32: return sum2_dispatch<kI32>(dst, a, b, n, mode, unroll, nt, blocks, s);
+    case kI64: return sum2_dispatch<kI64>(dst, a, b, n, mode, unroll, nt, blocks, s);
+    case kF16: return sum2_dispatch<kF16>(dst, a, b, n, mode, unroll, nt, blocks, s);
+    case kBF16: return sum2_dispatch<kBF16>(dst, a, b, n, mode, unroll, nt, blocks, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_sum2(void* dst, const void* a, const void* b, int64_t n, int dtype, hipStream_t s) {
+  return launch_sum2_variant(dst, a, b, n, dtype, kDefMode, kDefUnroll, kDefNT, 0, s);
+}
+
+hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (nsrc < 1 || nsrc > kMaxSrcs) return hipErrorInvalidValue;
+  if (nsrc == 1) {
+    if (dst == srcs[0]) return hipSuccess;
+    return hipMemcpyAsync(dst, srcs[0], (size_t)n * dtype_size(dtype), hipMemcpyDeviceToDevice, s);
+  }
+  switch (dtype) {
+    case kF32: return multi_dispatch<kF32>(dst, srcs, nsrc, n, s);
+    case kF64: return multi_dispatch<kF64>(dst, srcs, nsrc, n, s);
+    case kI32: return multi_dispatch<kI32>(dst, srcs, nsrc, n, s);
+    case kI64: return multi_dispatch<kI64>(dst, srcs, nsrc, n, s);
+    case kF16: return multi_dispatch<kF16>(dst, srcs, nsrc, n, s);
+    case kBF16: return multi_dispatch<kBF16>(dst, srcs, nsrc, n, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(copy_tiles_kernel, dim3((unsigned)ntiles), dim3(kBlock), 0, s, tiles_dev);
+  return hipGetLastError();
+}
+
+}  // namespace tips

@@ -1,0 +1,834 @@
+// runtime.cc — host runtime and C-ABI of libtips_hip.so.
+//
+// Replaces, for the allreduce-SUM path of Superjomn/TiPS:
+//   tips/core/operations.{h,cc}           lifecycle C-ABI (tips_init/shutdown/size/rank)
+//   tips/core/collective/utils.h:52-67    AllreduceCpu<T> -> tips_allreduce
+//   tips/core/collective/coordinator.cc   negotiation: with one process per GPU and
+//                                         stream-ordered calls there is nothing to
+//                                         negotiate per tensor (DESIGN.md §Control plane)
+//   tips/core/mpi/tips_mpi.h:13-55        dtype traits -> RCCL byte transfers + dtype enum
+// The data moves over RCCL point-to-point (xGMI) and is summed by the HIP
+// kernels of kernels.hip. One comm stream carries every RCCL call of a rank
+// (one ordered channel, as the reference's single MPI_COMM_WORLD); sums run on
+// a separate compute stream so sub-chunk k+1's transfer overlaps sub-chunk k's sum.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/tips_hip.h"
+#include "kernels.h"
+
+namespace tips {
+int bootstrap_exchange(int rank, int size, const char* host, int port, void* id, int id_bytes, int timeout_s,
+                       std::string* err);
+}
+
+namespace {
+
+using tips::CopyTile;
+
+constexpr int64_t kAlignBytes = 256;  // chunk / bucket-slot alignment (dwordx4 + 128-B lines)
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  if (getenv("TIPS_VERBOSE")) fprintf(stderr, "[tips] error %d: %s\n", code, buf);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                                  \
+  do {                                                                                                 \
+    hipError_t e_ = (expr);                                                                            \
+    if (e_ != hipSuccess) return fail(TIPS_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));    \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                                 \
+  do {                                                                                                 \
+    ncclResult_t r_ = (expr);                                                                          \
+    if (r_ != ncclSuccess) return fail(TIPS_ERR_RCCL, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
+  } while (0)
+
+#define TRY(expr)            \
+  do {                       \
+    int rc_ = (expr);        \
+    if (rc_ != 0) return rc_; \
+  } while (0)
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return strtoll(v, nullptr, 10);
+}
+
+int env_first_int(const char* const* names, int dflt) {
+  for (int i = 0; names[i]; i++) {
+    const char* v = getenv(names[i]);
+    if (v && *v) return atoi(v);
+  }
+  return dflt;
+}
+
+int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+int mod(int a, int p) { return ((a % p) + p) % p; }
+
+// ---------------------------------------------------------------------------
+// chunk / sub-chunk partition (shared by ring, direct and the simulators;
+// restated by oracle_chunk_bounds in oracle/oracle.c)
+
+struct Range {
+  int64_t b, e;
+  int64_t len() const { return e - b; }
+};
+
+Range chunk_of(int64_t n, int p, int64_t align, int c) {
+  int64_t per = round_up((n + p - 1) / p, align);
+  int64_t b = std::min((int64_t)c * per, n), e = std::min(b + per, n);
+  return {b, e};
+}
+
+Range sub_of(Range ch, int K, int64_t align, int k) {
+  int64_t per = round_up((ch.len() + K - 1) / K, align);
+  int64_t b = std::min(ch.b + (int64_t)k * per, ch.e), e = std::min(b + per, ch.e);
+  return {b, e};
+}
+
+// ---------------------------------------------------------------------------
+// device buffers that only grow
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want, bool zero = false) {
+    if (want <= bytes) return 0;
+    if (p) {
+      hipError_t e = hipFree(p);
+      (void)e;
+      p = nullptr;
+      bytes = 0;
+    }
+    want = (size_t)round_up((int64_t)want, 1 << 20);
+    HIP_TRY(hipMalloc(&p, want));
+    if (zero) HIP_TRY(hipMemset(p, 0, want));
+    bytes = want;
+    return 0;
+  }
+  void release() {
+    if (p) {
+      hipError_t e = hipFree(p);
+      (void)e;
+    }
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+struct EventPool {
+  std::vector<hipEvent_t> ev;
+  int ensure(size_t n) {
+    while (ev.size() < n) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev.push_back(e);
+    }
+    return 0;
+  }
+  void release() {
+    for (auto e : ev) {
+      hipError_t r = hipEventDestroy(e);
+      (void)r;
+    }
+    ev.clear();
+  }
+};
+
+// fusion plan: cached per (dtype, tensor list)
+struct FusionBucket {
+  int64_t bytes = 0;          // padded bucket size
+  int ntiles = 0;
+  CopyTile* pack = nullptr;   // device descriptor arrays
+  CopyTile* unpack = nullptr;
+  std::vector<int> direct;    // tensors too large to fuse: allreduced in place
+};
+struct FusionPlan {
+  int dtype;
+  std::vector<void*> ptrs;
+  std::vector<int64_t> counts;
+  std::vector<FusionBucket> buckets;
+  std::vector<int> unfused;  // indices allreduced in place
+};
+
+struct State {
+  std::mutex mu;
+  bool initialized = false;
+  int rank = -1, size = -1, device = -1;
+  ncclComm_t comm = nullptr;
+  hipStream_t comm_stream = nullptr, comp_stream = nullptr, io_stream = nullptr;
+  hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr;
+  EventPool recv_ev, sum_ev;
+  DevBuf staging, host_in, host_out, fusion;
+  int algo = TIPS_ALGO_AUTO;
+  std::unordered_map<uint64_t, FusionPlan> plans;
+};
+
+State& S() {
+  static State* s = new State();  // never destroyed: safe at exit
+  return *s;
+}
+
+int ensure_streams(State& st) {
+  if (!st.comm_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comm_stream, hipStreamNonBlocking));
+  if (!st.comp_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comp_stream, hipStreamNonBlocking));
+  if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
+  if (!st.ev_start) HIP_TRY(hipEventCreateWithFlags(&st.ev_start, hipEventDisableTiming));
+  if (!st.ev_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
+  if (!st.ev_comp_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_done, hipEventDisableTiming));
+  return 0;
+}
+
+ncclDataType_t nccl_type(int dtype) {
+  switch (dtype) {
+    case TIPS_FLOAT32: return ncclFloat32;
+    case TIPS_FLOAT64: return ncclFloat64;
+    case TIPS_INT32: return ncclInt32;
+    case TIPS_INT64: return ncclInt64;
+    case TIPS_FLOAT16: return ncclFloat16;
+    case TIPS_BFLOAT16: return ncclBfloat16;
+    default: return ncclInt8;
+  }
+}
+
+int pipeline_depth(int64_t chunk_bytes) {
+  int64_t kmax = std::max<int64_t>(1, env_i64("TIPS_PIPELINE_DEPTH", 4));
+  int64_t min_sub = std::max<int64_t>(kAlignBytes, env_i64("TIPS_MIN_SUBCHUNK_BYTES", 8 << 20));
+  int64_t k = (chunk_bytes + min_sub - 1) / min_sub;
+  return (int)std::max<int64_t>(1, std::min(k, kmax));
+}
+
+// The sum kernel launch used by every schedule (ring step: out = local + received).
+int sum2(void* dst, const void* a, const void* b, int64_t n, int dtype, hipStream_t s) {
+  HIP_TRY(tips::launch_sum2(dst, a, b, n, dtype, s));
+  return 0;
+}
+
+// Join: `waiter` waits for all work queued so far on `src`.
+int join(hipStream_t waiter, hipStream_t src, hipEvent_t ev) {
+  HIP_TRY(hipEventRecord(ev, src));
+  HIP_TRY(hipStreamWaitEvent(waiter, ev, 0));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Ring allreduce over RCCL send/recv. Own rank only.
+
+int ring_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
+  const int p = st.size, r = st.rank, next = mod(r + 1, p), prev = mod(r - 1, p);
+  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
+  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
+  const int K = pipeline_depth(max_chunk * es);
+  TRY(st.staging.ensure((size_t)(2 * max_chunk * es)));
+  TRY(st.recv_ev.ensure(2 * K));
+  TRY(st.sum_ev.ensure(2 * K));
+  char* stg[2] = {(char*)st.staging.p, (char*)st.staging.p + max_chunk * es};
+  TRY(join(st.comm_stream, user, st.ev_start));
+  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
+
+  // reduce-scatter: at step s send chunk (r-s), receive chunk (r-s-1) and add it in
+  for (int s = 0; s < p - 1; s++) {
+    const Range sc = chunk_of(n, p, align, mod(r - s, p)), rc = chunk_of(n, p, align, mod(r - s - 1, p));
+    const char* src = (s == 0) ? in : out;
+    for (int k = 0; k < K; k++) {
+      const Range ss = sub_of(sc, K, align, k), rs = sub_of(rc, K, align, k);
+      if (s > 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((s - 1) & 1) * K + k], 0));
+      char* land = stg[s & 1] + (rs.b - rc.b) * es;
+      if (ss.len() > 0 || rs.len() > 0) {
+        NCCL_TRY(ncclGroupStart());
+        if (ss.len() > 0) NCCL_TRY(ncclSend(src + ss.b * es, ss.len() * es, ncclInt8, next, st.comm, st.comm_stream));
+        if (rs.len() > 0) NCCL_TRY(ncclRecv(land, rs.len() * es, ncclInt8, prev, st.comm, st.comm_stream));
+        NCCL_TRY(ncclGroupEnd());
+      }
+      hipEvent_t rev = st.recv_ev.ev[(s & 1) * K + k];
+      HIP_TRY(hipEventRecord(rev, st.comm_stream));
+      HIP_TRY(hipStreamWaitEvent(st.comp_stream, rev, 0));
+      TRY(sum2(out + rs.b * es, in + rs.b * es, land, rs.len(), dtype, st.comp_stream));
+      HIP_TRY(hipEventRecord(st.sum_ev.ev[(s & 1) * K + k], st.comp_stream));
+    }
+  }
+  // allgather: rank r owns chunk (r+1); at step s forward chunk (r+1-s), receive chunk (r-s)
+  for (int s = 0; s < p - 1; s++) {
+    const Range sc = chunk_of(n, p, align, mod(r + 1 - s, p)), rc = chunk_of(n, p, align, mod(r - s, p));
+    for (int k = 0; k < K; k++) {
+      const Range ss = sub_of(sc, K, align, k), rs = sub_of(rc, K, align, k);
+      if (s == 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((p - 2) & 1) * K + k], 0));
+      if (ss.len() > 0 || rs.len() > 0) {
+        NCCL_TRY(ncclGroupStart());
+        if (ss.len() > 0) NCCL_TRY(ncclSend(out + ss.b * es, ss.len() * es, ncclInt8, next, st.comm, st.comm_stream));
+        if (rs.len() > 0) NCCL_TRY(ncclRecv(out + rs.b * es, rs.len() * es, ncclInt8, prev, st.comm, st.comm_stream));
+        NCCL_TRY(ncclGroupEnd());
+      }
+    }
+  }
+  TRY(join(user, st.comm_stream, st.ev_done));
+  TRY(join(user, st.comp_stream, st.ev_comp_done));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Direct (all-pairs) allreduce: rank r owns chunk r. Every
+// peer's slice of chunk r arrives over its own xGMI link at once; one p-input
+// kernel folds them in rank order; then chunk r goes to every peer at once.
+
+int direct_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
+  const int p = st.size, r = st.rank;
+  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
+  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
+  const int K = pipeline_depth(max_chunk * es);
+  TRY(st.staging.ensure((size_t)((p - 1) * max_chunk * es)));
+  TRY(st.recv_ev.ensure(K));
+  TRY(st.sum_ev.ensure(K));
+  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * max_chunk * es; };
+  const Range mine = chunk_of(n, p, align, r);
+  TRY(join(st.comm_stream, user, st.ev_start));
+  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
+  for (int k = 0; k < K; k++) {
+    const Range ms = sub_of(mine, K, align, k);
+    NCCL_TRY(ncclGroupStart());
+    for (int d = 1; d < p; d++) {
+      const int to = mod(r + d, p), from = mod(r - d, p);
+      const Range ts = sub_of(chunk_of(n, p, align, to), K, align, k);
+      if (ts.len() > 0) NCCL_TRY(ncclSend(in + ts.b * es, ts.len() * es, ncclInt8, to, st.comm, st.comm_stream));
+      if (ms.len() > 0)
+        NCCL_TRY(ncclRecv(slot(from) + (ms.b - mine.b) * es, ms.len() * es, ncclInt8, from, st.comm, st.comm_stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    HIP_TRY(hipEventRecord(st.recv_ev.ev[k], st.comm_stream));
+    HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[k], 0));
+    const void* srcs[tips::kMaxSrcs];
+    for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)(in + ms.b * es) : slot(j) + (ms.b - mine.b) * es;
+    HIP_TRY(tips::launch_multi_sum(out + ms.b * es, srcs, p, ms.len(), dtype, st.comp_stream));
+    HIP_TRY(hipEventRecord(st.sum_ev.ev[k], st.comp_stream));
+  }
+  for (int k = 0; k < K; k++) {
+    const Range ms = sub_of(mine, K, align, k);
+    HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[k], 0));
+    NCCL_TRY(ncclGroupStart());
+    for (int d = 1; d < p; d++) {
+      const int to = mod(r + d, p), from = mod(r - d, p);
+      const Range fs = sub_of(chunk_of(n, p, align, from), K, align, k);
+      if (ms.len() > 0) NCCL_TRY(ncclSend(out + ms.b * es, ms.len() * es, ncclInt8, to, st.comm, st.comm_stream));
+      if (fs.len() > 0) NCCL_TRY(ncclRecv(out + fs.b * es, fs.len() * es, ncclInt8, from, st.comm, st.comm_stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+  }
+  TRY(join(user, st.comm_stream, st.ev_done));
+  TRY(join(user, st.comp_stream, st.ev_comp_done));
+  return 0;
+}
+
+int resolve_algo(int algo, int p) {
+  if (algo != TIPS_ALGO_AUTO) return algo;
+  const char* e = getenv("TIPS_ALGO");
+  if (e && *e) {
+    if (!strcmp(e, "ring")) return TIPS_ALGO_RING;
+    if (!strcmp(e, "direct")) return TIPS_ALGO_DIRECT;
+    if (!strcmp(e, "rccl")) return TIPS_ALGO_RCCL;
+  }
+  return p <= 2 ? TIPS_ALGO_RING : TIPS_ALGO_DIRECT;
+}
+
+int ensure_comm(State& st) {
+  if (st.comm) return 0;
+  if (st.size != 1) return fail(TIPS_ERR_NOT_INITIALIZED, "no RCCL communicator");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  NCCL_TRY(ncclCommInitRank(&st.comm, 1, id, 0));
+  return 0;
+}
+
+// device-resident allreduce, caller holds st.mu
+int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream) {
+  if (n == 0) return 0;
+  const int64_t es = tips::dtype_size(dtype);
+  const int algo = resolve_algo(st.algo, st.size);
+  if (algo == TIPS_ALGO_RCCL) {
+    TRY(ensure_comm(st));
+    NCCL_TRY(ncclAllReduce(in, out, (size_t)n, nccl_type(dtype), ncclSum, st.comm, stream));
+    return 0;
+  }
+  if (st.size == 1) {  // MPI_Allreduce on one rank returns the input
+    if (in != out) HIP_TRY(hipMemcpyAsync(out, in, (size_t)(n * es), hipMemcpyDeviceToDevice, stream));
+    return 0;
+  }
+  if (st.size > tips::kMaxSrcs && algo == TIPS_ALGO_DIRECT)
+    return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
+  if (algo == TIPS_ALGO_DIRECT) return direct_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
+  return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
+}
+
+bool is_device_ptr(const void* p) {
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
+}
+
+int check_dtype(int dtype) {
+  if (tips::dtype_size(dtype) == 0) return fail(TIPS_ERR_INVALID_ARG, "unsupported dtype %d", dtype);
+  return 0;
+}
+
+int set_device(State& st) {
+  if (st.device >= 0) HIP_TRY(hipSetDevice(st.device));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// fusion plans
+
+uint64_t plan_key(void* const* ptrs, const int64_t* counts, int n, int dtype) {
+  uint64_t h = 1469598103934665603ull ^ (uint64_t)dtype;
+  auto mix = [&](uint64_t v) {
+    h ^= v;
+    h *= 1099511628211ull;
+  };
+  mix((uint64_t)n);
+  for (int i = 0; i < n; i++) {
+    mix((uint64_t)(uintptr_t)ptrs[i]);
+    mix((uint64_t)counts[i]);
+  }
+  return h;
+}
+
+void free_plan(FusionPlan& pl) {
+  for (auto& b : pl.buckets) {
+    if (b.pack) (void)hipFree(b.pack);
+    if (b.unpack) (void)hipFree(b.unpack);
+  }
+  pl.buckets.clear();
+}
+
+int build_plan(State& st, FusionPlan& pl, int64_t threshold) {
+  const int64_t es = tips::dtype_size(pl.dtype);
+  const int n = (int)pl.ptrs.size();
+  std::vector<std::vector<CopyTile>> packs(1), unpacks(1);
+  std::vector<int64_t> sizes(1, 0);
+  for (int i = 0; i < n; i++) {
+    const int64_t bytes = pl.counts[i] * es;
+    if (bytes == 0) continue;
+    if (bytes >= threshold) {  // already bucket-sized: reduce in place
+      pl.unfused.push_back(i);
+      continue;
+    }
+    int64_t off = round_up(sizes.back(), kAlignBytes);
+    if (off + bytes > threshold) {
+      packs.emplace_back();
+      unpacks.emplace_back();
+      sizes.push_back(0);
+      off = 0;
+    }
+    char* base = (char*)pl.ptrs[i];
+    for (int64_t t = 0; t < bytes; t += tips::kCopyTileBytes) {
+      const int64_t tb = std::min(tips::kCopyTileBytes, bytes - t);
+      // bucket addresses are filled in as offsets; rebased onto the fusion buffer below
+      packs.back().push_back(CopyTile{base + t, (char*)(uintptr_t)(off + t), tb});
+      unpacks.back().push_back(CopyTile{(const char*)(uintptr_t)(off + t), base + t, tb});
+    }
+    sizes.back() = off + bytes;
+  }
+  TRY(st.fusion.ensure((size_t)threshold, /*zero=*/true));
+  char* fb = (char*)st.fusion.p;
+  for (size_t b = 0; b < sizes.size(); b++) {
+    if (sizes[b] == 0) continue;
+    FusionBucket fbk;
+    fbk.bytes = round_up(sizes[b], kAlignBytes);
+    fbk.ntiles = (int)packs[b].size();
+    for (auto& t : packs[b]) t.dst = fb + (uintptr_t)t.dst;
+    for (auto& t : unpacks[b]) t.src = fb + (uintptr_t)t.src;
+    const size_t tb = sizeof(CopyTile) * packs[b].size();
+    HIP_TRY(hipMalloc(&fbk.pack, tb));
+    HIP_TRY(hipMalloc(&fbk.unpack, tb));
+    HIP_TRY(hipMemcpy(fbk.pack, packs[b].data(), tb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(fbk.unpack, unpacks[b].data(), tb, hipMemcpyHostToDevice));
+    pl.buckets.push_back(fbk);
+  }
+  return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+
+extern "C" {
+
+const char* tips_last_error(void) { return g_last_error.c_str(); }
+const char* tips_version(void) { return "tips_hip 0.1.0 (gfx950)"; }
+int tips_unique_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
+
+int tips_get_unique_id(void* out, int64_t cap) {
+  if (!out || cap < (int64_t)sizeof(ncclUniqueId)) return fail(TIPS_ERR_INVALID_ARG, "unique id buffer too small");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  memcpy(out, &id, sizeof id);
+  return (int)sizeof id;
+}
+
+int tips_init_rank(int rank, int size, int device, const void* unique_id, int64_t id_bytes) {
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (st.initialized) return 0;
+  if (size < 1 || rank < 0 || rank >= size) return fail(TIPS_ERR_INVALID_ARG, "bad rank %d / size %d", rank, size);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (ndev < 1) return fail(TIPS_ERR_HIP, "no HIP device visible");
+  static const char* const local_vars[] = {"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr};
+  if (device < 0) device = env_first_int(local_vars, rank) % ndev;
+  HIP_TRY(hipSetDevice(device));
+  st.device = device;
+  TRY(ensure_streams(st));
+  if (size > 1) {
+    if (!unique_id || id_bytes != (int64_t)sizeof(ncclUniqueId))
+      return fail(TIPS_ERR_INVALID_ARG, "size > 1 needs a %zu-byte unique id", sizeof(ncclUniqueId));
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof id);
+    NCCL_TRY(ncclCommInitRank(&st.comm, size, id, rank));
+  }
+  st.rank = rank;
+  st.size = size;
+  st.initialized = true;
+  return 0;
+}
+
+void tips_init(void) {
+  const char* const rank_vars[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", nullptr};
+  const char* const size_vars[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", nullptr};
+  const int rank = env_first_int(rank_vars, 0), size = env_first_int(size_vars, 1);
+  if (S().initialized) return;
+  ncclUniqueId id;
+  memset(&id, 0, sizeof id);
+  if (size > 1) {
+    const char* host = getenv("MASTER_ADDR");
+    if (!host || !*host) host = "127.0.0.1";
+    const int port = (int)env_i64("TIPS_BOOTSTRAP_PORT", env_i64("MASTER_PORT", 29500) + 17);
+    if (rank == 0 && ncclGetUniqueId(&id) != ncclSuccess) {
+      fail(TIPS_ERR_RCCL, "ncclGetUniqueId failed");
+      return;
+    }
+    std::string err;
+    if (tips::bootstrap_exchange(rank, size, host, port, &id, (int)sizeof id, (int)env_i64("TIPS_BOOTSTRAP_TIMEOUT", 300),
+                                 &err) != 0) {
+      fail(TIPS_ERR_BOOTSTRAP, "%s", err.c_str());
+      return;
+    }
+  }
+  tips_init_rank(rank, size, -1, size > 1 ? &id : nullptr, size > 1 ? (int64_t)sizeof id : 0);
+}
+
+void tips_shutdown(void) {
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return;
+  if (st.device >= 0) (void)hipSetDevice(st.device);
+  if (st.comm_stream) (void)hipStreamSynchronize(st.comm_stream);
+  if (st.comp_stream) (void)hipStreamSynchronize(st.comp_stream);
+  if (st.comm) {
+    (void)ncclCommDestroy(st.comm);
+    st.comm = nullptr;
+  }
+  for (auto& kv : st.plans) free_plan(kv.second);
+  st.plans.clear();
+  st.staging.release();
+  st.host_in.release();
+  st.host_out.release();
+  st.fusion.release();
+  st.recv_ev.release();
+  st.sum_ev.release();
+  for (hipEvent_t* e : {&st.ev_start, &st.ev_done, &st.ev_comp_done})
+    if (*e) {
+      (void)hipEventDestroy(*e);
+      *e = nullptr;
+    }
+  for (hipStream_t* s : {&st.comm_stream, &st.comp_stream, &st.io_stream})
+    if (*s) {
+      (void)hipStreamDestroy(*s);
+      *s = nullptr;
+    }
+  st.initialized = false;
+  st.rank = st.size = -1;
+}
+
+int tips_bootstrap_broadcast(int rank, int size, const char* host, int port, void* buf, int64_t bytes, int timeout_s) {
+  if (size < 1 || rank < 0 || rank >= size || port <= 0 || port > 65535 || bytes < 0 || bytes > (1 << 20) ||
+      (bytes > 0 && !buf))
+    return fail(TIPS_ERR_INVALID_ARG, "bad bootstrap args");
+  std::string err;
+  if (tips::bootstrap_exchange(rank, size, (host && *host) ? host : "127.0.0.1", port, buf, (int)bytes,
+                               timeout_s > 0 ? timeout_s : 300, &err) != 0)
+    return fail(TIPS_ERR_BOOTSTRAP, "%s", err.c_str());
+  return 0;
+}
+
+bool tips_is_initialize(void) { return S().initialized; }
+int tips_size(void) { return S().initialized ? S().size : -1; }
+int tips_rank(void) { return S().initialized ? S().rank : -1; }
+
+int tips_set_algorithm(int algo) {
+  if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_RCCL) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  int prev = st.algo;
+  st.algo = algo;
+  return prev;
+}
+
+int tips_resolve_algorithm(int nranks) { return resolve_algo(S().algo, nranks); }
+
+int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end) {
+  TRY(check_dtype(dtype));
+  if (p < 1 || c < 0 || c >= p || count < 0 || !begin || !end) return fail(TIPS_ERR_INVALID_ARG, "bad chunk query");
+  Range r = chunk_of(count, p, kAlignBytes / tips::dtype_size(dtype), c);
+  *begin = r.b;
+  *end = r.e;
+  return 0;
+}
+
+int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count");
+  if (count == 0) return 0;
+  if (!dst || !a || !b) return fail(TIPS_ERR_INVALID_ARG, "null pointer");
+  HIP_TRY(tips::launch_sum2(dst, a, b, count, dtype, (hipStream_t)stream));
+  return 0;
+}
+
+int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
+                     int blocks, void* stream) {
+  TRY(check_dtype(dtype));
+  if (count <= 0) return 0;
+  HIP_TRY(tips::launch_sum2_variant(dst, a, b, count, dtype, mode, unroll, nt, blocks, (hipStream_t)stream));
+  return 0;
+}
+
+int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  if (nsrc < 1 || nsrc > tips::kMaxSrcs) return fail(TIPS_ERR_INVALID_ARG, "nsrc must be 1..%d", tips::kMaxSrcs);
+  if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count");
+  if (count == 0) return 0;
+  HIP_TRY(tips::launch_multi_sum(dst, srcs, nsrc, count, dtype, (hipStream_t)stream));
+  return 0;
+}
+
+int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream) {
+  TRY(check_dtype(dtype));
+  if (op != TIPS_OP_SUM) return fail(TIPS_ERR_UNSUPPORTED, "only SUM is implemented (op %d)", op);
+  if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+  if (count == 0) return 0;
+  if (!in || !out) return fail(TIPS_ERR_INVALID_ARG, "null pointer");
+  TRY(set_device(st));
+  const bool din = is_device_ptr(in), dout = is_device_ptr(out);
+  if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "in and out must both be device or both be host memory");
+  hipStream_t s = (hipStream_t)stream;
+  if (din) return allreduce_device(st, in, out, count, dtype, s);
+  // host tensors (the reference's TF CPU tensors, ops.cc:88-90): stage through HBM
+  const size_t bytes = (size_t)count * tips::dtype_size(dtype);
+  TRY(st.host_in.ensure(bytes));
+  TRY(st.host_out.ensure(bytes));
+  HIP_TRY(hipMemcpyAsync(st.host_in.p, in, bytes, hipMemcpyHostToDevice, st.io_stream));
+  TRY(allreduce_device(st, st.host_in.p, st.host_out.p, count, dtype, st.io_stream));
+  HIP_TRY(hipMemcpyAsync(out, st.host_out.p, bytes, hipMemcpyDeviceToHost, st.io_stream));
+  HIP_TRY(hipStreamSynchronize(st.io_stream));
+  return 0;
+}
+
+int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  if (n < 0 || (n > 0 && (!ptrs || !counts))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+  if (n == 0) return 0;
+  TRY(set_device(st));
+  for (int i = 0; i < n; i++)
+    if (counts[i] < 0 || (counts[i] > 0 && !ptrs[i])) return fail(TIPS_ERR_INVALID_ARG, "bad tensor %d", i);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t es = tips::dtype_size(dtype);
+  const int64_t threshold = round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_FUSION_THRESHOLD", 64 << 20)), kAlignBytes);
+  const uint64_t key = plan_key(ptrs, counts, n, dtype);
+  auto it = st.plans.find(key);
+  bool hit = it != st.plans.end() && it->second.dtype == dtype && (int)it->second.ptrs.size() == n &&
+             std::equal(ptrs, ptrs + n, it->second.ptrs.begin()) && std::equal(counts, counts + n, it->second.counts.begin());
+  if (!hit) {
+    if (it != st.plans.end()) {
+      free_plan(it->second);
+      st.plans.erase(it);
+    }
+    if (st.plans.size() >= 64) {
+      HIP_TRY(hipDeviceSynchronize());
+      for (auto& kv : st.plans) free_plan(kv.second);
+      st.plans.clear();
+    }
+    FusionPlan pl;
+    pl.dtype = dtype;
+    pl.ptrs.assign(ptrs, ptrs + n);
+    pl.counts.assign(counts, counts + n);
+    int rc = build_plan(st, pl, threshold);
+    if (rc) {
+      free_plan(pl);
+      return rc;
+    }
+    it = st.plans.emplace(key, std::move(pl)).first;
+  }
+  const FusionPlan& pl = it->second;
+  for (const auto& b : pl.buckets) {
+    HIP_TRY(tips::launch_copy_tiles(b.pack, b.ntiles, s));
+    TRY(allreduce_device(st, st.fusion.p, st.fusion.p, b.bytes / es, dtype, s));
+    HIP_TRY(tips::launch_copy_tiles(b.unpack, b.ntiles, s));
+  }
+  for (int i : pl.unfused) TRY(allreduce_device(st, ptrs[i], ptrs[i], counts[i], dtype, s));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// single-GPU schedule simulators (test harnesses)
+
+int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  if (p < 1 || p > 64 || n < 0 || !outs || !ins) return fail(TIPS_ERR_INVALID_ARG, "bad simulate args");
+  if (n == 0) return 0;
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  TRY(ensure_streams(st));
+  hipStream_t user = (hipStream_t)stream;
+  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
+  if (p == 1) {
+    if (outs[0] != ins[0]) HIP_TRY(hipMemcpyAsync(outs[0], ins[0], (size_t)(n * es), hipMemcpyDeviceToDevice, user));
+    return 0;
+  }
+  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
+  const int K = pipeline_depth(max_chunk * es);
+  TRY(st.staging.ensure((size_t)(2 * p * max_chunk * es)));
+  TRY(st.recv_ev.ensure(2 * K));
+  TRY(st.sum_ev.ensure(2 * K));
+  auto stg = [&](int r, int par) { return (char*)st.staging.p + ((int64_t)r * 2 + par) * max_chunk * es; };
+  TRY(join(st.comm_stream, user, st.ev_start));
+  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
+  for (int s = 0; s < p - 1; s++) {
+    for (int k = 0; k < K; k++) {
+      if (s > 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((s - 1) & 1) * K + k], 0));
+      for (int r = 0; r < p; r++) {  // virtual rank r receives from r-1
+        const int prev = mod(r - 1, p);
+        const Range rc = chunk_of(n, p, align, mod(r - s - 1, p));
+        const Range rs = sub_of(rc, K, align, k);
+        if (rs.len() == 0) continue;
+        const char* src = (s == 0) ? (const char*)ins[prev] : (const char*)outs[prev];
+        HIP_TRY(hipMemcpyAsync(stg(r, s & 1) + (rs.b - rc.b) * es, src + rs.b * es, (size_t)(rs.len() * es),
+                               hipMemcpyDeviceToDevice, st.comm_stream));
+      }
+      hipEvent_t rev = st.recv_ev.ev[(s & 1) * K + k];
+      HIP_TRY(hipEventRecord(rev, st.comm_stream));
+      HIP_TRY(hipStreamWaitEvent(st.comp_stream, rev, 0));
+      for (int r = 0; r < p; r++) {
+        const Range rc = chunk_of(n, p, align, mod(r - s - 1, p));
+        const Range rs = sub_of(rc, K, align, k);
+        TRY(sum2((char*)outs[r] + rs.b * es, (const char*)ins[r] + rs.b * es, stg(r, s & 1) + (rs.b - rc.b) * es,
+                 rs.len(), dtype, st.comp_stream));
+      }
+      HIP_TRY(hipEventRecord(st.sum_ev.ev[(s & 1) * K + k], st.comp_stream));
+    }
+  }
+  for (int s = 0; s < p - 1; s++) {
+    for (int k = 0; k < K; k++) {
+      if (s == 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((p - 2) & 1) * K + k], 0));
+      for (int r = 0; r < p; r++) {
+        const int prev = mod(r - 1, p);
+        const Range rs = sub_of(chunk_of(n, p, align, mod(r - s, p)), K, align, k);
+        if (rs.len() == 0) continue;
+        HIP_TRY(hipMemcpyAsync((char*)outs[r] + rs.b * es, (const char*)outs[prev] + rs.b * es, (size_t)(rs.len() * es),
+                               hipMemcpyDeviceToDevice, st.comm_stream));
+      }
+    }
+  }
+  TRY(join(user, st.comm_stream, st.ev_done));
+  TRY(join(user, st.comp_stream, st.ev_comp_done));
+  return 0;
+}
+
+int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  if (p < 1 || p > tips::kMaxSrcs || n < 0 || !outs || !ins) return fail(TIPS_ERR_INVALID_ARG, "bad simulate args");
+  if (n == 0) return 0;
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  TRY(ensure_streams(st));
+  hipStream_t user = (hipStream_t)stream;
+  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
+  if (p == 1) {
+    if (outs[0] != ins[0]) HIP_TRY(hipMemcpyAsync(outs[0], ins[0], (size_t)(n * es), hipMemcpyDeviceToDevice, user));
+    return 0;
+  }
+  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
+  const int K = pipeline_depth(max_chunk * es);
+  // staging[r][j]: slice of chunk r sent by virtual rank j
+  TRY(st.staging.ensure((size_t)((int64_t)p * p * max_chunk * es)));
+  TRY(st.recv_ev.ensure(K));
+  TRY(st.sum_ev.ensure(K));
+  auto slot = [&](int r, int j) { return (char*)st.staging.p + ((int64_t)r * p + j) * max_chunk * es; };
+  TRY(join(st.comm_stream, user, st.ev_start));
+  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
+  for (int k = 0; k < K; k++) {
+    for (int r = 0; r < p; r++) {
+      const Range mine = chunk_of(n, p, align, r), ms = sub_of(mine, K, align, k);
+      if (ms.len() == 0) continue;
+      for (int j = 0; j < p; j++)
+        if (j != r)
+          HIP_TRY(hipMemcpyAsync(slot(r, j) + (ms.b - mine.b) * es, (const char*)ins[j] + ms.b * es,
+                                 (size_t)(ms.len() * es), hipMemcpyDeviceToDevice, st.comm_stream));
+    }
+    HIP_TRY(hipEventRecord(st.recv_ev.ev[k], st.comm_stream));
+    HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[k], 0));
+    for (int r = 0; r < p; r++) {
+      const Range mine = chunk_of(n, p, align, r), ms = sub_of(mine, K, align, k);
+      const void* srcs[tips::kMaxSrcs];
+      for (int j = 0; j < p; j++)
+        srcs[j] = (j == r) ? (const void*)((const char*)ins[r] + ms.b * es) : slot(r, j) + (ms.b - mine.b) * es;
+      HIP_TRY(tips::launch_multi_sum((char*)outs[r] + ms.b * es, srcs, p, ms.len(), dtype, st.comp_stream));
+    }
+    HIP_TRY(hipEventRecord(st.sum_ev.ev[k], st.comp_stream));
+  }
+  for (int k = 0; k < K; k++) {
+    HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[k], 0));
+    for (int r = 0; r < p; r++) {
+      const Range ms = sub_of(chunk_of(n, p, align, r), K, align, k);
+      if (ms.len() == 0) continue;
+      for (int j = 0; j < p; j++)
+        if (j != r)
+          HIP_TRY(hipMemcpyAsync((char*)outs[j] + ms.b * es, (const char*)outs[r] + ms.b * es, (size_t)(ms.len() * es),
+                                 hipMemcpyDeviceToDevice, st.comm_stream));
+    }
+  }
+  TRY(join(user, st.comm_stream, st.ev_done));
+  TRY(join(user, st.comp_stream, st.ev_comp_done));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+"""Tensor adapters: numpy arrays and torch tensors -> (pointer, count, dtype code).
+
+The reference's op accepts TF tensors of T in {int32, int64, float32, float64}
+(tips/tensorflow/ops.cc:121) and LOG(FATAL)s on anything else
+(tips/core/collective/utils.h:29-46). Here the same four plus float16 and
+bfloat16 are accepted; anything else raises TypeError with the reference's
+message text.
+"""
+import numpy as np
+
+from . import _lib
+
+_NP_CODES = {
+    np.dtype(np.float32): _lib.FLOAT32,
+    np.dtype(np.float64): _lib.FLOAT64,
+    np.dtype(np.int32): _lib.INT32,
+    np.dtype(np.int64): _lib.INT64,
+    np.dtype(np.float16): _lib.FLOAT16,
+}
+
+
+def _torch():
+    try:
+        import torch
+        return torch
+    except ImportError:  # pragma: no cover - torch is in the image
+        return None
+
+
+def _torch_codes(torch):
+    return {
+        torch.float32: _lib.FLOAT32,
+        torch.float64: _lib.FLOAT64,
+        torch.int32: _lib.INT32,
+        torch.int64: _lib.INT64,
+        torch.float16: _lib.FLOAT16,
+        torch.bfloat16: _lib.BFLOAT16,
+    }
+
+
+def is_torch(t):
+    torch = _torch()
+    return torch is not None and isinstance(t, torch.Tensor)
+
+
+def dtype_code(t):
+    """Dtype code of a numpy array or torch tensor; TypeError if unsupported."""
+    if is_torch(t):
+        code = _torch_codes(_torch()).get(t.dtype)
+    else:
+        code = _NP_CODES.get(np.asarray(t).dtype)
+    if code is None:
+        raise TypeError("Not supported dtype found: %s" % (t.dtype,))
+    return code
+
+
+def is_device(t):
+    return is_torch(t) and t.is_cuda
+
+
+def stream_of(t):
+    """hipStream_t (as int) the caller's work on `t` is ordered on; 0 for host tensors."""
+    if is_device(t):
+        return _torch().cuda.current_stream(t.device).cuda_stream
+    return 0
+
+
+def contiguous(t):
+    if is_torch(t):
+        return t.contiguous()
+    return np.ascontiguousarray(t)
+
+
+def empty_like(t):
+    if is_torch(t):
+        return _torch().empty_like(t, memory_format=_torch().contiguous_format)
+    return np.empty_like(t)
+
+
+def data_ptr(t):
+    if is_torch(t):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def numel(t):
+    if is_torch(t):
+        return t.numel()
+    return int(np.asarray(t).size)

@@ -1,0 +1,117 @@
+// sum_sweep.cc — gfx950 tuning sweep for the 2-input bucket-sum kernel.
+//
+// Config 2 of BASELINE.json: c = a + b over two 256 MiB fp32 buffers, all
+// variants of tips_sum_variant interleaved in ONE process (guide §5.4 rule 24:
+// N variants x M rounds, report median and min), plus hipMemcpy D2D as the
+// streaming reference on the same device. Random data (rule 25).
+// Prints one JSON object per variant.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../include/tips_hip.h"
+
+#define CHECK(x)                                                                              \
+  do {                                                                                        \
+    hipError_t e = (x);                                                                       \
+    if (e != hipSuccess) {                                                                    \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));        \
+      exit(1);                                                                                \
+    }                                                                                         \
+  } while (0)
+
+struct Variant {
+  std::string name;
+  int mode, unroll, nt, blocks;  // mode -1 = memcpy reference, -2 = in-place default
+  std::vector<double> ms;
+};
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : (int64_t)67108864;  // 256 MiB fp32
+  const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+  const int iters = argc > 3 ? atoi(argv[3]) : 20;
+  const size_t bytes = (size_t)n * 4;
+  float *a, *b, *c;
+  CHECK(hipMalloc(&a, bytes));
+  CHECK(hipMalloc(&b, bytes));
+  CHECK(hipMalloc(&c, bytes));
+  {
+    std::vector<float> h(n);
+    std::mt19937 g(1);
+    std::uniform_real_distribution<float> u(-1.f, 1.f);
+    for (auto& x : h) x = u(g);
+    CHECK(hipMemcpy(a, h.data(), bytes, hipMemcpyHostToDevice));
+    for (auto& x : h) x = u(g);
+    CHECK(hipMemcpy(b, h.data(), bytes, hipMemcpyHostToDevice));
+  }
+  std::vector<Variant> vs;
+  vs.push_back({"memcpy_d2d", -1, 0, 0, 0, {}});
+  vs.push_back({"default", -3, 0, 0, 0, {}});
+  for (int nt = 0; nt <= 1; nt++)
+    for (int u : {1, 2, 4, 8}) vs.push_back({"tile_u" + std::to_string(u) + (nt ? "_nt" : ""), 1, u, nt, 0, {}});
+  for (int nt = 0; nt <= 1; nt++)
+    for (int u : {1, 2, 4})
+      for (int bpc : {2, 4, 8, 16})
+        vs.push_back({"gs_u" + std::to_string(u) + "_b" + std::to_string(bpc) + (nt ? "_nt" : ""), 0, u, nt, 256 * bpc, {}});
+  hipStream_t s;
+  CHECK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  auto run = [&](Variant& v) {
+    if (v.mode == -1) {
+      CHECK(hipMemcpyAsync(c, a, bytes, hipMemcpyDeviceToDevice, s));
+    } else if (v.mode == -3) {
+      if (tips_bucket_sum(c, a, b, n, TIPS_FLOAT32, s) != 0) {
+        fprintf(stderr, "bucket_sum: %s\n", tips_last_error());
+        exit(1);
+      }
+    } else if (tips_sum_variant(c, a, b, n, TIPS_FLOAT32, v.mode, v.unroll, v.nt, v.blocks, s) != 0) {
+      fprintf(stderr, "variant %s: %s\n", v.name.c_str(), tips_last_error());
+      exit(1);
+    }
+  };
+  // correctness spot check of every sum variant
+  {
+    std::vector<float> ha(n), hb(n), hc(n);
+    CHECK(hipMemcpy(ha.data(), a, bytes, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(hb.data(), b, bytes, hipMemcpyDeviceToHost));
+    for (auto& v : vs) {
+      if (v.mode == -1) continue;
+      CHECK(hipMemset(c, 0, bytes));
+      run(v);
+      CHECK(hipStreamSynchronize(s));
+      CHECK(hipMemcpy(hc.data(), c, bytes, hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < n; i++)
+        if (hc[i] != ha[i] + hb[i]) {
+          fprintf(stderr, "variant %s wrong at %lld\n", v.name.c_str(), (long long)i);
+          return 1;
+        }
+    }
+  }
+  for (int r = 0; r < rounds; r++) {
+    for (auto& v : vs) {
+      run(v);  // warm
+      CHECK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; i++) run(v);
+      CHECK(hipEventRecord(e1, s));
+      CHECK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      v.ms.push_back(ms / iters);
+    }
+  }
+  for (auto& v : vs) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
+    const double moved = (v.mode == -1) ? 2.0 * bytes : 3.0 * bytes;
+    printf("{\"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f, \"GBps_median\": %.1f, \"GBps_best\": %.1f}\n",
+           v.name.c_str(), med * 1e3, mn * 1e3, moved / (med * 1e-3) / 1e9, moved / (mn * 1e-3) / 1e9);
+  }
+  return 0;
+}
