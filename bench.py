@@ -1,0 +1,338 @@
+#!/usr/bin/env python3
+"""bench.py — the TiPS gradient-bucket reduction path on MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...     (N > 1, one rank per GPU)
+
+N == 1 (BASELINE.json configs[1], the config the metric's first half is
+quoted on): one step = the device-resident sum of two 256 MiB fp32 gradient
+buffers, c = a + b (tips_bucket_sum: the per-chunk MPI_SUM of
+tips/core/collective/utils.h:60-65 as a gfx950 kernel). value = algorithmic
+bytes moved (2 reads + 1 write = 805,306,368 B per step) / time, GiB/s.
+
+N > 1 (configs[2]): one step = allreduce of one 1 GiB fp32 bucket per GPU
+(tips_allreduce: RCCL send/recv over xGMI + the sum kernels).
+value = N x 1 GiB / time (bucket bytes reduced by the whole job per second,
+GiB/s); algbw / busbw and the xGMI fraction are extra fields. Each rank checks
+its result against the fold of all ranks' seeded inputs after timing.
+
+Inputs are synthetic seeded uniforms generated on the device and resident in
+HBM before the timed region. At N == 1, rank 0 also times the reference's CPU
+path (MPI_Allreduce, MPI_SUM under MPICH on host cores) on a bounded sample —
+a reported baseline, not the target.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+METRIC = "device-resident fp32 bucket-sum GiB/s (% HBM peak); allreduce GiB/s 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+XGMI_LINK_GBPS = 153.0   # per link per direction (task / SURVEY §8d)
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--algo", default=os.environ.get("TIPS_ALGO", "auto"), choices=["auto", "ring", "direct", "rccl"])
+    ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
+    return ap.parse_args()
+
+
+# ----------------------------------------------------------------------------- CPU baseline (rank 0, N == 1)
+
+def cpu_baseline(bucket_elems):
+    """Time the reference's data-path call on host cores: MPI_Allreduce(MPI_FLOAT, MPI_SUM) with
+    np=2, one 256 MiB fp32 bucket per rank, i.e. the reference computing config 2's c = a + b.
+    Runs BEFORE anything touches the GPU (it starts child processes)."""
+    harness = os.path.join(REPO, "oracle", "build", "mpi_allreduce_ref")
+    mpirun = "/opt/conda/bin/mpirun"
+    out = {"value": None, "unit": "GiB/s", "cores": None, "kind": "reference", "sample": None}
+    if os.path.exists(harness) and os.path.exists(mpirun):
+        iters = 6
+        try:
+            r = subprocess.run([mpirun, "-np", "2", harness, "bench", "0", str(bucket_elems), str(iters)],
+                               capture_output=True, text=True, timeout=240)
+            line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+            res = json.loads(line)
+            t = res["sec_per_call"]
+            out.update(value=3 * bucket_elems * 4 / t / GIB, cores=2,
+                       sample="MPI_Allreduce(in,out,%d,MPI_FLOAT,MPI_SUM,MPI_COMM_WORLD) as in "
+                              "tips/core/collective/utils.h:60-65, MPICH 3.3.2, mpirun -np 2 (1 core each), "
+                              "one %d MiB fp32 bucket per rank (= config 2's a + b), %d timed calls after 1 warm-up, "
+                              "%.1f ms/call; value counts the same 3 x bucket bytes as the GPU metric"
+                              % (bucket_elems, bucket_elems * 4 >> 20, iters, t * 1e3))
+            out["ms_per_call"] = t * 1e3
+        except Exception as e:  # noqa: BLE001 - report, never fail the bench on the baseline leg
+            out["error"] = "reference MPI baseline failed: %r" % (e,)
+    else:
+        out["error"] = "reference MPI baseline unavailable on box (no MPICH harness)"
+    # the oracle port (single thread, plain C loop) on a 64 Mi-element sample
+    try:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import numpy as np
+        import oracle_bind
+        n = bucket_elems
+        a = np.random.default_rng(1).random(n, dtype=np.float32)
+        b = np.random.default_rng(2).random(n, dtype=np.float32)
+        oracle_bind.sum2(a, b)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            oracle_bind.sum2(a, b)
+        t = (time.perf_counter() - t0) / reps
+        out["port_single_thread"] = {"value": 3 * n * 4 / t / GIB, "unit": "GiB/s", "cores": 1, "kind": "port",
+                                     "sample": "oracle_sum2 (oracle/oracle.c) c=a+b, %d fp32, %d reps" % (n, reps)}
+        if out["value"] is None:
+            out.update({k: out["port_single_thread"][k] for k in ("value", "cores", "kind", "sample")})
+    except Exception as e:  # noqa: BLE001
+        out["port_error"] = repr(e)
+    return out
+
+
+def pmc_traffic(kernel_substr):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            k = d.get("kernels", {})
+            for name, v in k.items():
+                if kernel_substr in name and v.get("hbm_bytes_per_launch"):
+                    return {"bytes": v["hbm_bytes_per_launch"], "source": os.path.relpath(path, REPO)}
+        except Exception:  # noqa: BLE001
+            continue
+    return None
+
+
+# ----------------------------------------------------------------------------- N == 1: bucket sum
+
+def bench_sum(args):
+    steps = args.steps if args.steps is not None else 200
+    warmup = args.warmup if args.warmup is not None else 20
+    n = (args.bucket_mib or 256) * (1 << 20) // 4
+    cpu = None if args.no_cpu_baseline else cpu_baseline(n)
+
+    import torch
+    import tips_amd
+    from tips_amd import _lib
+    L = _lib.lib()
+    torch.cuda.set_device(0)
+    g = torch.Generator(device="cuda")
+    a = torch.empty(n, dtype=torch.float32, device="cuda")
+    b = torch.empty(n, dtype=torch.float32, device="cuda")
+    c = torch.empty(n, dtype=torch.float32, device="cuda")
+    g.manual_seed(1)
+    a.uniform_(-1.0, 1.0, generator=g)
+    g.manual_seed(2)
+    b.uniform_(-1.0, 1.0, generator=g)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step():
+        rc = L.tips_bucket_sum(c.data_ptr(), a.data_ptr(), b.data_ptr(), n, _lib.FLOAT32, sp)
+        if rc:
+            raise _lib.TipsError("tips_bucket_sum", rc, _lib.last_error())
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = ev0.elapsed_time(ev1) / steps  # HIP events on the kernel's stream = avg launch duration
+    ok = bool(torch.equal(c, a + b))   # one IEEE add per element: bit-exact vs torch
+
+    # PCIe-inclusive rate (the path starts and ends in host memory): pinned H2D a,b + sum + D2H c
+    ha, hb, hc = (torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(3))
+    ha.copy_(a)
+    hb.copy_(b)
+    torch.cuda.synchronize()
+    reps = 3
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        a.copy_(ha, non_blocking=True)
+        b.copy_(hb, non_blocking=True)
+        step()
+        hc.copy_(c, non_blocking=True)
+    torch.cuda.synchronize()
+    t_host = (time.perf_counter() - t1) / reps
+
+    moved = 3 * n * 4
+    t_s = ms / 1e3
+    achieved = moved / t_s / 1e9
+    tr = pmc_traffic("sum2_kernel")
+    line = {
+        "metric": METRIC, "value": round(moved / t_s / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(ms, 6), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: fp32 U[-1,1), torch cuda generator seeds 1 and 2, resident in HBM",
+        "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
+                   "bucket_bytes": n * 4, "elements": n, "kernel": "tips_bucket_sum (sum2_kernel<f32, tile, u4, nt>)",
+                   "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": (tr["bytes"] if tr else None)},
+        "cpu_baseline": cpu,
+        "input_bucket_gib_s": round(n * 4 / t_s / GIB, 2),
+        "algorithmic_bytes_per_step": moved,
+        "pcie_inclusive_gib_s": round(n * 4 / t_host / GIB, 3),
+        "pcie_inclusive_note": "pinned H2D of a and b + kernel + D2H of c, bucket bytes / wall time",
+        "check": "bit-exact vs torch a+b" if ok else "FAIL",
+        "wall_s_timed_region": round(wall, 4),
+    }
+    if tr:
+        line["roofline"]["traffic_source"] = tr["source"]
+    print(json.dumps(line), flush=True)
+    return 0 if ok else 1
+
+
+# ----------------------------------------------------------------------------- N > 1: allreduce
+
+def bench_allreduce(args):
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import tips_amd
+    from tips_amd import _lib
+    tips_amd.init()  # unique id through the gloo group, RCCL comm per GPU
+    L = _lib.lib()
+    algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL}
+    L.tips_set_algorithm(algo_names[args.algo])
+    algo = L.tips_resolve_algorithm(world)
+    inv = {v: k for k, v in algo_names.items()}
+
+    steps = args.steps if args.steps is not None else 20
+    warmup = args.warmup if args.warmup is not None else 5
+    n = (args.bucket_mib or 1024) * (1 << 20) // 4
+    g = torch.Generator(device="cuda")
+
+    def fill(t, r):
+        g.manual_seed(3000 + r)
+        t.uniform_(0.5, 1.5, generator=g)
+
+    x = torch.empty(n, dtype=torch.float32, device="cuda")
+    fill(x, rank)
+    y = torch.empty_like(x)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step():
+        rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, sp)
+        if rc:
+            raise _lib.TipsError("tips_allreduce", rc, _lib.last_error())
+
+    def timed(k):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        dist.barrier()
+        tmax = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        return tmax.item()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t = timed(steps)
+    ms = t / steps * 1e3
+
+    # parity: fold all ranks' seeded inputs on this device (rank order) and compare
+    ref = torch.zeros_like(x)
+    tmp = torch.empty_like(x)
+    for r in range(world):
+        fill(tmp, r)
+        ref = ref + tmp if r else tmp.clone()
+    if algo == _lib.ALGO_DIRECT:
+        ok = bool(torch.equal(y, ref))
+        check = "bit-exact vs rank-order fold" if ok else "FAIL"
+    else:
+        rel = ((y.double() - ref.double()).abs() / ref.double()).max().item()
+        ok = rel <= 1e-6
+        check = ("max rel err %.2e vs rank-order fold (<= 1e-6)" % rel) if ok else ("FAIL rel %.2e" % rel)
+    okt = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    del ref, tmp
+
+    # comparison points (same bucket): the other schedules and ncclAllReduce
+    compare = {}
+    if not args.no_compare:
+        for name in ("ring", "direct", "rccl"):
+            if algo_names[name] == algo:
+                continue
+            L.tips_set_algorithm(algo_names[name])
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            tc = timed(max(3, steps // 4))
+            compare[name] = round(n * 4 / (tc / max(3, steps // 4)) / GIB, 2)
+        L.tips_set_algorithm(algo_names[args.algo])
+
+    algbw = n * 4 / (ms / 1e3)  # bytes/s per rank
+    busbw = algbw * 2 * (world - 1) / world
+    links = 1 if algo == _lib.ALGO_RING else world - 1
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(world * n * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed 3000+rank, resident in HBM",
+            "config": {"workload": "config 3: allreduce of one 1 GiB fp32 bucket per GPU over xGMI",
+                       "bucket_bytes": n * 4, "algorithm": inv.get(algo, str(algo)),
+                       "parallelism": "dp%d (one process per GPU, RCCL p2p)" % world},
+            "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
+            "xgmi": {"busbw_GBps": round(busbw / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS, "links_used": links,
+                     "frac_of_links_used": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4),
+                     "frac_of_one_link": round(busbw / 1e9 / XGMI_LINK_GBPS, 4)},
+            "roofline": {"bound": "xgmi-link", "achieved": round(busbw / 1e9, 1),
+                         "peak": XGMI_LINK_GBPS * links, "unit": "GB/s",
+                         "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None},
+            "cpu_baseline": None,
+            "compare_algbw_gib_s": compare,
+            "check": check if okt.item() == 1 else "FAIL on some rank",
+        }
+        print(json.dumps(line), flush=True)
+    dist.barrier()
+    tips_amd.shutdown()
+    dist.destroy_process_group()
+    return 0 if okt.item() == 1 else 1
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1:
+        # launched without torchrun: start it as a child (never exec from a process that touched the GPU)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29511"),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.call(cmd)
+    if world > 1:
+        return bench_allreduce(args)
+    return bench_sum(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

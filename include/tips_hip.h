@@ -125,8 +125,10 @@ int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, 
  * (TIPS_FUSION_THRESHOLD bytes, default 64 MiB). One dtype for all. */
 int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
 
-/* Select the allreduce algorithm (enum tips_algorithm). Returns the previous one. */
+/* Select the allreduce algorithm (enum tips_algorithm). Returns TIPS_OK or an error. */
 int tips_set_algorithm(int algo);
+/* The algorithm currently selected (may be TIPS_ALGO_AUTO). */
+int tips_get_algorithm(void);
 /* The algorithm AUTO resolves to for a given rank count. */
 int tips_resolve_algorithm(int nranks);
 

@@ -1,0 +1,161 @@
+"""The C-ABI boundary without a GPU: the library loads, exports every symbol
+include/tips_hip.h declares, the Python binding declares each of them, and the
+argument / lifecycle error paths behave (no compute calls here)."""
+import ctypes
+import multiprocessing as mp
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "tips_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tips_\w+)\s*\(", src)))
+
+
+def test_header_parses():
+    names = header_functions()
+    # the reference's lifecycle names (tips/core/operations.h:7-21) are all kept
+    for ref in ("tips_init", "tips_shutdown", "tips_is_initialize", "tips_size", "tips_rank"):
+        assert ref in names
+    assert "tips_allreduce" in names and "tips_bucket_sum" in names
+
+
+def test_library_exports_every_header_symbol():
+    from tips_amd import _lib
+    L = _lib.lib()
+    missing = [n for n in header_functions() if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_python_binding_declares_every_symbol():
+    from tips_amd import _lib
+    declared = {n for n, _, _ in _lib._SIGNATURES}
+    assert set(header_functions()) == declared
+
+
+def test_lifecycle_before_init():
+    from tips_amd import _lib
+    L = _lib.lib()
+    assert not L.tips_is_initialize()
+    assert L.tips_size() == -1 and L.tips_rank() == -1
+    assert L.tips_version().startswith(b"tips_hip")
+    assert L.tips_unique_id_bytes() == 128
+    L.tips_shutdown()  # no-op when not initialised
+
+
+def test_error_codes():
+    from tips_amd import _lib
+    L = _lib.lib()
+    assert L.tips_allreduce(None, None, 10, _lib.FLOAT32, _lib.OP_SUM, None) == -2  # not initialised
+    assert b"tips_init" in L.tips_last_error()
+    assert L.tips_allreduce(None, None, 10, 99, _lib.OP_SUM, None) == -1  # bad dtype
+    assert L.tips_allreduce(None, None, 10, _lib.FLOAT32, _lib.OP_MAX, None) == -5  # only SUM
+    assert L.tips_bucket_sum(None, None, None, -1, _lib.FLOAT32, None) == -1
+    assert L.tips_bucket_sum(None, None, None, 0, _lib.FLOAT32, None) == 0  # empty is a no-op
+    assert L.tips_multi_sum(None, None, 17, 10, _lib.FLOAT32, None) == -1
+    assert L.tips_set_algorithm(7) == -1
+    assert L.tips_fused_allreduce(None, None, 0, _lib.FLOAT32, None) == -2
+    with pytest.raises(_lib.TipsError) as ei:
+        _lib.call("tips_allreduce", None, None, 10, 99, 0, None)
+    assert ei.value.code == -1
+
+
+def test_algorithm_resolution():
+    from tips_amd import _lib
+    L = _lib.lib()
+    prev = L.tips_get_algorithm()
+    assert L.tips_set_algorithm(_lib.ALGO_AUTO) == 0 and L.tips_get_algorithm() == _lib.ALGO_AUTO
+    assert L.tips_resolve_algorithm(2) == _lib.ALGO_RING
+    assert L.tips_resolve_algorithm(8) == _lib.ALGO_DIRECT
+    L.tips_set_algorithm(_lib.ALGO_RING)
+    assert L.tips_resolve_algorithm(8) == _lib.ALGO_RING
+    L.tips_set_algorithm(prev)
+
+
+@pytest.mark.parametrize("dtype,es", [(0, 4), (1, 8), (2, 4), (3, 8), (4, 2), (5, 2)])
+def test_chunk_bounds_match_oracle(oracle, dtype, es):
+    from tips_amd import _lib
+    L = _lib.lib()
+    b, e = ctypes.c_int64(), ctypes.c_int64()
+    for n in (0, 1, 7, 4099, 262144, 67108864 + 5):
+        for p in (1, 2, 3, 4, 8):
+            for c in range(p):
+                assert L.tips_chunk_bounds(n, p, dtype, c, ctypes.byref(b), ctypes.byref(e)) == 0
+                assert (b.value, e.value) == oracle.chunk_bounds(n, p, 256 // es, c)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _bootstrap_worker(rank, size, port, q):
+    from tips_amd import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(128)
+    if rank == 0:
+        ctypes.memmove(buf, bytes(range(128)), 128)
+    rc = L.tips_bootstrap_broadcast(rank, size, b"127.0.0.1", port, buf, 128, 60)
+    q.put((rank, rc, buf.raw))
+
+
+@pytest.mark.parametrize("size", [2, 4])
+def test_bootstrap_broadcast_multiprocess(size):
+    """The TCP id exchange tips_init uses, across real processes on CPU."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bootstrap_worker, args=(r, size, port, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+    for rank, rc, raw in res:
+        assert rc == 0, rank
+        assert raw == bytes(range(128))
+
+
+def test_bootstrap_timeout():
+    from tips_amd import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(16)
+    assert L.tips_bootstrap_broadcast(1, 2, b"127.0.0.1", _free_port(), buf, 16, 1) == -6
+    assert b"could not reach" in L.tips_last_error()
+
+
+def test_product_has_no_oracle_dependency():
+    """The shipped path never imports, links or loads oracle/ (DESIGN.md §Oracle)."""
+    for root, _, files in os.walk(os.path.join(REPO, "tips_amd")):
+        for f in files:
+            if f.endswith((".py", ".cc", ".hip", ".h")):
+                text = open(os.path.join(root, f)).read()
+                assert "oracle_bind" not in text and "liboracle" not in text and "import oracle" not in text, f
+
+
+def test_single_hip_runtime():
+    """Exactly one libamdhip64 / libhsa-runtime64 / librccl mapped after loading the library
+    (torch bundles copies with the same sonames; tips_amd._lib loads torch first)."""
+    import subprocess
+    import sys
+    code = ("import re\nfrom tips_amd import _lib\n_lib.lib()\nimport torch\n"
+            "m=open('/proc/self/maps').read()\n"
+            "for k in ('libamdhip64','libhsa-runtime64','librccl'):\n"
+            "    print(k, len(set(re.findall(r'(/\\S*'+k+r'\\S*)', m))))\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for line in r.stdout.strip().splitlines():
+        name, count = line.split()
+        assert count == "1", line

@@ -1,0 +1,176 @@
+"""-m gpu: the allreduce schedules and the drop-in surface, through the C-ABI.
+
+The ring and direct schedules are run for p virtual ranks on the one GPU of
+the test box (tips_ring_simulate / tips_direct_simulate: same chunking,
+sub-chunk pipeline, streams, events and sum kernels as the RCCL path; peer
+transfers become device copies) and compared bit-exact with the oracle's
+restatement of the same schedule; against the MPICH golden vectors they are
+held to the reference's tolerance (fp32 <= 1e-6 relative, ints bit-exact).
+The real RCCL exchange needs >1 GPU and is exercised by bench.py on the
+8-GPU node.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_cases, load_golden
+from gpu_util import ALL_DTYPES, BF16, F16, F32, F64, I32, I64, NPDT, from_dev, rand, same_bits, simulate, stream, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES)
+@pytest.mark.parametrize("p", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("n", [1, 7, 4099, 262144, 1000003])
+def test_ring_schedule_matches_oracle(gpu, oracle, dtype, p, n):
+    rng = np.random.default_rng(1000 * p + n % 997 + dtype)
+    ins = [rand(dtype, n, rng) for _ in range(p)]
+    exp = oracle.ring(ins, code=dtype)[0]
+    for got in simulate("ring", ins, dtype):
+        assert same_bits(got, exp, dtype)
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES)
+@pytest.mark.parametrize("p", [2, 3, 8, 16])
+@pytest.mark.parametrize("n", [1, 4099, 1000003])
+def test_direct_schedule_matches_oracle(gpu, oracle, dtype, p, n):
+    rng = np.random.default_rng(2000 * p + n % 991 + dtype)
+    ins = [rand(dtype, n, rng) for _ in range(p)]
+    exp = oracle.fold(ins, code=dtype, wide_acc=True)
+    for got in simulate("direct", ins, dtype):
+        assert same_bits(got, exp, dtype)
+
+
+@pytest.mark.parametrize("kind", ["ring", "direct"])
+@pytest.mark.parametrize("dtype", [F32, I64, F16])
+def test_pipelined_subchunks_inplace(gpu, oracle, monkeypatch, kind, dtype):
+    """Force K=4 sub-chunks on small buckets, in place (in == out)."""
+    monkeypatch.setenv("TIPS_MIN_SUBCHUNK_BYTES", "256")
+    monkeypatch.setenv("TIPS_PIPELINE_DEPTH", "4")
+    rng = np.random.default_rng(77)
+    for p, n in [(4, 50001), (7, 131), (8, 262147)]:
+        ins = [rand(dtype, n, rng) for _ in range(p)]
+        exp = oracle.ring(ins, code=dtype)[0] if kind == "ring" else oracle.fold(ins, code=dtype, wide_acc=True)
+        for got in simulate(kind, ins, dtype, inplace=True):
+            assert same_bits(got, exp, dtype)
+
+
+CASES = golden_cases()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("kind", ["ring", "direct"])
+def test_golden_vectors(gpu, name, kind):
+    ins, exp = load_golden(name)
+    dtype = {"f32": F32, "f64": F64, "i32": I32, "i64": I64}[CASES[name]["dtype"]]
+    outs = simulate(kind, [ins[r] for r in range(ins.shape[0])], dtype)
+    for got in outs:
+        assert np.array_equal(bits(got), bits(outs[0])), "every rank ends with the same bits"
+        if exp.dtype.kind == "i":
+            assert np.array_equal(got, exp)
+        elif name.startswith("signed"):
+            bound = 1e-6 * np.sum(np.abs(ins.astype(np.float64)), axis=0)
+            assert np.all(np.abs(got.astype(np.float64) - exp) <= bound)
+        elif name.startswith("kat"):
+            # the reference KAT tolerances: utils_test 1e-5, coordinator_test 1e-4, mpi_allreduce_test 1e-5
+            assert np.allclose(got, exp, rtol=0, atol=1e-6)
+        else:
+            assert (np.abs(got.astype(np.float64) - exp) / np.abs(exp)).max() <= 1e-6
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def test_reference_kats_formulas(gpu):
+    """The three reference KATs through both device schedules, with their own formulas/tolerances."""
+    p, n = 5, 4
+    ins = [np.array([i * 0.1 * r for i in range(n)], np.float64).astype(np.float32) for r in range(p)]
+    for kind in ("ring", "direct"):
+        out = simulate(kind, ins, F32)[0]
+        assert all(abs(out[i] - i * 0.1 * ((p - 1) * p / 2)) <= 1e-5 for i in range(n))
+        x = np.array([i * 0.1 for i in range(8)], np.float64).astype(np.float32)
+        out = simulate(kind, [x] * 3, F32)[0]
+        assert np.all(np.abs(x * 3 - out) <= 1e-4)
+        x = np.array([i * 0.1 for i in range(10)], np.float64).astype(np.float32)
+        out = simulate(kind, [x] * 3, F32)[0]
+        assert all(abs(out[i] - i * 0.1 * 3) <= 1e-5 for i in range(10))
+
+
+def test_empty_and_single_rank(gpu, oracle):
+    x = np.arange(10, dtype=np.float32)
+    assert np.array_equal(simulate("ring", [x], F32)[0], x)
+    assert np.array_equal(simulate("direct", [x], F32)[0], x)
+    from tips_amd import _lib
+    pp, _k = _lib.ptr_array([0, 0])
+    assert _lib.lib().tips_ring_simulate(pp, pp, 2, 0, F32, None) == 0
+
+
+@pytest.mark.slow
+def test_ring_p8_256MiB_property(gpu, oracle):
+    """8 virtual ranks x 256 MiB fp32 (config-3 shape at 1/4 size): ring == oracle ring, bitwise,
+    every rank identical, and within 1e-6 relative of a float64 sum (positive data)."""
+    p, n = 8, 67108864
+    ins = [(0.5 + np.random.default_rng(3000 + r).random(n)).astype(np.float32) for r in range(p)]
+    outs = simulate("ring", ins, F32, inplace=True)
+    exp = oracle.ring(ins)[0]
+    for got in outs:
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
+    ref = np.sum(np.stack(ins).astype(np.float64), axis=0)
+    assert (np.abs(outs[0] - ref) / ref).max() <= 1e-6
+
+
+# ------------------------------------------------------------------ drop-in surface (one rank)
+
+def test_allreduce_single_rank_device_and_host(gpu):
+    import torch
+    assert gpu.size() == 1 and gpu.rank() == 0
+    t = torch.randn(12345, device="cuda")
+    assert torch.equal(gpu.allreduce(t), t)
+    assert torch.equal(gpu.allreduce_op(t), t)
+    h = np.random.default_rng(0).random(1001).astype(np.float64)
+    assert np.array_equal(gpu.allreduce(h), h)
+    c = torch.arange(77, dtype=torch.int64)
+    assert torch.equal(gpu.allreduce(c), c)
+    f = torch.randn(999, device="cuda")
+    out = gpu.allreduce(f, compression=gpu.Compression.fp16)
+    assert out.dtype == torch.float32 and torch.equal(out, f.half().float())
+    with pytest.raises(TypeError, match="Not supported dtype"):
+        gpu.allreduce(torch.zeros(3, dtype=torch.uint8, device="cuda"))
+
+
+def test_rccl_allreduce_single_rank(gpu):
+    import torch
+    prev = gpu.set_algorithm("rccl")
+    try:
+        t = torch.randn(4096, device="cuda")
+        assert torch.equal(gpu.allreduce(t), t)
+    finally:
+        gpu.set_algorithm(prev)
+
+
+@pytest.mark.parametrize("threshold", [4096, 64 << 20])
+def test_fused_pack_unpack_round_trip(gpu, monkeypatch, threshold):
+    """One rank: fused allreduce == identity, so pack -> bucket -> unpack must move every byte exactly,
+    across many buckets, odd sizes, misaligned views and tensors larger than the threshold."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(threshold))
+    rng = np.random.default_rng(20261015)
+    sizes = [int(round(2 ** rng.uniform(0, 14))) for _ in range(300)] + [5000, 1]
+    base = torch.randn(sum(sizes) + 1, device="cuda")
+    views, off = [], 1  # offset 1: misaligned views
+    for s in sizes:
+        views.append(base[off:off + s])
+        off += s
+    before = [v.clone() for v in views]
+    gpu.fused_allreduce_(views)
+    gpu.fused_allreduce_(views)  # second call hits the plan cache
+    torch.cuda.synchronize()
+    for v, b in zip(views, before):
+        assert torch.equal(v, b)
+
+
+def test_allreduce_grads_identity_single_rank(gpu):
+    import torch
+    grads = [torch.randn(10, device="cuda"), None, torch.randn(3, 3, device="cuda")]
+    out = gpu.allreduce_grads(grads)
+    assert out[1] is None and torch.equal(out[0], grads[0]) and torch.equal(out[2], grads[2])

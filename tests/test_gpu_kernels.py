@@ -1,0 +1,121 @@
+"""-m gpu: the gfx950 bucket-sum kernels against the oracle, through the C-ABI.
+
+Bar (BASELINE.json north_star): bit-exact for integers; floats here are
+bit-exact too, because one IEEE add per element is order-free (f16 =
+correctly rounded half add, bf16 = fp32 add rounded to nearest-even).
+"""
+import numpy as np
+import pytest
+
+from gpu_util import (ALL_DTYPES, BF16, F16, F32, F64, I32, I64, NPDT, from_dev, rand, same_bits, stream, to_dev,
+                      with_specials)
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 7, 8, 9, 63, 4099, 65539, 1 << 20]
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES)
+@pytest.mark.parametrize("n", SIZES)
+def test_bucket_sum_matches_oracle(gpu, oracle, dtype, n):
+    import torch
+    from tips_amd import _lib
+    rng = np.random.default_rng(100 + n + dtype)
+    a, b = with_specials(rand(dtype, n, rng), dtype), rand(dtype, n, rng)
+    da, db = to_dev(a), to_dev(b)
+    dc = torch.empty_like(da)
+    _lib.call("tips_bucket_sum", dc.data_ptr(), da.data_ptr(), db.data_ptr(), n, dtype, stream())
+    torch.cuda.synchronize()
+    assert same_bits(from_dev(dc, dtype), oracle.sum2(a, b, code=dtype), dtype)
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES)
+def test_bucket_sum_inplace_and_unaligned(gpu, oracle, dtype):
+    import torch
+    from tips_amd import _lib
+    rng = np.random.default_rng(7)
+    n = 100003
+    a, b = rand(dtype, n, rng), rand(dtype, n, rng)
+    da, db = to_dev(a), to_dev(b)
+    _lib.call("tips_bucket_sum", da.data_ptr(), da.data_ptr(), db.data_ptr(), n, dtype, stream())  # a += b
+    torch.cuda.synchronize()
+    assert same_bits(from_dev(da, dtype), oracle.sum2(a, b, code=dtype), dtype)
+    # views offset by one element: not 16-B aligned -> scalar path
+    da, db = to_dev(a), to_dev(b)
+    dc = torch.empty_like(da)
+    _lib.call("tips_bucket_sum", dc[1:].data_ptr(), da[1:].data_ptr(), db[1:].data_ptr(), n - 1, dtype, stream())
+    torch.cuda.synchronize()
+    assert same_bits(from_dev(dc, dtype)[1:], oracle.sum2(a[1:], b[1:], code=dtype), dtype)
+
+
+def test_int_wrap_on_device(gpu, oracle):
+    import torch
+    from tips_amd import _lib
+    a = np.array([2**31 - 1] * 37, dtype=np.int32)
+    b = np.array([1] * 37, dtype=np.int32)
+    da, db = to_dev(a), to_dev(b)
+    _lib.call("tips_bucket_sum", da.data_ptr(), da.data_ptr(), db.data_ptr(), 37, I32, stream())
+    torch.cuda.synchronize()
+    assert (from_dev(da, I32) == -2**31).all()
+
+
+@pytest.mark.parametrize("mode,unroll,nt", [(m, u, t) for m in (0, 1) for u in (1, 2, 4, 8) for t in (0, 1)])
+def test_every_sum_variant_is_exact(gpu, oracle, mode, unroll, nt):
+    import torch
+    from tips_amd import _lib
+    rng = np.random.default_rng(11)
+    n = (1 << 20) + 5
+    a, b = rand(F32, n, rng), rand(F32, n, rng)
+    da, db = to_dev(a), to_dev(b)
+    dc = torch.empty_like(da)
+    _lib.call("tips_sum_variant", dc.data_ptr(), da.data_ptr(), db.data_ptr(), n, F32, mode, unroll, nt, 512,
+              stream())
+    torch.cuda.synchronize()
+    assert same_bits(from_dev(dc, F32), oracle.sum2(a, b), F32)
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES)
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 5, 8, 16])
+def test_multi_sum_matches_oracle_fold(gpu, oracle, dtype, nsrc):
+    import torch
+    from tips_amd import _lib
+    rng = np.random.default_rng(200 + nsrc * 7 + dtype)
+    n = 4099 * 3
+    ins = [rand(dtype, n, rng) for _ in range(nsrc)]
+    devs = [to_dev(x) for x in ins]
+    out = torch.empty_like(devs[0])
+    pp, _keep = _lib.ptr_array([d.data_ptr() for d in devs])
+    _lib.call("tips_multi_sum", out.data_ptr(), pp, nsrc, n, dtype, stream())
+    torch.cuda.synchronize()
+    assert same_bits(from_dev(out, dtype), oracle.fold(ins, code=dtype, wide_acc=True), dtype)
+    # in place into the last source, unaligned view
+    pp, _keep = _lib.ptr_array([d[1:].data_ptr() for d in devs])
+    _lib.call("tips_multi_sum", devs[-1][1:].data_ptr(), pp, nsrc, n - 1, dtype, stream())
+    torch.cuda.synchronize()
+    exp = oracle.fold([x[1:] for x in ins], code=dtype, wide_acc=True)
+    assert same_bits(from_dev(devs[-1], dtype)[1:], exp, dtype)
+
+
+@pytest.mark.slow
+def test_config2_full_size(gpu, oracle):
+    """BASELINE config 2: two 256 MiB fp32 buffers, U[-1,1), seeds 1 and 2; out-of-place and in-place."""
+    import torch
+    from tips_amd import _lib
+    n = 67108864
+    a = (np.random.default_rng(1).random(n) * 2 - 1).astype(np.float32)
+    b = (np.random.default_rng(2).random(n) * 2 - 1).astype(np.float32)
+    exp = oracle.sum2(a, b)
+    da, db = to_dev(a), to_dev(b)
+    dc = torch.empty_like(da)
+    _lib.call("tips_bucket_sum", dc.data_ptr(), da.data_ptr(), db.data_ptr(), n, F32, stream())
+    _lib.call("tips_bucket_sum", da.data_ptr(), da.data_ptr(), db.data_ptr(), n, F32, stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(from_dev(dc, F32).view(np.uint32), exp.view(np.uint32))
+    assert np.array_equal(from_dev(da, F32).view(np.uint32), exp.view(np.uint32))
+
+
+def test_python_bucket_sum(gpu):
+    import torch
+    a = torch.randn(1000, device="cuda")
+    b = torch.randn(1000, device="cuda")
+    assert torch.equal(gpu.bucket_sum(a, b), a + b)

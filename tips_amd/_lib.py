@@ -69,6 +69,7 @@ _SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),
+    ("tips_get_algorithm", ctypes.c_int, []),
     ("tips_resolve_algorithm", ctypes.c_int, [ctypes.c_int]),
     ("tips_ring_simulate", ctypes.c_int,
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
@@ -84,11 +85,29 @@ _SIGNATURES = [
 ]
 
 
+def _share_torch_runtime():
+    """Import torch before dlopen-ing libtips_hip.so.
+
+    torch-ROCm bundles its own libamdhip64 / libhsa-runtime64 / librccl with
+    the same sonames as /opt/rocm's (libamdhip64.so.7, ...). If our library is
+    loaded first, torch later maps a second HIP runtime into the process and
+    torch's streams / allocations would be handed to a runtime that does not
+    own them. Loaded after torch, our DT_NEEDED entries resolve to the copies
+    torch already mapped, so the process has exactly one HIP runtime and one
+    RCCL (tests/test_abi.py::test_single_hip_runtime checks /proc/self/maps).
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - standalone use: /opt/rocm's runtime
+        pass
+
+
 def lib():
     """Load (once) and return the ctypes handle; raises TipsLibraryError if absent."""
     global _lib
     if _lib is not None:
         return _lib
+    _share_torch_runtime()
     with _lock:
         if _lib is None:
             if not os.path.exists(LIB_PATH):

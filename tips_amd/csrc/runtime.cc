@@ -593,10 +593,11 @@ int tips_set_algorithm(int algo) {
   if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_RCCL) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
-  int prev = st.algo;
   st.algo = algo;
-  return prev;
+  return 0;
 }
+
+int tips_get_algorithm(void) { return S().algo; }
 
 int tips_resolve_algorithm(int nranks) { return resolve_algo(S().algo, nranks); }
 

@@ -84,5 +84,6 @@ def set_algorithm(algo):
     """Select 'auto', 'ring', 'direct' or 'rccl'; returns the previous selection's name."""
     names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL}
     inv = {v: k for k, v in names.items()}
-    prev = _lib.call("tips_set_algorithm", names[algo])
+    prev = _lib.lib().tips_get_algorithm()
+    _lib.call("tips_set_algorithm", names[algo])
     return inv.get(prev, str(prev))
