@@ -182,7 +182,7 @@ def bench_sum(args):
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: fp32 U[-1,1), torch cuda generator seeds 1 and 2, resident in HBM",
         "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
-                   "bucket_bytes": n * 4, "elements": n, "kernel": "tips_bucket_sum (sum2_kernel<f32, tile, u4, nt>)",
+                   "bucket_bytes": n * 4, "elements": n, "kernel": "tips_bucket_sum (sum2_kernel<f32, one tile/workgroup, one 16-B vector per lane per operand, nt loads, plain stores, 256 threads>)",
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),

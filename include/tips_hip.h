@@ -145,11 +145,13 @@ int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64
 
 /* Explicit variant of the 2-input sum kernel, for the gfx950 tuning sweep
  * (tools/sum_sweep.cc): mode 0 = grid-stride over `blocks` workgroups,
- * mode 1 = one tile per workgroup; unroll = 16-B vectors per lane in flight
- * (1/2/4/8); nt = non-temporal loads and stores. tips_bucket_sum uses the
- * default chosen from that sweep. */
+ * mode 1 = one tile per workgroup; unroll = 16-B vectors per lane in flight;
+ * nt: 0 plain, 1 non-temporal loads+stores, 2 nt loads only, 3 nt stores only;
+ * threads = workgroup size. Non-default variants exist for f32 only
+ * (others return TIPS_ERR_HIP). tips_bucket_sum uses the default chosen
+ * from that sweep. */
 int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
-                     int blocks, void* stream);
+                     int blocks, int threads, void* stream);
 
 /* Chunk partition the ring uses (element offsets), for tests. */
 int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end);

@@ -59,8 +59,16 @@ def test_int_wrap_on_device(gpu, oracle):
     assert (from_dev(da, I32) == -2**31).all()
 
 
-@pytest.mark.parametrize("mode,unroll,nt", [(m, u, t) for m in (0, 1) for u in (1, 2, 4, 8) for t in (0, 1)])
-def test_every_sum_variant_is_exact(gpu, oracle, mode, unroll, nt):
+SWEEP_VARIANTS = ([(m, u, t, 256) for m in (0, 1) for u in (1, 2, 4, 8) for t in (0, 1)]
+                  + [(1, 2, 2, 256), (1, 4, 2, 256), (1, 2, 3, 256), (1, 4, 3, 256), (1, 2, 1, 512), (1, 4, 1, 512),
+                     (1, 8, 1, 512), (1, 1, 1, 1024), (1, 2, 1, 1024), (1, 4, 1, 1024), (1, 4, 2, 512),
+                     (1, 4, 3, 512), (1, 16, 1, 256), (1, 16, 1, 128), (1, 8, 1, 128), (1, 4, 1, 128), (1, 8, 1, 64),
+                     (1, 1, 2, 256), (1, 8, 2, 256), (1, 2, 2, 512), (1, 2, 2, 128), (1, 1, 2, 512), (0, 2, 2, 256),
+                     (0, 4, 2, 256)])
+
+
+@pytest.mark.parametrize("mode,unroll,nt,threads", SWEEP_VARIANTS)
+def test_every_sum_variant_is_exact(gpu, oracle, mode, unroll, nt, threads):
     import torch
     from tips_amd import _lib
     rng = np.random.default_rng(11)
@@ -69,7 +77,7 @@ def test_every_sum_variant_is_exact(gpu, oracle, mode, unroll, nt):
     da, db = to_dev(a), to_dev(b)
     dc = torch.empty_like(da)
     _lib.call("tips_sum_variant", dc.data_ptr(), da.data_ptr(), db.data_ptr(), n, F32, mode, unroll, nt, 512,
-              stream())
+              threads, stream())
     torch.cuda.synchronize()
     assert same_bits(from_dev(dc, F32), oracle.sum2(a, b), F32)
 

@@ -77,7 +77,7 @@ _SIGNATURES = [
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_sum_variant", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-      ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_chunk_bounds", ctypes.c_int,
      [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p]),
     ("tips_bootstrap_broadcast", ctypes.c_int,

@@ -27,8 +27,9 @@ hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t 
 
 // Tuning/sweep entry: explicit variant of the 2-input sum.
 //   mode 0 = grid-stride over (blocks) workgroups, mode 1 = one tile per workgroup
-//   unroll = 16-B vectors per lane in flight (1, 2, 4, 8), nt = non-temporal loads/stores
+//   unroll = 16-B vectors per lane in flight, nt: 0 plain, 1 non-temporal loads+stores,
+//   2 nt loads only, 3 nt stores only; threads = workgroup size. Non-default variants are f32 only.
 hipError_t launch_sum2_variant(void* dst, const void* a, const void* b, int64_t n, int dtype, int mode, int unroll,
-                               int nt, int blocks, hipStream_t s);
+                               int nt, int blocks, int threads, hipStream_t s);
 
 }  // namespace tips

@@ -147,29 +147,29 @@ __device__ __forceinline__ void add_elem<kBF16>(void* d, const void* a, const vo
 // ---------------------------------------------------------------------------
 // 2-input sum: dst = a + b
 
-template <int DT, int MODE, int UNROLL, bool NT>
-__global__ __launch_bounds__(kBlock) void sum2_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
-                                                     const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
-                                                     int64_t n) {
-  constexpr int64_t kTile = (int64_t)kBlock * UNROLL;  // vectors per workgroup-iteration
+template <int DT, int MODE, int UNROLL, bool NTL, bool NTS, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
+                                                    const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
+                                                    int64_t n) {
+  constexpr int64_t kTile = (int64_t)BLOCK * UNROLL;  // vectors per workgroup-iteration
   const int tid = threadIdx.x;
   int64_t t = blockIdx.x;
   const int64_t tstride = (MODE == 0) ? (int64_t)gridDim.x : 0;
   do {
     const int64_t base = t * kTile + tid;
-    if (base + (UNROLL - 1) * kBlock < nvec) {
+    if (base + (UNROLL - 1) * BLOCK < nvec) {
       u32x4 x[UNROLL], y[UNROLL];
 #pragma unroll
-      for (int u = 0; u < UNROLL; u++) x[u] = ld16<NT>(a + base + u * kBlock);
+      for (int u = 0; u < UNROLL; u++) x[u] = ld16<NTL>(a + base + u * BLOCK);
 #pragma unroll
-      for (int u = 0; u < UNROLL; u++) y[u] = ld16<NT>(b + base + u * kBlock);
+      for (int u = 0; u < UNROLL; u++) y[u] = ld16<NTL>(b + base + u * BLOCK);
 #pragma unroll
-      for (int u = 0; u < UNROLL; u++) st16<NT>(dst + base + u * kBlock, add16<DT>(x[u], y[u]));
+      for (int u = 0; u < UNROLL; u++) st16<NTS>(dst + base + u * BLOCK, add16<DT>(x[u], y[u]));
     } else {
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
-        const int64_t i = base + u * kBlock;
-        if (i < nvec) st16<NT>(dst + i, add16<DT>(ld16<NT>(a + i), ld16<NT>(b + i)));
+        const int64_t i = base + u * BLOCK;
+        if (i < nvec) st16<NTS>(dst + i, add16<DT>(ld16<NTL>(a + i), ld16<NTL>(b + i)));
       }
     }
     t += tstride;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
     if (i < nvec) {
       u32x4 v[NSRC];
 #pragma unroll
-      for (int j = 0; j < NSRC; j++) v[j] = srcs.p[j][i];
+      for (int j = 0; j < NSRC; j++) v[j] = ld16<true>(srcs.p[j] + i);
       typename W::A acc = W::load(v[0]);
 #pragma unroll
       for (int j = 1; j < NSRC; j++) acc = acc + W::load(v[j]);
@@ -356,23 +356,24 @@ constexpr int kNumCUs = 256;
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-template <int DT, int MODE, int UNROLL, bool NT>
+template <int DT, int MODE, int UNROLL, bool NTL, bool NTS, int BLOCK>
 hipError_t run_sum2(void* dst, const void* a, const void* b, int64_t n, int blocks, hipStream_t s) {
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
-  const int64_t tiles = (nvec + (int64_t)kBlock * UNROLL - 1) / ((int64_t)kBlock * UNROLL);
+  const int64_t tiles = (nvec + (int64_t)BLOCK * UNROLL - 1) / ((int64_t)BLOCK * UNROLL);
   int64_t grid = (MODE == 1) ? tiles : (blocks > 0 ? blocks : kNumCUs * 8);
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((sum2_kernel<DT, MODE, UNROLL, NT>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst,
-                     (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);
+  hipLaunchKernelGGL((sum2_kernel<DT, MODE, UNROLL, NTL, NTS, BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
+                     (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);
   return hipGetLastError();
 }
 
+// nt: 0 = plain, 1 = non-temporal loads and stores, 2 = nt loads only, 3 = nt stores only
 template <int DT>
 hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int mode, int unroll, int nt, int blocks,
-                         hipStream_t s) {
+                         int threads, hipStream_t s) {
   if (!(aligned16(dst) && aligned16(a) && aligned16(b))) {
     int64_t grid = (n + kBlock - 1) / kBlock;
     if (grid > kNumCUs * 16) grid = kNumCUs * 16;
@@ -380,31 +381,59 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     hipLaunchKernelGGL((sum2_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, a, b, n);
     return hipGetLastError();
   }
-#define TIPS_SUM2_CASE(M, U, NTV) \
-  if (mode == M && unroll == U && (nt != 0) == NTV) return run_sum2<DT, M, U, NTV>(dst, a, b, n, blocks, s);
-  TIPS_SUM2_CASE(1, 1, false)
-  TIPS_SUM2_CASE(1, 2, false)
-  TIPS_SUM2_CASE(1, 4, false)
-  TIPS_SUM2_CASE(1, 8, false)
-  TIPS_SUM2_CASE(1, 1, true)
-  TIPS_SUM2_CASE(1, 2, true)
-  TIPS_SUM2_CASE(1, 4, true)
-  TIPS_SUM2_CASE(1, 8, true)
-  TIPS_SUM2_CASE(0, 1, false)
-  TIPS_SUM2_CASE(0, 2, false)
-  TIPS_SUM2_CASE(0, 4, false)
-  TIPS_SUM2_CASE(0, 8, false)
-  TIPS_SUM2_CASE(0, 1, true)
-  TIPS_SUM2_CASE(0, 2, true)
-  TIPS_SUM2_CASE(0, 4, true)
-  TIPS_SUM2_CASE(0, 8, true)
+#define TIPS_SUM2_CASE(M, U, NTV, L, S_, B)                      \
+  if (mode == M && unroll == U && nt == NTV && threads == B) \
+    return run_sum2<DT, M, U, L, S_, B>(dst, a, b, n, blocks, s);
+  // the product default first; the rest exist for the tuning sweep (f32 only)
+  TIPS_SUM2_CASE(1, 1, 2, true, false, 256)
+  if constexpr (DT == kF32) {
+    TIPS_SUM2_CASE(1, 4, 1, true, true, 256)
+    TIPS_SUM2_CASE(1, 2, 2, true, false, 256)
+    TIPS_SUM2_CASE(1, 8, 2, true, false, 256)
+    TIPS_SUM2_CASE(1, 2, 2, true, false, 512)
+    TIPS_SUM2_CASE(1, 2, 2, true, false, 128)
+    TIPS_SUM2_CASE(1, 1, 2, true, false, 512)
+    TIPS_SUM2_CASE(0, 2, 2, true, false, 256)
+    TIPS_SUM2_CASE(0, 4, 2, true, false, 256)
+    TIPS_SUM2_CASE(1, 1, 0, false, false, 256)
+    TIPS_SUM2_CASE(1, 2, 0, false, false, 256)
+    TIPS_SUM2_CASE(1, 4, 0, false, false, 256)
+    TIPS_SUM2_CASE(1, 8, 0, false, false, 256)
+    TIPS_SUM2_CASE(1, 1, 1, true, true, 256)
+    TIPS_SUM2_CASE(1, 2, 1, true, true, 256)
+    TIPS_SUM2_CASE(1, 8, 1, true, true, 256)
+    TIPS_SUM2_CASE(0, 1, 0, false, false, 256)
+    TIPS_SUM2_CASE(0, 2, 0, false, false, 256)
+    TIPS_SUM2_CASE(0, 4, 0, false, false, 256)
+    TIPS_SUM2_CASE(0, 8, 0, false, false, 256)
+    TIPS_SUM2_CASE(0, 1, 1, true, true, 256)
+    TIPS_SUM2_CASE(0, 2, 1, true, true, 256)
+    TIPS_SUM2_CASE(0, 4, 1, true, true, 256)
+    TIPS_SUM2_CASE(0, 8, 1, true, true, 256)
+    TIPS_SUM2_CASE(1, 4, 2, true, false, 256)
+    TIPS_SUM2_CASE(1, 2, 3, false, true, 256)
+    TIPS_SUM2_CASE(1, 4, 3, false, true, 256)
+    TIPS_SUM2_CASE(1, 2, 1, true, true, 512)
+    TIPS_SUM2_CASE(1, 4, 1, true, true, 512)
+    TIPS_SUM2_CASE(1, 8, 1, true, true, 512)
+    TIPS_SUM2_CASE(1, 1, 1, true, true, 1024)
+    TIPS_SUM2_CASE(1, 2, 1, true, true, 1024)
+    TIPS_SUM2_CASE(1, 4, 1, true, true, 1024)
+    TIPS_SUM2_CASE(1, 4, 2, true, false, 512)
+    TIPS_SUM2_CASE(1, 4, 3, false, true, 512)
+    TIPS_SUM2_CASE(1, 16, 1, true, true, 256)
+    TIPS_SUM2_CASE(1, 16, 1, true, true, 128)
+    TIPS_SUM2_CASE(1, 8, 1, true, true, 128)
+    TIPS_SUM2_CASE(1, 4, 1, true, true, 128)
+    TIPS_SUM2_CASE(1, 8, 1, true, true, 64)
+  }
 #undef TIPS_SUM2_CASE
   return hipErrorInvalidValue;
 }
 
 // Default variant for the product path (chosen from the gfx950 sweep,
 // profiles/ + DESIGN.md §Kernels).
-constexpr int kDefMode = 1, kDefUnroll = 4, kDefNT = 1;
+constexpr int kDefMode = 1, kDefUnroll = 1, kDefNT = 2, kDefThreads = 256;
 
 template <int DT, int NSRC>
 hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
@@ -457,21 +486,21 @@ hipError_t multi_dispatch(void* dst, const void* const* srcs, int nsrc, int64_t 
 }  // namespace
 
 hipError_t launch_sum2_variant(void* dst, const void* a, const void* b, int64_t n, int dtype, int mode, int unroll,
-                               int nt, int blocks, hipStream_t s) {
+                               int nt, int blocks, int threads, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   switch (dtype) {
-    case kF32: return sum2_dispatch<kF32>(dst, a, b, n, mode, unroll, nt, blocks, s);
-    case kF64: return sum2_dispatch<kF64>(dst, a, b, n, mode, unroll, nt, blocks, s);
-    case kI32: return sum2_dispatch<kI32>(dst, a, b, n, mode, unroll, nt, blocks, s);
-    case kI64: return sum2_dispatch<kI64>(dst, a, b, n, mode, unroll, nt, blocks, s);
-    case kF16: return sum2_dispatch<kF16>(dst, a, b, n, mode, unroll, nt, blocks, s);
-    case kBF16: return sum2_dispatch<kBF16>(dst, a, b, n, mode, unroll, nt, blocks, s);
+    case kF32: return sum2_dispatch<kF32>(dst, a, b, n, mode, unroll, nt, blocks, threads, s);
+    case kF64: return sum2_dispatch<kF64>(dst, a, b, n, mode, unroll, nt, blocks, threads, s);
+    case kI32: return sum2_dispatch<kI32>(dst, a, b, n, mode, unroll, nt, blocks, threads, s);
+    case kI64: return sum2_dispatch<kI64>(dst, a, b, n, mode, unroll, nt, blocks, threads, s);
+    case kF16: return sum2_dispatch<kF16>(dst, a, b, n, mode, unroll, nt, blocks, threads, s);
+    case kBF16: return sum2_dispatch<kBF16>(dst, a, b, n, mode, unroll, nt, blocks, threads, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t launch_sum2(void* dst, const void* a, const void* b, int64_t n, int dtype, hipStream_t s) {
-  return launch_sum2_variant(dst, a, b, n, dtype, kDefMode, kDefUnroll, kDefNT, 0, s);
+  return launch_sum2_variant(dst, a, b, n, dtype, kDefMode, kDefUnroll, kDefNT, 0, kDefThreads, s);
 }
 
 hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t s) {

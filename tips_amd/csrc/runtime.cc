@@ -620,10 +620,10 @@ int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int 
 }
 
 int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
-                     int blocks, void* stream) {
+                     int blocks, int threads, void* stream) {
   TRY(check_dtype(dtype));
   if (count <= 0) return 0;
-  HIP_TRY(tips::launch_sum2_variant(dst, a, b, count, dtype, mode, unroll, nt, blocks, (hipStream_t)stream));
+  HIP_TRY(tips::launch_sum2_variant(dst, a, b, count, dtype, mode, unroll, nt, blocks, threads, (hipStream_t)stream));
   return 0;
 }
 

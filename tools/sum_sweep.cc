@@ -27,7 +27,7 @@
 
 struct Variant {
   std::string name;
-  int mode, unroll, nt, blocks;  // mode -1 = memcpy reference, -2 = in-place default
+  int mode, unroll, nt, blocks, threads;  // mode -1 = memcpy reference, -3 = tips_bucket_sum default
   std::vector<double> ms;
 };
 
@@ -50,14 +50,24 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(b, h.data(), bytes, hipMemcpyHostToDevice));
   }
   std::vector<Variant> vs;
-  vs.push_back({"memcpy_d2d", -1, 0, 0, 0, {}});
-  vs.push_back({"default", -3, 0, 0, 0, {}});
-  for (int nt = 0; nt <= 1; nt++)
-    for (int u : {1, 2, 4, 8}) vs.push_back({"tile_u" + std::to_string(u) + (nt ? "_nt" : ""), 1, u, nt, 0, {}});
-  for (int nt = 0; nt <= 1; nt++)
-    for (int u : {1, 2, 4})
-      for (int bpc : {2, 4, 8, 16})
-        vs.push_back({"gs_u" + std::to_string(u) + "_b" + std::to_string(bpc) + (nt ? "_nt" : ""), 0, u, nt, 256 * bpc, {}});
+  vs.push_back({"memcpy_d2d", -1, 0, 0, 0, 0, {}});
+  vs.push_back({"default", -3, 0, 0, 0, 0, {}});
+  vs.push_back({"multi_sum_8src", -4, 0, 0, 0, 0, {}});  // 8 x (n/8) sources -> n/8 output (direct-algorithm kernel)
+  const char* ntn[] = {"", "_nt", "_ntld", "_ntst"};
+  // (mode 1 = one tile per workgroup) unroll, nt, threads — the f32 variants kernels.hip instantiates
+  const int tiles[][3] = {{1, 0, 256}, {2, 0, 256}, {4, 0, 256}, {8, 0, 256}, {1, 1, 256}, {2, 1, 256}, {4, 1, 256},
+                          {8, 1, 256}, {2, 2, 256}, {4, 2, 256}, {2, 3, 256}, {4, 3, 256}, {2, 1, 512}, {4, 1, 512},
+                          {8, 1, 512}, {1, 1, 1024}, {2, 1, 1024}, {4, 1, 1024}, {4, 2, 512}, {4, 3, 512},
+                          {16, 1, 256}, {16, 1, 128}, {8, 1, 128}, {4, 1, 128}, {8, 1, 64},
+                          {1, 2, 256}, {8, 2, 256}, {2, 2, 512}, {2, 2, 128}, {1, 2, 512}};
+  for (auto& t : tiles)
+    vs.push_back({"tile_u" + std::to_string(t[0]) + ntn[t[1]] + "_t" + std::to_string(t[2]), 1, t[0], t[1], 0, t[2], {}});
+  for (int u : {1, 2, 4, 8})
+    for (int bpc : {2, 8, 16})
+      vs.push_back({"gs_u" + std::to_string(u) + "_b" + std::to_string(bpc) + "_nt", 0, u, 1, 256 * bpc, 256, {}});
+  for (int u : {2, 4})
+    for (int bpc : {2, 4, 8})
+      vs.push_back({"gs_u" + std::to_string(u) + "_b" + std::to_string(bpc) + "_ntld", 0, u, 2, 256 * bpc, 256, {}});
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
@@ -66,12 +76,19 @@ int main(int argc, char** argv) {
   auto run = [&](Variant& v) {
     if (v.mode == -1) {
       CHECK(hipMemcpyAsync(c, a, bytes, hipMemcpyDeviceToDevice, s));
+    } else if (v.mode == -4) {
+      const void* srcs[8];
+      for (int j = 0; j < 8; j++) srcs[j] = (j < 4 ? a : b) + (j % 4) * (n / 8);
+      if (tips_multi_sum(c, srcs, 8, n / 8, TIPS_FLOAT32, s) != 0) {
+        fprintf(stderr, "multi_sum: %s\n", tips_last_error());
+        exit(1);
+      }
     } else if (v.mode == -3) {
       if (tips_bucket_sum(c, a, b, n, TIPS_FLOAT32, s) != 0) {
         fprintf(stderr, "bucket_sum: %s\n", tips_last_error());
         exit(1);
       }
-    } else if (tips_sum_variant(c, a, b, n, TIPS_FLOAT32, v.mode, v.unroll, v.nt, v.blocks, s) != 0) {
+    } else if (tips_sum_variant(c, a, b, n, TIPS_FLOAT32, v.mode, v.unroll, v.nt, v.blocks, v.threads, s) != 0) {
       fprintf(stderr, "variant %s: %s\n", v.name.c_str(), tips_last_error());
       exit(1);
     }
@@ -82,7 +99,7 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(ha.data(), a, bytes, hipMemcpyDeviceToHost));
     CHECK(hipMemcpy(hb.data(), b, bytes, hipMemcpyDeviceToHost));
     for (auto& v : vs) {
-      if (v.mode == -1) continue;
+      if (v.mode == -1 || v.mode == -4) continue;
       CHECK(hipMemset(c, 0, bytes));
       run(v);
       CHECK(hipStreamSynchronize(s));
@@ -109,7 +126,7 @@ int main(int argc, char** argv) {
   for (auto& v : vs) {
     std::sort(v.ms.begin(), v.ms.end());
     const double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
-    const double moved = (v.mode == -1) ? 2.0 * bytes : 3.0 * bytes;
+    const double moved = (v.mode == -1) ? 2.0 * bytes : (v.mode == -4) ? 9.0 * bytes / 8 : 3.0 * bytes;
     printf("{\"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f, \"GBps_median\": %.1f, \"GBps_best\": %.1f}\n",
            v.name.c_str(), med * 1e3, mn * 1e3, moved / (med * 1e-3) / 1e9, moved / (mn * 1e-3) / 1e9);
   }
