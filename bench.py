@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
+    ap.add_argument("--workload", default="auto", choices=["auto", "sum", "bucket", "fused1000", "resnet50"],
+                    help="auto: config 2 (sum) at N=1, config 3 (bucket allreduce) at N>1")
     return ap.parse_args()
 
 
@@ -203,42 +205,128 @@ def bench_sum(args):
 
 # ----------------------------------------------------------------------------- N > 1: allreduce
 
+def fused1000_sizes():
+    """Config 4: 1000 fp32 gradients, sizes round(2**U(8,17)) from default_rng(20261015)."""
+    import numpy as np
+    rng = np.random.default_rng(20261015)
+    return [int(round(2 ** u)) for u in rng.uniform(8, 17, size=1000)]
+
+
+def resnet50_grad_sizes():
+    """Config 5: Keras ResNet-50 trainable-gradient shapes, in layer-creation order:
+    stem conv 7x7x3x64 + bias, BN gamma/beta; bottleneck stages [3,4,6,3] x widths 64/128/256/512
+    (x4 expansion, conv biases, projection shortcut in each stage's first block); dense 2048x1000 + bias.
+    214 tensors, 25,583,592 parameters."""
+    shapes = [(7, 7, 3, 64), (64,), (64,), (64,)]
+    cin = 64
+    for f, blocks in ((64, 3), (128, 4), (256, 6), (512, 3)):
+        for b in range(blocks):
+            if b == 0:
+                shapes += [(1, 1, cin, 4 * f), (4 * f,), (4 * f,), (4 * f,)]
+            shapes += [(1, 1, cin, f), (f,), (f,), (f,), (3, 3, f, f), (f,), (f,), (f,),
+                       (1, 1, f, 4 * f), (4 * f,), (4 * f,), (4 * f,)]
+            cin = 4 * f
+    shapes += [(2048, 1000), (1000,)]
+    sizes = []
+    for sh in shapes:
+        k = 1
+        for d in sh:
+            k *= d
+        sizes.append(k)
+    return sizes
+
+
+def max_over_ranks(dist, seconds):
+    """The contract's job time: the slowest rank's timed region (gloo all-reduce MAX on the host)."""
+    import torch
+    t = torch.tensor([float(seconds)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def all_ranks_ok(dist, ok):
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def start_watchdog(seconds, rank):
+    """A hung collective must end the run with a message, never hang the box."""
+    import threading
+
+    def fire():
+        sys.stderr.write("bench.py rank %d: watchdog fired after %d s (hung collective?)\n" % (rank, seconds))
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "error": "watchdog: no progress in %d s" % seconds}),
+                  flush=True)
+        os._exit(3)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def bench_allreduce(args):
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "900")), rank)
     torch.cuda.set_device(local)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import tips_amd
     from tips_amd import _lib
-    tips_amd.init()  # unique id through the gloo group, RCCL comm per GPU
+    tips_amd.init()  # unique id through the gloo group, one RCCL communicator per GPU
     L = _lib.lib()
     algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL}
-    L.tips_set_algorithm(algo_names[args.algo])
-    algo = L.tips_resolve_algorithm(world)
     inv = {v: k for k, v in algo_names.items()}
+    _lib.call("tips_set_algorithm", algo_names[args.algo])
+    algo = L.tips_resolve_algorithm(world)
 
+    workload = args.workload if args.workload != "auto" else "bucket"
     steps = args.steps if args.steps is not None else 20
     warmup = args.warmup if args.warmup is not None else 5
-    n = (args.bucket_mib or 1024) * (1 << 20) // 4
     g = torch.Generator(device="cuda")
-
-    def fill(t, r):
-        g.manual_seed(3000 + r)
-        t.uniform_(0.5, 1.5, generator=g)
-
-    x = torch.empty(n, dtype=torch.float32, device="cuda")
-    fill(x, rank)
-    y = torch.empty_like(x)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
+    if workload == "bucket":
+        sizes = [(args.bucket_mib or 1024) * (1 << 20) // 4]
+        seed0, desc = 3000, "config 3: allreduce of one 1 GiB fp32 bucket per GPU over xGMI"
+    elif workload == "fused1000":
+        sizes, seed0 = fused1000_sizes(), 4000
+        desc = "config 4: 1000 fp32 grads (2^U(8,17) elems) fused into 64 MiB buckets, allreduced in place"
+    else:
+        sizes, seed0 = resnet50_grad_sizes(), 5000
+        desc = "config 5: ResNet-50 gradient set (214 tensors, 25.6 M fp32) fused into 64 MiB buckets, in place"
+    # every tensor at a 256-B aligned offset of one flat buffer (what a caching allocator hands out)
+    offs, total = [], 0
+    for k in sizes:
+        offs.append(total)
+        total += (k + 63) // 64 * 64
+    total_elems = sum(sizes)
+
+    def fill(t, r):
+        g.manual_seed(seed0 + r)
+        t.uniform_(0.5, 1.5, generator=g)
+
+    x = torch.empty(total, dtype=torch.float32, device="cuda")
+    fill(x, rank)
+    y = torch.empty_like(x) if workload == "bucket" else x
+    views = [x[o:o + k] for o, k in zip(offs, sizes)]
+    pp, _keep1 = _lib.ptr_array([v.data_ptr() for v in views])
+    cp, _keep2 = _lib.i64_array(sizes)
+
     def step():
-        rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, sp)
+        if workload == "bucket":
+            rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), sizes[0], _lib.FLOAT32, _lib.OP_SUM, sp)
+        else:
+            rc = L.tips_fused_allreduce(pp, cp, len(sizes), _lib.FLOAT32, sp)
         if rc:
-            raise _lib.TipsError("tips_allreduce", rc, _lib.last_error())
+            raise _lib.TipsError("allreduce", rc, _lib.last_error())
 
     def timed(k):
         dist.barrier()
@@ -249,9 +337,7 @@ def bench_allreduce(args):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         dist.barrier()
-        tmax = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        return tmax.item()
+        return max_over_ranks(dist, dt)
 
     for _ in range(warmup):
         step()
@@ -259,65 +345,71 @@ def bench_allreduce(args):
     t = timed(steps)
     ms = t / steps * 1e3
 
-    # parity: fold all ranks' seeded inputs on this device (rank order) and compare
-    ref = torch.zeros_like(x)
+    # parity: one fresh call, then fold all ranks' seeded inputs on this device (rank order) and compare
+    fill(x, rank)
+    step()
+    torch.cuda.synchronize()
     tmp = torch.empty_like(x)
+    ref = None
     for r in range(world):
         fill(tmp, r)
-        ref = ref + tmp if r else tmp.clone()
-    if algo == _lib.ALGO_DIRECT:
-        ok = bool(torch.equal(y, ref))
-        check = "bit-exact vs rank-order fold" if ok else "FAIL"
+        ref = tmp.clone() if ref is None else ref + tmp
+    got = torch.cat([y[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else y
+    exp = torch.cat([ref[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else ref
+    if algo == _lib.ALGO_DIRECT or world == 1:
+        ok = bool(torch.equal(got, exp))
+        check = "bit-exact vs rank-order fold of all ranks' inputs" if ok else "FAIL (not bit-exact)"
     else:
-        rel = ((y.double() - ref.double()).abs() / ref.double()).max().item()
+        rel = ((got.double() - exp.double()).abs() / exp.double()).max().item()
         ok = rel <= 1e-6
-        check = ("max rel err %.2e vs rank-order fold (<= 1e-6)" % rel) if ok else ("FAIL rel %.2e" % rel)
-    okt = torch.tensor([1 if ok else 0], dtype=torch.int32)
-    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    del ref, tmp
+        check = ("max rel err %.2e vs rank-order fold (bound 1e-6)" % rel) if ok else ("FAIL rel %.2e" % rel)
+    all_ok = all_ranks_ok(dist, ok)
+    del ref, tmp, got, exp
 
-    # comparison points (same bucket): the other schedules and ncclAllReduce
+    # comparison points on the same workload: the other schedules and ncclAllReduce
     compare = {}
     if not args.no_compare:
+        kc = max(3, steps // 4)
         for name in ("ring", "direct", "rccl"):
             if algo_names[name] == algo:
                 continue
-            L.tips_set_algorithm(algo_names[name])
+            _lib.call("tips_set_algorithm", algo_names[name])
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
-            tc = timed(max(3, steps // 4))
-            compare[name] = round(n * 4 / (tc / max(3, steps // 4)) / GIB, 2)
-        L.tips_set_algorithm(algo_names[args.algo])
+            tc = timed(kc)
+            compare[name] = round(total_elems * 4 / (tc / kc) / GIB, 2)
+        _lib.call("tips_set_algorithm", algo_names[args.algo])
 
-    algbw = n * 4 / (ms / 1e3)  # bytes/s per rank
+    algbw = total_elems * 4 / (ms / 1e3)  # bytes/s per rank
     busbw = algbw * 2 * (world - 1) / world
     links = 1 if algo == _lib.ALGO_RING else world - 1
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(world * n * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
+            "metric": METRIC, "value": round(world * total_elems * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed 3000+rank, resident in HBM",
-            "config": {"workload": "config 3: allreduce of one 1 GiB fp32 bucket per GPU over xGMI",
-                       "bucket_bytes": n * 4, "algorithm": inv.get(algo, str(algo)),
-                       "parallelism": "dp%d (one process per GPU, RCCL p2p)" % world},
+            "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % seed0,
+            "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
+                       "algorithm": inv.get(algo, str(algo)),
+                       "parallelism": "dp%d (one process per GPU, RCCL p2p over xGMI)" % world},
             "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
             "xgmi": {"busbw_GBps": round(busbw / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS, "links_used": links,
                      "frac_of_links_used": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4),
                      "frac_of_one_link": round(busbw / 1e9 / XGMI_LINK_GBPS, 4)},
-            "roofline": {"bound": "xgmi-link", "achieved": round(busbw / 1e9, 1),
-                         "peak": XGMI_LINK_GBPS * links, "unit": "GB/s",
-                         "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None},
+            "roofline": {"bound": "xgmi", "achieved": round(busbw / 1e9, 1), "peak": XGMI_LINK_GBPS * links,
+                         "unit": "GB/s", "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None,
+                         "note": "multi-GPU: the ring/all-pairs transfer, not the sum kernel, bounds the step"},
             "cpu_baseline": None,
             "compare_algbw_gib_s": compare,
-            "check": check if okt.item() == 1 else "FAIL on some rank",
+            "check": check if all_ok else "FAIL on some rank",
         }
         print(json.dumps(line), flush=True)
     dist.barrier()
+    wd.cancel()
     tips_amd.shutdown()
     dist.destroy_process_group()
-    return 0 if okt.item() == 1 else 1
+    return 0 if all_ok else 1
 
 
 def main():
@@ -329,7 +421,12 @@ def main():
                "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29511"),
                os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
-    if world > 1:
+    if world > 1 or args.workload in ("bucket", "fused1000", "resnet50"):
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29512")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         return bench_allreduce(args)
     return bench_sum(args)
 

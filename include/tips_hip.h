@@ -143,6 +143,12 @@ int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t
 /* The same for the direct algorithm (checked against oracle_fold, wide_acc=1). */
 int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
 
+/* How the simulators move a virtual rank's bytes to its peer: 0 = device
+ * copies (default), 1 = ncclSend/ncclRecv pairs from this rank to itself in
+ * one group per pipeline step (exercises the RCCL p2p calls on one GPU;
+ * needs a single-rank setup). */
+int tips_set_sim_transport(int transport);
+
 /* Explicit variant of the 2-input sum kernel, for the gfx950 tuning sweep
  * (tools/sum_sweep.cc): mode 0 = grid-stride over `blocks` workgroups,
  * mode 1 = one tile per workgroup; unroll = 16-B vectors per lane in flight;

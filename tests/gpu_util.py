@@ -68,14 +68,18 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def simulate(kind, ins, dtype, inplace=False):
+def simulate(kind, ins, dtype, inplace=False, transport=0):
     import torch
     from tips_amd import _lib
+    _lib.call("tips_set_sim_transport", transport)
     devs = [to_dev(x) for x in ins]
     outs = devs if inplace else [torch.empty_like(d) for d in devs]
     pi, _k1 = _lib.ptr_array([d.data_ptr() for d in devs])
     po, _k2 = _lib.ptr_array([o.data_ptr() for o in outs])
     fn = "tips_ring_simulate" if kind == "ring" else "tips_direct_simulate"
-    _lib.call(fn, po, pi, len(ins), ins[0].size, dtype, stream())
-    torch.cuda.synchronize()
+    try:
+        _lib.call(fn, po, pi, len(ins), ins[0].size, dtype, stream())
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("tips_set_sim_transport", 0)
     return [from_dev(o, dtype) for o in outs]

@@ -1,0 +1,68 @@
+"""N > 1 host-side plumbing on CPU: world_size-2 (and 4) gloo groups.
+
+The device exchange itself needs >1 GPU (driver's 8-GPU run); what runs here is
+everything around it that bench.py and tips_amd rely on at N > 1: the RCCL
+unique id reaching every rank through torch.distributed, the TCP bootstrap
+tips_init uses, the max-over-ranks timing and all-ranks parity vote, and the
+workload shapes of configs 4 and 5.
+"""
+import os
+import socket
+import sys
+
+import pytest
+
+from conftest import REPO
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tips_amd.basics import share_unique_id
+    import bench
+    uid = share_unique_id(dist, lambda: bytes((7 * i) % 256 for i in range(128)))
+    t = bench.max_over_ranks(dist, 0.5 + rank)
+    ok_all = bench.all_ranks_ok(dist, True)
+    ok_one_bad = bench.all_ranks_ok(dist, rank != world - 1)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, uid, t, ok_all, ok_one_bad))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_plumbing(world):
+    import torch.multiprocessing as tmp
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    expect_uid = bytes((7 * i) % 256 for i in range(128))
+    for rank, uid, t, ok_all, ok_one_bad in res:
+        assert uid == expect_uid
+        assert t == pytest.approx(0.5 + world - 1)
+        assert ok_all is True and ok_one_bad is False
+
+
+def test_workload_shapes():
+    sys.path.insert(0, REPO)
+    import bench
+    r50 = bench.resnet50_grad_sizes()
+    assert len(r50) == 214 and sum(r50) == 25583592
+    f = bench.fused1000_sizes()
+    assert len(f) == 1000 and sum(f) == 20680288 and min(f) == 257 and max(f) == 130946  # config 4

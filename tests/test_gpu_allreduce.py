@@ -54,6 +54,19 @@ def test_pipelined_subchunks_inplace(gpu, oracle, monkeypatch, kind, dtype):
             assert same_bits(got, exp, dtype)
 
 
+@pytest.mark.parametrize("kind", ["ring", "direct"])
+@pytest.mark.parametrize("dtype", [F32, I32, BF16, F64])
+@pytest.mark.parametrize("p,n", [(2, 4099), (4, 1000003), (8, 262147)])
+def test_schedules_over_rccl_selfloop(gpu, oracle, monkeypatch, kind, dtype, p, n):
+    """Same schedules with every peer transfer as a grouped ncclSend/ncclRecv (RCCL, rank to itself)."""
+    monkeypatch.setenv("TIPS_MIN_SUBCHUNK_BYTES", "65536")
+    rng = np.random.default_rng(31 * p + dtype)
+    ins = [rand(dtype, n, rng) for _ in range(p)]
+    exp = oracle.ring(ins, code=dtype)[0] if kind == "ring" else oracle.fold(ins, code=dtype, wide_acc=True)
+    for got in simulate(kind, ins, dtype, transport=1):
+        assert same_bits(got, exp, dtype)
+
+
 CASES = golden_cases()
 
 

@@ -75,6 +75,7 @@ _SIGNATURES = [
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_direct_simulate", ctypes.c_int,
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_set_sim_transport", ctypes.c_int, [ctypes.c_int]),
     ("tips_sum_variant", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),

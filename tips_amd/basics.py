@@ -29,6 +29,13 @@ def _torch_dist():
     return None
 
 
+def share_unique_id(dist, make_id):
+    """Rank 0's make_id() bytes, delivered to every rank of the torch.distributed group."""
+    payload = [make_id() if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(payload, src=0)
+    return payload[0]
+
+
 class TipsBasics(object):
     """Wrapper class for the basic TiPS APIs (basics.py:5-31)."""
 
@@ -46,13 +53,13 @@ class TipsBasics(object):
             if dist is not None:
                 rank, size = dist.get_rank(), dist.get_world_size()
                 nbytes = L.tips_unique_id_bytes()
-                payload = [None]
-                if rank == 0:
+
+                def make_id():
                     buf = ctypes.create_string_buffer(nbytes)
                     _lib.check("tips_get_unique_id", L.tips_get_unique_id(buf, nbytes))
-                    payload = [buf.raw]
-                dist.broadcast_object_list(payload, src=0)
-                idbuf = ctypes.create_string_buffer(payload[0], nbytes)
+                    return buf.raw
+
+                idbuf = ctypes.create_string_buffer(share_unique_id(dist, make_id), nbytes)
                 _lib.check("tips_init_rank", L.tips_init_rank(rank, size, -1, idbuf, nbytes))
             else:
                 L.tips_init()

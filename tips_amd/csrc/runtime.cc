@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -182,6 +183,7 @@ struct State {
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion;
   int algo = TIPS_ALGO_AUTO;
+  int sim_transport = 0;  // simulators: 0 = device copies, 1 = RCCL send/recv to self
   std::unordered_map<uint64_t, FusionPlan> plans;
 };
 
@@ -471,6 +473,47 @@ int build_plan(State& st, FusionPlan& pl, int64_t threshold) {
   return 0;
 }
 
+// Peer transfers of the single-GPU simulators, batched per pipeline step:
+// device-to-device copies, or (sim_transport 1) the same bytes as grouped
+// ncclSend/ncclRecv pairs to this rank itself, so the RCCL p2p calls the real
+// schedules make (byte counts, grouping, stream order) run on a 1-GPU box.
+struct SimXfer {
+  State& st;
+  std::vector<std::tuple<void*, const void*, size_t>> ops;
+  explicit SimXfer(State& s) : st(s) {}
+  void add(void* dst, const void* src, int64_t bytes) {
+    if (bytes > 0) ops.emplace_back(dst, src, (size_t)bytes);
+  }
+  int flush() {
+    if (ops.empty()) return 0;
+    if (st.sim_transport == 1) {
+      NCCL_TRY(ncclGroupStart());
+      for (auto& o : ops) {
+        NCCL_TRY(ncclSend(std::get<1>(o), std::get<2>(o), ncclInt8, 0, st.comm, st.comm_stream));
+        NCCL_TRY(ncclRecv(std::get<0>(o), std::get<2>(o), ncclInt8, 0, st.comm, st.comm_stream));
+      }
+      NCCL_TRY(ncclGroupEnd());
+    } else {
+      for (auto& o : ops)
+        HIP_TRY(hipMemcpyAsync(std::get<0>(o), std::get<1>(o), std::get<2>(o), hipMemcpyDeviceToDevice, st.comm_stream));
+    }
+    ops.clear();
+    return 0;
+  }
+};
+
+int sim_prepare(State& st) {
+  TRY(ensure_streams(st));
+  if (st.sim_transport == 1) {
+    if (!st.comm && st.size > 1) return fail(TIPS_ERR_UNSUPPORTED, "RCCL self-loop simulation needs a 1-rank setup");
+    if (!st.comm) {
+      if (st.size < 1) st.size = 1, st.rank = 0;
+      TRY(ensure_comm(st));
+    }
+  }
+  return 0;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -599,6 +642,14 @@ int tips_set_algorithm(int algo) {
 
 int tips_get_algorithm(void) { return S().algo; }
 
+int tips_set_sim_transport(int transport) {
+  if (transport != 0 && transport != 1) return fail(TIPS_ERR_INVALID_ARG, "bad sim transport %d", transport);
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  st.sim_transport = transport;
+  return 0;
+}
+
 int tips_resolve_algorithm(int nranks) { return resolve_algo(S().algo, nranks); }
 
 int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end) {
@@ -718,7 +769,8 @@ int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t
   if (n == 0) return 0;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
-  TRY(ensure_streams(st));
+  TRY(sim_prepare(st));
+  SimXfer xf(st);
   hipStream_t user = (hipStream_t)stream;
   const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
   if (p == 1) {
@@ -742,9 +794,9 @@ int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t
         const Range rs = sub_of(rc, K, align, k);
         if (rs.len() == 0) continue;
         const char* src = (s == 0) ? (const char*)ins[prev] : (const char*)outs[prev];
-        HIP_TRY(hipMemcpyAsync(stg(r, s & 1) + (rs.b - rc.b) * es, src + rs.b * es, (size_t)(rs.len() * es),
-                               hipMemcpyDeviceToDevice, st.comm_stream));
+        xf.add(stg(r, s & 1) + (rs.b - rc.b) * es, src + rs.b * es, rs.len() * es);
       }
+      TRY(xf.flush());
       hipEvent_t rev = st.recv_ev.ev[(s & 1) * K + k];
       HIP_TRY(hipEventRecord(rev, st.comm_stream));
       HIP_TRY(hipStreamWaitEvent(st.comp_stream, rev, 0));
@@ -764,9 +816,9 @@ int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t
         const int prev = mod(r - 1, p);
         const Range rs = sub_of(chunk_of(n, p, align, mod(r - s, p)), K, align, k);
         if (rs.len() == 0) continue;
-        HIP_TRY(hipMemcpyAsync((char*)outs[r] + rs.b * es, (const char*)outs[prev] + rs.b * es, (size_t)(rs.len() * es),
-                               hipMemcpyDeviceToDevice, st.comm_stream));
+        xf.add((char*)outs[r] + rs.b * es, (const char*)outs[prev] + rs.b * es, rs.len() * es);
       }
+      TRY(xf.flush());
     }
   }
   TRY(join(user, st.comm_stream, st.ev_done));
@@ -780,7 +832,8 @@ int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64
   if (n == 0) return 0;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
-  TRY(ensure_streams(st));
+  TRY(sim_prepare(st));
+  SimXfer xf(st);
   hipStream_t user = (hipStream_t)stream;
   const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
   if (p == 1) {
@@ -801,10 +854,9 @@ int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64
       const Range mine = chunk_of(n, p, align, r), ms = sub_of(mine, K, align, k);
       if (ms.len() == 0) continue;
       for (int j = 0; j < p; j++)
-        if (j != r)
-          HIP_TRY(hipMemcpyAsync(slot(r, j) + (ms.b - mine.b) * es, (const char*)ins[j] + ms.b * es,
-                                 (size_t)(ms.len() * es), hipMemcpyDeviceToDevice, st.comm_stream));
+        if (j != r) xf.add(slot(r, j) + (ms.b - mine.b) * es, (const char*)ins[j] + ms.b * es, ms.len() * es);
     }
+    TRY(xf.flush());
     HIP_TRY(hipEventRecord(st.recv_ev.ev[k], st.comm_stream));
     HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[k], 0));
     for (int r = 0; r < p; r++) {
@@ -822,10 +874,9 @@ int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64
       const Range ms = sub_of(chunk_of(n, p, align, r), K, align, k);
       if (ms.len() == 0) continue;
       for (int j = 0; j < p; j++)
-        if (j != r)
-          HIP_TRY(hipMemcpyAsync((char*)outs[j] + ms.b * es, (const char*)outs[r] + ms.b * es, (size_t)(ms.len() * es),
-                                 hipMemcpyDeviceToDevice, st.comm_stream));
+        if (j != r) xf.add((char*)outs[j] + ms.b * es, (const char*)outs[r] + ms.b * es, ms.len() * es);
     }
+    TRY(xf.flush());
   }
   TRY(join(user, st.comm_stream, st.ev_done));
   TRY(join(user, st.comp_stream, st.ev_comp_done));

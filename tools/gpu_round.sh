@@ -29,6 +29,12 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 run bench 600 python bench.py ${BENCH_ARGS:-}
 rc=$?; fatal $rc && exit $rc
+if [ "${EXTRA:-1}" = "1" ]; then
+  for w in bucket fused1000 resnet50; do
+    run bench_$w 300 python bench.py --workload $w --no-compare
+    rc=$?; fatal $rc && exit $rc
+  done
+fi
 if [ "${PROFILE:-1}" = "1" ]; then
   export TMPDIR=/tmp
   run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_stats" -o bench \
