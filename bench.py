@@ -33,6 +33,9 @@ METRIC = "device-resident fp32 bucket-sum GiB/s (% HBM peak); allreduce GiB/s 1/
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 XGMI_LINK_GBPS = 153.0   # per link per direction (task / SURVEY §8d)
 GIB = float(1 << 30)
+# the exact instantiation tips_bucket_sum launches for f32 (kernels.hip kDef*): PMC traffic is only
+# reported from a profile of this kernel
+DEFAULT_SUM_KERNEL = "sum2_kernel<0, 1, 1, true, false, 256>"
 
 
 def parse():
@@ -177,7 +180,7 @@ def bench_sum(args):
     moved = 3 * n * 4
     t_s = ms / 1e3
     achieved = moved / t_s / 1e9
-    tr = pmc_traffic("sum2_kernel")
+    tr = pmc_traffic(DEFAULT_SUM_KERNEL)
     line = {
         "metric": METRIC, "value": round(moved / t_s / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
         "warmup": warmup, "ms_per_step": round(ms, 6), "higher_is_better": True, "scaling": "weak",
@@ -274,7 +277,7 @@ def bench_allreduce(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "900")), rank)
+    wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "420")), rank)
     torch.cuda.set_device(local)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import tips_amd

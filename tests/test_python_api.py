@@ -1,0 +1,87 @@
+"""The tips_amd Python surface on CPU: it mirrors tips.tensorflow's names and
+signatures, maps dtypes like the reference (plus f16/bf16), and fails loudly
+when the HIP library is missing (no CPU fallback)."""
+import inspect
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def test_reference_names_exist():
+    import tips_amd
+    # tips/tensorflow/__init__.py:8,17-18 and ops.py/basics.py names used on the allreduce path
+    for name in ("allreduce", "allreduce_op", "size", "rank", "shutdown", "size_op", "rank_op", "Compression",
+                 "Average", "Sum", "TipsBasics"):
+        assert hasattr(tips_amd, name), name
+    assert tips_amd.Average == 'Average' and tips_amd.Sum == 'Sum'
+
+
+def test_allreduce_signature_matches_reference():
+    import tips_amd
+    params = list(inspect.signature(tips_amd.allreduce).parameters)
+    # tips/tensorflow/__init__.py:20-28
+    assert params == ["tensor", "average", "device_dense", "device_sparse", "compression", "op", "prescale_factor",
+                      "postscale_factor", "name"]
+    assert list(inspect.signature(tips_amd.allreduce_op).parameters) == ["tensor", "name"]  # ops.py:61
+
+
+def test_dtype_codes():
+    import torch
+    from tips_amd import tensors
+    assert tensors.dtype_code(np.zeros(1, np.float32)) == 0
+    assert tensors.dtype_code(np.zeros(1, np.float64)) == 1
+    assert tensors.dtype_code(np.zeros(1, np.int32)) == 2
+    assert tensors.dtype_code(np.zeros(1, np.int64)) == 3
+    assert tensors.dtype_code(np.zeros(1, np.float16)) == 4
+    assert tensors.dtype_code(torch.zeros(1, dtype=torch.bfloat16)) == 5
+    assert tensors.dtype_code(torch.zeros(1, dtype=torch.float32)) == 0
+    for bad in (np.zeros(1, np.uint8), torch.zeros(1, dtype=torch.bool), np.zeros(1, np.complex64)):
+        with pytest.raises(TypeError, match="Not supported dtype found"):
+            tensors.dtype_code(bad)
+
+
+def test_compression_round_trip():
+    import torch
+    from tips_amd import Compression
+    x = np.linspace(-3, 3, 17).astype(np.float32)
+    c, ctx = Compression.fp16.compress(x)
+    assert c.dtype == np.float16
+    assert Compression.fp16.decompress(c, ctx).dtype == np.float32
+    t = torch.linspace(-3, 3, 17)
+    c, ctx = Compression.fp16.compress(t)
+    assert c.dtype == torch.float16 and Compression.fp16.decompress(c, ctx).dtype == torch.float32
+    i = np.arange(5, dtype=np.int32)
+    c, ctx = Compression.fp16.compress(i)
+    assert c is i  # integers are not compressed (compression.py:55-57)
+    assert Compression.none.compress(x) == (x, None)
+
+
+def test_missing_library_fails_loudly():
+    code = ("import tips_amd, numpy as np\n"
+            "try:\n"
+            "    tips_amd.allreduce(np.ones(3, np.float32))\n"
+            "except tips_amd.TipsLibraryError as e:\n"
+            "    print('LOUD', e)\n")
+    env = dict(os.environ, TIPS_HIP_LIB="/nonexistent/libtips_hip.so")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, env=env, timeout=300)
+    assert "LOUD" in r.stdout and "no CPU fallback" in r.stdout, r.stdout + r.stderr
+
+
+def test_allreduce_without_gpu_raises_not_computes():
+    """On a host with no HIP device the op must raise (init fails), never return a host-computed sum."""
+    code = ("import tips_amd, numpy as np\n"
+            "try:\n"
+            "    out = tips_amd.allreduce(np.ones(3, np.float32))\n"
+            "    print('COMPUTED', out)\n"
+            "except tips_amd.TipsError as e:\n"
+            "    print('RAISED', e.code)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, timeout=300)
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    assert "RAISED" in r.stdout, r.stdout + r.stderr
