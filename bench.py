@@ -177,6 +177,24 @@ def bench_sum(args):
     torch.cuda.synchronize()
     t_host = (time.perf_counter() - t1) / reps
 
+    # host-memory leg of the drop-in path: tips_allreduce on host buffers (1 rank: H2D, device copy, D2H)
+    host_rates = {}
+    import numpy as np
+    pinned_in = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    pinned_out = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    pageable_in = np.random.default_rng(1).random(n, dtype=np.float32)
+    pageable_out = np.empty_like(pageable_in)
+    tips_amd.init()
+    for label, src, dst in (("pageable_numpy", pageable_in.ctypes.data, pageable_out.ctypes.data),
+                            ("pinned", pinned_in.data_ptr(), pinned_out.data_ptr())):
+        _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)  # warm (allocates staging)
+        t2 = time.perf_counter()
+        for _ in range(3):
+            _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)
+        host_rates[label] = round(n * 4 / ((time.perf_counter() - t2) / 3) / GIB, 3)
+    host_ok = bool(np.array_equal(pageable_out, pageable_in))
+    del pinned_in, pinned_out, pageable_in, pageable_out
+
     moved = 3 * n * 4
     t_s = ms / 1e3
     achieved = moved / t_s / 1e9
@@ -197,6 +215,9 @@ def bench_sum(args):
         "algorithmic_bytes_per_step": moved,
         "pcie_inclusive_gib_s": round(n * 4 / t_host / GIB, 3),
         "pcie_inclusive_note": "pinned H2D of a and b + kernel + D2H of c, bucket bytes / wall time",
+        "host_allreduce_gib_s": host_rates,
+        "host_allreduce_note": "tips_allreduce(host in, host out) on one rank, 256 MiB: staged H2D + device + D2H, "
+                               "bucket bytes / wall time" + ("" if host_ok else " (RESULT MISMATCH)"),
         "check": "bit-exact vs torch a+b" if ok else "FAIL",
         "wall_s_timed_region": round(wall, 4),
     }

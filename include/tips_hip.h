@@ -120,6 +120,45 @@ int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, 
  * op must be TIPS_OP_SUM. */
 int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream);
 
+/* ---- control plane: cross-rank request validation ---- */
+
+/* request types = message::RequestType (collective_messages.fbs:3-7) */
+enum tips_request_type {
+  TIPS_REQ_ALLREDUCE = 0,
+  TIPS_REQ_ALLGATHER = 1,
+  TIPS_REQ_BROADCAST = 2,
+};
+#define TIPS_MAX_DIMS 8
+/* one request record: {request_type, dtype, ndim, dims[TIPS_MAX_DIMS]} */
+#define TIPS_REQUEST_WORDS (3 + TIPS_MAX_DIMS)
+
+/* Replaces ConstructResponseMessage (coordinator.cc:90-186) and
+ * GatherFirstRankSizes (coordinator.cc:40-88): table holds p request records
+ * (rank order); each is compared with rank 0's. Returns TIPS_OK, or
+ * TIPS_ERR_MISMATCH with the reference's error text in tips_last_error()
+ * ("Mismatch data types found: 0 vs 1.", "Mismatched allreduce tensor shapes:
+ * [2,4] vs [2,3]", "Mismatched allgather tensor shapes: 1-th dimension 3 vs 4",
+ * ...). Pure host function. */
+int tips_check_requests(const int64_t* table, int p);
+
+/* tips_allreduce preceded by that validation: the records of all ranks are
+ * exchanged (one small RCCL allgather + host sync), so every rank reaches the
+ * same verdict; on a mismatch no rank reduces. shape = the tensor's dims. */
+int tips_allreduce_checked(const void* in, void* out, const int64_t* shape, int ndim, int dtype, int op, void* stream);
+
+/* ---- the other collectives of the op surface ---- */
+
+/* out[r*words + w] = values[w] of rank r (host memory, blocking; words <= 4096). */
+int tips_allgather_i64(const int64_t* values, int words, int64_t* out);
+/* Replaces BroadcastCpu (utils.h:130-134) / MPIBroadcast (ops.cc:214-286):
+ * out = root's in on every rank (in == out allowed). Any root (the reference
+ * only supports 0, ops.cc:219). Host or device pointers, as tips_allreduce. */
+int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root, void* stream);
+/* Replaces AllgathervCpu (utils.h:83-128) / MPIAllgather (ops.cc:156-212):
+ * out = concatenation over ranks of in, rank r contributing counts[r]
+ * elements (counts[rank] must equal count). Host or device pointers. */
+int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* counts, int dtype, void* stream);
+
 /* Tensor fusion (no reference counterpart): allreduce n device
  * tensors in place, packed into buckets of at most the fusion threshold
  * (TIPS_FUSION_THRESHOLD bytes, default 64 MiB). One dtype for all. */

@@ -159,3 +159,37 @@ def test_single_hip_runtime():
     for line in r.stdout.strip().splitlines():
         name, count = line.split()
         assert count == "1", line
+
+
+# ---------------------------------------------------------------- control plane (pure host)
+
+def _table(*recs):
+    from tips_amd import _lib
+    flat = []
+    for typ, dt, shape in recs:
+        flat += [typ, dt, len(shape)] + list(shape) + [0] * (_lib.MAX_DIMS - len(shape))
+    return _lib.i64_array(flat)
+
+
+@pytest.mark.parametrize("recs,msg", [
+    ([(0, 0, (2, 4)), (0, 0, (2, 4)), (0, 0, (2, 4))], None),
+    ([(0, 0, (2, 4)), (0, 1, (2, 4))], b"Mismatch data types found: 0 vs 1."),
+    ([(0, 0, (2, 4)), (2, 0, (2, 4))], b"Mismatched operations found: 0 vs 2."),
+    ([(0, 0, (2, 4)), (0, 0, (2, 3))], b"Mismatched allreduce tensor shapes: [2,4] vs [2,3]"),
+    ([(2, 3, (5,)), (2, 3, (5, 1))], b"Mismatched broadcast tensor shapes: [5] vs [5,1]"),
+    ([(1, 0, (3, 4)), (1, 0, (7, 4))], None),  # allgather: first dimension may differ
+    ([(1, 0, (3, 4)), (1, 0, (3, 4, 1))], b"Mismatched allgather tensor shapes: rank 2 vs 3"),
+    ([(1, 0, (3, 4)), (1, 0, (3, 5))], b"Mismatched allgather tensor shapes: 1-th dimension 4 vs 5"),
+    ([(1, 0, ()), (1, 0, ())], b"An empty tensor found"),
+])
+def test_check_requests_reference_messages(recs, msg):
+    """The reference's ConstructResponseMessage / GatherFirstRankSizes verdicts and error text
+    (coordinator.cc:40-186), as a pure host function of the exchanged request records."""
+    from tips_amd import _lib
+    L = _lib.lib()
+    ptr, _keep = _table(*recs)
+    rc = L.tips_check_requests(ptr, len(recs))
+    if msg is None:
+        assert rc == 0
+    else:
+        assert rc == -7 and L.tips_last_error() == msg

@@ -187,3 +187,42 @@ def test_allreduce_grads_identity_single_rank(gpu):
     grads = [torch.randn(10, device="cuda"), None, torch.randn(3, 3, device="cuda")]
     out = gpu.allreduce_grads(grads)
     assert out[1] is None and torch.equal(out[0], grads[0]) and torch.equal(out[2], grads[2])
+
+
+# ------------------------------------------------------------------ the rest of the op surface (one rank)
+
+def test_broadcast_allgather_checked_single_rank(gpu, monkeypatch):
+    import torch
+    from tips_amd import _lib, ops
+    t = torch.randn(3, 5, device="cuda")
+    assert torch.equal(gpu.broadcast_op(t, root_rank=0), t)
+    h = np.arange(12, dtype=np.int64).reshape(3, 4)
+    assert np.array_equal(gpu.broadcast_op(h), h)
+    g = gpu.allgather_op(t)
+    assert g.shape == (3, 5) and torch.equal(g, t)
+    assert np.array_equal(gpu.allgather_op(h), h)
+    v = [torch.zeros(4, device="cuda") + 2, np.ones(3, np.float32)]
+    gpu.broadcast_variables(v, 0)
+    assert torch.equal(v[0], torch.full((4,), 2.0, device="cuda"))
+    with pytest.raises(gpu.TipsError):
+        gpu.broadcast_op(t, root_rank=1)  # only rank 0 exists
+    ops.set_consistency_check(True)
+    try:
+        assert torch.equal(gpu.allreduce(t), t)
+        assert np.array_equal(gpu.allgather_op(h), h)
+        s = torch.tensor(3.5, device="cuda")  # scalar -> shape [1] record
+        assert gpu.allreduce(s).item() == 3.5
+    finally:
+        ops.set_consistency_check(False)
+    rec = [_lib.REQ_ALLREDUCE, 0, 2, 3, 5] + [0] * 6
+    assert ops._allgather_i64(rec) == rec
+
+
+def test_allgatherv_counts_validation(gpu):
+    import torch
+    from tips_amd import _lib
+    x = torch.arange(6, dtype=torch.float32, device="cuda")
+    out = torch.empty(6, device="cuda")
+    cp, _k = _lib.i64_array([5])
+    assert _lib.lib().tips_allgatherv(x.data_ptr(), 6, out.data_ptr(), cp, 0, None) == -1  # counts[rank] != count
+    assert b"not match" in _lib.lib().tips_last_error()

@@ -8,7 +8,8 @@ libtips_hip.so (include/tips_hip.h); there is no CPU fallback.
 """
 from .basics import TipsBasics, init, is_initialized, rank, shutdown, size
 from .compression import Compression, Compressor, FP16Compressor, NoneCompressor
-from .ops import allreduce_op, bucket_sum, fused_allreduce_, rank_op, set_algorithm, size_op
+from .ops import (allgather_op, allreduce_op, broadcast_op, broadcast_variables, bucket_sum, fused_allreduce_,
+                  rank_op, set_algorithm, set_consistency_check, size_op)
 from ._lib import TipsError, TipsLibraryError
 from . import tensors as _tensors
 
@@ -16,7 +17,8 @@ Average = 'Average'
 Sum = 'Sum'
 
 __all__ = [
-    "allreduce", "allreduce_grads", "allreduce_op", "bucket_sum", "fused_allreduce_", "init", "shutdown",
+    "allreduce", "allreduce_grads", "allreduce_op", "allgather_op", "broadcast_op", "broadcast_variables",
+    "set_consistency_check", "bucket_sum", "fused_allreduce_", "init", "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
 ]

@@ -16,6 +16,9 @@ LIB_PATH = os.environ.get("TIPS_HIP_LIB", os.path.join(_HERE, "lib", "libtips_hi
 # dtype codes (include/tips_hip.h enum tips_dtype; 0-3 = collective_messages.fbs:17-23)
 FLOAT32, FLOAT64, INT32, INT64, FLOAT16, BFLOAT16 = 0, 1, 2, 3, 4, 5
 OP_SUM, OP_MAX, OP_MIN = 0, 1, 2
+REQ_ALLREDUCE, REQ_ALLGATHER, REQ_BROADCAST = 0, 1, 2
+MAX_DIMS = 8
+REQUEST_WORDS = 3 + MAX_DIMS
 ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL = -1, 0, 1, 2
 
 STATUS_NAMES = {
@@ -67,6 +70,14 @@ _SIGNATURES = [
      [ctypes.c_void_p, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_allreduce", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_check_requests", ctypes.c_int, [_c_i64_p, ctypes.c_int]),
+    ("tips_allreduce_checked", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_allgather_i64", ctypes.c_int, [_c_i64_p, ctypes.c_int, _c_i64_p]),
+    ("tips_broadcast", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_allgatherv", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_void_p]),
     ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),
     ("tips_get_algorithm", ctypes.c_int, []),

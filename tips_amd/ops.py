@@ -6,6 +6,7 @@ one tensor over all ranks, output of the input's shape and dtype. Device
 stream; host tensors (numpy / CPU torch) are staged through HBM and the call
 returns when the result is in host memory, like the reference's CPU op.
 """
+import os
 import re
 
 from . import _lib
@@ -28,6 +29,20 @@ def rank_op(name=None):
     return basics.rank()
 
 
+_check = os.environ.get("TIPS_CHECK_CONSISTENCY", "0") == "1"
+
+
+def set_consistency_check(enabled):
+    """Validate dtype/shape across ranks before every allreduce (the reference's rank-0
+    negotiation, coordinator.cc:90-186): one small exchange per call. Off by default."""
+    global _check
+    _check = bool(enabled)
+
+
+def _shape(t):
+    return tuple(int(d) for d in t.shape)
+
+
 def allreduce_op(tensor, name=None):
     """Sum `tensor` over all ranks (ops.py:61-65 -> MPIAllreduce, ops.cc:86-115)."""
     basics.init()
@@ -35,10 +50,85 @@ def allreduce_op(tensor, name=None):
     src = tensors.contiguous(tensor)
     out = tensors.empty_like(src)
     n = tensors.numel(src)
-    if n:
+    if _check:
+        shape = _shape(src) or (1,)  # scalars travel as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
+        sp, _keep = _lib.i64_array(shape)
+        _lib.call("tips_allreduce_checked", tensors.data_ptr(src), tensors.data_ptr(out), sp, len(shape), code,
+                  _lib.OP_SUM, tensors.stream_of(src))
+    elif n:
         _lib.call("tips_allreduce", tensors.data_ptr(src), tensors.data_ptr(out), n, code, _lib.OP_SUM,
                   tensors.stream_of(src))
     return out
+
+
+def allgather_op(tensor, name=None):
+    """Concatenate `tensor` from all ranks along dimension 0 (ops.py:72-76 -> MPIAllgather,
+    ops.cc:156-212; sizes exchanged as GatherFirstRankSizes does, coordinator.cc:40-88)."""
+    basics.init()
+    code = tensors.dtype_code(tensor)
+    src = tensors.contiguous(tensor)
+    shape = _shape(src)
+    if not shape:
+        raise ValueError("An empty tensor found")
+    if _check:
+        rec = [_lib.REQ_ALLGATHER, code, len(shape)] + list(shape) + [0] * (_lib.MAX_DIMS - len(shape))
+        table = _gather_records(rec)
+        _lib.call("tips_check_requests", _lib.i64_array(table)[0], len(table) // _lib.REQUEST_WORDS)
+    firsts = _allgather_i64([shape[0]])
+    row = 1
+    for d in shape[1:]:
+        row *= d
+    counts = [int(f) * row for f in firsts]
+    out_shape = (sum(int(f) for f in firsts),) + shape[1:]
+    if tensors.is_torch(src):
+        import torch
+        out = torch.empty(out_shape, dtype=src.dtype, device=src.device)
+    else:
+        import numpy as np
+        out = np.empty(out_shape, dtype=src.dtype)
+    cp, _keep = _lib.i64_array(counts)
+    _lib.call("tips_allgatherv", tensors.data_ptr(src), tensors.numel(src), tensors.data_ptr(out), cp, code,
+              tensors.stream_of(src))
+    return out
+
+
+def _allgather_i64(values):
+    """Every rank's int64 words, rank-major (tips_allgather_i64)."""
+    import ctypes
+    p = basics.size()
+    vp, _keep = _lib.i64_array(values)
+    out = (ctypes.c_int64 * (p * len(values)))()
+    _lib.call("tips_allgather_i64", vp, len(values), out)
+    return [int(v) for v in out]
+
+
+def _gather_records(rec):
+    """Every rank's request record (rank-major table for tips_check_requests)."""
+    return _allgather_i64(rec)
+
+
+def broadcast_op(tensor, root_rank=0, name=None):
+    """`tensor` of rank `root_rank`, on every rank (ops.py:83-87 -> MPIBroadcast, ops.cc:214-286)."""
+    basics.init()
+    code = tensors.dtype_code(tensor)
+    src = tensors.contiguous(tensor)
+    out = tensors.empty_like(src)
+    n = tensors.numel(src)
+    if n:
+        _lib.call("tips_broadcast", tensors.data_ptr(src), tensors.data_ptr(out), n, code, int(root_rank),
+                  tensors.stream_of(src))
+    return out
+
+
+def broadcast_variables(variables, root_rank=0):
+    """Overwrite each tensor in place with root_rank's value (functions.py:36-46)."""
+    for v in variables:
+        b = broadcast_op(v, root_rank)
+        if tensors.is_torch(v):
+            v.copy_(b)
+        else:
+            v[...] = b
+    return variables
 
 
 def fused_allreduce_(tensor_list):
