@@ -226,3 +226,18 @@ def test_allgatherv_counts_validation(gpu):
     cp, _k = _lib.i64_array([5])
     assert _lib.lib().tips_allgatherv(x.data_ptr(), 6, out.data_ptr(), cp, 0, None) == -1  # counts[rank] != count
     assert b"not match" in _lib.lib().tips_last_error()
+
+
+@pytest.mark.parametrize("piece", [4096, 1 << 20])
+def test_host_pipeline_pieces(gpu, monkeypatch, piece):
+    """Host buffers larger than a piece take the pipelined H2D || allreduce || D2H path."""
+    import torch
+    monkeypatch.setenv("TIPS_HOST_PIECE_BYTES", str(piece))
+    rng = np.random.default_rng(5)
+    for n in (1000003, 262144 + 7):
+        h = rng.standard_normal(n).astype(np.float32)
+        assert np.array_equal(gpu.allreduce(h), h)  # one rank: SUM = identity, every piece moved exactly
+        pt = torch.from_numpy(h).pin_memory()
+        assert torch.equal(gpu.allreduce(pt), pt)
+        hi = rng.integers(-2**62, 2**62, size=n // 3, dtype=np.int64)
+        assert np.array_equal(gpu.allreduce(hi), hi)

@@ -20,6 +20,8 @@
 
 #include <algorithm>
 #include <mutex>
+#include <thread>
+#include <condition_variable>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -179,6 +181,8 @@ struct State {
   int rank = -1, size = -1, device = -1;
   ncclComm_t comm = nullptr;
   hipStream_t comm_stream = nullptr, comp_stream = nullptr, io_stream = nullptr;
+  hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // host-memory pipeline (both PCIe directions)
+  EventPool pipe_ev;
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
@@ -196,6 +200,8 @@ int ensure_streams(State& st) {
   if (!st.comm_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comm_stream, hipStreamNonBlocking));
   if (!st.comp_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comp_stream, hipStreamNonBlocking));
   if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
+  if (!st.h2d_stream) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream, hipStreamNonBlocking));
+  if (!st.d2h_stream) HIP_TRY(hipStreamCreateWithFlags(&st.d2h_stream, hipStreamNonBlocking));
   if (!st.ev_start) HIP_TRY(hipEventCreateWithFlags(&st.ev_start, hipEventDisableTiming));
   if (!st.ev_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
   if (!st.ev_comp_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_done, hipEventDisableTiming));
@@ -419,6 +425,78 @@ int run_staged(State& st, const void* in, size_t in_bytes, void* out, size_t out
   TRY(enqueue(st.host_in.p, st.host_out.p, st.io_stream));
   if (out_bytes) HIP_TRY(hipMemcpyAsync(out, st.host_out.p, out_bytes, hipMemcpyDeviceToHost, st.io_stream));
   HIP_TRY(hipStreamSynchronize(st.io_stream));
+  return 0;
+}
+
+// Host-resident allreduce, pipelined over pieces so both PCIe directions and
+// the device work overlap: H2D of piece i+1 (h2d stream) || allreduce of piece
+// i (io stream) || D2H of piece i-1 (d2h stream). Each piece is a complete
+// allreduce (same piece boundaries on every rank). A second host thread
+// issues the D2H copies, because a copy from/to pageable memory blocks the
+// thread that issues it. Caller holds st.mu; returns when `out` is written.
+int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype) {
+  const int64_t es = tips::dtype_size(dtype);
+  const int64_t piece =
+      round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_PIECE_BYTES", 32 << 20)), kAlignBytes) / es;
+  const int np = (int)((n + piece - 1) / piece);
+  TRY(st.host_in.ensure((size_t)(n * es)));
+  TRY(st.host_out.ensure((size_t)(n * es)));
+  TRY(st.pipe_ev.ensure(2 * (size_t)np));
+  char* din = (char*)st.host_in.p;
+  char* dout = (char*)st.host_out.p;
+  std::mutex m;
+  std::condition_variable cv;
+  int issued = 0;
+  bool abort = false;
+  std::string drain_err;
+  const int device = st.device;
+  std::thread drain([&] {
+    if (device >= 0) (void)hipSetDevice(device);
+    for (int i = 0; i < np; i++) {
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return issued > i || abort; });
+        if (issued <= i) return;  // aborted before piece i was issued
+      }
+      const int64_t off = (int64_t)i * piece * es, len = std::min(piece, n - (int64_t)i * piece) * es;
+      hipError_t e = hipStreamWaitEvent(st.d2h_stream, st.pipe_ev.ev[2 * i + 1], 0);
+      if (e == hipSuccess) e = hipMemcpyAsync(out + off, dout + off, (size_t)len, hipMemcpyDeviceToHost, st.d2h_stream);
+      if (e != hipSuccess) {
+        std::lock_guard<std::mutex> l(m);
+        drain_err = std::string("D2H: ") + hipGetErrorString(e);
+        return;
+      }
+    }
+  });
+  int rc = 0;
+  for (int i = 0; i < np && rc == 0; i++) {
+    const int64_t off = (int64_t)i * piece * es, cnt = std::min(piece, n - (int64_t)i * piece);
+    hipError_t e = hipMemcpyAsync(din + off, in + off, (size_t)(cnt * es), hipMemcpyHostToDevice, st.h2d_stream);
+    if (e == hipSuccess) e = hipEventRecord(st.pipe_ev.ev[2 * i], st.h2d_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st.io_stream, st.pipe_ev.ev[2 * i], 0);
+    if (e != hipSuccess) {
+      rc = fail(TIPS_ERR_HIP, "H2D piece %d: %s", i, hipGetErrorString(e));
+      break;
+    }
+    rc = allreduce_device(st, din + off, dout + off, cnt, dtype, st.io_stream);
+    if (rc == 0 && (e = hipEventRecord(st.pipe_ev.ev[2 * i + 1], st.io_stream)) != hipSuccess)
+      rc = fail(TIPS_ERR_HIP, "event: %s", hipGetErrorString(e));
+    if (rc == 0) {
+      std::lock_guard<std::mutex> l(m);
+      issued = i + 1;
+    }
+    cv.notify_one();
+  }
+  {
+    std::lock_guard<std::mutex> l(m);
+    abort = true;
+  }
+  cv.notify_one();
+  drain.join();
+  hipError_t e = hipStreamSynchronize(st.d2h_stream);
+  if (rc) return rc;
+  if (!drain_err.empty()) return fail(TIPS_ERR_HIP, "%s", drain_err.c_str());
+  if (e != hipSuccess) return fail(TIPS_ERR_HIP, "d2h sync: %s", hipGetErrorString(e));
   return 0;
 }
 
@@ -693,7 +771,8 @@ void tips_shutdown(void) {
       (void)hipEventDestroy(*e);
       *e = nullptr;
     }
-  for (hipStream_t* s : {&st.comm_stream, &st.comp_stream, &st.io_stream})
+  st.pipe_ev.release();
+  for (hipStream_t* s : {&st.comm_stream, &st.comp_stream, &st.io_stream, &st.h2d_stream, &st.d2h_stream})
     if (*s) {
       (void)hipStreamDestroy(*s);
       *s = nullptr;
@@ -783,6 +862,9 @@ int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, 
   if (!in || !out) return fail(TIPS_ERR_INVALID_ARG, "null pointer");
   TRY(set_device(st));
   const size_t bytes = (size_t)count * tips::dtype_size(dtype);
+  const bool dout = is_device_ptr(out);
+  if (!dout && !is_device_ptr(in) && (int64_t)bytes > env_i64("TIPS_HOST_PIECE_BYTES", 32 << 20))
+    return allreduce_host_pipelined(st, (const char*)in, (char*)out, count, dtype);
   return run_staged(st, in, bytes, out, bytes, (hipStream_t)stream, [&](const void* i, void* o, hipStream_t s) {
     return allreduce_device(st, i, o, count, dtype, s);
   });
