@@ -241,3 +241,35 @@ def test_host_pipeline_pieces(gpu, monkeypatch, piece):
         assert torch.equal(gpu.allreduce(pt), pt)
         hi = rng.integers(-2**62, 2**62, size=n // 3, dtype=np.int64)
         assert np.array_equal(gpu.allreduce(hi), hi)
+
+
+def test_torch_bootstrap_creates_rccl_comm_subprocess(gpu):
+    """The N>1 bootstrap flow on one GPU, in a fresh process: torch.distributed (gloo) hands rank 0's
+    ncclGetUniqueId to tips_init_rank -> ncclCommInitRank; then RCCL-backed work runs on that comm."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    code = r'''
+import os, numpy as np, torch, torch.distributed as dist
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", TIPS_BOOTSTRAP="torch")
+dist.init_process_group("gloo", rank=0, world_size=1)
+import tips_amd
+from tips_amd import _lib
+tips_amd.init()
+assert tips_amd.size() == 1 and tips_amd.rank() == 0
+tips_amd.set_algorithm("rccl")
+t = torch.randn(100003, device="cuda")
+assert torch.equal(tips_amd.allreduce(t), t)
+tips_amd.set_algorithm("auto")
+import sys; sys.path.insert(0, "tests")
+from gpu_util import simulate, F32
+ins = [np.random.default_rng(r).standard_normal(5000).astype(np.float32) for r in range(4)]
+import oracle_bind
+out = simulate("ring", ins, F32, transport=1)
+assert np.array_equal(out[0], oracle_bind.ring(ins)[0])
+tips_amd.shutdown()
+dist.destroy_process_group()
+print("BOOTSTRAP_OK")
+'''
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, timeout=600)
+    assert "BOOTSTRAP_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -11,6 +11,7 @@ Differences from the reference, on purpose:
 """
 import atexit
 import ctypes
+import os
 import threading
 
 from . import _lib
@@ -24,7 +25,8 @@ def _torch_dist():
         import torch.distributed as dist
     except ImportError:  # pragma: no cover
         return None
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    force = os.environ.get("TIPS_BOOTSTRAP", "") == "torch"  # use the group even at world size 1
+    if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or force):
         return dist
     return None
 

@@ -153,7 +153,10 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
                                                     int64_t n) {
   constexpr int64_t kTile = (int64_t)BLOCK * UNROLL;  // vectors per workgroup-iteration
   const int tid = threadIdx.x;
-  int64_t t = blockIdx.x;
+  // MODE 2: XCD-contiguous placement. Workgroups are dealt round-robin over the 8 XCDs
+  // (b and b+8 share one), so tile = (b % 8) * (grid / 8) + b / 8 gives each XCD one
+  // contiguous stretch of the bucket (speed only: any placement is correct).
+  int64_t t = (MODE == 2) ? (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : (int64_t)blockIdx.x;
   const int64_t tstride = (MODE == 0) ? (int64_t)gridDim.x : 0;
   do {
     const int64_t base = t * kTile + tid;
@@ -361,9 +364,10 @@ hipError_t run_sum2(void* dst, const void* a, const void* b, int64_t n, int bloc
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
   const int64_t tiles = (nvec + (int64_t)BLOCK * UNROLL - 1) / ((int64_t)BLOCK * UNROLL);
-  int64_t grid = (MODE == 1) ? tiles : (blocks > 0 ? blocks : kNumCUs * 8);
+  int64_t grid = (MODE != 0) ? tiles : (blocks > 0 ? blocks : kNumCUs * 8);
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
+  if (MODE == 2) grid = (grid + 7) / 8 * 8;  // whole XCD rounds; surplus tiles fall off the bounds checks
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL((sum2_kernel<DT, MODE, UNROLL, NTL, NTS, BLOCK>), dim3((unsigned)grid), dim3(BLOCK), 0, s,
                      (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);
@@ -395,6 +399,10 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     TIPS_SUM2_CASE(1, 1, 2, true, false, 512)
     TIPS_SUM2_CASE(0, 2, 2, true, false, 256)
     TIPS_SUM2_CASE(0, 4, 2, true, false, 256)
+    TIPS_SUM2_CASE(2, 1, 2, true, false, 256)
+    TIPS_SUM2_CASE(2, 2, 2, true, false, 256)
+    TIPS_SUM2_CASE(2, 1, 2, true, false, 512)
+    TIPS_SUM2_CASE(2, 4, 1, true, true, 256)
     TIPS_SUM2_CASE(1, 1, 0, false, false, 256)
     TIPS_SUM2_CASE(1, 2, 0, false, false, 256)
     TIPS_SUM2_CASE(1, 4, 0, false, false, 256)

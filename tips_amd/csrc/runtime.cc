@@ -708,9 +708,10 @@ int tips_init_rank(int rank, int size, int device, const void* unique_id, int64_
   HIP_TRY(hipSetDevice(device));
   st.device = device;
   TRY(ensure_streams(st));
-  if (size > 1) {
-    if (!unique_id || id_bytes != (int64_t)sizeof(ncclUniqueId))
-      return fail(TIPS_ERR_INVALID_ARG, "size > 1 needs a %zu-byte unique id", sizeof(ncclUniqueId));
+  if (size > 1 && !unique_id) return fail(TIPS_ERR_INVALID_ARG, "size > 1 needs a unique id");
+  if (unique_id) {  // (a 1-rank id is accepted too: the same bootstrap, exercised on one GPU)
+    if (id_bytes != (int64_t)sizeof(ncclUniqueId))
+      return fail(TIPS_ERR_INVALID_ARG, "unique id must be %zu bytes", sizeof(ncclUniqueId));
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof id);
     NCCL_TRY(ncclCommInitRank(&st.comm, size, id, rank));

@@ -22,7 +22,11 @@ run() {  # name seconds cmd...
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -m pytest tests -q -m gpu ${PYTEST_ARGS:-}
+  if [ -n "${PYTEST_K:-}" ]; then
+    run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -m pytest tests -q -m gpu -k "$PYTEST_K"
+  else
+    run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -m pytest tests -q -m gpu
+  fi
   rc=$?; fatal $rc && exit $rc
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
   rc=$?; fatal $rc && exit $rc

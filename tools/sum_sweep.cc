@@ -62,6 +62,9 @@ int main(int argc, char** argv) {
                           {1, 2, 256}, {8, 2, 256}, {2, 2, 512}, {2, 2, 128}, {1, 2, 512}};
   for (auto& t : tiles)
     vs.push_back({"tile_u" + std::to_string(t[0]) + ntn[t[1]] + "_t" + std::to_string(t[2]), 1, t[0], t[1], 0, t[2], {}});
+  const int xcd[][3] = {{1, 2, 256}, {2, 2, 256}, {1, 2, 512}, {4, 1, 256}};
+  for (auto& t : xcd)
+    vs.push_back({"xcd_u" + std::to_string(t[0]) + ntn[t[1]] + "_t" + std::to_string(t[2]), 2, t[0], t[1], 0, t[2], {}});
   for (int u : {1, 2, 4, 8})
     for (int bpc : {2, 8, 16})
       vs.push_back({"gs_u" + std::to_string(u) + "_b" + std::to_string(bpc) + "_nt", 0, u, 1, 256 * bpc, 256, {}});
