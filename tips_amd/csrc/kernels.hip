@@ -9,13 +9,16 @@
 // load/store (global_load_dwordx4 / global_store_dwordx4: one wave touches
 // 1 KiB contiguous), UNROLL independent 16-B vectors per operand are issued
 // before the first add so each lane keeps 2*UNROLL loads in flight, and the
-// grid either covers the bucket one tile per workgroup (mode 1) or
-// grid-strides over a CU-multiple of workgroups (mode 0). Elements that do
+// grid either covers the bucket one tile per workgroup (mode 1; mode 2 = the
+// same with an XCD-contiguous tile order, the default) or grid-strides over a
+// CU-multiple of workgroups (mode 0). Elements that do
 // not fill a 16-B vector (the "tail", < 8 elements) are done scalar by
 // workgroup 0. Integer adds wrap (two's complement, as MPI_SUM on MPI_INT /
 // MPI_LONG_LONG); f16 adds are v_pk_add_f16 (correctly rounded, = fp32 add
 // rounded to half); bf16 adds in fp32 and rounds to nearest-even.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "kernels.h"
 
@@ -144,6 +147,13 @@ __device__ __forceinline__ void add_elem<kBF16>(void* d, const void* a, const vo
   ((unsigned short*)d)[i] = (unsigned short)bf16_round_bits(__builtin_bit_cast(unsigned, s));
 }
 
+// XCD-contiguous tile order: workgroups are dealt round-robin over the 8 XCDs
+// (b and b+8 share one), so tile = (b % 8) * (grid / 8) + b / 8 hands each XCD
+// one contiguous stretch. Needs grid % 8 == 0; speed only, never correctness.
+__device__ __forceinline__ int64_t xcd_tile(unsigned b, unsigned grid) {
+  return (int64_t)(b & 7u) * (grid >> 3) + (b >> 3);
+}
+
 // ---------------------------------------------------------------------------
 // 2-input sum: dst = a + b
 
@@ -156,7 +166,7 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
   // MODE 2: XCD-contiguous placement. Workgroups are dealt round-robin over the 8 XCDs
   // (b and b+8 share one), so tile = (b % 8) * (grid / 8) + b / 8 gives each XCD one
   // contiguous stretch of the bucket (speed only: any placement is correct).
-  int64_t t = (MODE == 2) ? (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : (int64_t)blockIdx.x;
+  int64_t t = (MODE == 2) ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const int64_t tstride = (MODE == 0) ? (int64_t)gridDim.x : 0;
   do {
     const int64_t base = t * kTile + tid;
@@ -291,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
   using W = Wide<DT>;
   constexpr int64_t kTile = (int64_t)kBlock * UNROLL;
   const int tid = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile + tid;
+  const int64_t base = xcd_tile(blockIdx.x, gridDim.x) * kTile + tid;
 #pragma unroll
   for (int u = 0; u < UNROLL; u++) {
     const int64_t i = base + u * kBlock;
@@ -324,8 +334,10 @@ __global__ __launch_bounds__(kBlock) void multi_sum_scalar_kernel(void* dst, Src
 // ---------------------------------------------------------------------------
 // Batched copy (fusion pack / unpack)
 
-__global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __restrict__ tiles) {
-  const CopyTile t = tiles[blockIdx.x];
+__global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __restrict__ tiles, int ntiles) {
+  const int64_t ti = xcd_tile(blockIdx.x, gridDim.x);
+  if (ti >= ntiles) return;
+  const CopyTile t = tiles[ti];
   const int tid = threadIdx.x;
   if (((reinterpret_cast<uintptr_t>(t.src) | reinterpret_cast<uintptr_t>(t.dst) | (uintptr_t)t.bytes) & 15) == 0) {
     const u32x4* s = reinterpret_cast<const u32x4*>(t.src);
@@ -389,8 +401,9 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
   if (mode == M && unroll == U && nt == NTV && threads == B) \
     return run_sum2<DT, M, U, L, S_, B>(dst, a, b, n, blocks, s);
   // the product default first; the rest exist for the tuning sweep (f32 only)
-  TIPS_SUM2_CASE(1, 1, 2, true, false, 256)
+  TIPS_SUM2_CASE(2, 1, 2, true, false, 256)
   if constexpr (DT == kF32) {
+    TIPS_SUM2_CASE(1, 1, 2, true, false, 256)
     TIPS_SUM2_CASE(1, 4, 1, true, true, 256)
     TIPS_SUM2_CASE(1, 2, 2, true, false, 256)
     TIPS_SUM2_CASE(1, 8, 2, true, false, 256)
@@ -399,7 +412,6 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     TIPS_SUM2_CASE(1, 1, 2, true, false, 512)
     TIPS_SUM2_CASE(0, 2, 2, true, false, 256)
     TIPS_SUM2_CASE(0, 4, 2, true, false, 256)
-    TIPS_SUM2_CASE(2, 1, 2, true, false, 256)
     TIPS_SUM2_CASE(2, 2, 2, true, false, 256)
     TIPS_SUM2_CASE(2, 1, 2, true, false, 512)
     TIPS_SUM2_CASE(2, 4, 1, true, true, 256)
@@ -441,7 +453,7 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
 
 // Default variant for the product path (chosen from the gfx950 sweep,
 // profiles/ + DESIGN.md §Kernels).
-constexpr int kDefMode = 1, kDefUnroll = 1, kDefNT = 2, kDefThreads = 256;
+constexpr int kDefMode = 2, kDefUnroll = 1, kDefNT = 2, kDefThreads = 256;
 
 template <int DT, int NSRC>
 hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
@@ -449,7 +461,7 @@ hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
   int64_t grid = (nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
-  if (grid < 1) grid = 1;
+  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
   hipLaunchKernelGGL((multi_sum_kernel<DT, NSRC, U>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst, sl, nvec,
                      nvec * ve, n);
   return hipGetLastError();
@@ -531,7 +543,8 @@ hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_
 
 hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(copy_tiles_kernel, dim3((unsigned)ntiles), dim3(kBlock), 0, s, tiles_dev);
+  const unsigned grid = (unsigned)((ntiles + 7) / 8 * 8);
+  hipLaunchKernelGGL(copy_tiles_kernel, dim3(grid), dim3(kBlock), 0, s, tiles_dev, ntiles);
   return hipGetLastError();
 }
 
