@@ -193,3 +193,20 @@ def test_check_requests_reference_messages(recs, msg):
         assert rc == 0
     else:
         assert rc == -7 and L.tips_last_error() == msg
+
+
+def test_header_is_c99(tmp_path):
+    """include/tips_hip.h compiles as strict C99 and links against the library (what an FFI binds)."""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    exe = str(tmp_path / "abi_check")
+    lib_dir = os.path.join(REPO, "tips_amd", "lib")
+    r = subprocess.run(["gcc", "-std=c99", "-pedantic", "-Wall", "-Werror", "-I" + os.path.join(REPO, "include"),
+                        os.path.join(REPO, "tests", "c", "abi_check.c"), "-L" + lib_dir, "-ltips_hip",
+                        "-Wl,-rpath," + lib_dir, "-o", exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert "Mismatch data types found: 0 vs 1." in r.stdout

@@ -273,3 +273,26 @@ print("BOOTSTRAP_OK")
 '''
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, timeout=600)
     assert "BOOTSTRAP_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+FUZZ = [np.random.default_rng(20261015 + i) for i in range(40)]
+
+
+@pytest.mark.parametrize("case", range(40))
+def test_schedule_fuzz(gpu, oracle, monkeypatch, case):
+    """Random (schedule, p, n, dtype, in-place, transport, pipeline depth/sub-chunk) vs the oracle, bit-exact."""
+    r = FUZZ[case]
+    kind = ["ring", "direct"][int(r.integers(2))]
+    p = int(r.integers(2, 17 if kind == "direct" else 13))
+    n = int(r.choice([0, 1, 2, 63, 64, 65, 255, 4096, int(r.integers(1, 300000))]))
+    dtype = int(r.choice(ALL_DTYPES))
+    inplace = bool(r.integers(2))
+    transport = int(r.integers(2))
+    monkeypatch.setenv("TIPS_PIPELINE_DEPTH", str(int(r.integers(1, 7))))
+    monkeypatch.setenv("TIPS_MIN_SUBCHUNK_BYTES", str(int(r.choice([256, 4096, 65536, 8 << 20]))))
+    ins = [rand(dtype, n, r) for _ in range(p)]
+    if n == 0:
+        return
+    exp = oracle.ring(ins, code=dtype)[0] if kind == "ring" else oracle.fold(ins, code=dtype, wide_acc=True)
+    for got in simulate(kind, ins, dtype, inplace=inplace, transport=transport):
+        assert same_bits(got, exp, dtype), (kind, p, n, dtype, inplace, transport)
