@@ -390,6 +390,42 @@ def bench_allreduce(args):
     all_ok = all_ranks_ok(dist, ok)
     del ref, tmp, got, exp
 
+    # the reduce kernel of this schedule, timed alone at its per-launch shape (HBM roofline)
+    kernel_roof = None
+    if world > 1 and workload == "bucket" and algo in (_lib.ALGO_RING, _lib.ALGO_DIRECT):
+        import ctypes
+        depth, sub = ctypes.c_int(), ctypes.c_int64()
+        _lib.call("tips_schedule_shape", sizes[0], world, _lib.FLOAT32, ctypes.byref(depth), ctypes.byref(sub))
+        m = sub.value
+        nsrc = world if algo == _lib.ALGO_DIRECT else 2
+        bufs = torch.empty((nsrc + 1) * m, dtype=torch.float32, device="cuda").uniform_(0.5, 1.5)
+        srcs = [bufs[j * m:(j + 1) * m] for j in range(nsrc)]
+        dst = bufs[nsrc * m:]
+        sp_arr, _keep3 = _lib.ptr_array([t.data_ptr() for t in srcs])
+
+        def kern():
+            if nsrc == 2:
+                _lib.call("tips_bucket_sum", dst.data_ptr(), srcs[0].data_ptr(), srcs[1].data_ptr(), m, _lib.FLOAT32, sp)
+            else:
+                _lib.call("tips_multi_sum", dst.data_ptr(), sp_arr, nsrc, m, _lib.FLOAT32, sp)
+
+        for _ in range(3):
+            kern()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(50):
+            kern()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 50 * 1e3
+        kbytes = (nsrc + 1) * m * 4
+        kernel_roof = {"kernel": "multi_sum_kernel" if nsrc > 2 else "sum2_kernel", "sources": nsrc,
+                       "elements_per_launch": m, "launches_per_step": depth.value * (world - 1 if nsrc == 2 else 1),
+                       "bound": "hbm", "achieved": round(kbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                       "unit": "GB/s", "frac": round(kbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": kbytes}
+        del bufs, srcs, dst
+
     # comparison points on the same workload: the other schedules and ncclAllReduce
     compare = {}
     if not args.no_compare:
@@ -425,6 +461,7 @@ def bench_allreduce(args):
                          "unit": "GB/s", "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None,
                          "note": "multi-GPU: the ring/all-pairs transfer, not the sum kernel, bounds the step"},
             "cpu_baseline": None,
+            "reduce_kernel_roofline": kernel_roof,
             "compare_algbw_gib_s": compare,
             "check": check if all_ok else "FAIL on some rank",
         }

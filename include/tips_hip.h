@@ -198,6 +198,11 @@ int tips_set_sim_transport(int transport);
 int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
                      int blocks, int threads, void* stream);
 
+/* Pipeline shape the ring/direct schedules use for a bucket: depth = K
+ * sub-chunks per chunk, sub_elems = elements in a (first) sub-chunk, i.e. the
+ * size of one reduce-kernel launch (TIPS_PIPELINE_DEPTH, TIPS_MIN_SUBCHUNK_BYTES). */
+int tips_schedule_shape(int64_t count, int p, int dtype, int* depth, int64_t* sub_elems);
+
 /* Chunk partition the ring uses (element offsets), for tests. */
 int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end);
 

@@ -210,3 +210,18 @@ def test_header_is_c99(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     assert "Mismatch data types found: 0 vs 1." in r.stdout
+
+
+@pytest.mark.parametrize("count,p", [(268435456, 8), (268435456, 2), (262144, 2), (1000, 4), (0, 3)])
+def test_schedule_shape(count, p, monkeypatch):
+    """K = min(depth, ceil(chunk_bytes / min_sub)), sub = round_up(ceil(chunk/K), 256 B) (runtime.cc)."""
+    import ctypes
+    from tips_amd import _lib
+    L = _lib.lib()
+    d, sub = ctypes.c_int(), ctypes.c_int64()
+    assert L.tips_schedule_shape(count, p, 0, ctypes.byref(d), ctypes.byref(sub)) == 0
+    align = 64
+    chunk = min(count, -(-(-(-count // p)) // align) * align)
+    k = max(1, min(4, -(-chunk * 4 // (8 << 20))))
+    assert d.value == k
+    assert sub.value == min(chunk, -(-(-(-chunk // k)) // align) * align)

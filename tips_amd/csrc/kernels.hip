@@ -190,6 +190,29 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
   if (blockIdx.x == 0 && tail_begin + tid < n) add_elem<DT>(dst, a, b, tail_begin + tid);
 }
 
+// Cache-policy sweep variant (f32, tuning only): the same tile as MODE 2, through
+// buffer_load/store_dwordx4 with explicit CPol bits (aux: 1 = sc0, 2 = nt,
+// 16 = sc1). The per-workgroup descriptor covers exactly its tile, so the
+// hardware range check drops the lanes past the end of the bucket.
+template <int LAUX, int SAUX>
+__global__ __launch_bounds__(256) void sum2_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
+                                                      const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
+                                                      int64_t n) {
+  const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t first = t * 256;
+  if (first < nvec) {
+    const int rec = (int)(((nvec - first) < 256 ? (nvec - first) : 256) * 16);
+    __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)(a + first), (short)0, rec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(b + first), (short)0, rec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
+    const int off = threadIdx.x * 16;
+    u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, LAUX);
+    u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, LAUX);
+    __builtin_amdgcn_raw_buffer_store_b128(add16<kF32>(x, y), rd, off, 0, SAUX);
+  }
+  if (blockIdx.x == 0 && tail_begin + threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
+}
+
 // Unaligned fallback (any pointer not 16-B aligned): one element per lane.
 template <int DT>
 __global__ __launch_bounds__(kBlock) void sum2_scalar_kernel(void* dst, const void* a, const void* b, int64_t n) {
@@ -400,6 +423,28 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
 #define TIPS_SUM2_CASE(M, U, NTV, L, S_, B)                      \
   if (mode == M && unroll == U && nt == NTV && threads == B) \
     return run_sum2<DT, M, U, L, S_, B>(dst, a, b, n, blocks, s);
+  if constexpr (DT == kF32) {
+    if (mode == 3 && threads == 256) {  // cache-policy variants: nt = index into (load aux, store aux)
+      const int64_t nvec = n / 4, tiles = (nvec + 255) / 256;
+      const unsigned grid = (unsigned)std::max<int64_t>(8, (tiles + 7) / 8 * 8);
+#define TIPS_BUF_CASE(I, L, S_)                                                                             \
+  if (nt == I) {                                                                                        \
+    hipLaunchKernelGGL((sum2_buf_kernel<L, S_>), dim3(grid), dim3(256), 0, s, (u32x4*)dst, (const u32x4*)a, \
+                       (const u32x4*)b, nvec, nvec * 4, n);                                             \
+    return hipGetLastError();                                                                           \
+  }
+      TIPS_BUF_CASE(0, 2, 0)
+      TIPS_BUF_CASE(1, 2, 16)
+      TIPS_BUF_CASE(2, 2, 17)
+      TIPS_BUF_CASE(3, 18, 0)
+      TIPS_BUF_CASE(4, 3, 0)
+      TIPS_BUF_CASE(5, 16, 0)
+      TIPS_BUF_CASE(6, 18, 16)
+      TIPS_BUF_CASE(7, 2, 2)
+#undef TIPS_BUF_CASE
+      return hipErrorInvalidValue;
+    }
+  }
   // the product default first; the rest exist for the tuning sweep (f32 only)
   TIPS_SUM2_CASE(2, 1, 2, true, false, 256)
   if constexpr (DT == kF32) {

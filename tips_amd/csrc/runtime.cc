@@ -826,6 +826,16 @@ int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, in
   return 0;
 }
 
+int tips_schedule_shape(int64_t count, int p, int dtype, int* depth, int64_t* sub_elems) {
+  TRY(check_dtype(dtype));
+  if (p < 1 || count < 0 || !depth || !sub_elems) return fail(TIPS_ERR_INVALID_ARG, "bad schedule query");
+  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
+  const Range c0 = chunk_of(count, p, align, 0);
+  *depth = pipeline_depth(c0.len() * es);
+  *sub_elems = sub_of(c0, *depth, align, 0).len();
+  return 0;
+}
+
 int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int dtype, void* stream) {
   TRY(check_dtype(dtype));
   if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count");
