@@ -161,6 +161,7 @@ struct EventPool {
 
 // fusion plan: cached per (dtype, tensor list)
 struct FusionBucket {
+  char* buf = nullptr;        // the fusion slot this bucket packs into (slot b % 2)
   int64_t bytes = 0;          // padded bucket size
   int ntiles = 0;
   CopyTile* pack = nullptr;   // device descriptor arrays
@@ -183,6 +184,9 @@ struct State {
   hipStream_t comm_stream = nullptr, comp_stream = nullptr, io_stream = nullptr;
   hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // host-memory pipeline (both PCIe directions)
   EventPool pipe_ev;
+  hipStream_t fuse_stream = nullptr, bucket_stream = nullptr;  // fusion: pack/unpack || bucket allreduce
+  EventPool fuse_ev;
+  int64_t fusion_threshold = 0;  // the fusion slots' size; plans hold addresses into them
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
@@ -202,6 +206,8 @@ int ensure_streams(State& st) {
   if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
   if (!st.h2d_stream) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream, hipStreamNonBlocking));
   if (!st.d2h_stream) HIP_TRY(hipStreamCreateWithFlags(&st.d2h_stream, hipStreamNonBlocking));
+  if (!st.fuse_stream) HIP_TRY(hipStreamCreateWithFlags(&st.fuse_stream, hipStreamNonBlocking));
+  if (!st.bucket_stream) HIP_TRY(hipStreamCreateWithFlags(&st.bucket_stream, hipStreamNonBlocking));
   if (!st.ev_start) HIP_TRY(hipEventCreateWithFlags(&st.ev_start, hipEventDisableTiming));
   if (!st.ev_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
   if (!st.ev_comp_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_done, hipEventDisableTiming));
@@ -616,11 +622,12 @@ int build_plan(State& st, FusionPlan& pl, int64_t threshold) {
     }
     sizes.back() = off + bytes;
   }
-  TRY(st.fusion.ensure((size_t)threshold, /*zero=*/true));
-  char* fb = (char*)st.fusion.p;
+  // two slots: bucket b packs into slot b % 2, so pack(b+1) can run while bucket b is reduced
   for (size_t b = 0; b < sizes.size(); b++) {
     if (sizes[b] == 0) continue;
     FusionBucket fbk;
+    char* fb = (char*)st.fusion.p + (int64_t)(pl.buckets.size() % 2) * threshold;
+    fbk.buf = fb;
     fbk.bytes = round_up(sizes[b], kAlignBytes);
     fbk.ntiles = (int)packs[b].size();
     for (auto& t : packs[b]) t.dst = fb + (uintptr_t)t.dst;
@@ -773,7 +780,10 @@ void tips_shutdown(void) {
       *e = nullptr;
     }
   st.pipe_ev.release();
-  for (hipStream_t* s : {&st.comm_stream, &st.comp_stream, &st.io_stream, &st.h2d_stream, &st.d2h_stream})
+  st.fuse_ev.release();
+  st.fusion_threshold = 0;
+  for (hipStream_t* s : {&st.comm_stream, &st.comp_stream, &st.io_stream, &st.h2d_stream, &st.d2h_stream,
+                         &st.fuse_stream, &st.bucket_stream})
     if (*s) {
       (void)hipStreamDestroy(*s);
       *s = nullptr;
@@ -991,19 +1001,29 @@ int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dt
   hipStream_t s = (hipStream_t)stream;
   const int64_t es = tips::dtype_size(dtype);
   const int64_t threshold = round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_FUSION_THRESHOLD", 64 << 20)), kAlignBytes);
+  if (threshold != st.fusion_threshold) {  // slots (re)sized: every cached plan points into the old ones
+    HIP_TRY(hipDeviceSynchronize());
+    for (auto& kv : st.plans) free_plan(kv.second);
+    st.plans.clear();
+    st.fusion.release();
+    TRY(st.fusion.ensure((size_t)(2 * threshold), /*zero=*/true));
+    st.fusion_threshold = threshold;
+  }
   const uint64_t key = plan_key(ptrs, counts, n, dtype);
   auto it = st.plans.find(key);
   bool hit = it != st.plans.end() && it->second.dtype == dtype && (int)it->second.ptrs.size() == n &&
              std::equal(ptrs, ptrs + n, it->second.ptrs.begin()) && std::equal(counts, counts + n, it->second.counts.begin());
   if (!hit) {
-    if (it != st.plans.end()) {
-      free_plan(it->second);
-      st.plans.erase(it);
-    }
-    if (st.plans.size() >= 64) {
+    if (it != st.plans.end() || st.plans.size() >= 64) {  // descriptors may still be read by queued kernels
       HIP_TRY(hipDeviceSynchronize());
-      for (auto& kv : st.plans) free_plan(kv.second);
-      st.plans.clear();
+      if (it != st.plans.end()) {
+        free_plan(it->second);
+        st.plans.erase(it);
+      }
+      if (st.plans.size() >= 64) {
+        for (auto& kv : st.plans) free_plan(kv.second);
+        st.plans.clear();
+      }
     }
     FusionPlan pl;
     pl.dtype = dtype;
@@ -1017,10 +1037,30 @@ int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dt
     it = st.plans.emplace(key, std::move(pl)).first;
   }
   const FusionPlan& pl = it->second;
-  for (const auto& b : pl.buckets) {
-    HIP_TRY(tips::launch_copy_tiles(b.pack, b.ntiles, s));
-    TRY(allreduce_device(st, st.fusion.p, st.fusion.p, b.bytes / es, dtype, s));
-    HIP_TRY(tips::launch_copy_tiles(b.unpack, b.ntiles, s));
+  const int B = (int)pl.buckets.size();
+  if (B > 0) {
+    // fuse stream: pack(0) pack(1) unpack(0) pack(2) unpack(1) ... unpack(B-1)
+    // bucket stream: allreduce(b) after pack(b); unpack(b) after allreduce(b); pack(b+2) after unpack(b)
+    TRY(st.fuse_ev.ensure(2 * (size_t)B));
+    hipEvent_t* packed = st.fuse_ev.ev.data();
+    hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
+    TRY(join(st.fuse_stream, s, st.ev_start));
+    auto pack = [&](int b) -> int {
+      HIP_TRY(tips::launch_copy_tiles(pl.buckets[b].pack, pl.buckets[b].ntiles, st.fuse_stream));
+      HIP_TRY(hipEventRecord(packed[b], st.fuse_stream));
+      return 0;
+    };
+    TRY(pack(0));
+    for (int b = 0; b < B; b++) {
+      if (b + 1 < B && b + 1 < 2) TRY(pack(b + 1));  // slot 1 is free from the start
+      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[b], 0));
+      TRY(allreduce_device(st, pl.buckets[b].buf, pl.buckets[b].buf, pl.buckets[b].bytes / es, dtype, st.bucket_stream));
+      HIP_TRY(hipEventRecord(reduced[b], st.bucket_stream));
+      HIP_TRY(hipStreamWaitEvent(st.fuse_stream, reduced[b], 0));
+      HIP_TRY(tips::launch_copy_tiles(pl.buckets[b].unpack, pl.buckets[b].ntiles, st.fuse_stream));
+      if (b + 2 < B) TRY(pack(b + 2));  // reuses slot b % 2, after unpack(b) in stream order
+    }
+    TRY(join(s, st.fuse_stream, st.ev_done));
   }
   for (int i : pl.unfused) TRY(allreduce_device(st, ptrs[i], ptrs[i], counts[i], dtype, s));
   return 0;
