@@ -35,7 +35,7 @@ XGMI_LINK_GBPS = 153.0   # per link per direction (task / SURVEY §8d)
 GIB = float(1 << 30)
 # the exact instantiation tips_bucket_sum launches for f32 (kernels.hip kDef*): PMC traffic is only
 # reported from a profile of this kernel
-DEFAULT_SUM_KERNEL = "sum2_kernel<0, 2, 1, true, false, 256>"
+DEFAULT_SUM_KERNEL = "sum2_buf_kernel<0, 2, 16>"
 
 
 def parse():
@@ -205,7 +205,7 @@ def bench_sum(args):
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: fp32 U[-1,1), torch cuda generator seeds 1 and 2, resident in HBM",
         "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
-                   "bucket_bytes": n * 4, "elements": n, "kernel": "tips_bucket_sum (sum2_kernel<f32, one tile/workgroup in XCD-contiguous order, one 16-B vector per lane per operand, nt loads, plain stores, 256 threads>)",
+                   "bucket_bytes": n * 4, "elements": n, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, XCD-contiguous order, buffer_load/store_dwordx4)",
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),

@@ -296,3 +296,45 @@ def test_schedule_fuzz(gpu, oracle, monkeypatch, case):
     exp = oracle.ring(ins, code=dtype)[0] if kind == "ring" else oracle.fold(ins, code=dtype, wide_acc=True)
     for got in simulate(kind, ins, dtype, inplace=inplace, transport=transport):
         assert same_bits(got, exp, dtype), (kind, p, n, dtype, inplace, transport)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["ring", "direct"])
+def test_config3_full_size_8ranks(gpu, kind):
+    """BASELINE config 3 at full size on one GPU: 8 virtual ranks x 1 GiB fp32, U[0.5,1.5), seeds 3000+r.
+    Expected values are recomputed on the device with torch adds in the schedule's own order
+    (ring: chunk c folded in[c], in[c+1] + acc, ...; direct: rank-order fold) -> bit-exact; plus every
+    rank identical and <= 1e-6 relative to the float64 sum on a strided sample."""
+    import ctypes
+    import torch
+    from tips_amd import _lib
+    p, n = 8, 268435456
+    g = torch.Generator(device="cuda")
+    ins = []
+    for r in range(p):
+        g.manual_seed(3000 + r)
+        ins.append(torch.empty(n, dtype=torch.float32, device="cuda").uniform_(0.5, 1.5, generator=g))
+    outs = [torch.empty_like(x) for x in ins]
+    pi, _k1 = _lib.ptr_array([x.data_ptr() for x in ins])
+    po, _k2 = _lib.ptr_array([o.data_ptr() for o in outs])
+    fn = "tips_ring_simulate" if kind == "ring" else "tips_direct_simulate"
+    _lib.call(fn, po, pi, p, n, F32, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    exp = torch.empty_like(ins[0])
+    if kind == "ring":
+        b, e = ctypes.c_int64(), ctypes.c_int64()
+        for c in range(p):
+            _lib.call("tips_chunk_bounds", n, p, F32, c, ctypes.byref(b), ctypes.byref(e))
+            acc = ins[c][b.value:e.value].clone()
+            for k in range(1, p):
+                acc = ins[(c + k) % p][b.value:e.value] + acc
+            exp[b.value:e.value] = acc
+    else:
+        exp.copy_(ins[0])
+        for r in range(1, p):
+            exp += ins[r]
+    for o in outs:
+        assert torch.equal(o, exp)
+    idx = torch.arange(0, n, 9973, device="cuda")
+    ref = sum(x[idx].double() for x in ins)
+    assert ((outs[0][idx].double() - ref).abs() / ref).max().item() <= 1e-6

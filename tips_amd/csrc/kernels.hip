@@ -190,11 +190,14 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
   if (blockIdx.x == 0 && tail_begin + tid < n) add_elem<DT>(dst, a, b, tail_begin + tid);
 }
 
-// Cache-policy sweep variant (f32, tuning only): the same tile as MODE 2, through
-// buffer_load/store_dwordx4 with explicit CPol bits (aux: 1 = sc0, 2 = nt,
-// 16 = sc1). The per-workgroup descriptor covers exactly its tile, so the
-// hardware range check drops the lanes past the end of the bucket.
-template <int LAUX, int SAUX>
+// The shipped 2-input sum (and, with other CPol bits, the cache-policy sweep
+// variants): one 4 KiB tile per operand per workgroup in XCD-contiguous order,
+// through buffer_load/store_dwordx4 with explicit CPol bits (aux: 1 = sc0,
+// 2 = nt, 16 = sc1). Default LAUX = 2 (nt loads), SAUX = 16 (sc1 stores: the
+// written line leaves the XCD's L2 instead of occupying it — 7.46 vs 7.10 TB/s
+// on config 2, profiles/r01_sum_sweep_f.jsonl). Each workgroup's descriptors
+// cover exactly its tile, so the hardware range check drops lanes past the end.
+template <int DT, int LAUX, int SAUX>
 __global__ __launch_bounds__(256) void sum2_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
                                                       const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
                                                       int64_t n) {
@@ -208,9 +211,9 @@ __global__ __launch_bounds__(256) void sum2_buf_kernel(u32x4* __restrict__ dst, 
     const int off = threadIdx.x * 16;
     u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, LAUX);
     u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, LAUX);
-    __builtin_amdgcn_raw_buffer_store_b128(add16<kF32>(x, y), rd, off, 0, SAUX);
+    __builtin_amdgcn_raw_buffer_store_b128(add16<DT>(x, y), rd, off, 0, SAUX);
   }
-  if (blockIdx.x == 0 && tail_begin + threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
+  if (blockIdx.x == 0 && tail_begin + threadIdx.x < n) add_elem<DT>(dst, a, b, tail_begin + threadIdx.x);
 }
 
 // Unaligned fallback (any pointer not 16-B aligned): one element per lane.
@@ -324,7 +327,12 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
   using W = Wide<DT>;
   constexpr int64_t kTile = (int64_t)kBlock * UNROLL;
   const int tid = threadIdx.x;
-  const int64_t base = xcd_tile(blockIdx.x, gridDim.x) * kTile + tid;
+  const int64_t first = xcd_tile(blockIdx.x, gridDim.x) * kTile;
+  const int64_t base = first + tid;
+  // sc1 stores through a descriptor covering this tile (as sum2_buf_kernel)
+  const int64_t left = nvec - first;
+  __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dst + first), (short)0, (int)((left < kTile ? (left > 0 ? left : 0) : kTile) * 16), 0x00020000);
 #pragma unroll
   for (int u = 0; u < UNROLL; u++) {
     const int64_t i = base + u * kBlock;
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
       typename W::A acc = W::load(v[0]);
 #pragma unroll
       for (int j = 1; j < NSRC; j++) acc = acc + W::load(v[j]);
-      dst[i] = W::store(acc);
+      __builtin_amdgcn_raw_buffer_store_b128(W::store(acc), rd, (int)((i - first) * 16), 0, 16);
     }
   }
   if (blockIdx.x == 0 && NSRC > 1 && tail_begin + tid < n) {
@@ -364,17 +372,17 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __re
   const int tid = threadIdx.x;
   if (((reinterpret_cast<uintptr_t>(t.src) | reinterpret_cast<uintptr_t>(t.dst) | (uintptr_t)t.bytes) & 15) == 0) {
     const u32x4* s = reinterpret_cast<const u32x4*>(t.src);
-    u32x4* d = reinterpret_cast<u32x4*>(t.dst);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(t.dst, (short)0, (int)t.bytes, 0x00020000);
     const int64_t nv = t.bytes >> 4;
     constexpr int U = 4;
     for (int64_t i = tid; i < nv; i += kBlock * U) {
-      u32x4 v[U];
+      u32x4 v[U] = {};
 #pragma unroll
       for (int u = 0; u < U; u++)
-        if (i + u * kBlock < nv) v[u] = s[i + u * kBlock];
+        if (i + u * kBlock < nv) v[u] = ld16<true>(s + i + u * kBlock);
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (i + u * kBlock < nv) d[i + u * kBlock] = v[u];
+      for (int u = 0; u < U; u++)  // sc1 stores; lanes past the tile fall off the descriptor's range
+        __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (int)((i + u * kBlock) * 16), 0, 16);
     }
   } else if (((reinterpret_cast<uintptr_t>(t.src) | reinterpret_cast<uintptr_t>(t.dst) | (uintptr_t)t.bytes) & 3) == 0) {
     const unsigned* s = reinterpret_cast<const unsigned*>(t.src);
@@ -423,31 +431,34 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
 #define TIPS_SUM2_CASE(M, U, NTV, L, S_, B)                      \
   if (mode == M && unroll == U && nt == NTV && threads == B) \
     return run_sum2<DT, M, U, L, S_, B>(dst, a, b, n, blocks, s);
-  if constexpr (DT == kF32) {
-    if (mode == 3 && threads == 256) {  // cache-policy variants: nt = index into (load aux, store aux)
-      const int64_t nvec = n / 4, tiles = (nvec + 255) / 256;
-      const unsigned grid = (unsigned)std::max<int64_t>(8, (tiles + 7) / 8 * 8);
-#define TIPS_BUF_CASE(I, L, S_)                                                                             \
-  if (nt == I) {                                                                                        \
-    hipLaunchKernelGGL((sum2_buf_kernel<L, S_>), dim3(grid), dim3(256), 0, s, (u32x4*)dst, (const u32x4*)a, \
-                       (const u32x4*)b, nvec, nvec * 4, n);                                             \
-    return hipGetLastError();                                                                           \
+  if (mode == 3 && threads == 256) {  // buffer-op variants: nt = index into (load aux, store aux)
+    const int64_t ve = 16 / (int64_t)dtype_size(DT);
+    const int64_t nvec = n / ve, tiles = (nvec + 255) / 256;
+    const unsigned grid = (unsigned)std::max<int64_t>(8, (tiles + 7) / 8 * 8);
+#define TIPS_BUF_CASE(I, L, S_)                                                                              \
+  if (nt == I) {                                                                                         \
+    hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_>), dim3(grid), dim3(256), 0, s, (u32x4*)dst,             \
+                       (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);                            \
+    return hipGetLastError();                                                                            \
   }
+    TIPS_BUF_CASE(1, 2, 16)  // the product default: nt loads, sc1 stores
+    if constexpr (DT == kF32) {
       TIPS_BUF_CASE(0, 2, 0)
-      TIPS_BUF_CASE(1, 2, 16)
       TIPS_BUF_CASE(2, 2, 17)
       TIPS_BUF_CASE(3, 18, 0)
       TIPS_BUF_CASE(4, 3, 0)
       TIPS_BUF_CASE(5, 16, 0)
       TIPS_BUF_CASE(6, 18, 16)
       TIPS_BUF_CASE(7, 2, 2)
-#undef TIPS_BUF_CASE
-      return hipErrorInvalidValue;
+      TIPS_BUF_CASE(8, 0, 16)
+      TIPS_BUF_CASE(9, 3, 17)
     }
+#undef TIPS_BUF_CASE
+    return hipErrorInvalidValue;
   }
-  // the product default first; the rest exist for the tuning sweep (f32 only)
-  TIPS_SUM2_CASE(2, 1, 2, true, false, 256)
+  // global_load/store forms: the tuning sweep's other variants (f32 only)
   if constexpr (DT == kF32) {
+    TIPS_SUM2_CASE(2, 1, 2, true, false, 256)
     TIPS_SUM2_CASE(1, 1, 2, true, false, 256)
     TIPS_SUM2_CASE(1, 4, 1, true, true, 256)
     TIPS_SUM2_CASE(1, 2, 2, true, false, 256)
@@ -498,7 +509,7 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
 
 // Default variant for the product path (chosen from the gfx950 sweep,
 // profiles/ + DESIGN.md §Kernels).
-constexpr int kDefMode = 2, kDefUnroll = 1, kDefNT = 2, kDefThreads = 256;
+constexpr int kDefMode = 3, kDefUnroll = 1, kDefNT = 1, kDefThreads = 256;
 
 template <int DT, int NSRC>
 hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {

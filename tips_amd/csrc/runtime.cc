@@ -1038,7 +1038,13 @@ int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dt
   }
   const FusionPlan& pl = it->second;
   const int B = (int)pl.buckets.size();
-  if (B > 0) {
+  if (B > 0 && st.size == 1) {  // nothing to overlap with: pack, (no-op) reduce, unpack on the caller's stream
+    for (const auto& b : pl.buckets) {
+      HIP_TRY(tips::launch_copy_tiles(b.pack, b.ntiles, s));
+      TRY(allreduce_device(st, b.buf, b.buf, b.bytes / es, dtype, s));
+      HIP_TRY(tips::launch_copy_tiles(b.unpack, b.ntiles, s));
+    }
+  } else if (B > 0) {
     // fuse stream: pack(0) pack(1) unpack(0) pack(2) unpack(1) ... unpack(B-1)
     // bucket stream: allreduce(b) after pack(b); unpack(b) after allreduce(b); pack(b+2) after unpack(b)
     TRY(st.fuse_ev.ensure(2 * (size_t)B));

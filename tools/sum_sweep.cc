@@ -63,9 +63,10 @@ int main(int argc, char** argv) {
   for (auto& t : tiles)
     vs.push_back({"tile_u" + std::to_string(t[0]) + ntn[t[1]] + "_t" + std::to_string(t[2]), 1, t[0], t[1], 0, t[2], {}});
   const int xcd[][3] = {{1, 2, 256}, {2, 2, 256}, {1, 2, 512}, {4, 1, 256}};
-  const char* cpol[] = {"ld_nt/st_plain", "ld_nt/st_sc1", "ld_nt/st_sc0sc1", "ld_ntsc1/st_plain",
-                        "ld_sc0nt/st_plain", "ld_sc1/st_plain", "ld_ntsc1/st_sc1", "ld_nt/st_nt"};
-  for (int i = 0; i < 8; i++) vs.push_back({std::string("buf_") + cpol[i], 3, 1, i, 0, 256, {}});
+  const char* cpol[] = {"ld_nt/st_plain",   "ld_nt/st_sc1",    "ld_nt/st_sc0sc1", "ld_ntsc1/st_plain",
+                        "ld_sc0nt/st_plain", "ld_sc1/st_plain", "ld_ntsc1/st_sc1", "ld_nt/st_nt",
+                        "ld_plain/st_sc1",   "ld_sc0nt/st_sc0sc1"};
+  for (int i = 0; i < 10; i++) vs.push_back({std::string("buf_") + cpol[i], 3, 1, i, 0, 256, {}});
   for (auto& t : xcd)
     vs.push_back({"xcd_u" + std::to_string(t[0]) + ntn[t[1]] + "_t" + std::to_string(t[2]), 2, t[0], t[1], 0, t[2], {}});
   for (int u : {1, 2, 4, 8})
