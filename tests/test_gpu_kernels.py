@@ -128,3 +128,22 @@ def test_python_bucket_sum(gpu):
     a = torch.randn(1000, device="cuda")
     b = torch.randn(1000, device="cuda")
     assert torch.equal(gpu.bucket_sum(a, b), a + b)
+
+
+@pytest.mark.slow
+def test_count_beyond_int32(gpu):
+    """count > 2^31 elements (the reference passes an int count, utils.h:62; the C-ABI takes int64):
+    2^31 + 13 fp16 elements (4 GiB per buffer), compared with torch's fp16 add (same correctly
+    rounded result) on the device, including the scalar tail."""
+    import torch
+    from tips_amd import _lib
+    n = (1 << 31) + 13
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    a = torch.empty(n, dtype=torch.float16, device="cuda").uniform_(-100, 100, generator=g)
+    b = torch.empty(n, dtype=torch.float16, device="cuda").uniform_(-100, 100, generator=g)
+    c = torch.empty_like(a)
+    _lib.call("tips_bucket_sum", c.data_ptr(), a.data_ptr(), b.data_ptr(), n, F16, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(c, a + b)
+    assert torch.equal(c[-13:], a[-13:] + b[-13:])
