@@ -17,6 +17,12 @@
 #include <stdbool.h>
 #include <stdint.h>
 
+#if defined(__GNUC__)
+#define TIPS_API __attribute__((visibility("default")))
+#else
+#define TIPS_API
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -71,33 +77,33 @@ enum tips_algorithm {
  * id is exchanged over TCP: rank 0 listens on MASTER_ADDR:TIPS_BOOTSTRAP_PORT
  * (default MASTER_PORT + 17). Errors are reported by tips_last_error() and
  * tips_is_initialize() stays false (the reference CHECK-fails instead). */
-void tips_init(void);
+TIPS_API void tips_init(void);
 /* Replaces tips_shutdown (operations.cc:24-44). Safe to call twice. */
-void tips_shutdown(void);
+TIPS_API void tips_shutdown(void);
 /* Replaces tips_is_initialize (operations.cc:46). */
-bool tips_is_initialize(void);
+TIPS_API bool tips_is_initialize(void);
 /* Replace tips_size / tips_rank (operations.cc:48,50). -1 before init. */
-int tips_size(void);
-int tips_rank(void);
+TIPS_API int tips_size(void);
+TIPS_API int tips_rank(void);
 
 /* ---- lifecycle extensions (no reference counterpart) ---- */
 
 /* Bytes of an RCCL unique id (128). */
-int tips_unique_id_bytes(void);
+TIPS_API int tips_unique_id_bytes(void);
 /* Writes a fresh unique id into out[0..cap). Call on rank 0 only; returns bytes or <0. */
-int tips_get_unique_id(void* out, int64_t cap);
+TIPS_API int tips_get_unique_id(void* out, int64_t cap);
 /* Initialise with an id distributed by the caller (e.g. through a
  * torch.distributed store). device < 0: LOCAL_RANK % device count. */
-int tips_init_rank(int rank, int size, int device, const void* unique_id, int64_t id_bytes);
+TIPS_API int tips_init_rank(int rank, int size, int device, const void* unique_id, int64_t id_bytes);
 /* The TCP exchange tips_init uses for the unique id, exposed for callers
  * that bootstrap themselves (and for CPU tests): rank 0's buf[0..bytes) is
  * delivered into every other rank's buf. Rank 0 listens on port; others
  * connect to host:port, retrying for up to timeout_s seconds. */
-int tips_bootstrap_broadcast(int rank, int size, const char* host, int port, void* buf, int64_t bytes, int timeout_s);
+TIPS_API int tips_bootstrap_broadcast(int rank, int size, const char* host, int port, void* buf, int64_t bytes, int timeout_s);
 /* Message of the calling thread's last failed call ("" if none). */
-const char* tips_last_error(void);
+TIPS_API const char* tips_last_error(void);
 /* Library version string. */
-const char* tips_version(void);
+TIPS_API const char* tips_version(void);
 
 /* ---- data path ---- */
 
@@ -106,11 +112,11 @@ const char* tips_version(void);
  * AllreduceCpu<T>, tips/core/collective/utils.h:60-65). In-place (dst == a
  * or dst == b) allowed. count in elements (int64: lifts the reference's
  * int limit, utils.h:62). Device pointers only. Stream-ordered, async. */
-int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int dtype, void* stream);
+TIPS_API int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int dtype, void* stream);
 
 /* dst[i] = ((srcs[0][i] + srcs[1][i]) + srcs[2][i]) + ... (rank-order fold),
  * 1 <= nsrc <= 16. f16/bf16 partials are kept in fp32 and rounded once. */
-int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, void* stream);
+TIPS_API int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, void* stream);
 
 /* Replaces AllreduceCpu<T> (tips/core/collective/utils.h:52-67) and the
  * MPIAllreduce op's data path (tips/tensorflow/ops.cc:86-115):
@@ -118,7 +124,7 @@ int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, 
  * Device pointers: stream-ordered, returns after enqueue.
  * Host pointers (both): staged through HBM, returns when out is written.
  * op must be TIPS_OP_SUM. */
-int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream);
+TIPS_API int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream);
 
 /* ---- control plane: cross-rank request validation ---- */
 
@@ -139,37 +145,37 @@ enum tips_request_type {
  * ("Mismatch data types found: 0 vs 1.", "Mismatched allreduce tensor shapes:
  * [2,4] vs [2,3]", "Mismatched allgather tensor shapes: 1-th dimension 3 vs 4",
  * ...). Pure host function. */
-int tips_check_requests(const int64_t* table, int p);
+TIPS_API int tips_check_requests(const int64_t* table, int p);
 
 /* tips_allreduce preceded by that validation: the records of all ranks are
  * exchanged (one small RCCL allgather + host sync), so every rank reaches the
  * same verdict; on a mismatch no rank reduces. shape = the tensor's dims. */
-int tips_allreduce_checked(const void* in, void* out, const int64_t* shape, int ndim, int dtype, int op, void* stream);
+TIPS_API int tips_allreduce_checked(const void* in, void* out, const int64_t* shape, int ndim, int dtype, int op, void* stream);
 
 /* ---- the other collectives of the op surface ---- */
 
 /* out[r*words + w] = values[w] of rank r (host memory, blocking; words <= 4096). */
-int tips_allgather_i64(const int64_t* values, int words, int64_t* out);
+TIPS_API int tips_allgather_i64(const int64_t* values, int words, int64_t* out);
 /* Replaces BroadcastCpu (utils.h:130-134) / MPIBroadcast (ops.cc:214-286):
  * out = root's in on every rank (in == out allowed). Any root (the reference
  * only supports 0, ops.cc:219). Host or device pointers, as tips_allreduce. */
-int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root, void* stream);
+TIPS_API int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root, void* stream);
 /* Replaces AllgathervCpu (utils.h:83-128) / MPIAllgather (ops.cc:156-212):
  * out = concatenation over ranks of in, rank r contributing counts[r]
  * elements (counts[rank] must equal count). Host or device pointers. */
-int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* counts, int dtype, void* stream);
+TIPS_API int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* counts, int dtype, void* stream);
 
 /* Tensor fusion (no reference counterpart): allreduce n device
  * tensors in place, packed into buckets of at most the fusion threshold
  * (TIPS_FUSION_THRESHOLD bytes, default 64 MiB). One dtype for all. */
-int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
+TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
 
 /* Select the allreduce algorithm (enum tips_algorithm). Returns TIPS_OK or an error. */
-int tips_set_algorithm(int algo);
+TIPS_API int tips_set_algorithm(int algo);
 /* The algorithm currently selected (may be TIPS_ALGO_AUTO). */
-int tips_get_algorithm(void);
+TIPS_API int tips_get_algorithm(void);
 /* The algorithm AUTO resolves to for a given rank count. */
-int tips_resolve_algorithm(int nranks);
+TIPS_API int tips_resolve_algorithm(int nranks);
 
 /* ---- single-GPU harnesses (tests and benchmarks) ---- */
 
@@ -178,15 +184,15 @@ int tips_resolve_algorithm(int nranks);
  * device-to-device copies in the same order the RCCL ring issues them, and
  * the sums are the same tips_bucket_sum launches. Lets the ring's chunk
  * arithmetic be checked bit-exact against oracle_ring on one device. */
-int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
+TIPS_API int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
 /* The same for the direct algorithm (checked against oracle_fold, wide_acc=1). */
-int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
+TIPS_API int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
 
 /* How the simulators move a virtual rank's bytes to its peer: 0 = device
  * copies (default), 1 = ncclSend/ncclRecv pairs from this rank to itself in
  * one group per pipeline step (exercises the RCCL p2p calls on one GPU;
  * needs a single-rank setup). */
-int tips_set_sim_transport(int transport);
+TIPS_API int tips_set_sim_transport(int transport);
 
 /* Explicit variant of the 2-input sum kernel, for the gfx950 tuning sweep
  * (tools/sum_sweep.cc): mode 0 = grid-stride over `blocks` workgroups,
@@ -195,16 +201,16 @@ int tips_set_sim_transport(int transport);
  * threads = workgroup size. Non-default variants exist for f32 only
  * (others return TIPS_ERR_HIP). tips_bucket_sum uses the default chosen
  * from that sweep. */
-int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
+TIPS_API int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
                      int blocks, int threads, void* stream);
 
 /* Pipeline shape the ring/direct schedules use for a bucket: depth = K
  * sub-chunks per chunk, sub_elems = elements in a (first) sub-chunk, i.e. the
  * size of one reduce-kernel launch (TIPS_PIPELINE_DEPTH, TIPS_MIN_SUBCHUNK_BYTES). */
-int tips_schedule_shape(int64_t count, int p, int dtype, int* depth, int64_t* sub_elems);
+TIPS_API int tips_schedule_shape(int64_t count, int p, int dtype, int* depth, int64_t* sub_elems);
 
 /* Chunk partition the ring uses (element offsets), for tests. */
-int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end);
+TIPS_API int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end);
 
 #ifdef __cplusplus
 }

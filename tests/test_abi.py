@@ -225,3 +225,16 @@ def test_schedule_shape(count, p, monkeypatch):
     k = max(1, min(4, -(-chunk * 4 // (8 << 20))))
     assert d.value == k
     assert sub.value == min(chunk, -(-(-(-chunk // k)) // align) * align)
+
+
+def test_only_the_c_abi_is_exported():
+    """libtips_hip.so is built with -fvisibility=hidden: its dynamic symbol table holds exactly the
+    functions include/tips_hip.h declares (internal runtime symbols stay private)."""
+    import shutil
+    import subprocess
+    if not shutil.which("nm"):
+        pytest.skip("no nm")
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(REPO, "tips_amd", "lib", "libtips_hip.so")],
+                         capture_output=True, text=True, check=True).stdout
+    text_syms = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert text_syms == set(header_functions())

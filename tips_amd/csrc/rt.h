@@ -1,0 +1,198 @@
+// rt.h — internal state and helpers shared by the runtime's translation units
+// (runtime.cc: lifecycle + data-path C-ABI; schedules.cc: ring / direct /
+// simulators; fusion.cc; host_staging.cc; control.cc). Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/tips_hip.h"
+#include "kernels.h"
+
+namespace tips {
+namespace rt {
+
+using tips::CopyTile;
+
+constexpr int64_t kAlignBytes = 256;  // chunk / bucket-slot alignment (dwordx4 + 128-B lines)
+
+// Records the calling thread's last error (tips_last_error) and returns `code`.
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+const std::string& last_error();
+
+#define HIP_TRY(expr)                                                                                  \
+  do {                                                                                                 \
+    hipError_t e_ = (expr);                                                                            \
+    if (e_ != hipSuccess) return fail(TIPS_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));    \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                                 \
+  do {                                                                                                 \
+    ncclResult_t r_ = (expr);                                                                          \
+    if (r_ != ncclSuccess) return fail(TIPS_ERR_RCCL, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
+  } while (0)
+
+#define TRY(expr)            \
+  do {                       \
+    int rc_ = (expr);        \
+    if (rc_ != 0) return rc_; \
+  } while (0)
+
+int64_t env_i64(const char* name, int64_t dflt);
+int env_first_int(const char* const* names, int dflt);
+inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+inline int mod(int a, int p) { return ((a % p) + p) % p; }
+
+// ---------------------------------------------------------------------------
+// chunk / sub-chunk partition (shared by ring, direct and the simulators;
+// restated by oracle_chunk_bounds in oracle/oracle.c)
+
+struct Range {
+  int64_t b, e;
+  int64_t len() const { return e - b; }
+};
+
+inline Range chunk_of(int64_t n, int p, int64_t align, int c) {
+  int64_t per = round_up((n + p - 1) / p, align);
+  int64_t b = std::min((int64_t)c * per, n), e = std::min(b + per, n);
+  return {b, e};
+}
+
+inline Range sub_of(Range ch, int K, int64_t align, int k) {
+  int64_t per = round_up((ch.len() + K - 1) / K, align);
+  int64_t b = std::min(ch.b + (int64_t)k * per, ch.e), e = std::min(b + per, ch.e);
+  return {b, e};
+}
+
+// ---------------------------------------------------------------------------
+// device buffers that only grow, and event pools
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want, bool zero = false) {
+    if (want <= bytes) return 0;
+    if (p) {
+      hipError_t e = hipFree(p);
+      (void)e;
+      p = nullptr;
+      bytes = 0;
+    }
+    want = (size_t)round_up((int64_t)want, 1 << 20);
+    HIP_TRY(hipMalloc(&p, want));
+    if (zero) HIP_TRY(hipMemset(p, 0, want));
+    bytes = want;
+    return 0;
+  }
+  void release() {
+    if (p) {
+      hipError_t e = hipFree(p);
+      (void)e;
+    }
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+struct EventPool {
+  std::vector<hipEvent_t> ev;
+  int ensure(size_t n) {
+    while (ev.size() < n) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev.push_back(e);
+    }
+    return 0;
+  }
+  void release() {
+    for (auto e : ev) {
+      hipError_t r = hipEventDestroy(e);
+      (void)r;
+    }
+    ev.clear();
+  }
+};
+
+// fusion plan: cached per (dtype, tensor list)
+struct FusionBucket {
+  char* buf = nullptr;        // the fusion slot this bucket packs into (slot b % 2)
+  int64_t bytes = 0;          // padded bucket size
+  int ntiles = 0;
+  CopyTile* pack = nullptr;   // device descriptor arrays
+  CopyTile* unpack = nullptr;
+};
+struct FusionPlan {
+  int dtype;
+  std::vector<void*> ptrs;
+  std::vector<int64_t> counts;
+  std::vector<FusionBucket> buckets;
+  std::vector<int> unfused;  // indices allreduced in place
+};
+
+struct State {
+  std::mutex mu;
+  bool initialized = false;
+  int rank = -1, size = -1, device = -1;
+  ncclComm_t comm = nullptr;
+  hipStream_t comm_stream = nullptr, comp_stream = nullptr, io_stream = nullptr;
+  hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // host-memory pipeline (both PCIe directions)
+  EventPool pipe_ev;
+  hipStream_t fuse_stream = nullptr, bucket_stream = nullptr;  // fusion: pack/unpack || bucket allreduce
+  EventPool fuse_ev;
+  int64_t fusion_threshold = 0;  // the fusion slots' size; plans hold addresses into them
+  hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr;
+  EventPool recv_ev, sum_ev;
+  DevBuf staging, host_in, host_out, fusion, small;
+  int algo = TIPS_ALGO_AUTO;
+  int sim_transport = 0;  // simulators: 0 = device copies, 1 = RCCL send/recv to self
+  std::unordered_map<uint64_t, FusionPlan> plans;
+};
+
+State& S();
+
+int ensure_streams(State& st);
+ncclDataType_t nccl_type(int dtype);
+int pipeline_depth(int64_t chunk_bytes);
+int join(hipStream_t waiter, hipStream_t src, hipEvent_t ev);  // waiter waits for all work queued on src
+bool is_device_ptr(const void* p);
+int check_dtype(int dtype);
+int set_device(State& st);
+int resolve_algo(int algo, int p);
+int ensure_comm(State& st);
+
+// schedules.cc: device-resident allreduce, caller holds st.mu
+int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream);
+// host_staging.cc: host-resident allreduce over pipelined pieces, caller holds st.mu
+int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
+// fusion.cc
+void free_plan(FusionPlan& pl);
+
+// ---------------------------------------------------------------------------
+// host staging: the reference's ops work on host (TF CPU) tensors (ops.cc:88-90)
+
+// Runs enqueue(dev_in, dev_out, stream). Device pointers: on the caller's
+// stream, asynchronous. Host pointers: staged through HBM on the io stream and
+// synchronous on return. Caller holds st.mu.
+template <class F>
+int run_staged(State& st, const void* in, size_t in_bytes, void* out, size_t out_bytes, hipStream_t user, F&& enqueue) {
+  const bool dout = is_device_ptr(out);
+  const bool din = in_bytes == 0 ? dout : is_device_ptr(in);
+  if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "in and out must both be device or both be host memory");
+  if (dout) return enqueue(in, out, user);
+  TRY(st.host_in.ensure(std::max<size_t>(in_bytes, 1)));
+  TRY(st.host_out.ensure(std::max<size_t>(out_bytes, 1)));
+  if (in_bytes) HIP_TRY(hipMemcpyAsync(st.host_in.p, in, in_bytes, hipMemcpyHostToDevice, st.io_stream));
+  TRY(enqueue(st.host_in.p, st.host_out.p, st.io_stream));
+  if (out_bytes) HIP_TRY(hipMemcpyAsync(out, st.host_out.p, out_bytes, hipMemcpyDeviceToHost, st.io_stream));
+  HIP_TRY(hipStreamSynchronize(st.io_stream));
+  return 0;
+}
+
+}  // namespace rt
+}  // namespace tips

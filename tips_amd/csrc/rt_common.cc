@@ -1,0 +1,129 @@
+// rt_common.cc — error reporting, process state, streams and small helpers of the runtime.
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "rt.h"
+
+namespace tips {
+namespace rt {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  if (getenv("TIPS_VERBOSE")) fprintf(stderr, "[tips] error %d: %s\n", code, buf);
+  return code;
+}
+
+const std::string& last_error() { return g_last_error; }
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return strtoll(v, nullptr, 10);
+}
+
+int env_first_int(const char* const* names, int dflt) {
+  for (int i = 0; names[i]; i++) {
+    const char* v = getenv(names[i]);
+    if (v && *v) return atoi(v);
+  }
+  return dflt;
+}
+
+State& S() {
+  static State* s = new State();  // never destroyed: safe at exit
+  return *s;
+}
+
+int ensure_streams(State& st) {
+  if (!st.comm_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comm_stream, hipStreamNonBlocking));
+  if (!st.comp_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comp_stream, hipStreamNonBlocking));
+  if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
+  if (!st.h2d_stream) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream, hipStreamNonBlocking));
+  if (!st.d2h_stream) HIP_TRY(hipStreamCreateWithFlags(&st.d2h_stream, hipStreamNonBlocking));
+  if (!st.fuse_stream) HIP_TRY(hipStreamCreateWithFlags(&st.fuse_stream, hipStreamNonBlocking));
+  if (!st.bucket_stream) HIP_TRY(hipStreamCreateWithFlags(&st.bucket_stream, hipStreamNonBlocking));
+  if (!st.ev_start) HIP_TRY(hipEventCreateWithFlags(&st.ev_start, hipEventDisableTiming));
+  if (!st.ev_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
+  if (!st.ev_comp_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_done, hipEventDisableTiming));
+  return 0;
+}
+
+ncclDataType_t nccl_type(int dtype) {
+  switch (dtype) {
+    case TIPS_FLOAT32: return ncclFloat32;
+    case TIPS_FLOAT64: return ncclFloat64;
+    case TIPS_INT32: return ncclInt32;
+    case TIPS_INT64: return ncclInt64;
+    case TIPS_FLOAT16: return ncclFloat16;
+    case TIPS_BFLOAT16: return ncclBfloat16;
+    default: return ncclInt8;
+  }
+}
+
+int pipeline_depth(int64_t chunk_bytes) {
+  int64_t kmax = std::max<int64_t>(1, env_i64("TIPS_PIPELINE_DEPTH", 4));
+  int64_t min_sub = std::max<int64_t>(kAlignBytes, env_i64("TIPS_MIN_SUBCHUNK_BYTES", 8 << 20));
+  int64_t k = (chunk_bytes + min_sub - 1) / min_sub;
+  return (int)std::max<int64_t>(1, std::min(k, kmax));
+}
+
+// Join: `waiter` waits for all work queued so far on `src`.
+int join(hipStream_t waiter, hipStream_t src, hipEvent_t ev) {
+  HIP_TRY(hipEventRecord(ev, src));
+  HIP_TRY(hipStreamWaitEvent(waiter, ev, 0));
+  return 0;
+}
+
+int resolve_algo(int algo, int p) {
+  if (algo != TIPS_ALGO_AUTO) return algo;
+  const char* e = getenv("TIPS_ALGO");
+  if (e && *e) {
+    if (!strcmp(e, "ring")) return TIPS_ALGO_RING;
+    if (!strcmp(e, "direct")) return TIPS_ALGO_DIRECT;
+    if (!strcmp(e, "rccl")) return TIPS_ALGO_RCCL;
+  }
+  return p <= 2 ? TIPS_ALGO_RING : TIPS_ALGO_DIRECT;
+}
+
+int ensure_comm(State& st) {
+  if (st.comm) return 0;
+  if (st.size != 1) return fail(TIPS_ERR_NOT_INITIALIZED, "no RCCL communicator");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  NCCL_TRY(ncclCommInitRank(&st.comm, 1, id, 0));
+  return 0;
+}
+
+bool is_device_ptr(const void* p) {
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
+}
+
+int check_dtype(int dtype) {
+  if (tips::dtype_size(dtype) == 0) return fail(TIPS_ERR_INVALID_ARG, "unsupported dtype %d", dtype);
+  return 0;
+}
+
+int set_device(State& st) {
+  if (st.device >= 0) HIP_TRY(hipSetDevice(st.device));
+  return 0;
+}
+
+}  // namespace rt
+}  // namespace tips
