@@ -14,6 +14,7 @@ namespace tips {
 namespace rt {
 
 namespace {
+
 uint64_t plan_key(void* const* ptrs, const int64_t* counts, int n, int dtype) {
   uint64_t h = 1469598103934665603ull ^ (uint64_t)dtype;
   auto mix = [&](uint64_t v) {
