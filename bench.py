@@ -35,7 +35,7 @@ XGMI_LINK_GBPS = 153.0   # per link per direction (task / SURVEY §8d)
 GIB = float(1 << 30)
 # the exact instantiation tips_bucket_sum launches for f32 (kernels.hip kDef*): PMC traffic is only
 # reported from a profile of this kernel
-DEFAULT_SUM_KERNEL = "sum2_buf_kernel<0, 2, 16>"
+DEFAULT_SUM_KERNEL = "sum2_buf_kernel<0, 2, 16, 1, 256>"
 
 
 def parse():

@@ -15,6 +15,8 @@ namespace rt {
 
 namespace {
 
+constexpr int64_t kDefaultCopyTile = 8 * 1024;  // tools/fusion_tile_sweep.sh: 8 KiB beat 16-64 KiB
+
 uint64_t plan_key(void* const* ptrs, const int64_t* counts, int n, int dtype) {
   uint64_t h = 1469598103934665603ull ^ (uint64_t)dtype;
   auto mix = [&](uint64_t v) {
@@ -42,6 +44,9 @@ void free_plan(FusionPlan& pl) {
 namespace {
 
 int build_plan(State& st, FusionPlan& pl, int64_t threshold) {
+  // pack/unpack work unit (one workgroup each); TIPS_COPY_TILE_BYTES for tuning
+  const int64_t tile_bytes = std::min<int64_t>(
+      tips::kCopyTileBytes, round_up(std::max<int64_t>(4096, env_i64("TIPS_COPY_TILE_BYTES", kDefaultCopyTile)), 4096));
   const int64_t es = tips::dtype_size(pl.dtype);
   const int n = (int)pl.ptrs.size();
   std::vector<std::vector<CopyTile>> packs(1), unpacks(1);
@@ -61,8 +66,8 @@ int build_plan(State& st, FusionPlan& pl, int64_t threshold) {
       off = 0;
     }
     char* base = (char*)pl.ptrs[i];
-    for (int64_t t = 0; t < bytes; t += tips::kCopyTileBytes) {
-      const int64_t tb = std::min(tips::kCopyTileBytes, bytes - t);
+    for (int64_t t = 0; t < bytes; t += tile_bytes) {
+      const int64_t tb = std::min(tile_bytes, bytes - t);
       // bucket addresses are filled in as offsets; rebased onto the fusion buffer below
       packs.back().push_back(CopyTile{base + t, (char*)(uintptr_t)(off + t), tb});
       unpacks.back().push_back(CopyTile{(const char*)(uintptr_t)(off + t), base + t, tb});
@@ -110,13 +115,15 @@ int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dt
   hipStream_t s = (hipStream_t)stream;
   const int64_t es = tips::dtype_size(dtype);
   const int64_t threshold = round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_FUSION_THRESHOLD", 64 << 20)), kAlignBytes);
-  if (threshold != st.fusion_threshold) {  // slots (re)sized: every cached plan points into the old ones
+  const int64_t tile_env = env_i64("TIPS_COPY_TILE_BYTES", 0);
+  if (threshold != st.fusion_threshold || tile_env != st.fusion_tile_env) {  // slots (re)sized: every cached plan points into the old ones
     HIP_TRY(hipDeviceSynchronize());
     for (auto& kv : st.plans) free_plan(kv.second);
     st.plans.clear();
     st.fusion.release();
     TRY(st.fusion.ensure((size_t)(2 * threshold), /*zero=*/true));
     st.fusion_threshold = threshold;
+    st.fusion_tile_env = tile_env;
   }
   const uint64_t key = plan_key(ptrs, counts, n, dtype);
   auto it = st.plans.find(key);

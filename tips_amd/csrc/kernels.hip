@@ -197,23 +197,28 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
 // written line leaves the XCD's L2 instead of occupying it — 7.46 vs 7.10 TB/s
 // on config 2, profiles/r01_sum_sweep_f.jsonl). Each workgroup's descriptors
 // cover exactly its tile, so the hardware range check drops lanes past the end.
-template <int DT, int LAUX, int SAUX>
-__global__ __launch_bounds__(256) void sum2_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
-                                                      const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
-                                                      int64_t n) {
+template <int DT, int LAUX, int SAUX, int U = 1, int BLOCK = 256>
+__global__ __launch_bounds__(BLOCK) void sum2_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
+                                                        const u32x4* __restrict__ b, int64_t nvec,
+                                                        int64_t tail_begin, int64_t n) {
+  constexpr int64_t kTile = (int64_t)BLOCK * U;
   const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t first = t * 256;
+  const int64_t first = t * kTile;
   if (first < nvec) {
-    const int rec = (int)(((nvec - first) < 256 ? (nvec - first) : 256) * 16);
+    const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
     __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)(a + first), (short)0, rec, 0x00020000);
     __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(b + first), (short)0, rec, 0x00020000);
     __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
-    const int off = threadIdx.x * 16;
-    u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, LAUX);
-    u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, LAUX);
-    __builtin_amdgcn_raw_buffer_store_b128(add16<DT>(x, y), rd, off, 0, SAUX);
+    u32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, (u * BLOCK + (int)threadIdx.x) * 16, 0, LAUX);
+#pragma unroll
+    for (int u = 0; u < U; u++) y[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, (u * BLOCK + (int)threadIdx.x) * 16, 0, LAUX);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(add16<DT>(x[u], y[u]), rd, (u * BLOCK + (int)threadIdx.x) * 16, 0, SAUX);
   }
-  if (blockIdx.x == 0 && tail_begin + threadIdx.x < n) add_elem<DT>(dst, a, b, tail_begin + threadIdx.x);
+  if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<DT>(dst, a, b, tail_begin + threadIdx.x);
 }
 
 // Unaligned fallback (any pointer not 16-B aligned): one element per lane.
@@ -431,27 +436,34 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
 #define TIPS_SUM2_CASE(M, U, NTV, L, S_, B)                      \
   if (mode == M && unroll == U && nt == NTV && threads == B) \
     return run_sum2<DT, M, U, L, S_, B>(dst, a, b, n, blocks, s);
-  if (mode == 3 && threads == 256) {  // buffer-op variants: nt = index into (load aux, store aux)
+  if (mode == 3) {  // buffer-op variants: nt = index into (load aux, store aux); unroll x threads = tile
     const int64_t ve = 16 / (int64_t)dtype_size(DT);
-    const int64_t nvec = n / ve, tiles = (nvec + 255) / 256;
-    const unsigned grid = (unsigned)std::max<int64_t>(8, (tiles + 7) / 8 * 8);
-#define TIPS_BUF_CASE(I, L, S_)                                                                              \
-  if (nt == I) {                                                                                         \
-    hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_>), dim3(grid), dim3(256), 0, s, (u32x4*)dst,             \
-                       (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);                            \
-    return hipGetLastError();                                                                            \
+    const int64_t nvec = n / ve;
+    auto grid_for = [&](int64_t tile) { return (unsigned)std::max<int64_t>(8, ((nvec + tile - 1) / tile + 7) / 8 * 8); };
+#define TIPS_BUF_CASE(I, L, S_, U, B)                                                                          \
+  if (nt == I && unroll == U && threads == B) {                                                            \
+    hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_, U, B>), dim3(grid_for((int64_t)U * B)), dim3(B), 0, s,     \
+                       (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);                 \
+    return hipGetLastError();                                                                              \
   }
-    TIPS_BUF_CASE(1, 2, 16)  // the product default: nt loads, sc1 stores
+    TIPS_BUF_CASE(1, 2, 16, 1, 256)  // the product default: nt loads, sc1 stores, 1 x 16 B per lane, 256 lanes
     if constexpr (DT == kF32) {
-      TIPS_BUF_CASE(0, 2, 0)
-      TIPS_BUF_CASE(2, 2, 17)
-      TIPS_BUF_CASE(3, 18, 0)
-      TIPS_BUF_CASE(4, 3, 0)
-      TIPS_BUF_CASE(5, 16, 0)
-      TIPS_BUF_CASE(6, 18, 16)
-      TIPS_BUF_CASE(7, 2, 2)
-      TIPS_BUF_CASE(8, 0, 16)
-      TIPS_BUF_CASE(9, 3, 17)
+      TIPS_BUF_CASE(0, 2, 0, 1, 256)
+      TIPS_BUF_CASE(2, 2, 17, 1, 256)
+      TIPS_BUF_CASE(3, 18, 0, 1, 256)
+      TIPS_BUF_CASE(4, 3, 0, 1, 256)
+      TIPS_BUF_CASE(5, 16, 0, 1, 256)
+      TIPS_BUF_CASE(6, 18, 16, 1, 256)
+      TIPS_BUF_CASE(7, 2, 2, 1, 256)
+      TIPS_BUF_CASE(8, 0, 16, 1, 256)
+      TIPS_BUF_CASE(9, 3, 17, 1, 256)
+      TIPS_BUF_CASE(1, 2, 16, 2, 256)
+      TIPS_BUF_CASE(1, 2, 16, 4, 256)
+      TIPS_BUF_CASE(1, 2, 16, 1, 512)
+      TIPS_BUF_CASE(1, 2, 16, 2, 128)
+      TIPS_BUF_CASE(1, 2, 16, 1, 1024)
+      TIPS_BUF_CASE(1, 2, 16, 1, 128)
+      TIPS_BUF_CASE(1, 2, 16, 2, 512)
     }
 #undef TIPS_BUF_CASE
     return hipErrorInvalidValue;

@@ -146,6 +146,7 @@ struct State {
   hipStream_t fuse_stream = nullptr, bucket_stream = nullptr;  // fusion: pack/unpack || bucket allreduce
   EventPool fuse_ev;
   int64_t fusion_threshold = 0;  // the fusion slots' size; plans hold addresses into them
+  int64_t fusion_tile_env = 0;   // TIPS_COPY_TILE_BYTES the cached plans were built with
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
