@@ -275,16 +275,26 @@ def all_ranks_ok(dist, ok):
     return bool(t.item())
 
 
+_RESULT = {}  # rank 0's finished result line, if the main measurement completed
+
+
 def start_watchdog(seconds, rank):
-    """A hung collective must end the run with a message, never hang the box."""
+    """A hung collective must end the run with a message, never hang the box. If the main
+    measurement already finished (only the optional comparison runs hung), its line is printed."""
     import threading
 
     def fire():
         sys.stderr.write("bench.py rank %d: watchdog fired after %d s (hung collective?)\n" % (rank, seconds))
+        line = _RESULT.get("line")
+        if _RESULT.get("printed"):  # the one JSON line is out; only teardown hung
+            os._exit(0)
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "error": "watchdog: no progress in %d s" % seconds}),
-                  flush=True)
-        os._exit(3)
+            if line is not None:
+                line = dict(line, compare_error="comparison runs did not finish within %d s" % seconds)
+            else:
+                line = {"metric": METRIC, "value": None, "error": "watchdog: no progress in %d s" % seconds}
+            print(json.dumps(line), flush=True)
+        os._exit(0 if _RESULT.get("done") else 3)
 
     t = threading.Timer(seconds, fire)
     t.daemon = True
@@ -426,7 +436,33 @@ def bench_allreduce(args):
                        "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": kbytes}
         del bufs, srcs, dst
 
-    # comparison points on the same workload: the other schedules and ncclAllReduce
+    algbw = total_elems * 4 / (ms / 1e3)  # bytes/s per rank
+    busbw = algbw * 2 * (world - 1) / world
+    links = 1 if algo == _lib.ALGO_RING else world - 1
+    line = {
+        "metric": METRIC, "value": round(world * total_elems * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % seed0,
+        "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
+                   "algorithm": inv.get(algo, str(algo)),
+                   "parallelism": "dp%d (one process per GPU, RCCL p2p over xGMI)" % world},
+        "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
+        "xgmi": {"busbw_GBps": round(busbw / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS, "links_used": links,
+                 "frac_of_links_used": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4),
+                 "frac_of_one_link": round(busbw / 1e9 / XGMI_LINK_GBPS, 4)},
+        "roofline": {"bound": "xgmi", "achieved": round(busbw / 1e9, 1), "peak": XGMI_LINK_GBPS * links,
+                     "unit": "GB/s", "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None,
+                     "note": "multi-GPU: the ring/all-pairs transfer, not the sum kernel, bounds the step"},
+        "cpu_baseline": None,
+        "reduce_kernel_roofline": kernel_roof,
+        "check": check if all_ok else "FAIL on some rank",
+    }
+    _RESULT["line"] = line if rank == 0 else None
+    _RESULT["done"] = True
+
+    # comparison points on the same workload: the other schedules and ncclAllReduce (optional; a hang
+    # here is caught by the watchdog, which then still prints the line above)
     compare = {}
     if not args.no_compare:
         kc = max(3, steps // 4)
@@ -440,32 +476,10 @@ def bench_allreduce(args):
             tc = timed(kc)
             compare[name] = round(total_elems * 4 / (tc / kc) / GIB, 2)
         _lib.call("tips_set_algorithm", algo_names[args.algo])
-
-    algbw = total_elems * 4 / (ms / 1e3)  # bytes/s per rank
-    busbw = algbw * 2 * (world - 1) / world
-    links = 1 if algo == _lib.ALGO_RING else world - 1
+    line["compare_algbw_gib_s"] = compare
     if rank == 0:
-        line = {
-            "metric": METRIC, "value": round(world * total_elems * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
-            "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % seed0,
-            "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
-                       "algorithm": inv.get(algo, str(algo)),
-                       "parallelism": "dp%d (one process per GPU, RCCL p2p over xGMI)" % world},
-            "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
-            "xgmi": {"busbw_GBps": round(busbw / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS, "links_used": links,
-                     "frac_of_links_used": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4),
-                     "frac_of_one_link": round(busbw / 1e9 / XGMI_LINK_GBPS, 4)},
-            "roofline": {"bound": "xgmi", "achieved": round(busbw / 1e9, 1), "peak": XGMI_LINK_GBPS * links,
-                         "unit": "GB/s", "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None,
-                         "note": "multi-GPU: the ring/all-pairs transfer, not the sum kernel, bounds the step"},
-            "cpu_baseline": None,
-            "reduce_kernel_roofline": kernel_roof,
-            "compare_algbw_gib_s": compare,
-            "check": check if all_ok else "FAIL on some rank",
-        }
         print(json.dumps(line), flush=True)
+    _RESULT["printed"] = True  # the watchdog must not print a second line
     dist.barrier()
     wd.cancel()
     tips_amd.shutdown()

@@ -66,3 +66,27 @@ def test_workload_shapes():
     assert len(r50) == 214 and sum(r50) == 25583592
     f = bench.fused1000_sizes()
     assert len(f) == 1000 and sum(f) == 20680288 and min(f) == 257 and max(f) == 130946  # config 4
+
+
+@pytest.mark.parametrize("state,code,expect", [
+    ("done", 0, "compare_error"),     # main result finished, comparison runs hung -> the result is printed
+    ("none", 3, "watchdog: no progress"),
+    ("printed", 0, None),             # line already out, teardown hung -> no second line
+])
+def test_bench_watchdog(state, code, expect):
+    import json
+    import subprocess
+    prog = ("import sys, time\nsys.path.insert(0, %r)\nimport bench\n" % REPO)
+    if state in ("done", "printed"):
+        prog += "bench._RESULT.update(line={'metric': 'm', 'value': 1.0}, done=True)\n"
+    if state == "printed":
+        prog += "bench._RESULT['printed'] = True\n"
+    prog += "bench.start_watchdog(1, 0)\ntime.sleep(30)\n"
+    r = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True, timeout=120)
+    assert r.returncode == code
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if expect is None:
+        assert lines == []
+    else:
+        assert len(lines) == 1 and expect in lines[0]
+        json.loads(lines[0])
