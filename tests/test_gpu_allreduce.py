@@ -338,3 +338,11 @@ def test_config3_full_size_8ranks(gpu, kind):
     idx = torch.arange(0, n, 9973, device="cuda")
     ref = sum(x[idx].double() for x in ins)
     assert ((outs[0][idx].double() - ref).abs() / ref).max().item() <= 1e-6
+
+
+def test_registered_host_buffer(gpu, monkeypatch):
+    monkeypatch.setenv("TIPS_HOST_PIECE_BYTES", str(1 << 20))
+    h = np.random.default_rng(9).standard_normal(3_000_001).astype(np.float32)
+    with gpu.registered_host_buffer(h):
+        assert np.array_equal(gpu.allreduce(h), h)
+    assert np.array_equal(gpu.allreduce(h), h)

@@ -78,6 +78,8 @@ _SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_allgatherv", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_host_register", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    ("tips_host_unregister", ctypes.c_int, [ctypes.c_void_p]),
     ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),
     ("tips_get_algorithm", ctypes.c_int, []),

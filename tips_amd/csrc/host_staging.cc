@@ -85,3 +85,27 @@ int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, in
 
 }  // namespace rt
 }  // namespace tips
+
+using namespace tips::rt;
+
+extern "C" {
+
+int tips_host_register(void* ptr, int64_t bytes) {
+  if (!ptr || bytes <= 0) return fail(TIPS_ERR_INVALID_ARG, "bad host range");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  TRY(set_device(st));
+  HIP_TRY(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault));
+  return 0;
+}
+
+int tips_host_unregister(void* ptr) {
+  if (!ptr) return fail(TIPS_ERR_INVALID_ARG, "null pointer");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  TRY(set_device(st));
+  HIP_TRY(hipHostUnregister(ptr));
+  return 0;
+}
+
+}  // extern "C"

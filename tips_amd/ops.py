@@ -170,6 +170,25 @@ def bucket_sum(a, b, out=None):
     return out
 
 
+class registered_host_buffer(object):
+    """Context manager: page-lock a long-lived host (numpy / CPU torch) buffer for the
+    duration, so host-memory allreduces on it use asynchronous DMA (tips_host_register)."""
+
+    def __init__(self, array):
+        self.array = array
+
+    def __enter__(self):
+        basics.init()
+        _lib.call("tips_host_register", tensors.data_ptr(self.array),
+                  tensors.numel(self.array) * self.array.dtype.itemsize if not tensors.is_torch(self.array)
+                  else self.array.numel() * self.array.element_size())
+        return self.array
+
+    def __exit__(self, *exc):
+        _lib.call("tips_host_unregister", tensors.data_ptr(self.array))
+        return False
+
+
 def set_algorithm(algo):
     """Select 'auto', 'ring', 'direct' or 'rccl'; returns the previous selection's name."""
     names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL}
