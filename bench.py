@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--algo", default=os.environ.get("TIPS_ALGO", "auto"), choices=["auto", "ring", "direct", "rccl"])
+    ap.add_argument("--algo", default=os.environ.get("TIPS_ALGO", "auto"),
+                    choices=["auto", "ring", "direct", "rccl", "oneshot"])
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
@@ -322,10 +323,10 @@ def bench_allreduce(args):
     from tips_amd import _lib
     tips_amd.init()  # unique id through the gloo group, one RCCL communicator per GPU
     L = _lib.lib()
-    algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL}
+    algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL,
+                  "oneshot": _lib.ALGO_ONESHOT}
     inv = {v: k for k, v in algo_names.items()}
     _lib.call("tips_set_algorithm", algo_names[args.algo])
-    algo = L.tips_resolve_algorithm(world)
 
     workload = args.workload if args.workload != "auto" else "bucket"
     steps = args.steps if args.steps is not None else 20
@@ -343,6 +344,8 @@ def bench_allreduce(args):
     else:
         sizes, seed0 = resnet50_grad_sizes(), 5000
         desc = "config 5: ResNet-50 gradient set (214 tensors, 25.6 M fp32) fused into 64 MiB buckets, in place"
+    # the schedule the (largest) reduced buffer gets: the bucket itself, or a <= 64 MiB fusion bucket
+    algo = L.tips_resolve_algorithm(world, sizes[0] * 4 if workload == "bucket" else 64 << 20)
     # every tensor at a 256-B aligned offset of one flat buffer (what a caching allocator hands out)
     offs, total = [], 0
     for k in sizes:
@@ -473,7 +476,7 @@ def bench_allreduce(args):
     compare = {}
     if not args.no_compare:
         kc = max(3, steps // 4)
-        for name in ("ring", "direct", "rccl"):
+        for name in ("ring", "direct", "rccl"):  # (oneshot targets small buckets only)
             if algo_names[name] == algo:
                 continue
             _lib.call("tips_set_algorithm", algo_names[name])

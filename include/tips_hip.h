@@ -63,10 +63,12 @@ enum tips_status {
 
 /* allreduce algorithms (tips_set_algorithm). */
 enum tips_algorithm {
-  TIPS_ALGO_AUTO = -1,  /* ring for p <= 2, direct otherwise */
+  TIPS_ALGO_AUTO = -1,  /* oneshot for small buckets (<= TIPS_ONESHOT_BYTES, 256 KiB), else ring for
+                           p <= 2 and direct otherwise; TIPS_ALGO env overrides */
   TIPS_ALGO_RING = 0,   /* RCCL send/recv ring, RS + AG, sub-chunk pipelined */
   TIPS_ALGO_DIRECT = 1, /* all-pairs RS over every xGMI link + p-input sum kernel + AG */
   TIPS_ALGO_RCCL = 2,   /* ncclAllReduce, kept as a comparison point only */
+  TIPS_ALGO_ONESHOT = 3, /* whole bucket to every peer in one step + one p-input fold (small buckets) */
 };
 
 /* ---- lifecycle: same names and types as tips/core/operations.h:7-21 ---- */
@@ -181,8 +183,8 @@ TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int 
 TIPS_API int tips_set_algorithm(int algo);
 /* The algorithm currently selected (may be TIPS_ALGO_AUTO). */
 TIPS_API int tips_get_algorithm(void);
-/* The algorithm AUTO resolves to for a given rank count. */
-TIPS_API int tips_resolve_algorithm(int nranks);
+/* The algorithm the current selection resolves to for a bucket of `bytes` on `nranks`. */
+TIPS_API int tips_resolve_algorithm(int nranks, int64_t bytes);
 
 /* ---- single-GPU harnesses (tests and benchmarks) ---- */
 
@@ -192,6 +194,9 @@ TIPS_API int tips_resolve_algorithm(int nranks);
  * the sums are the same tips_bucket_sum launches. Lets the ring's chunk
  * arithmetic be checked bit-exact against oracle_ring on one device. */
 TIPS_API int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
+/* The same for the one-shot schedule (checked against oracle_fold, wide_acc=1). */
+TIPS_API int tips_oneshot_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype,
+                                   void* stream);
 /* The same for the direct algorithm (checked against oracle_fold, wide_acc=1). */
 TIPS_API int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64_t count, int dtype, void* stream);
 

@@ -76,7 +76,7 @@ def simulate(kind, ins, dtype, inplace=False, transport=0):
     outs = devs if inplace else [torch.empty_like(d) for d in devs]
     pi, _k1 = _lib.ptr_array([d.data_ptr() for d in devs])
     po, _k2 = _lib.ptr_array([o.data_ptr() for o in outs])
-    fn = "tips_ring_simulate" if kind == "ring" else "tips_direct_simulate"
+    fn = {"ring": "tips_ring_simulate", "direct": "tips_direct_simulate", "oneshot": "tips_oneshot_simulate"}[kind]
     try:
         _lib.call(fn, po, pi, len(ins), ins[0].size, dtype, stream())
         torch.cuda.synchronize()

@@ -74,10 +74,15 @@ def test_algorithm_resolution():
     L = _lib.lib()
     prev = L.tips_get_algorithm()
     assert L.tips_set_algorithm(_lib.ALGO_AUTO) == 0 and L.tips_get_algorithm() == _lib.ALGO_AUTO
-    assert L.tips_resolve_algorithm(2) == _lib.ALGO_RING
-    assert L.tips_resolve_algorithm(8) == _lib.ALGO_DIRECT
+    big, small = 1 << 30, 64 << 10
+    assert L.tips_resolve_algorithm(2, big) == _lib.ALGO_RING
+    assert L.tips_resolve_algorithm(8, big) == _lib.ALGO_DIRECT
+    assert L.tips_resolve_algorithm(8, small) == _lib.ALGO_ONESHOT
+    assert L.tips_resolve_algorithm(2, small) == _lib.ALGO_ONESHOT
+    assert L.tips_resolve_algorithm(32, small) == _lib.ALGO_RING  # more ranks than the fold takes sources
     L.tips_set_algorithm(_lib.ALGO_RING)
-    assert L.tips_resolve_algorithm(8) == _lib.ALGO_RING
+    assert L.tips_resolve_algorithm(8, small) == _lib.ALGO_RING
+    assert L.tips_set_algorithm(4) == -1
     L.tips_set_algorithm(prev)
 
 

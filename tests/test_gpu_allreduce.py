@@ -40,6 +40,18 @@ def test_direct_schedule_matches_oracle(gpu, oracle, dtype, p, n):
         assert same_bits(got, exp, dtype)
 
 
+@pytest.mark.parametrize("dtype", ALL_DTYPES)
+@pytest.mark.parametrize("p", [2, 3, 8, 16])
+@pytest.mark.parametrize("n", [1, 4099, 262147])
+@pytest.mark.parametrize("transport", [0, 1])
+def test_oneshot_schedule_matches_oracle(gpu, oracle, dtype, p, n, transport):
+    rng = np.random.default_rng(3000 * p + n % 983 + dtype)
+    ins = [rand(dtype, n, rng) for _ in range(p)]
+    exp = oracle.fold(ins, code=dtype, wide_acc=True)
+    for got in simulate("oneshot", ins, dtype, transport=transport):
+        assert same_bits(got, exp, dtype)
+
+
 @pytest.mark.parametrize("kind", ["ring", "direct"])
 @pytest.mark.parametrize("dtype", [F32, I64, F16])
 def test_pipelined_subchunks_inplace(gpu, oracle, monkeypatch, kind, dtype):
@@ -71,7 +83,7 @@ CASES = golden_cases()
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
-@pytest.mark.parametrize("kind", ["ring", "direct"])
+@pytest.mark.parametrize("kind", ["ring", "direct", "oneshot"])
 def test_golden_vectors(gpu, name, kind):
     ins, exp = load_golden(name)
     dtype = {"f32": F32, "f64": F64, "i32": I32, "i64": I64}[CASES[name]["dtype"]]
@@ -282,8 +294,8 @@ FUZZ = [np.random.default_rng(20261015 + i) for i in range(40)]
 def test_schedule_fuzz(gpu, oracle, monkeypatch, case):
     """Random (schedule, p, n, dtype, in-place, transport, pipeline depth/sub-chunk) vs the oracle, bit-exact."""
     r = FUZZ[case]
-    kind = ["ring", "direct"][int(r.integers(2))]
-    p = int(r.integers(2, 17 if kind == "direct" else 13))
+    kind = ["ring", "direct", "oneshot"][int(r.integers(3))]
+    p = int(r.integers(2, 13 if kind == "ring" else 17))
     n = int(r.choice([0, 1, 2, 63, 64, 65, 255, 4096, int(r.integers(1, 300000))]))
     dtype = int(r.choice(ALL_DTYPES))
     inplace = bool(r.integers(2))

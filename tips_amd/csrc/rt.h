@@ -164,7 +164,7 @@ int join(hipStream_t waiter, hipStream_t src, hipEvent_t ev);  // waiter waits f
 bool is_device_ptr(const void* p);
 int check_dtype(int dtype);
 int set_device(State& st);
-int resolve_algo(int algo, int p);
+int resolve_algo(int algo, int p, int64_t bytes);
 int ensure_comm(State& st);
 
 // schedules.cc: device-resident allreduce, caller holds st.mu

@@ -85,15 +85,21 @@ int join(hipStream_t waiter, hipStream_t src, hipEvent_t ev) {
   return 0;
 }
 
-int resolve_algo(int algo, int p) {
-  if (algo != TIPS_ALGO_AUTO) return algo;
-  const char* e = getenv("TIPS_ALGO");
-  if (e && *e) {
-    if (!strcmp(e, "ring")) return TIPS_ALGO_RING;
-    if (!strcmp(e, "direct")) return TIPS_ALGO_DIRECT;
-    if (!strcmp(e, "rccl")) return TIPS_ALGO_RCCL;
+int resolve_algo(int algo, int p, int64_t bytes) {
+  if (algo == TIPS_ALGO_AUTO) {
+    const char* e = getenv("TIPS_ALGO");
+    if (e && *e) {
+      if (!strcmp(e, "ring")) algo = TIPS_ALGO_RING;
+      if (!strcmp(e, "direct")) algo = TIPS_ALGO_DIRECT;
+      if (!strcmp(e, "rccl")) algo = TIPS_ALGO_RCCL;
+      if (!strcmp(e, "oneshot")) algo = TIPS_ALGO_ONESHOT;
+    }
   }
-  return p <= 2 ? TIPS_ALGO_RING : TIPS_ALGO_DIRECT;
+  if (algo != TIPS_ALGO_AUTO) return algo;
+  // small buckets: one exchange + one kernel beats 2(p-1) pipelined steps (latency-bound);
+  // large: ring on one link pair (p <= 2), all-pairs over every xGMI link otherwise
+  if (p > 1 && p <= tips::kMaxSrcs && bytes <= env_i64("TIPS_ONESHOT_BYTES", 256 << 10)) return TIPS_ALGO_ONESHOT;
+  return (p <= 2 || p > tips::kMaxSrcs) ? TIPS_ALGO_RING : TIPS_ALGO_DIRECT;
 }
 
 int ensure_comm(State& st) {

@@ -144,7 +144,7 @@ int tips_size(void) { return S().initialized ? S().size : -1; }
 int tips_rank(void) { return S().initialized ? S().rank : -1; }
 
 int tips_set_algorithm(int algo) {
-  if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_RCCL) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
+  if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_ONESHOT) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   st.algo = algo;
@@ -161,7 +161,7 @@ int tips_set_sim_transport(int transport) {
   return 0;
 }
 
-int tips_resolve_algorithm(int nranks) { return resolve_algo(S().algo, nranks); }
+int tips_resolve_algorithm(int nranks, int64_t bytes) { return resolve_algo(S().algo, nranks, bytes); }
 
 int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int dtype, void* stream) {
   TRY(check_dtype(dtype));

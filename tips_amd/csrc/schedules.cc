@@ -132,13 +132,38 @@ int direct_allreduce(State& st, const char* in, char* out, int64_t n, int dtype,
   return 0;
 }
 
+// One-shot (small buckets): every rank sends its whole bucket to
+// every peer in one grouped step (all xGMI links at once) and folds the p
+// buckets locally in rank order with one multi_sum launch. (p-1)·S bytes per
+// rank instead of 2(p-1)/p·S, but 1 exchange + 1 kernel instead of 2(p-1)
+// pipelined steps: latency-optimal. Same bits as direct (rank-order fold).
+int oneshot_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
+  const int p = st.size, r = st.rank;
+  const int64_t bytes = n * tips::dtype_size(dtype);
+  TRY(st.staging.ensure((size_t)((p - 1) * bytes)));
+  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * bytes; };
+  TRY(join(st.comm_stream, user, st.ev_start));
+  NCCL_TRY(ncclGroupStart());
+  for (int d = 1; d < p; d++) {
+    const int to = mod(r + d, p), from = mod(r - d, p);
+    NCCL_TRY(ncclSend(in, (size_t)bytes, ncclInt8, to, st.comm, st.comm_stream));
+    NCCL_TRY(ncclRecv(slot(from), (size_t)bytes, ncclInt8, from, st.comm, st.comm_stream));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  TRY(join(user, st.comm_stream, st.ev_done));  // the fold runs on the caller's stream
+  const void* srcs[tips::kMaxSrcs];
+  for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)in : slot(j);
+  HIP_TRY(tips::launch_multi_sum(out, srcs, p, n, dtype, user));
+  return 0;
+}
+
 }  // namespace
 
 // device-resident allreduce, caller holds st.mu
 int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream) {
   if (n == 0) return 0;
   const int64_t es = tips::dtype_size(dtype);
-  const int algo = resolve_algo(st.algo, st.size);
+  const int algo = resolve_algo(st.algo, st.size, n * es);
   if (algo == TIPS_ALGO_RCCL) {
     TRY(ensure_comm(st));
     NCCL_TRY(ncclAllReduce(in, out, (size_t)n, nccl_type(dtype), ncclSum, st.comm, stream));
@@ -148,8 +173,9 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
     if (in != out) HIP_TRY(hipMemcpyAsync(out, in, (size_t)(n * es), hipMemcpyDeviceToDevice, stream));
     return 0;
   }
-  if (st.size > tips::kMaxSrcs && algo == TIPS_ALGO_DIRECT)
+  if (st.size > tips::kMaxSrcs && (algo == TIPS_ALGO_DIRECT || algo == TIPS_ALGO_ONESHOT))
     return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
+  if (algo == TIPS_ALGO_ONESHOT) return oneshot_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
   if (algo == TIPS_ALGO_DIRECT) return direct_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
   return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
 }
@@ -341,6 +367,37 @@ int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64
   }
   TRY(join(user, st.comm_stream, st.ev_done));
   TRY(join(user, st.comp_stream, st.ev_comp_done));
+  return 0;
+}
+
+int tips_oneshot_simulate(void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  if (p < 1 || p > tips::kMaxSrcs || n < 0 || !outs || !ins) return fail(TIPS_ERR_INVALID_ARG, "bad simulate args");
+  if (n == 0) return 0;
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  TRY(sim_prepare(st));
+  SimXfer xf(st);
+  hipStream_t user = (hipStream_t)stream;
+  const int64_t bytes = n * tips::dtype_size(dtype);
+  if (p == 1) {
+    if (outs[0] != ins[0]) HIP_TRY(hipMemcpyAsync(outs[0], ins[0], (size_t)bytes, hipMemcpyDeviceToDevice, user));
+    return 0;
+  }
+  // staging[r][j]: rank j's bucket as received by virtual rank r
+  TRY(st.staging.ensure((size_t)((int64_t)p * p * bytes)));
+  auto slot = [&](int r, int j) { return (char*)st.staging.p + ((int64_t)r * p + j) * bytes; };
+  TRY(join(st.comm_stream, user, st.ev_start));
+  for (int r = 0; r < p; r++)
+    for (int j = 0; j < p; j++)
+      if (j != r) xf.add(slot(r, j), ins[j], bytes);
+  TRY(xf.flush());
+  TRY(join(user, st.comm_stream, st.ev_done));
+  for (int r = 0; r < p; r++) {
+    const void* srcs[tips::kMaxSrcs];
+    for (int j = 0; j < p; j++) srcs[j] = (j == r) ? ins[r] : (const void*)slot(r, j);
+    HIP_TRY(tips::launch_multi_sum(outs[r], srcs, p, n, dtype, user));
+  }
   return 0;
 }
 
