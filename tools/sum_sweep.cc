@@ -133,6 +133,26 @@ int main(int argc, char** argv) {
       v.ms.push_back(ms / iters);
     }
   }
+  // the shipped kernel for every dtype on the same 256 MiB buffers (bytes moved are dtype-independent)
+  const char* dnames[] = {"f32", "f64", "i32", "i64", "f16", "bf16"};
+  for (int dt = 0; dt < 6; dt++) {
+    const int64_t cnt = (int64_t)bytes / (dt == 1 || dt == 3 ? 8 : dt >= 4 ? 2 : 4);
+    std::vector<double> ms;
+    for (int r = 0; r < rounds; r++) {
+      (void)tips_bucket_sum(c, a, b, cnt, dt, s);
+      CHECK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; i++) (void)tips_bucket_sum(c, a, b, cnt, dt, s);
+      CHECK(hipEventRecord(e1, s));
+      CHECK(hipEventSynchronize(e1));
+      float t = 0;
+      CHECK(hipEventElapsedTime(&t, e0, e1));
+      ms.push_back(t / iters);
+    }
+    std::sort(ms.begin(), ms.end());
+    printf("{\"variant\": \"default_%s\", \"median_us\": %.2f, \"min_us\": %.2f, \"GBps_median\": %.1f, \"GBps_best\": %.1f}\n",
+           dnames[dt], ms[ms.size() / 2] * 1e3, ms[0] * 1e3, 3.0 * bytes / (ms[ms.size() / 2] * 1e-3) / 1e9,
+           3.0 * bytes / (ms[0] * 1e-3) / 1e9);
+  }
   for (auto& v : vs) {
     std::sort(v.ms.begin(), v.ms.end());
     const double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
