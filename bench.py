@@ -512,7 +512,14 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29512")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        return bench_allreduce(args)
+        try:
+            return bench_allreduce(args)
+        except Exception as e:  # one diagnosable line instead of a bare traceback
+            if int(os.environ.get("RANK", "0")) == 0 and not _RESULT.get("printed"):
+                line = _RESULT.get("line") or {"metric": METRIC, "value": None, "unit": "GiB/s",
+                                               "n_gpus": world}
+                print(json.dumps(dict(line, error="%s: %s" % (type(e).__name__, e))), flush=True)
+            raise
     return bench_sum(args)
 
 
