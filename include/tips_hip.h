@@ -179,6 +179,30 @@ TIPS_API int tips_host_unregister(void* ptr);
  * (TIPS_FUSION_THRESHOLD bytes, default 64 MiB). One dtype for all. */
 TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
 
+/* ---- named, asynchronous allreduce with cross-rank negotiation ---- */
+
+/* Replaces EnqueueTensorCollective + the coordinator's background loop
+ * (coordinator.cc:223-241, 355-513): requests may be enqueued in any order on
+ * different ranks. A background thread per rank agrees with rank 0 (TCP,
+ * MASTER_ADDR:TIPS_NEGOTIATION_PORT, default MASTER_PORT + 19) which names
+ * every rank has enqueued, validates them with ConstructResponseMessage's
+ * rules and error text, and every rank reduces them in rank 0's
+ * first-announcement order, on the stream passed here. Device pointers only.
+ * Returns a handle > 0, or a negative status. The first call starts the
+ * thread (collective); tips_shutdown stops it (collective). */
+TIPS_API int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype,
+                                        void* stream);
+/* 1 = done (handle released), 0 = pending, < 0 = error (message in tips_last_error). */
+TIPS_API int tips_poll(int64_t handle);
+/* Blocks until the request is reduced (TIPS_OK, handle released) or failed (< 0). */
+TIPS_API int tips_wait(int64_t handle);
+/* The negotiation protocol with an executor that only logs (no GPU): each
+ * rank enqueues the newline-separated "name dtype count" lines of `requests`
+ * ("@sleep ms" pauses), stops, and writes its execution log ("name OK" /
+ * "name ERR message", one per line, in execution order) into out. For tests. */
+TIPS_API int tips_negotiation_selftest(int rank, int size, const char* host, int port, const char* requests,
+                                       char* out, int64_t cap);
+
 /* Select the allreduce algorithm (enum tips_algorithm). Returns TIPS_OK or an error. */
 TIPS_API int tips_set_algorithm(int algo);
 /* The algorithm currently selected (may be TIPS_ALGO_AUTO). */

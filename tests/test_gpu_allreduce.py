@@ -358,3 +358,20 @@ def test_registered_host_buffer(gpu, monkeypatch):
     with gpu.registered_host_buffer(h):
         assert np.array_equal(gpu.allreduce(h), h)
     assert np.array_equal(gpu.allreduce(h), h)
+
+
+def test_named_async_allreduce_single_rank(gpu):
+    """The negotiated path (tips_enqueue_allreduce / tips_wait) end to end on one rank."""
+    import torch
+    ts = [torch.randn(1000 + 37 * i, device="cuda") for i in range(10)]
+    hs = [gpu.allreduce_async(t, "grad.%d" % i) for i, t in enumerate(ts)]
+    for h, t in zip(hs, ts):
+        assert torch.equal(gpu.synchronize(h), t)
+    h = gpu.allreduce_async(ts[0], "dup")
+    with pytest.raises(gpu.TipsError):
+        gpu.allreduce_async(ts[1], "dup")  # same name while pending
+    assert torch.equal(gpu.synchronize(h), ts[0])
+    while not gpu.poll(gpu.allreduce_async(ts[2], "polled")):
+        pass
+    with pytest.raises(ValueError):
+        gpu.allreduce_async(torch.zeros(3), "host")

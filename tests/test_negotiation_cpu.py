@@ -1,0 +1,89 @@
+"""The negotiation protocol (negotiate.cc; the reference's coordinator, coordinator.cc:15-513) across
+real processes on the CPU, with the dry-run executor: ranks enqueue named requests in DIFFERENT orders
+and at different times; every rank must execute the same names in the same order (rank 0's
+first-announcement order), mismatches must fail on every rank with the reference's error text, and names
+missing on some rank must fail at shutdown."""
+import multiprocessing as mp
+import socket
+
+import pytest
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, size, port, requests, q):
+    import ctypes
+    from tips_amd import _lib
+    L = _lib.lib()
+    out = ctypes.create_string_buffer(1 << 16)
+    rc = L.tips_negotiation_selftest(rank, size, b"127.0.0.1", port, requests.encode(), out, len(out))
+    q.put((rank, rc, out.value.decode(), L.tips_last_error().decode()))
+
+
+def run(per_rank):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    size = len(per_rank)
+    procs = [ctx.Process(target=_worker, args=(r, size, port, per_rank[r], q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+    return res
+
+
+def lines(log):
+    return [l for l in log.splitlines() if l]
+
+
+def test_same_order_everywhere_despite_different_enqueue_orders():
+    names = ["grad_%d" % i for i in range(40)]
+    reqs = []
+    for r in range(4):
+        order = names[r:] + names[:r] if r % 2 == 0 else list(reversed(names))
+        body = []
+        for i, n in enumerate(order):
+            body.append("%s 0 %d" % (n, 100 + names.index(n)))
+            if i % 7 == r:
+                body.append("@sleep 3")
+        reqs.append("\n".join(body))
+    res = run(reqs)
+    logs = [lines(log) for _, rc, log, _ in res]
+    for rank, rc, log, err in res:
+        assert rc == 0, err
+    assert all(l == logs[0] for l in logs)
+    assert sorted(logs[0]) == sorted(n + " OK" for n in names)
+
+
+def test_mismatch_fails_everywhere_with_reference_text():
+    reqs = ["a 0 8\nb 0 8\nc 0 8", "c 0 8\nb 1 8\na 0 9"]  # b: dtype mismatch; a: shape mismatch
+    res = run(reqs)
+    logs = [lines(log) for _, _, log, _ in res]
+    assert logs[0] == logs[1]
+    got = dict(l.split(" ", 1) for l in logs[0])
+    assert got["c"] == "OK"
+    assert got["b"] == "ERR Mismatch data types found: 0 vs 1."
+    assert got["a"] == "ERR Mismatched allreduce tensor shapes: [8] vs [9]"
+
+
+def test_missing_on_one_rank_fails_at_shutdown():
+    res = run(["x 0 4\nonly0 0 4", "x 0 4"])
+    for _, rc, log, _ in res:
+        assert rc == 0
+    l0 = dict(l.split(" ", 1) for l in lines(res[0][2]))
+    assert l0["x"] == "OK"
+    assert l0["only0"].startswith("ERR request only0 was not enqueued on every rank")
+    assert lines(res[1][2]) == ["x OK"]
+
+
+def test_single_rank_and_duplicate_names():
+    res = run(["a 3 5\nb 3 5"])
+    assert lines(res[0][2]) == ["a OK", "b OK"]

@@ -81,6 +81,12 @@ _SIGNATURES = [
     ("tips_host_register", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("tips_host_unregister", ctypes.c_int, [ctypes.c_void_p]),
     ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_enqueue_allreduce", ctypes.c_int64,
+     [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_poll", ctypes.c_int, [ctypes.c_int64]),
+    ("tips_wait", ctypes.c_int, [ctypes.c_int64]),
+    ("tips_negotiation_selftest", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),
     ("tips_get_algorithm", ctypes.c_int, []),
     ("tips_resolve_algorithm", ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),

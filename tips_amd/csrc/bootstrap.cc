@@ -6,15 +6,7 @@
 // GPU the only thing ranks must agree on before RCCL exists is the 128-byte
 // ncclUniqueId. Rank 0 listens, every other rank connects (retrying until a
 // deadline), says who it is, and receives the id.
-#include <arpa/inet.h>
-#include <errno.h>
-#include <netdb.h>
-#include <netinet/in.h>
-#include <netinet/tcp.h>
-#include <poll.h>
-#include <string.h>
-#include <sys/socket.h>
-#include <unistd.h>
+#include "net.h"
 
 #include <chrono>
 #include <string>
@@ -23,51 +15,8 @@
 
 namespace tips {
 
-namespace {
+using namespace net;
 
-bool send_all(int fd, const void* buf, size_t n) {
-  const char* p = static_cast<const char*>(buf);
-  while (n > 0) {
-    ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
-    if (k < 0 && errno == EINTR) continue;
-    if (k <= 0) return false;
-    p += k;
-    n -= (size_t)k;
-  }
-  return true;
-}
-
-bool recv_all(int fd, void* buf, size_t n, int timeout_ms) {
-  char* p = static_cast<char*>(buf);
-  while (n > 0) {
-    pollfd pfd{fd, POLLIN, 0};
-    int pr = ::poll(&pfd, 1, timeout_ms);
-    if (pr < 0 && errno == EINTR) continue;
-    if (pr <= 0) return false;
-    ssize_t k = ::recv(fd, p, n, 0);
-    if (k < 0 && errno == EINTR) continue;
-    if (k <= 0) return false;
-    p += k;
-    n -= (size_t)k;
-  }
-  return true;
-}
-
-bool resolve(const char* host, int port, sockaddr_in* out) {
-  memset(out, 0, sizeof *out);
-  out->sin_family = AF_INET;
-  out->sin_port = htons((uint16_t)port);
-  if (inet_pton(AF_INET, host, &out->sin_addr) == 1) return true;
-  addrinfo hints{}, *res = nullptr;
-  hints.ai_family = AF_INET;
-  hints.ai_socktype = SOCK_STREAM;
-  if (getaddrinfo(host, nullptr, &hints, &res) != 0 || !res) return false;
-  out->sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
-  freeaddrinfo(res);
-  return true;
-}
-
-}  // namespace
 
 // Returns 0 on success; on failure fills *err and returns -1.
 int bootstrap_exchange(int rank, int size, const char* host, int port, void* id, int id_bytes, int timeout_s,

@@ -30,6 +30,8 @@ int exchange_i64(State& st, const int64_t* mine, int words, std::vector<int64_t>
   return 0;
 }
 
+}  // namespace
+
 std::string shape_str(const int64_t* rec) {  // tensorflow::TensorShape::DebugString() form: [2,4]
   std::string s = "[";
   for (int64_t d = 0; d < rec[2]; d++) s += (d ? "," : "") + std::to_string(rec[3 + d]);
@@ -76,7 +78,6 @@ int check_records(const int64_t* t, int p) {
   return 0;
 }
 
-}  // namespace
 }  // namespace rt
 }  // namespace tips
 

@@ -1,0 +1,564 @@
+// negotiate.cc — asynchronous, named allreduce requests with cross-rank negotiation.
+//
+// Replaces the reference's coordinator (tips/core/collective/coordinator.cc):
+//   EnqueueTensorCollective (:223-241)  -> tips_enqueue_allreduce
+//   BackgroundThreadLoop (:355-513)     -> Negotiator::loop
+//   IncreTensorCount (:15-38)           -> Table::announce (per-name ready count)
+//   ConstructResponseMessage (:90-186)  -> check_records (control.cc), same error text
+//   PerformCollectiveOp (:243-353)      -> execute(): allreduce_device on the request's stream
+// TF runs ops in different orders on different ranks, so every rank must agree
+// on WHICH named tensors are ready everywhere and in WHAT order to reduce them.
+// Here one background thread per rank runs cycles in lockstep with rank 0 over
+// one persistent TCP connection (the reference: a ZeroMQ PUSH/PULL RPC with
+// flatbuffers, naive_rpc.cc): each cycle every rank sends the requests it has
+// newly enqueued; rank 0 records them in first-announcement order, validates
+// every name all ranks have announced, and answers with the list to run; every
+// rank then reduces that list in that order on the owning request's stream.
+// Only control records travel here; tensor bytes go over RCCL / xGMI.
+//
+// Dry-run mode (tips_negotiation_selftest) runs the same protocol with an
+// executor that only logs the order, so it is testable across processes on a
+// host without a GPU.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <thread>
+
+#include "net.h"
+#include "rt.h"
+
+namespace tips {
+namespace rt {
+namespace {
+
+using namespace tips::net;
+
+struct Req {
+  int64_t handle = 0;
+  std::string name;
+  const void* in = nullptr;
+  void* out = nullptr;
+  int64_t count = 0;
+  int dtype = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;
+  int state = 0;  // 0 queued, 1 announced, 2 launched (ev recorded), 3 done (dry run), -1 error
+  std::string err;
+};
+
+// ---- wire format: flat little-endian records ----------------------------------
+struct Writer {
+  std::string b;
+  template <class T>
+  void put(T v) {
+    b.append(reinterpret_cast<const char*>(&v), sizeof v);
+  }
+  void str(const std::string& s) {
+    put<uint32_t>((uint32_t)s.size());
+    b += s;
+  }
+};
+
+struct Reader {
+  const std::string& b;
+  size_t off = 0;
+  bool ok = true;
+  explicit Reader(const std::string& s) : b(s) {}
+  template <class T>
+  T get() {
+    T v{};
+    if (off + sizeof v > b.size()) {
+      ok = false;
+      return v;
+    }
+    memcpy(&v, b.data() + off, sizeof v);
+    off += sizeof v;
+    return v;
+  }
+  std::string str() {
+    const uint32_t n = get<uint32_t>();
+    if (!ok || off + n > b.size()) {
+      ok = false;
+      return std::string();
+    }
+    std::string s = b.substr(off, n);
+    off += n;
+    return s;
+  }
+};
+
+// announce (rank -> rank 0): u8 shutdown, u32 n, n x {i32 dtype, i64 count, str name}
+// response (rank 0 -> all):  u8 shutdown, u32 n, n x {u8 ok, str name, str error}
+struct Announce {
+  int dtype;
+  int64_t count;
+  std::string name;
+};
+
+struct Decision {
+  bool ok;
+  std::string name, err;
+};
+
+// ---- rank 0's table (IncreTensorCount + ConstructResponseMessage) ---------------
+struct Table {
+  struct Row {
+    std::vector<int64_t> rec;  // p records of TIPS_REQUEST_WORDS
+    std::vector<char> seen;
+    int nseen = 0;
+    std::string dup;  // set when a rank announced this name twice while unresolved
+  };
+  int p = 1;
+  std::unordered_map<std::string, Row> rows;
+  std::deque<std::string> arrival;  // first-announcement order
+
+  void announce(int rank, const Announce& a) {
+    auto it = rows.find(a.name);
+    if (it == rows.end()) {
+      Row r;
+      r.rec.assign((size_t)p * TIPS_REQUEST_WORDS, 0);
+      r.seen.assign(p, 0);
+      it = rows.emplace(a.name, std::move(r)).first;
+      arrival.push_back(a.name);
+    }
+    Row& r = it->second;
+    if (r.seen[rank]) {
+      r.dup = "rank " + std::to_string(rank) + " enqueued " + a.name + " twice";
+      return;
+    }
+    r.seen[rank] = 1;
+    r.nseen++;
+    int64_t* rec = &r.rec[(size_t)rank * TIPS_REQUEST_WORDS];
+    rec[0] = TIPS_REQ_ALLREDUCE;
+    rec[1] = a.dtype;
+    rec[2] = 1;  // the C-ABI carries element counts: shape [count]
+    rec[3] = a.count;
+  }
+
+  // names every rank has announced, in first-announcement order, with their verdicts
+  std::vector<Decision> ready() {
+    std::vector<Decision> out;
+    std::deque<std::string> rest;
+    for (auto& name : arrival) {
+      Row& r = rows[name];
+      if (!r.dup.empty()) {
+        out.push_back({false, name, r.dup});
+        rows.erase(name);
+        continue;
+      }
+      if (r.nseen < p) {
+        rest.push_back(name);
+        continue;
+      }
+      const int rc = check_records(r.rec.data(), p);
+      out.push_back({rc == 0, name, rc == 0 ? std::string() : last_error()});
+      rows.erase(name);
+    }
+    arrival.swap(rest);
+    return out;
+  }
+};
+
+class Negotiator {
+ public:
+  int start(int rank, int size, const char* host, int port, bool dry_run, int timeout_s) {
+    rank_ = rank;
+    size_ = size;
+    dry_ = dry_run;
+    timeout_ms_ = timeout_s * 1000;
+    table_.p = size;
+    std::string err;
+    if (size > 1) {
+      if (rank == 0) {
+        lfd_ = listen_on(port, size, &err);
+        if (lfd_ < 0) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: %s", err.c_str());
+        peers_.assign(size, -1);
+        for (int joined = 0; joined < size - 1;) {
+          pollfd pfd{lfd_, POLLIN, 0};
+          if (::poll(&pfd, 1, timeout_ms_) <= 0) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: ranks did not connect");
+          int c = ::accept(lfd_, nullptr, nullptr);
+          if (c < 0) continue;
+          int32_t peer = -1;
+          if (!recv_all(c, &peer, sizeof peer, timeout_ms_) || peer <= 0 || peer >= size || peers_[peer] >= 0) {
+            ::close(c);
+            continue;
+          }
+          set_nodelay(c);
+          peers_[peer] = c;
+          joined++;
+        }
+      } else {
+        sockaddr_in sa;
+        if (!resolve(host, port, &sa)) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: cannot resolve %s", host);
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
+        while (true) {
+          int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+          if (fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0) {
+            int32_t me = rank;
+            if (send_all(fd, &me, sizeof me)) {
+              set_nodelay(fd);
+              up_ = fd;
+              break;
+            }
+          }
+          if (fd >= 0) ::close(fd);
+          if (std::chrono::steady_clock::now() > deadline)
+            return fail(TIPS_ERR_BOOTSTRAP, "negotiation: rank %d could not reach rank 0 at %s:%d", rank, host, port);
+          std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        }
+      }
+    }
+    running_ = true;
+    thread_ = std::thread([this] { loop(); });
+    return 0;
+  }
+
+  int64_t enqueue(const std::string& name, const void* in, void* out, int64_t count, int dtype, hipStream_t s) {
+    auto r = std::make_shared<Req>();
+    r->name = name;
+    r->in = in;
+    r->out = out;
+    r->count = count;
+    r->dtype = dtype;
+    r->stream = s;
+    if (!dry_) {  // device-resident tensors only: the negotiated path runs on the caller's stream
+      State& st = S();
+      std::lock_guard<std::mutex> lk(st.mu);
+      TRY(set_device(st));
+      if (count > 0 && !(is_device_ptr(in) && is_device_ptr(out)))
+        return fail(TIPS_ERR_INVALID_ARG, "named allreduce needs device pointers");
+      HIP_TRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+    }
+    std::lock_guard<std::mutex> l(m_);
+    if (!running_) return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
+    if (by_name_.count(name)) return fail(TIPS_ERR_INVALID_ARG, "a request named %s is already pending", name.c_str());
+    r->handle = ++next_handle_;
+    by_name_[name] = r;
+    by_handle_[r->handle] = r;
+    fresh_.push_back(r);
+    cv_.notify_all();
+    return r->handle;
+  }
+
+  // 1 = done, 0 = pending, < 0 = error; a finished handle is released by the call that reports it
+  int poll(int64_t h, bool block) {
+    std::shared_ptr<Req> r;
+    {
+      std::unique_lock<std::mutex> l(m_);
+      auto it = by_handle_.find(h);
+      if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
+      r = it->second;
+      if (block) cv_.wait(l, [&] { return r->state >= 2 || r->state < 0; });
+      if (r->state == 0 || r->state == 1) return 0;
+    }
+    int rc = 1;
+    if (r->state < 0) {
+      rc = fail(TIPS_ERR_MISMATCH, "%s", r->err.c_str());
+    } else if (r->state == 2) {
+      hipError_t e = block ? hipEventSynchronize(r->ev) : hipEventQuery(r->ev);
+      if (e == hipErrorNotReady) return 0;
+      if (e != hipSuccess) rc = fail(TIPS_ERR_HIP, "request %s: %s", r->name.c_str(), hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> l(m_);
+    if (r->ev) (void)hipEventDestroy(r->ev);
+    r->ev = nullptr;
+    by_handle_.erase(h);
+    return rc;
+  }
+
+  // collective: every rank's loop learns from rank 0 that all ranks asked to stop
+  int stop() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      if (!running_ && !thread_.joinable()) return 0;
+      want_stop_ = true;
+      cv_.notify_all();
+    }
+    if (thread_.joinable()) thread_.join();
+    for (int fd : peers_)
+      if (fd >= 0) ::close(fd);
+    peers_.clear();
+    if (up_ >= 0) ::close(up_);
+    if (lfd_ >= 0) ::close(lfd_);
+    up_ = lfd_ = -1;
+    return loop_err_.empty() ? 0 : fail(TIPS_ERR_BOOTSTRAP, "%s", loop_err_.c_str());
+  }
+
+  bool running() {
+    std::lock_guard<std::mutex> l(m_);
+    return running_;
+  }
+  std::vector<std::string> log() {
+    std::lock_guard<std::mutex> l(m_);
+    return log_;
+  }
+
+ private:
+  void loop() {
+    const auto cycle = std::chrono::microseconds(std::max<int64_t>(50, env_i64("TIPS_CYCLE_TIME_US", 1000)));
+    while (true) {
+      std::vector<std::shared_ptr<Req>> batch;
+      bool stopping;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait_for(l, cycle, [&] { return !fresh_.empty() || want_stop_; });
+        batch.assign(fresh_.begin(), fresh_.end());
+        fresh_.clear();
+        for (auto& r : batch) r->state = 1;
+        stopping = want_stop_;
+      }
+      Writer w;
+      w.put<uint8_t>(stopping ? 1 : 0);
+      w.put<uint32_t>((uint32_t)batch.size());
+      for (auto& r : batch) {
+        w.put<int32_t>(r->dtype);
+        w.put<int64_t>(r->count);
+        w.str(r->name);
+      }
+      std::string resp;
+      if (!exchange(w.b, &resp)) break;
+      Reader rd(resp);
+      const bool shutdown = rd.get<uint8_t>() != 0;
+      const uint32_t n = rd.get<uint32_t>();
+      for (uint32_t i = 0; i < n && rd.ok; i++) {
+        const bool ok = rd.get<uint8_t>() != 0;
+        const std::string name = rd.str(), err = rd.str();
+        execute(name, ok, err);
+      }
+      if (!rd.ok) {
+        set_loop_error("negotiation: malformed response");
+        break;
+      }
+      if (shutdown) break;
+    }
+    std::lock_guard<std::mutex> l(m_);
+    running_ = false;
+    std::vector<std::string> unmatched;
+    for (auto& kv : by_name_) unmatched.push_back(kv.first);
+    std::sort(unmatched.begin(), unmatched.end());
+    for (auto& name : unmatched) {  // never matched on every rank before the stop
+      auto& r = by_name_[name];
+      r->state = -1;
+      r->err = "request " + name + " was not enqueued on every rank before shutdown";
+      if (dry_) log_.push_back(name + " ERR " + r->err);
+    }
+    by_name_.clear();
+    cv_.notify_all();
+  }
+
+  // One lockstep cycle: my announce goes up, rank 0's decision comes back.
+  bool exchange(const std::string& mine, std::string* resp) {
+    if (size_ == 1) return decide({mine}, resp);
+    if (rank_ != 0) {
+      if (!send_msg(up_, mine) || !recv_msg(up_, resp, timeout_ms_)) {
+        set_loop_error("negotiation: lost rank 0");
+        return false;
+      }
+      return true;
+    }
+    std::vector<std::string> all(size_);
+    all[0] = mine;
+    for (int r = 1; r < size_; r++)
+      if (!recv_msg(peers_[r], &all[r], timeout_ms_)) {
+        set_loop_error("negotiation: lost rank " + std::to_string(r));
+        return false;
+      }
+    if (!decide(all, resp)) return false;
+    for (int r = 1; r < size_; r++)
+      if (!send_msg(peers_[r], *resp)) {
+        set_loop_error("negotiation: lost rank " + std::to_string(r));
+        return false;
+      }
+    return true;
+  }
+
+  // rank 0: fold every rank's announce into the table, answer with the ready list
+  bool decide(const std::vector<std::string>& all, std::string* resp) {
+    bool everyone_stops = true;
+    for (int r = 0; r < (int)all.size(); r++) {
+      Reader rd(all[r]);
+      everyone_stops &= rd.get<uint8_t>() != 0;
+      const uint32_t n = rd.get<uint32_t>();
+      for (uint32_t i = 0; i < n && rd.ok; i++) {
+        Announce a;
+        a.dtype = rd.get<int32_t>();
+        a.count = rd.get<int64_t>();
+        a.name = rd.str();
+        if (rd.ok) table_.announce(r, a);
+      }
+      if (!rd.ok) {
+        set_loop_error("negotiation: malformed announce from rank " + std::to_string(r));
+        return false;
+      }
+    }
+    const std::vector<Decision> ready = table_.ready();
+    Writer w;
+    w.put<uint8_t>(everyone_stops ? 1 : 0);
+    w.put<uint32_t>((uint32_t)ready.size());
+    for (auto& d : ready) {
+      w.put<uint8_t>(d.ok ? 1 : 0);
+      w.str(d.name);
+      w.str(d.err);
+    }
+    *resp = w.b;
+    return true;
+  }
+
+  void execute(const std::string& name, bool ok, const std::string& err) {
+    std::shared_ptr<Req> r;
+    {
+      std::lock_guard<std::mutex> l(m_);
+      auto it = by_name_.find(name);
+      if (it == by_name_.end()) return;  // (cannot happen: every rank announced it)
+      r = it->second;
+      by_name_.erase(it);
+      if (dry_) log_.push_back(name + (ok ? " OK" : " ERR " + err));
+    }
+    int state = ok ? (dry_ ? 3 : 2) : -1;
+    std::string msg = err;
+    if (ok && !dry_) {  // PerformCollectiveOp: the device allreduce, on the request's stream
+      State& st = S();
+      std::lock_guard<std::mutex> lk(st.mu);
+      int rc = set_device(st);
+      if (rc == 0) rc = allreduce_device(st, r->in, r->out, r->count, r->dtype, r->stream);
+      if (rc == 0 && hipEventRecord(r->ev, r->stream) != hipSuccess) rc = fail(TIPS_ERR_HIP, "hipEventRecord failed");
+      if (rc != 0) {
+        state = -1;
+        msg = last_error();
+      }
+    }
+    std::lock_guard<std::mutex> l(m_);
+    r->state = state;
+    r->err = msg;
+    cv_.notify_all();
+  }
+
+  void set_loop_error(const std::string& e) {
+    std::lock_guard<std::mutex> l(m_);
+    if (loop_err_.empty()) loop_err_ = e;
+  }
+
+  int rank_ = 0, size_ = 1, timeout_ms_ = 600000;
+  bool dry_ = false;
+  int lfd_ = -1, up_ = -1;
+  std::vector<int> peers_;
+  Table table_;
+  std::thread thread_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool running_ = false, want_stop_ = false;
+  int64_t next_handle_ = 0;
+  std::deque<std::shared_ptr<Req>> fresh_;
+  std::unordered_map<std::string, std::shared_ptr<Req>> by_name_;
+  std::unordered_map<int64_t, std::shared_ptr<Req>> by_handle_;
+  std::vector<std::string> log_;
+  std::string loop_err_;
+};
+
+std::mutex g_neg_mu;
+std::unique_ptr<Negotiator> g_neg;
+
+int negotiation_port() {
+  return (int)env_i64("TIPS_NEGOTIATION_PORT", env_i64("MASTER_PORT", 29500) + 19);
+}
+
+const char* master_addr() {
+  const char* h = getenv("MASTER_ADDR");
+  return (h && *h) ? h : "127.0.0.1";
+}
+
+}  // namespace
+
+int negotiation_stop() {
+  std::unique_ptr<Negotiator> n;
+  {
+    std::lock_guard<std::mutex> l(g_neg_mu);
+    n.swap(g_neg);
+  }
+  return n ? n->stop() : 0;
+}
+
+}  // namespace rt
+}  // namespace tips
+
+using namespace tips::rt;
+
+extern "C" {
+
+int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  if (!name || !*name || count < 0 || (count > 0 && (!in || !out)))
+    return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
+  Negotiator* n = nullptr;
+  {
+    std::lock_guard<std::mutex> l(g_neg_mu);
+    if (!g_neg) {
+      State& st = S();
+      int rank, size;
+      {
+        std::lock_guard<std::mutex> lk(st.mu);
+        if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+        rank = st.rank;
+        size = st.size;
+      }
+      auto neg = std::make_unique<Negotiator>();
+      TRY(neg->start(rank, size, master_addr(), negotiation_port(), false,
+                     (int)env_i64("TIPS_NEGOTIATION_TIMEOUT", 600)));
+      g_neg = std::move(neg);
+    }
+    n = g_neg.get();
+  }
+  return n->enqueue(name, in, out, count, dtype, (hipStream_t)stream);
+}
+
+int tips_poll(int64_t handle) {
+  std::lock_guard<std::mutex> l(g_neg_mu);
+  if (!g_neg) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
+  return g_neg->poll(handle, false);
+}
+
+int tips_wait(int64_t handle) {
+  Negotiator* n;
+  {
+    std::lock_guard<std::mutex> l(g_neg_mu);
+    if (!g_neg) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
+    n = g_neg.get();
+  }
+  const int rc = n->poll(handle, true);
+  return rc == 1 ? 0 : rc;
+}
+
+int tips_negotiation_selftest(int rank, int size, const char* host, int port, const char* requests, char* out,
+                              int64_t cap) {
+  if (size < 1 || rank < 0 || rank >= size || !requests || !out || cap < 1)
+    return fail(TIPS_ERR_INVALID_ARG, "bad selftest args");
+  Negotiator neg;
+  TRY(neg.start(rank, size, (host && *host) ? host : "127.0.0.1", port, true, 120));
+  std::vector<int64_t> handles;
+  const char* p = requests;
+  while (*p) {  // lines: "name dtype count" or "@sleep ms"
+    const char* e = strchr(p, '\n');
+    std::string line(p, e ? (size_t)(e - p) : strlen(p));
+    p = e ? e + 1 : p + line.size();
+    if (line.empty()) continue;
+    char nm[256];
+    long long dt = 0, cnt = 0;
+    if (line.rfind("@sleep ", 0) == 0) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(atoi(line.c_str() + 7)));
+    } else if (sscanf(line.c_str(), "%255s %lld %lld", nm, &dt, &cnt) == 3) {
+      const int64_t h = neg.enqueue(nm, nullptr, nullptr, cnt, (int)dt, nullptr);
+      if (h < 0) return (int)h;
+      handles.push_back(h);
+    }
+  }
+  const int rc = neg.stop();  // collective: requests every rank announced are decided before it returns
+  for (int64_t h : handles) (void)neg.poll(h, false);
+  std::string log;
+  for (auto& s : neg.log()) log += s + "\n";
+  snprintf(out, (size_t)cap, "%s", log.c_str());
+  return rc;
+}
+
+}  // extern "C"

@@ -173,6 +173,10 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
 // fusion.cc
 void free_plan(FusionPlan& pl);
+// control.cc: ConstructResponseMessage's rules over p request records (TIPS_REQUEST_WORDS each)
+int check_records(const int64_t* t, int p);
+// negotiate.cc: stop the negotiation thread (collective; call without holding st.mu)
+int negotiation_stop();
 
 // ---------------------------------------------------------------------------
 // host staging: the reference's ops work on host (TF CPU) tensors (ops.cc:88-90)

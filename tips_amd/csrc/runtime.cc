@@ -91,6 +91,7 @@ void tips_init(void) {
 }
 
 void tips_shutdown(void) {
+  (void)negotiation_stop();  // collective, like the reference's collective_shutdown service
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return;

@@ -170,6 +170,56 @@ def bucket_sum(a, b, out=None):
     return out
 
 
+class Handle(object):
+    """An in-flight named allreduce (tips_enqueue_allreduce); see allreduce_async."""
+
+    def __init__(self, handle, output, name):
+        self.handle = handle
+        self.output = output
+        self.name = name
+        self.done = False
+
+
+def allreduce_async(tensor, name):
+    """Start a negotiated SUM of a device tensor under `name` and return a Handle.
+
+    The reference's op path (MPIAllreduce -> EnqueueTensorCollective -> rank-0
+    negotiation, ops.cc:86-115, coordinator.cc:223-513): ranks may call this in
+    any order; each named tensor is reduced once every rank has enqueued it, in
+    rank 0's order, with the reference's dtype/shape validation. `name` must be
+    the same on every rank (the reference uses the TF node name)."""
+    basics.init()
+    if not tensors.is_device(tensor):
+        raise ValueError("allreduce_async needs a device tensor")
+    code = tensors.dtype_code(tensor)
+    src = tensor.contiguous()
+    out = tensors.empty_like(src)
+    h = _lib.lib().tips_enqueue_allreduce(name.encode(), src.data_ptr(), out.data_ptr(), src.numel(), code,
+                                          tensors.stream_of(src))
+    if h < 0:
+        raise _lib.TipsError("tips_enqueue_allreduce", int(h), _lib.last_error())
+    hd = Handle(int(h), out, name)
+    hd._keep = src  # the input must stay alive until the reduction has run
+    return hd
+
+
+def poll(handle):
+    """True once the named allreduce has completed on the device."""
+    if handle.done:
+        return True
+    rc = _lib.call("tips_poll", handle.handle)
+    handle.done = rc == 1
+    return handle.done
+
+
+def synchronize(handle):
+    """Wait for a Handle and return its output tensor (raises TipsError on a negotiation error)."""
+    if not handle.done:
+        _lib.call("tips_wait", handle.handle)
+        handle.done = True
+    return handle.output
+
+
 class registered_host_buffer(object):
     """Context manager: page-lock a long-lived host (numpy / CPU torch) buffer for the
     duration, so host-memory allreduces on it use asynchronous DMA (tips_host_register)."""
