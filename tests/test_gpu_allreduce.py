@@ -371,7 +371,9 @@ def test_named_async_allreduce_single_rank(gpu):
     with pytest.raises(gpu.TipsError):
         gpu.allreduce_async(ts[1], "dup")  # same name while pending
     assert torch.equal(gpu.synchronize(h), ts[0])
-    while not gpu.poll(gpu.allreduce_async(ts[2], "polled")):
+    hp = gpu.allreduce_async(ts[2], "polled")
+    while not gpu.poll(hp):
         pass
+    assert torch.equal(hp.output, ts[2])
     with pytest.raises(ValueError):
         gpu.allreduce_async(torch.zeros(3), "host")
