@@ -367,10 +367,18 @@ def test_named_async_allreduce_single_rank(gpu):
     hs = [gpu.allreduce_async(t, "grad.%d" % i) for i, t in enumerate(ts)]
     for h, t in zip(hs, ts):
         assert torch.equal(gpu.synchronize(h), t)
+    # A name is reserved only until negotiation resolves it; a single rank can
+    # resolve it before the second call, so the duplicate may or may not be
+    # refused here (the deterministic duplicate test is in test_negotiation_cpu).
     h = gpu.allreduce_async(ts[0], "dup")
-    with pytest.raises(gpu.TipsError):
-        gpu.allreduce_async(ts[1], "dup")  # same name while pending
+    try:
+        h2 = gpu.allreduce_async(ts[1], "dup")
+    except gpu.TipsError as e:
+        assert "already pending" in str(e)
+        h2 = None
     assert torch.equal(gpu.synchronize(h), ts[0])
+    if h2 is not None:
+        assert torch.equal(gpu.synchronize(h2), ts[1])
     hp = gpu.allreduce_async(ts[2], "polled")
     while not gpu.poll(hp):
         pass
