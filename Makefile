@@ -17,13 +17,16 @@ $(LIB): $(SRCS) $(HDRS)
 oracle:
 	$(MAKE) -C oracle
 
-tools: tools/sum_sweep
+tools: tools/sum_sweep tools/cpu_sum_bench
+
+tools/cpu_sum_bench: tools/cpu_sum_bench.c
+	gcc -O3 -fopenmp -o $@ $<
 
 tools/sum_sweep: tools/sum_sweep.cc $(LIB)
 	$(HIPCC) -O2 -std=c++17 -o $@ $< -Itips_amd -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../tips_amd/lib'
 
 clean:
-	rm -f $(LIB) tools/sum_sweep
+	rm -f $(LIB) tools/sum_sweep tools/cpu_sum_bench
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle tools clean

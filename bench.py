@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
-    ap.add_argument("--workload", default="auto", choices=["auto", "sum", "bucket", "fused1000", "resnet50"],
+    ap.add_argument("--workload", default="auto", choices=["auto", "sum", "bucket", "fused1000", "resnet50", "negotiated1000"],
                     help="auto: config 2 (sum) at N=1, config 3 (bucket allreduce) at N>1")
     return ap.parse_args()
 
@@ -341,11 +341,16 @@ def bench_allreduce(args):
     elif workload == "fused1000":
         sizes, seed0 = fused1000_sizes(), 4000
         desc = "config 4: 1000 fp32 grads (2^U(8,17) elems) fused into 64 MiB buckets, allreduced in place"
+    elif workload == "negotiated1000":
+        sizes, seed0 = fused1000_sizes(), 4000
+        desc = ("config 4 without fusion: 1000 fp32 grads, one named allreduce each through the negotiated "
+                "path (tips_enqueue_allreduce/tips_wait), the reference's per-tensor structure")
     else:
         sizes, seed0 = resnet50_grad_sizes(), 5000
         desc = "config 5: ResNet-50 gradient set (214 tensors, 25.6 M fp32) fused into 64 MiB buckets, in place"
     # the schedule the (largest) reduced buffer gets: the bucket itself, or a <= 64 MiB fusion bucket
-    algo = L.tips_resolve_algorithm(world, sizes[0] * 4 if workload == "bucket" else 64 << 20)
+    algo = L.tips_resolve_algorithm(world, sizes[0] * 4 if workload == "bucket" else
+                                    max(sizes) * 4 if workload == "negotiated1000" else 64 << 20)
     # every tensor at a 256-B aligned offset of one flat buffer (what a caching allocator hands out)
     offs, total = [], 0
     for k in sizes:
@@ -364,9 +369,19 @@ def bench_allreduce(args):
     pp, _keep1 = _lib.ptr_array([v.data_ptr() for v in views])
     cp, _keep2 = _lib.i64_array(sizes)
 
+    names = [("grad.%d" % i).encode() for i in range(len(sizes))]
+
     def step():
         if workload == "bucket":
             rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), sizes[0], _lib.FLOAT32, _lib.OP_SUM, sp)
+        elif workload == "negotiated1000":
+            hs = [L.tips_enqueue_allreduce(nm, v.data_ptr(), v.data_ptr(), v.numel(), _lib.FLOAT32, sp)
+                  for nm, v in zip(names, views)]
+            rc = next((int(h) for h in hs if h < 0), 0)
+            for h in hs:
+                if h > 0:
+                    w = L.tips_wait(h)
+                    rc = rc or (w if w < 0 else 0)
         else:
             rc = L.tips_fused_allreduce(pp, cp, len(sizes), _lib.FLOAT32, sp)
         if rc:
@@ -468,6 +483,8 @@ def bench_allreduce(args):
         "reduce_kernel_roofline": kernel_roof,
         "check": check if all_ok else "FAIL on some rank",
     }
+    if workload == "negotiated1000":
+        line["per_tensor_us"] = round(ms * 1e3 / len(sizes), 2)
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True
 
@@ -506,7 +523,7 @@ def main():
                "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29511"),
                os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
-    if world > 1 or args.workload in ("bucket", "fused1000", "resnet50"):
+    if world > 1 or args.workload in ("bucket", "fused1000", "resnet50", "negotiated1000"):
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29512")

@@ -34,10 +34,14 @@ fi
 run bench 600 python bench.py ${BENCH_ARGS:-}
 rc=$?; fatal $rc && exit $rc
 if [ "${EXTRA:-1}" = "1" ]; then
-  for w in bucket fused1000 resnet50; do
+  for w in ${WORKLOADS:-bucket fused1000 resnet50 negotiated1000}; do
     run bench_$w 300 python bench.py --workload $w --no-compare
     rc=$?; fatal $rc && exit $rc
   done
+fi
+if [ "${CPU_SWEEP:-0}" = "1" ]; then  # host cores only: the reference's MPI path and c = a + b
+  run cpu_ref_sweep 900 python tools/cpu_ref_sweep.py
+  rc=$?; fatal $rc && exit $rc
 fi
 if [ "${PROFILE:-1}" = "1" ]; then
   export TMPDIR=/tmp
