@@ -198,8 +198,10 @@ TIPS_API int tips_poll(int64_t handle);
 TIPS_API int tips_wait(int64_t handle);
 /* The negotiation protocol with an executor that only logs (no GPU): each
  * rank enqueues the newline-separated "name dtype count" lines of `requests`
- * ("@sleep ms" pauses), stops, and writes its execution log ("name OK" /
- * "name ERR message", one per line, in execution order) into out. For tests. */
+ * ("@sleep ms" pauses, "@wait" blocks until every earlier request is
+ * decided, "@mark" logs "# mark <microseconds since the call began>"), stops,
+ * and writes its execution log ("name OK" / "name ERR message", one per line,
+ * in execution order) into out. For tests and the latency tool. */
 TIPS_API int tips_negotiation_selftest(int rank, int size, const char* host, int port, const char* requests,
                                        char* out, int64_t cap);
 

@@ -41,7 +41,7 @@ def run(per_rank):
 
 
 def lines(log):
-    return [l for l in log.splitlines() if l]
+    return [l for l in log.splitlines() if l and not l.startswith("#")]
 
 
 def test_same_order_everywhere_despite_different_enqueue_orders():

@@ -294,6 +294,10 @@ class Negotiator {
     std::lock_guard<std::mutex> l(m_);
     return log_;
   }
+  void note(const std::string& s) {
+    std::lock_guard<std::mutex> l(m_);
+    log_.push_back(s);
+  }
 
  private:
   void loop() {
@@ -538,7 +542,8 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   TRY(neg.start(rank, size, (host && *host) ? host : "127.0.0.1", port, true, 120));
   std::vector<int64_t> handles;
   const char* p = requests;
-  while (*p) {  // lines: "name dtype count" or "@sleep ms"
+  const auto t0 = std::chrono::steady_clock::now();
+  while (*p) {  // lines: "name dtype count", "@sleep ms", "@wait" (all so far resolved), "@mark" (log "# mark us")
     const char* e = strchr(p, '\n');
     std::string line(p, e ? (size_t)(e - p) : strlen(p));
     p = e ? e + 1 : p + line.size();
@@ -547,6 +552,12 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
     long long dt = 0, cnt = 0;
     if (line.rfind("@sleep ", 0) == 0) {
       std::this_thread::sleep_for(std::chrono::milliseconds(atoi(line.c_str() + 7)));
+    } else if (line == "@wait") {
+      for (int64_t h : handles) (void)neg.poll(h, true);
+      handles.clear();
+    } else if (line == "@mark") {
+      const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
+      neg.note("# mark " + std::to_string((long long)us.count()));
     } else if (sscanf(line.c_str(), "%255s %lld %lld", nm, &dt, &cnt) == 3) {
       const int64_t h = neg.enqueue(nm, nullptr, nullptr, cnt, (int)dt, nullptr);
       if (h < 0) return (int)h;
