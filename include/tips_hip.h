@@ -187,7 +187,7 @@ TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int 
  * MASTER_ADDR:TIPS_NEGOTIATION_PORT, default MASTER_PORT + 19) which names
  * every rank has enqueued, validates them with ConstructResponseMessage's
  * rules and error text, and every rank reduces them in rank 0's
- * first-announcement order, on the stream passed here. Device pointers only.
+ * readiness order (as ready_to_reduce), on the stream passed here. Device pointers only.
  * Returns a handle > 0, or a negative status. The first call starts the
  * thread (collective); tips_shutdown stops it (collective). */
 TIPS_API int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype,

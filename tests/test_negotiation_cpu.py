@@ -1,7 +1,7 @@
 """The negotiation protocol (negotiate.cc; the reference's coordinator, coordinator.cc:15-513) across
 real processes on the CPU, with the dry-run executor: ranks enqueue named requests in DIFFERENT orders
 and at different times; every rank must execute the same names in the same order (rank 0's
-first-announcement order), mismatches must fail on every rank with the reference's error text, and names
+readiness order), mismatches must fail on every rank with the reference's error text, and names
 missing on some rank must fail at shutdown."""
 import multiprocessing as mp
 import socket
@@ -87,3 +87,12 @@ def test_missing_on_one_rank_fails_at_shutdown():
 def test_single_rank_and_duplicate_names():
     res = run(["a 3 5\nb 3 5"])
     assert lines(res[0][2]) == ["a OK", "b OK"]
+
+
+def test_readiness_order():
+    """A name runs when its LAST rank announces it (ready_to_reduce, coordinator.cc:451-455): rank 1
+    holds `a` back for 300 ms, so `b` (announced by both at once) is reduced first on every rank."""
+    res = run(["a 0 4\nb 0 4", "b 0 4\n@sleep 300\na 0 4"])
+    for _, rc, log, err in res:
+        assert rc == 0, err
+        assert lines(log) == ["b OK", "a OK"]

@@ -11,7 +11,7 @@
 // Here one background thread per rank runs cycles in lockstep with rank 0 over
 // one persistent TCP connection (the reference: a ZeroMQ PUSH/PULL RPC with
 // flatbuffers, naive_rpc.cc): each cycle every rank sends the requests it has
-// newly enqueued; rank 0 records them in first-announcement order, validates
+// newly enqueued; rank 0 queues each name when its last rank announces it, validates
 // every name all ranks have announced, and answers with the list to run; every
 // rank then reduces that list in that order on the owning request's stream.
 // Only control records travel here; tensor bytes go over RCCL / xGMI.
@@ -103,16 +103,20 @@ struct Decision {
 };
 
 // ---- rank 0's table (IncreTensorCount + ConstructResponseMessage) ---------------
+// A name joins the ready queue the moment its last rank announces it (or a
+// rank announces it twice), as IncreTensorCount feeds ready_to_reduce
+// (coordinator.cc:15-38, 451-455): rank 0's readiness order, O(1) per announce.
 struct Table {
   struct Row {
     std::vector<int64_t> rec;  // p records of TIPS_REQUEST_WORDS
     std::vector<char> seen;
     int nseen = 0;
+    bool queued = false;
     std::string dup;  // set when a rank announced this name twice while unresolved
   };
   int p = 1;
   std::unordered_map<std::string, Row> rows;
-  std::deque<std::string> arrival;  // first-announcement order
+  std::vector<std::string> ready_q;
 
   void announce(int rank, const Announce& a) {
     auto it = rows.find(a.name);
@@ -121,42 +125,41 @@ struct Table {
       r.rec.assign((size_t)p * TIPS_REQUEST_WORDS, 0);
       r.seen.assign(p, 0);
       it = rows.emplace(a.name, std::move(r)).first;
-      arrival.push_back(a.name);
     }
     Row& r = it->second;
     if (r.seen[rank]) {
-      r.dup = "rank " + std::to_string(rank) + " enqueued " + a.name + " twice";
-      return;
+      if (r.dup.empty()) r.dup = "rank " + std::to_string(rank) + " enqueued " + a.name + " twice";
+    } else {
+      r.seen[rank] = 1;
+      r.nseen++;
+      int64_t* rec = &r.rec[(size_t)rank * TIPS_REQUEST_WORDS];
+      rec[0] = TIPS_REQ_ALLREDUCE;
+      rec[1] = a.dtype;
+      rec[2] = 1;  // the C-ABI carries element counts: shape [count]
+      rec[3] = a.count;
     }
-    r.seen[rank] = 1;
-    r.nseen++;
-    int64_t* rec = &r.rec[(size_t)rank * TIPS_REQUEST_WORDS];
-    rec[0] = TIPS_REQ_ALLREDUCE;
-    rec[1] = a.dtype;
-    rec[2] = 1;  // the C-ABI carries element counts: shape [count]
-    rec[3] = a.count;
+    if (!r.queued && (!r.dup.empty() || r.nseen == p)) {
+      r.queued = true;
+      ready_q.push_back(a.name);
+    }
   }
 
-  // names every rank has announced, in first-announcement order, with their verdicts
+  // the names that became ready since the last call, in readiness order, with their verdicts
   std::vector<Decision> ready() {
     std::vector<Decision> out;
-    std::deque<std::string> rest;
-    for (auto& name : arrival) {
-      Row& r = rows[name];
+    out.reserve(ready_q.size());
+    for (auto& name : ready_q) {
+      auto it = rows.find(name);
+      Row& r = it->second;
       if (!r.dup.empty()) {
         out.push_back({false, name, r.dup});
-        rows.erase(name);
-        continue;
+      } else {
+        const int rc = check_records(r.rec.data(), p);
+        out.push_back({rc == 0, name, rc == 0 ? std::string() : last_error()});
       }
-      if (r.nseen < p) {
-        rest.push_back(name);
-        continue;
-      }
-      const int rc = check_records(r.rec.data(), p);
-      out.push_back({rc == 0, name, rc == 0 ? std::string() : last_error()});
-      rows.erase(name);
+      rows.erase(it);
     }
-    arrival.swap(rest);
+    ready_q.clear();
     return out;
   }
 };
@@ -229,7 +232,14 @@ class Negotiator {
       TRY(set_device(st));
       if (count > 0 && !(is_device_ptr(in) && is_device_ptr(out)))
         return fail(TIPS_ERR_INVALID_ARG, "named allreduce needs device pointers");
-      HIP_TRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+      {
+        std::lock_guard<std::mutex> l(m_);
+        if (!ev_pool_.empty()) {
+          r->ev = ev_pool_.back();
+          ev_pool_.pop_back();
+        }
+      }
+      if (!r->ev) HIP_TRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
     }
     std::lock_guard<std::mutex> l(m_);
     if (!running_) return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
@@ -262,7 +272,7 @@ class Negotiator {
       if (e != hipSuccess) rc = fail(TIPS_ERR_HIP, "request %s: %s", r->name.c_str(), hipGetErrorString(e));
     }
     std::lock_guard<std::mutex> l(m_);
-    if (r->ev) (void)hipEventDestroy(r->ev);
+    if (r->ev) ev_pool_.push_back(r->ev);  // reused by the next request
     r->ev = nullptr;
     by_handle_.erase(h);
     return rc;
@@ -284,6 +294,12 @@ class Negotiator {
     if (lfd_ >= 0) ::close(lfd_);
     up_ = lfd_ = -1;
     return loop_err_.empty() ? 0 : fail(TIPS_ERR_BOOTSTRAP, "%s", loop_err_.c_str());
+  }
+
+  ~Negotiator() {
+    for (auto& kv : by_handle_)  // never polled to completion
+      if (kv.second->ev) ev_pool_.push_back(kv.second->ev);
+    for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
   }
 
   bool running() {
@@ -458,6 +474,7 @@ class Negotiator {
   std::unordered_map<std::string, std::shared_ptr<Req>> by_name_;
   std::unordered_map<int64_t, std::shared_ptr<Req>> by_handle_;
   std::vector<std::string> log_;
+  std::vector<hipEvent_t> ev_pool_;
   std::string loop_err_;
 };
 
