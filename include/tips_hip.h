@@ -242,6 +242,14 @@ TIPS_API int tips_set_sim_transport(int transport);
 TIPS_API int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
                      int blocks, int threads, void* stream);
 
+/* Tuning entry for the multi-input sum (tools/sum_sweep.cc): f32 only,
+ * nsrc 2, 4 or 8, 16-B aligned pointers. variant 0 = global non-temporal
+ * loads, 1 = buffer nt loads 1 vector per lane, 2 = the same with 2 vectors,
+ * 3 = buffer plain loads, 4 = buffer nt loads 4 vectors per lane.
+ * Others: TIPS_ERR_HIP. tips_multi_sum uses the default chosen from that sweep. */
+TIPS_API int tips_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, int variant,
+                                    void* stream);
+
 /* Pipeline shape the ring/direct schedules use for a bucket: depth = K
  * sub-chunks per chunk, sub_elems = elements in a (first) sub-chunk, i.e. the
  * size of one reduce-kernel launch (TIPS_PIPELINE_DEPTH, TIPS_MIN_SUBCHUNK_BYTES). */

@@ -25,6 +25,10 @@ struct CopyTile {
 constexpr int64_t kCopyTileBytes = 64 * 1024;
 hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t s);
 
+// Tuning/sweep entry for the multi-input sum (f32, nsrc 2/4/8); variants in kernels.hip.
+hipError_t launch_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, int variant,
+                                   hipStream_t s);
+
 // Tuning/sweep entry: explicit variant of the 2-input sum.
 //   mode 0 = grid-stride over (blocks) workgroups, mode 1 = one tile per workgroup
 //   unroll = 16-B vectors per lane in flight, nt: 0 plain, 1 non-temporal loads+stores,

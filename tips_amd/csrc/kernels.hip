@@ -359,6 +359,42 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
   }
 }
 
+// Buffer-op form of the multi-input sum: one descriptor per source covering
+// this workgroup's tile, cache-policy bits on the loads (LAUX) and sc1 stores,
+// every source's vectors in flight before the fold (as sum2_buf_kernel).
+template <int DT, int NSRC, int U, int LAUX>
+__global__ __launch_bounds__(kBlock) void multi_sum_buf_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
+                                                              int64_t tail_begin, int64_t n) {
+  using W = Wide<DT>;
+  constexpr int64_t kTile = (int64_t)kBlock * U;
+  const int tid = threadIdx.x;
+  const int64_t first = xcd_tile(blockIdx.x, gridDim.x) * kTile;
+  if (first < nvec) {
+    const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
+    u32x4 v[U][NSRC];
+#pragma unroll
+    for (int j = 0; j < NSRC; j++) {
+      __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(srcs.p[j] + first), (short)0, rec, 0x00020000);
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, LAUX);
+    }
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      typename W::A acc = W::load(v[u][0]);
+#pragma unroll
+      for (int j = 1; j < NSRC; j++) acc = acc + W::load(v[u][j]);
+      __builtin_amdgcn_raw_buffer_store_b128(W::store(acc), rd, (u * kBlock + tid) * 16, 0, 16);
+    }
+  }
+  if (blockIdx.x == 0 && NSRC > 1 && tail_begin + tid < n) {
+    const void* s[NSRC];
+#pragma unroll
+    for (int j = 0; j < NSRC; j++) s[j] = srcs.p[j];
+    fold_elem<DT>(dst, s, NSRC, tail_begin + tid);
+  }
+}
+
 template <int DT>
 __global__ __launch_bounds__(kBlock) void multi_sum_scalar_kernel(void* dst, SrcList srcs, int nsrc, int64_t n) {
   const void* s[kMaxSrcs];
@@ -525,13 +561,54 @@ constexpr int kDefMode = 3, kDefUnroll = 1, kDefNT = 1, kDefThreads = 256;
 
 template <int DT, int NSRC>
 hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
-  constexpr int U = NSRC <= 4 ? 2 : 1;
+  // buffer loads, 1 vector per lane; non-temporal up to 4 sources, plain beyond
+  // (sweep: profiles/r01_sum_sweep_multi*.jsonl)
+  constexpr int LAUX = NSRC <= 4 ? 2 : 0;
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
-  int64_t grid = (nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
+  int64_t grid = (nvec + (int64_t)kBlock - 1) / (int64_t)kBlock;
   grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
-  hipLaunchKernelGGL((multi_sum_kernel<DT, NSRC, U>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst, sl, nvec,
-                     nvec * ve, n);
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst,
+                     sl, nvec, nvec * ve, n);
+  return hipGetLastError();
+}
+
+// Sweep entry (f32; nsrc 2, 4, 8): 0 = global nt loads (U 2 for nsrc <= 4, else 1),
+// 1 = buffer nt loads U 1, 2 = buffer nt loads U 2, 3 = buffer plain loads U 1, 4 = buffer nt loads U 4.
+template <int NSRC>
+hipError_t run_multi_variant(void* dst, const SrcList& sl, int64_t n, int variant, hipStream_t s) {
+  const int64_t nvec = n / 4;
+  auto grid_for = [&](int u) {
+    int64_t g = (nvec + (int64_t)kBlock * u - 1) / ((int64_t)kBlock * u);
+    return (unsigned)std::max<int64_t>(8, (g + 7) / 8 * 8);
+  };
+  switch (variant) {
+    case 0: {
+      constexpr int U = NSRC <= 4 ? 2 : 1;
+      hipLaunchKernelGGL((multi_sum_kernel<kF32, NSRC, U>), dim3(grid_for(U)), dim3(kBlock), 0, s, (u32x4*)dst, sl,
+                         nvec, nvec * 4, n);
+      break;
+    }
+    case 1:
+      hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 2>), dim3(grid_for(1)), dim3(kBlock), 0, s,
+                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+      break;
+    case 2:
+      hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 2, 2>), dim3(grid_for(2)), dim3(kBlock), 0, s,
+                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+      break;
+    case 3:
+      hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 0>), dim3(grid_for(1)), dim3(kBlock), 0, s,
+                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+      break;
+    case 4:
+      hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 4, 2>), dim3(grid_for(4)), dim3(kBlock), 0, s,
+                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -605,6 +682,23 @@ hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_
     case kI64: return multi_dispatch<kI64>(dst, srcs, nsrc, n, s);
     case kF16: return multi_dispatch<kF16>(dst, srcs, nsrc, n, s);
     case kBF16: return multi_dispatch<kBF16>(dst, srcs, nsrc, n, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, int variant,
+                                   hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (dtype != kF32 || !aligned16(dst)) return hipErrorInvalidValue;
+  SrcList sl{};
+  for (int j = 0; j < nsrc && j < kMaxSrcs; j++) {
+    if (!aligned16(srcs[j])) return hipErrorInvalidValue;
+    sl.p[j] = (const u32x4*)srcs[j];
+  }
+  switch (nsrc) {
+    case 2: return run_multi_variant<2>(dst, sl, n, variant, s);
+    case 4: return run_multi_variant<4>(dst, sl, n, variant, s);
+    case 8: return run_multi_variant<8>(dst, sl, n, variant, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -181,6 +181,15 @@ int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int
   return 0;
 }
 
+int tips_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, int variant,
+                           void* stream) {
+  TRY(check_dtype(dtype));
+  if (count <= 0) return 0;
+  if (!srcs || nsrc < 1 || nsrc > tips::kMaxSrcs) return fail(TIPS_ERR_INVALID_ARG, "bad source list");
+  HIP_TRY(tips::launch_multi_sum_variant(dst, srcs, nsrc, count, dtype, variant, (hipStream_t)stream));
+  return 0;
+}
+
 int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, void* stream) {
   TRY(check_dtype(dtype));
   if (nsrc < 1 || nsrc > tips::kMaxSrcs) return fail(TIPS_ERR_INVALID_ARG, "nsrc must be 1..%d", tips::kMaxSrcs);

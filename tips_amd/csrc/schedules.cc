@@ -19,6 +19,10 @@ namespace tips {
 namespace rt {
 namespace {
 
+// Staging slots that feed one multi_sum launch sit one slot plus 4 KiB apart:
+// sources at power-of-two strides read ~7 % slower (profiles/r01_sum_sweep_multi_pad.jsonl).
+constexpr int64_t kSlotPad = 4096;
+
 // The sum kernel launch used by every schedule (ring step: out = local + received).
 int sum2(void* dst, const void* a, const void* b, int64_t n, int dtype, hipStream_t s) {
   HIP_TRY(tips::launch_sum2(dst, a, b, n, dtype, s));
@@ -90,10 +94,11 @@ int direct_allreduce(State& st, const char* in, char* out, int64_t n, int dtype,
   const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
   const int64_t max_chunk = chunk_of(n, p, align, 0).len();
   const int K = pipeline_depth(max_chunk * es);
-  TRY(st.staging.ensure((size_t)((p - 1) * max_chunk * es)));
+  const int64_t stride = max_chunk * es + kSlotPad;
+  TRY(st.staging.ensure((size_t)((p - 1) * stride)));
   TRY(st.recv_ev.ensure(K));
   TRY(st.sum_ev.ensure(K));
-  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * max_chunk * es; };
+  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * stride; };
   const Range mine = chunk_of(n, p, align, r);
   TRY(join(st.comm_stream, user, st.ev_start));
   HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
@@ -140,8 +145,9 @@ int direct_allreduce(State& st, const char* in, char* out, int64_t n, int dtype,
 int oneshot_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
   const int p = st.size, r = st.rank;
   const int64_t bytes = n * tips::dtype_size(dtype);
-  TRY(st.staging.ensure((size_t)((p - 1) * bytes)));
-  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * bytes; };
+  const int64_t stride = (bytes + kAlignBytes - 1) / kAlignBytes * kAlignBytes + kSlotPad;
+  TRY(st.staging.ensure((size_t)((p - 1) * stride)));
+  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * stride; };
   TRY(join(st.comm_stream, user, st.ev_start));
   NCCL_TRY(ncclGroupStart());
   for (int d = 1; d < p; d++) {

@@ -78,6 +78,19 @@ int main(int argc, char** argv) {
   for (int u : {2, 4})
     for (int bpc : {2, 4, 8})
       vs.push_back({"gs_u" + std::to_string(u) + "_b" + std::to_string(bpc) + "_ntld", 0, u, 2, 256 * bpc, 256, {}});
+  // multi-input sum variants (tips_multi_sum_variant): unroll field = nsrc, nt field = variant
+  // blocks field = extra bytes between consecutive sources (0 = back to back, power-of-2 strides)
+  for (int ns : {4, 8})
+    for (int var = 0; var <= 4; var++)
+      for (int pad : {0, 256, 4096, 65536 + 256})
+        vs.push_back({"multi" + std::to_string(ns) + "_v" + std::to_string(var) + "_pad" + std::to_string(pad), -5, ns,
+                      var, pad, 0, {}});
+  if (argc > 4) {  // optional name filter; the references always stay
+    std::vector<Variant> keep;
+    for (auto& v : vs)
+      if (v.mode == -1 || v.mode == -3 || v.name.find(argv[4]) != std::string::npos) keep.push_back(v);
+    vs.swap(keep);
+  }
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
@@ -91,6 +104,15 @@ int main(int argc, char** argv) {
       for (int j = 0; j < 8; j++) srcs[j] = (j < 4 ? a : b) + (j % 4) * (n / 8);
       if (tips_multi_sum(c, srcs, 8, n / 8, TIPS_FLOAT32, s) != 0) {
         fprintf(stderr, "multi_sum: %s\n", tips_last_error());
+        exit(1);
+      }
+    } else if (v.mode == -5) {
+      const int ns = v.unroll;
+      const void* srcs[8];
+      for (int j = 0; j < ns; j++)
+        srcs[j] = (const char*)((j < ns / 2 ? a : b) + (j % (ns / 2)) * (n / ns)) + (j % (ns / 2)) * (int64_t)v.blocks;
+      if (tips_multi_sum_variant(c, srcs, ns, n / ns, TIPS_FLOAT32, v.nt, s) != 0) {
+        fprintf(stderr, "multi variant %s: %s\n", v.name.c_str(), tips_last_error());
         exit(1);
       }
     } else if (v.mode == -3) {
@@ -114,6 +136,19 @@ int main(int argc, char** argv) {
       run(v);
       CHECK(hipStreamSynchronize(s));
       CHECK(hipMemcpy(hc.data(), c, bytes, hipMemcpyDeviceToHost));
+      if (v.mode == -5) {  // rank-order fold of the ns slices
+        const int ns = v.unroll;
+        const int64_t m = n / ns;
+        for (int64_t i = 0; i < m; i++) {
+          float acc = ha[i];
+          for (int j = 1; j < ns; j++) acc += (j < ns / 2 ? ha : hb)[(j % (ns / 2)) * (m + v.blocks / 4) + i];
+          if (hc[i] != acc) {
+            fprintf(stderr, "variant %s wrong at %lld\n", v.name.c_str(), (long long)i);
+            return 1;
+          }
+        }
+        continue;
+      }
       for (int64_t i = 0; i < n; i++)
         if (hc[i] != ha[i] + hb[i]) {
           fprintf(stderr, "variant %s wrong at %lld\n", v.name.c_str(), (long long)i);
@@ -156,7 +191,10 @@ int main(int argc, char** argv) {
   for (auto& v : vs) {
     std::sort(v.ms.begin(), v.ms.end());
     const double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
-    const double moved = (v.mode == -1) ? 2.0 * bytes : (v.mode == -4) ? 9.0 * bytes / 8 : 3.0 * bytes;
+    const double moved = (v.mode == -1)   ? 2.0 * bytes
+                         : (v.mode == -4) ? 9.0 * bytes / 8
+                         : (v.mode == -5) ? (double)bytes * (v.unroll + 1) / v.unroll
+                                          : 3.0 * bytes;
     printf("{\"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f, \"GBps_median\": %.1f, \"GBps_best\": %.1f}\n",
            v.name.c_str(), med * 1e3, mn * 1e3, moved / (med * 1e-3) / 1e9, moved / (mn * 1e-3) / 1e9);
   }
