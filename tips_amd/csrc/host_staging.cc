@@ -14,19 +14,35 @@ namespace rt {
 // Host-resident allreduce, pipelined over pieces so both PCIe directions and
 // the device work overlap: H2D of piece i+1 (h2d stream) || allreduce of piece
 // i (io stream) || D2H of piece i-1 (d2h stream). Each piece is a complete
-// allreduce (same piece boundaries on every rank). A second host thread
-// issues the D2H copies, because a copy from/to pageable memory blocks the
-// thread that issues it. Caller holds st.mu; returns when `out` is written.
+// allreduce (same piece boundaries on every rank). When both buffers are
+// page-locked every copy is asynchronous and one thread issues all three
+// stages; otherwise a second host thread issues the D2H copies, because a
+// copy from/to pageable memory blocks the thread that issues it. Caller holds
+// st.mu; returns when `out` is written.
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype) {
   const int64_t es = tips::dtype_size(dtype);
   const int64_t piece =
-      round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_PIECE_BYTES", 32 << 20)), kAlignBytes) / es;
+      round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_PIECE_BYTES", kHostPieceBytes)), kAlignBytes) / es;
   const int np = (int)((n + piece - 1) / piece);
   TRY(st.host_in.ensure((size_t)(n * es)));
   TRY(st.host_out.ensure((size_t)(n * es)));
   TRY(st.pipe_ev.ensure(2 * (size_t)np));
   char* din = (char*)st.host_in.p;
   char* dout = (char*)st.host_out.p;
+  if (is_pinned_host(in, n * es) && is_pinned_host(out, n * es)) {
+    for (int i = 0; i < np; i++) {
+      const int64_t off = (int64_t)i * piece * es, cnt = std::min(piece, n - (int64_t)i * piece);
+      HIP_TRY(hipMemcpyAsync(din + off, in + off, (size_t)(cnt * es), hipMemcpyHostToDevice, st.h2d_stream));
+      HIP_TRY(hipEventRecord(st.pipe_ev.ev[2 * i], st.h2d_stream));
+      HIP_TRY(hipStreamWaitEvent(st.io_stream, st.pipe_ev.ev[2 * i], 0));
+      TRY(allreduce_device(st, din + off, dout + off, cnt, dtype, st.io_stream));
+      HIP_TRY(hipEventRecord(st.pipe_ev.ev[2 * i + 1], st.io_stream));
+      HIP_TRY(hipStreamWaitEvent(st.d2h_stream, st.pipe_ev.ev[2 * i + 1], 0));
+      HIP_TRY(hipMemcpyAsync(out + off, dout + off, (size_t)(cnt * es), hipMemcpyDeviceToHost, st.d2h_stream));
+    }
+    HIP_TRY(hipStreamSynchronize(st.d2h_stream));
+    return 0;
+  }
   std::mutex m;
   std::condition_variable cv;
   int issued = 0;

@@ -21,6 +21,8 @@ namespace rt {
 using tips::CopyTile;
 
 constexpr int64_t kAlignBytes = 256;  // chunk / bucket-slot alignment (dwordx4 + 128-B lines)
+// host-staging piece: 16 MiB sits at the top of the measured pipeline curve (profiles/r01_pcie_probe.jsonl)
+constexpr int64_t kHostPieceBytes = 16 << 20;
 
 // Records the calling thread's last error (tips_last_error) and returns `code`.
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -162,6 +164,7 @@ ncclDataType_t nccl_type(int dtype);
 int pipeline_depth(int64_t chunk_bytes);
 int join(hipStream_t waiter, hipStream_t src, hipEvent_t ev);  // waiter waits for all work queued on src
 bool is_device_ptr(const void* p);
+bool is_pinned_host(const void* p, int64_t bytes);
 int check_dtype(int dtype);
 int set_device(State& st);
 int resolve_algo(int algo, int p, int64_t bytes);

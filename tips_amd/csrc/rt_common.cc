@@ -121,6 +121,20 @@ bool is_device_ptr(const void* p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
 }
 
+// Page-locked host memory (hipHostMalloc / hipHostRegister / torch pin_memory) over the whole range:
+// copies from and to it are asynchronous DMA and never block the issuing thread.
+bool is_pinned_host(const void* p, int64_t bytes) {
+  for (const char* q : {(const char*)p, (const char*)p + (bytes > 0 ? bytes - 1 : 0)}) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
 int check_dtype(int dtype) {
   if (tips::dtype_size(dtype) == 0) return fail(TIPS_ERR_INVALID_ARG, "unsupported dtype %d", dtype);
   return 0;

@@ -211,7 +211,7 @@ int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, 
   TRY(set_device(st));
   const size_t bytes = (size_t)count * tips::dtype_size(dtype);
   const bool dout = is_device_ptr(out);
-  if (!dout && !is_device_ptr(in) && (int64_t)bytes > env_i64("TIPS_HOST_PIECE_BYTES", 32 << 20))
+  if (!dout && !is_device_ptr(in) && (int64_t)bytes > env_i64("TIPS_HOST_PIECE_BYTES", kHostPieceBytes))
     return allreduce_host_pipelined(st, (const char*)in, (char*)out, count, dtype);
   return run_staged(st, in, bytes, out, bytes, (hipStream_t)stream, [&](const void* i, void* o, hipStream_t s) {
     return allreduce_device(st, i, o, count, dtype, s);
