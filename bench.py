@@ -63,7 +63,7 @@ def cpu_baseline(bucket_elems):
     mpirun = "/opt/conda/bin/mpirun"
     out = {"value": None, "unit": "GiB/s", "cores": None, "kind": "reference", "sample": None}
     if os.path.exists(harness) and os.path.exists(mpirun):
-        iters = 6
+        iters = 50  # about 8-10 s of host work on the GPU box (a bounded sample, contract ④)
         try:
             r = subprocess.run([mpirun, "-np", "2", harness, "bench", "0", str(bucket_elems), str(iters)],
                                capture_output=True, text=True, timeout=240)
@@ -91,7 +91,7 @@ def cpu_baseline(bucket_elems):
         b = np.random.default_rng(2).random(n, dtype=np.float32)
         oracle_bind.sum2(a, b)
         t0 = time.perf_counter()
-        reps = 3
+        reps = 10
         for _ in range(reps):
             oracle_bind.sum2(a, b)
         t = (time.perf_counter() - t0) / reps

@@ -251,6 +251,15 @@ def test_host_pipeline_pieces(gpu, monkeypatch, piece):
         assert np.array_equal(gpu.allreduce(h), h)  # one rank: SUM = identity, every piece moved exactly
         pt = torch.from_numpy(h).pin_memory()
         assert torch.equal(gpu.allreduce(pt), pt)
+        # both buffers page-locked: the single-thread issue path of host_staging.cc
+        po = torch.empty_like(pt).pin_memory()
+        from tips_amd import _lib
+        _lib.call("tips_allreduce", pt.data_ptr(), po.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, None)
+        assert torch.equal(po, pt)
+        # page-locked in, pageable out: the drain-thread path
+        pg = np.empty_like(h)
+        _lib.call("tips_allreduce", pt.data_ptr(), pg.ctypes.data, n, _lib.FLOAT32, _lib.OP_SUM, None)
+        assert np.array_equal(pg, h)
         hi = rng.integers(-2**62, 2**62, size=n // 3, dtype=np.int64)
         assert np.array_equal(gpu.allreduce(hi), hi)
 
