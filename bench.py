@@ -454,7 +454,7 @@ def bench_allreduce(args):
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 50 * 1e3
         kbytes = (nsrc + 1) * m * 4
-        kernel_roof = {"kernel": "multi_sum_kernel" if nsrc > 2 else "sum2_kernel", "sources": nsrc,
+        kernel_roof = {"kernel": "multi_sum_buf_kernel" if nsrc > 2 else "sum2_buf_kernel", "sources": nsrc,
                        "elements_per_launch": m, "launches_per_step": depth.value * (world - 1 if nsrc == 2 else 1),
                        "bound": "hbm", "achieved": round(kbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                        "unit": "GB/s", "frac": round(kbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
