@@ -394,3 +394,23 @@ def test_named_async_allreduce_single_rank(gpu):
     assert torch.equal(hp.output, ts[2])
     with pytest.raises(ValueError):
         gpu.allreduce_async(torch.zeros(3), "host")
+
+
+def test_sparse_allreduce_single_rank(gpu):
+    """The reference's IndexedSlices branch (allgather of values and indices, __init__.py:59-74) through
+    tips_allgatherv on one rank: device and host, IndexedSlices and torch sparse COO."""
+    import torch
+    vals = torch.randn(7, 4, device="cuda")
+    idx = torch.tensor([3, 0, 3, 9, 1, 1, 2], device="cuda")
+    s = gpu.allreduce(gpu.IndexedSlices(vals, idx, dense_shape=(10, 4)))
+    assert torch.equal(s.values, vals) and torch.equal(s.indices, idx)
+    a = gpu.allreduce(gpu.IndexedSlices(vals, idx, dense_shape=(10, 4)), op=gpu.Average)
+    assert torch.equal(a.values, vals)  # size() == 1
+    hv = np.arange(12, dtype=np.float64).reshape(6, 2)
+    hs = gpu.allreduce(gpu.IndexedSlices(hv, np.arange(6), dense_shape=(6, 2)))
+    assert np.array_equal(hs.values, hv)
+    for dev in ("cuda", "cpu"):
+        dense = torch.zeros(50, 3, device=dev)
+        dense[[3, 17, 40], 1] = torch.tensor([1.0, -2.0, 0.5], device=dev)
+        out = gpu.allreduce(dense.to_sparse())
+        assert out.is_sparse and torch.equal(out.to_dense(), dense)

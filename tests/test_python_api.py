@@ -85,3 +85,42 @@ def test_allreduce_without_gpu_raises_not_computes():
     if torch.cuda.is_available():
         pytest.skip("a device is present")
     assert "RAISED" in r.stdout, r.stdout + r.stderr
+
+
+def _fake_two_ranks(monkeypatch):
+    """allgather over two ranks that hold the same tensor, without a GPU: the host logic of the sparse
+    branch (__init__.py:59-74 of the reference) is what is under test here."""
+    import torch
+    import tips_amd
+
+    def gather(t, name=None):
+        return torch.cat([t, t]) if isinstance(t, torch.Tensor) else np.concatenate([t, t])
+
+    monkeypatch.setattr(tips_amd, "allgather_op", gather)
+    monkeypatch.setattr(tips_amd, "size", lambda: 2)
+
+
+def test_indexed_slices_take_the_allgather_branch(monkeypatch):
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    vals = np.arange(6, dtype=np.float32).reshape(3, 2)
+    idx = np.array([4, 0, 4], dtype=np.int64)
+    s = tips_amd.allreduce(tips_amd.IndexedSlices(vals, idx, dense_shape=(5, 2)))
+    assert isinstance(s, tips_amd.IndexedSlices) and s.dense_shape == (5, 2)
+    assert np.array_equal(s.values, np.concatenate([vals, vals])) and np.array_equal(s.indices, np.tile(idx, 2))
+    a = tips_amd.allreduce(tips_amd.IndexedSlices(vals, idx, dense_shape=(5, 2)), op=tips_amd.Average)
+    assert np.array_equal(a.values, np.concatenate([vals, vals]) / 2)  # the reference divides here
+
+
+def test_torch_sparse_allreduce_represents_the_sum(monkeypatch):
+    import torch
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    dense = torch.zeros(6, 3)
+    dense[1, 2] = 1.5
+    dense[4, 0] = -2.0
+    sp = dense.to_sparse()
+    out = tips_amd.allreduce(sp)
+    assert out.is_sparse and out.shape == dense.shape
+    assert torch.equal(out.to_dense(), 2 * dense)
+    assert torch.equal(tips_amd.allreduce(sp, op=tips_amd.Average).to_dense(), dense)

@@ -16,8 +16,19 @@ from . import tensors as _tensors
 Average = 'Average'
 Sum = 'Sum'
 
+
+class IndexedSlices(object):
+    """A sparse gradient: rows `values` of a dense tensor of `dense_shape`, at row `indices`
+    (what tf.IndexedSlices carries, e.g. an embedding gradient). The represented tensor is the
+    sum over repeated indices."""
+
+    def __init__(self, values, indices, dense_shape=None):
+        self.values = values
+        self.indices = indices
+        self.dense_shape = dense_shape
+
 __all__ = [
-    "allreduce", "allreduce_async", "poll", "synchronize", "Handle", "allreduce_grads", "allreduce_op", "allgather_op", "broadcast_op", "broadcast_variables",
+    "allreduce", "IndexedSlices", "allreduce_async", "poll", "synchronize", "Handle", "allreduce_grads", "allreduce_op", "allgather_op", "broadcast_op", "broadcast_variables",
     "set_consistency_check", "registered_host_buffer", "bucket_sum", "fused_allreduce_", "init", "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
@@ -40,12 +51,28 @@ def allreduce(tensor,
     are commented out at the C++ boundary, __init__.py:82-87), so the result
     is the plain SUM for op=Average too — parity with the
     reference, not a recommendation. `average`, `device_dense` and
-    `device_sparse` are accepted for signature compatibility. Sparse
-    (IndexedSlices-style) tensors take the reference's allgather branch,
-    which is out of scope here: they raise.
+    `device_sparse` are accepted for signature compatibility.
+
+    Sparse gradients take the reference's allgather branch (__init__.py:59-74).
+    An `IndexedSlices` gets its values and indices allgathered, and they are
+    divided by size() for op=Average, as the reference does there. A torch
+    sparse COO tensor gets the same treatment on its nonzeros. The result
+    represents the summed tensor.
     """
+    if isinstance(tensor, IndexedSlices):
+        values = allgather_op(tensor.values)
+        indices = allgather_op(tensor.indices)
+        new_values = (values / size()) if op == Average else values
+        return IndexedSlices(new_values, indices, dense_shape=tensor.dense_shape)
     if _tensors.is_torch(tensor) and tensor.is_sparse:
-        raise NotImplementedError("sparse allreduce (allgather branch) is not part of this path")
+        import torch
+        idx = tensor._indices().t().contiguous()  # (nnz, ndim): rows concatenate along dim 0
+        vals = tensor._values().contiguous()
+        g_idx = allgather_op(idx).t()
+        g_vals = allgather_op(vals)
+        if op == Average:
+            g_vals = g_vals / size()
+        return torch.sparse_coo_tensor(g_idx, g_vals, tensor.shape)
     tensor_compressed, ctx = compression.compress(tensor)
     summed_tensor_compressed = allreduce_op(tensor_compressed, name=name)
     return compression.decompress(summed_tensor_compressed, ctx)

@@ -606,6 +606,18 @@ hipError_t run_multi_variant(void* dst, const SrcList& sl, int64_t n, int varian
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 4, 2>), dim3(grid_for(4)), dim3(kBlock), 0, s,
                          (u32x4*)dst, sl, nvec, nvec * 4, n);
       break;
+    case 5:  // sc0 loads
+      hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 1>), dim3(grid_for(1)), dim3(kBlock), 0, s,
+                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+      break;
+    case 6:  // sc1 loads
+      hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 16>), dim3(grid_for(1)), dim3(kBlock), 0, s,
+                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+      break;
+    case 7:  // plain loads, 2 vectors per lane
+      hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 2, 0>), dim3(grid_for(2)), dim3(kBlock), 0, s,
+                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+      break;
     default:
       return hipErrorInvalidValue;
   }

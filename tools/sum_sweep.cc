@@ -81,8 +81,8 @@ int main(int argc, char** argv) {
   // multi-input sum variants (tips_multi_sum_variant): unroll field = nsrc, nt field = variant
   // blocks field = extra bytes between consecutive sources (0 = back to back, power-of-2 strides)
   for (int ns : {4, 8})
-    for (int var = 0; var <= 4; var++)
-      for (int pad : {0, 256, 4096, 65536 + 256})
+    for (int var = 0; var <= 7; var++)
+      for (int pad : {0, 4096})
         vs.push_back({"multi" + std::to_string(ns) + "_v" + std::to_string(var) + "_pad" + std::to_string(pad), -5, ns,
                       var, pad, 0, {}});
   if (argc > 4) {  // optional name filter; the references always stay
