@@ -124,3 +124,16 @@ def test_torch_sparse_allreduce_represents_the_sum(monkeypatch):
     assert out.is_sparse and out.shape == dense.shape
     assert torch.equal(out.to_dense(), 2 * dense)
     assert torch.equal(tips_amd.allreduce(sp, op=tips_amd.Average).to_dense(), dense)
+
+
+def test_allreduce_grads_routes_sparse_to_allgather(monkeypatch):
+    import torch
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    dense = torch.zeros(4, 2)
+    dense[2, 1] = 3.0
+    sl = tips_amd.IndexedSlices(np.ones((1, 2), np.float32), np.array([3]), dense_shape=(4, 2))
+    out = tips_amd.allreduce_grads([None, dense.to_sparse(), sl])
+    assert out[0] is None
+    assert torch.equal(out[1].to_dense(), 2 * dense)
+    assert np.array_equal(out[2].indices, [3, 3])

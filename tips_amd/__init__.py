@@ -100,7 +100,7 @@ def allreduce_grads(grads, compression=Compression.none, op=None, fused=True):
     if fused:
         groups = {}
         for i, g in enumerate(grads):
-            if g is not None and _tensors.is_device(g):
+            if _fusable(g):
                 groups.setdefault(g.dtype, []).append(i)
         for idx in groups.values():
             clones = []
@@ -111,6 +111,11 @@ def allreduce_grads(grads, compression=Compression.none, op=None, fused=True):
             for i, c, ctx in clones:
                 out[i] = compression.decompress(c, ctx)
     for i, g in enumerate(grads):
-        if g is not None and (not fused or not _tensors.is_device(g)):
+        if g is not None and (not fused or not _fusable(g)):
             out[i] = allreduce(g, compression=compression, op=op)
     return out
+
+
+def _fusable(g):
+    """Dense device tensors go through the fusion buckets; sparse and host ones are reduced one by one."""
+    return g is not None and _tensors.is_device(g) and not g.is_sparse
