@@ -52,6 +52,9 @@ def main():
              ("registered_numpy", reg_in.ctypes.data, reg_out.ctypes.data),
              ("hipHostMalloc_default", hm[0][0], hm[0][1]),
              ("hipHostMalloc_mapped", hm[1][0], hm[1][1])]
+    if os.environ.get("PAGEABLE_FIRST") == "1":  # the order bench.py measures in
+        kinds = [kinds[1], kinds[0]] + kinds[2:]
+    extra = [torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(int(os.environ.get("EXTRA_PINNED", "0")))]
     sizes = [int(x) for x in os.environ.get("PIECES_MIB", "4,8,16,32,64").split(",")]
     rounds = int(os.environ.get("ROUNDS", "1"))
     for mib in [m for _ in range(rounds) for m in sizes]:
