@@ -189,7 +189,11 @@ TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int 
  * rules and error text, and every rank reduces them in rank 0's
  * readiness order (as ready_to_reduce), on the stream passed here. Device pointers only.
  * Returns a handle > 0, or a negative status. The first call starts the
- * thread (collective); tips_shutdown stops it (collective). */
+ * thread (collective); tips_shutdown stops it (collective).
+ * While named requests are in flight, do not issue the synchronous
+ * collectives (tips_allreduce, tips_broadcast, ...) from another thread:
+ * RCCL needs the same call order on every rank, and only the negotiated
+ * requests are ordered by rank 0. */
 TIPS_API int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype,
                                         void* stream);
 /* 1 = done (handle released), 0 = pending, < 0 = error (message in tips_last_error). */
