@@ -3,7 +3,7 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 LIB      := tips_amd/lib/libtips_hip.so
 SRCS     := tips_amd/csrc/kernels.hip tips_amd/csrc/runtime.cc tips_amd/csrc/rt_common.cc tips_amd/csrc/schedules.cc \
-            tips_amd/csrc/fusion.cc tips_amd/csrc/host_staging.cc tips_amd/csrc/control.cc tips_amd/csrc/negotiate.cc \
+            tips_amd/csrc/fusion.cc tips_amd/csrc/host_staging.cc tips_amd/csrc/control.cc tips_amd/csrc/negotiate.cc tips_amd/csrc/peer.cc \
             tips_amd/csrc/bootstrap.cc
 HDRS     := tips_amd/csrc/kernels.h tips_amd/csrc/rt.h tips_amd/csrc/net.h include/tips_hip.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-result -fvisibility=hidden

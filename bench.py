@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--algo", default=os.environ.get("TIPS_ALGO", "auto"),
-                    choices=["auto", "ring", "direct", "rccl", "oneshot"])
+                    choices=["auto", "ring", "direct", "rccl", "oneshot", "peer"])
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
@@ -320,14 +320,14 @@ def bench_allreduce(args):
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "420")), rank)
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))  # (several ranks per GPU only under TIPS_NO_RCCL)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import tips_amd
     from tips_amd import _lib
     tips_amd.init()  # unique id through the gloo group, one RCCL communicator per GPU
     L = _lib.lib()
     algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL,
-                  "oneshot": _lib.ALGO_ONESHOT}
+                  "oneshot": _lib.ALGO_ONESHOT, "peer": _lib.ALGO_PEER}
     inv = {v: k for k, v in algo_names.items()}
     _lib.call("tips_set_algorithm", algo_names[args.algo])
 
@@ -408,25 +408,29 @@ def bench_allreduce(args):
     ms = t / steps * 1e3
 
     # parity: one fresh call, then fold all ranks' seeded inputs on this device (rank order) and compare
-    fill(x, rank)
-    step()
-    torch.cuda.synchronize()
-    tmp = torch.empty_like(x)
-    ref = None
-    for r in range(world):
-        fill(tmp, r)
-        ref = tmp.clone() if ref is None else ref + tmp
-    got = torch.cat([y[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else y
-    exp = torch.cat([ref[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else ref
-    if algo == _lib.ALGO_DIRECT or world == 1:
-        ok = bool(torch.equal(got, exp))
-        check = "bit-exact vs rank-order fold of all ranks' inputs" if ok else "FAIL (not bit-exact)"
-    else:
-        rel = ((got.double() - exp.double()).abs() / exp.double()).max().item()
-        ok = rel <= 1e-6
-        check = ("max rel err %.2e vs rank-order fold (bound 1e-6)" % rel) if ok else ("FAIL rel %.2e" % rel)
+    def parity(algo_now):
+        fill(x, rank)
+        step()
+        torch.cuda.synchronize()
+        tmp = torch.empty_like(x)
+        ref = None
+        for r in range(world):
+            fill(tmp, r)
+            ref = tmp.clone() if ref is None else ref + tmp
+        got = torch.cat([y[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else y
+        exp = torch.cat([ref[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else ref
+        if algo_now in (_lib.ALGO_DIRECT, _lib.ALGO_PEER) or world == 1:
+            good = bool(torch.equal(got, exp))
+            msg = "bit-exact vs rank-order fold of all ranks' inputs" if good else "FAIL (not bit-exact)"
+        else:
+            rel = ((got.double() - exp.double()).abs() / exp.double()).max().item()
+            good = rel <= 1e-6
+            msg = ("max rel err %.2e vs rank-order fold (bound 1e-6)" % rel) if good else ("FAIL rel %.2e" % rel)
+        del ref, tmp, got, exp
+        return good, msg
+
+    ok, check = parity(algo)
     all_ok = all_ranks_ok(dist, ok)
-    del ref, tmp, got, exp
 
     # the reduce kernel of this schedule, timed alone at its per-launch shape (HBM roofline)
     kernel_roof = None
@@ -474,7 +478,9 @@ def bench_allreduce(args):
         "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % seed0,
         "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
                    "algorithm": inv.get(algo, str(algo)),
-                   "parallelism": "dp%d (one process per GPU, RCCL p2p over xGMI)" % world},
+                   "parallelism": "dp%d (one process per GPU, %s)" % (
+                       world, "our kernels through IPC-mapped peer memory over xGMI" if algo == _lib.ALGO_PEER
+                       else "ncclAllReduce" if algo == _lib.ALGO_RCCL else "RCCL p2p over xGMI")},
         "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
         "xgmi": {"busbw_GBps": round(busbw / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS, "links_used": links,
                  "frac_of_links_used": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4),
@@ -493,19 +499,28 @@ def bench_allreduce(args):
 
     # comparison points on the same workload: the other schedules and ncclAllReduce (optional; a hang
     # here is caught by the watchdog, which then still prints the line above)
-    compare = {}
+    compare, compare_check = {}, {}
     if not args.no_compare:
         kc = max(3, steps // 4)
-        for name in ("ring", "direct", "rccl"):  # (oneshot targets small buckets only)
-            if algo_names[name] == algo:
+        # (oneshot targets small buckets only). peer = the same exchange by our own kernels over
+        # IPC-mapped peer memory; measured here (the driver's 8-GPU run) before it can be a default.
+        for name in ("ring", "direct", "rccl", "peer"):
+            if algo_names[name] == algo or (name == "peer" and workload != "bucket"):
                 continue
-            _lib.call("tips_set_algorithm", algo_names[name])
-            for _ in range(2):
-                step()
-            torch.cuda.synchronize()
-            tc = timed(kc)
-            compare[name] = round(total_elems * 4 / (tc / kc) / GIB, 2)
+            try:
+                _lib.call("tips_set_algorithm", algo_names[name])
+                for _ in range(2):
+                    step()
+                torch.cuda.synchronize()
+                tc = timed(kc)
+                compare[name] = round(total_elems * 4 / (tc / kc) / GIB, 2)
+                good, msg = parity(algo_names[name])
+                compare_check[name] = msg if all_ranks_ok(dist, good) else "FAIL on some rank (%s here)" % msg
+            except Exception as e:  # noqa: BLE001 - a comparison point never costs the main line
+                compare[name] = None
+                compare_check[name] = "error: %s" % (e,)
         _lib.call("tips_set_algorithm", algo_names[args.algo])
+    line["compare_check"] = compare_check
     line["compare_algbw_gib_s"] = compare
     if rank == 0:
         print(json.dumps(line), flush=True)

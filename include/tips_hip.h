@@ -69,6 +69,8 @@ enum tips_algorithm {
   TIPS_ALGO_DIRECT = 1, /* all-pairs RS over every xGMI link + p-input sum kernel + AG */
   TIPS_ALGO_RCCL = 2,   /* ncclAllReduce, kept as a comparison point only */
   TIPS_ALGO_ONESHOT = 3, /* whole bucket to every peer in one step + one p-input fold (small buckets) */
+  TIPS_ALGO_PEER = 4,    /* direct's exchange by our own kernels through IPC-mapped peer memory (no RCCL):
+                            push + rank-order fold + pull, phases ordered by a node-local shared-memory barrier */
 };
 
 /* ---- lifecycle: same names and types as tips/core/operations.h:7-21 ---- */

@@ -1,0 +1,65 @@
+"""One rank of the peer schedule's multi-process test (tests/test_gpu_peer.py).
+
+Run as: python peer_worker.py RANK SIZE UID_HEX CASES_JSON
+Every rank of the job runs on GPU 0 of the test box (TIPS_NO_RCCL=1: no RCCL
+communicator, which would refuse two ranks on one device). The ranks share
+nothing but the IPC workspaces and the node-local control block, exactly as
+on an 8-GPU node, so this exercises the whole peer path: the shared-memory
+barriers, the handle exchange, the workspace growth, the push / fold / pull
+kernels and the cross-rank count check. Each case's inputs are seeded per
+rank; every rank regenerates all ranks' inputs and checks its result bit-exact
+against the oracle's rank-order fold (oracle/oracle.c: oracle_fold).
+Prints one JSON line: {"rank": r, "results": [...]}.
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+os.environ["TIPS_NO_RCCL"] = "1"
+
+
+def main():
+    rank, size, uid, cases = int(sys.argv[1]), int(sys.argv[2]), bytes.fromhex(sys.argv[3]), json.loads(sys.argv[4])
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    import oracle_bind
+    from gpu_util import from_dev, rand, same_bits, to_dev
+    from tips_amd import _lib
+
+    oracle_bind.load()
+    L = _lib.lib()
+    torch.cuda.set_device(0)
+    idbuf = ctypes.create_string_buffer(uid, len(uid))
+    _lib.call("tips_init_rank", rank, size, 0, idbuf, len(uid))
+    _lib.call("tips_set_algorithm", _lib.ALGO_PEER)
+    sp = torch.cuda.current_stream().cuda_stream
+    results = []
+    for c in cases:
+        dtype, n, seed = c["dtype"], c["n"], c["seed"]
+        if c.get("count_per_rank"):  # deliberately inconsistent counts: every rank must fail, none hang
+            n = c["count_per_rank"][rank]
+        ins = [rand(dtype, n, np.random.default_rng(seed + r)) for r in range(size)]
+        x = to_dev(ins[rank])
+        y = x if c.get("inplace") else torch.empty_like(x)
+        rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, sp)
+        torch.cuda.synchronize()
+        res = {"case": c, "rc": int(rc)}
+        if rc == 0:
+            exp = oracle_bind.fold(ins, code=dtype, wide_acc=True)
+            res["ok"] = bool(same_bits(from_dev(y, dtype), exp, dtype))
+        else:
+            res["error"] = _lib.last_error()
+            res["ok"] = bool(c.get("expect_error")) and rc == c["expect_error"]
+        results.append(res)
+    L.tips_shutdown()
+    print(json.dumps({"rank": rank, "results": results}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

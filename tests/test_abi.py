@@ -82,7 +82,7 @@ def test_algorithm_resolution():
     assert L.tips_resolve_algorithm(32, small) == _lib.ALGO_RING  # more ranks than the fold takes sources
     L.tips_set_algorithm(_lib.ALGO_RING)
     assert L.tips_resolve_algorithm(8, small) == _lib.ALGO_RING
-    assert L.tips_set_algorithm(4) == -1
+    assert L.tips_set_algorithm(5) == -1
     L.tips_set_algorithm(prev)
 
 

@@ -1,0 +1,84 @@
+"""-m gpu: the peer schedule (TIPS_ALGO_PEER) across real processes.
+
+p ranks run as p processes on the box's one GPU (tests/peer_worker.py,
+TIPS_NO_RCCL=1): each exports its uncached workspace over IPC, opens the
+others', and reduces through the push / rank-order fold / pull kernels with
+the shared-memory barriers between the phases — the same code that runs one
+rank per GPU over xGMI on an 8-GPU node. Results are checked bit-exact against
+the oracle's rank-order fold (the direct schedule's bits). Cases cover every
+dtype, ragged and empty-tail sizes, in place, workspace growth (small then
+large buckets) and a cross-rank count mismatch, which must fail on every rank
+with TIPS_ERR_MISMATCH and leave the job usable for the next call.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from gpu_util import ALL_DTYPES, F32, I64
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ERR_MISMATCH = -7
+
+
+def run_job(p, cases, timeout=300, **extra_env):
+    uid = os.urandom(128).hex()
+    env = dict(os.environ, TIPS_NO_RCCL="1", TIPS_PEER_TIMEOUT_S="60", TIPS_VERBOSE="1", **extra_env)
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "peer_worker.py"), str(r), str(p), uid,
+                               json.dumps(cases)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for r in range(p)]
+    outs = []
+    try:
+        for pr in procs:
+            o, e = pr.communicate(timeout=timeout)
+            outs.append((pr.returncode, o, e))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+                pr.wait()
+    results = []
+    for r, (rc, o, e) in enumerate(outs):
+        assert rc == 0, "rank %d exited %d:\n%s" % (r, rc, e[-3000:])
+        line = [ln for ln in o.splitlines() if ln.startswith("{")][-1]
+        res = json.loads(line)
+        res["stderr"] = e[-2000:]
+        results.append(res)
+    return results
+
+
+def check(results):
+    bad = ["rank %d: %r" % (res["rank"], c) for res in results for c in res["results"] if not c["ok"]]
+    errs = ["rank %d stderr: %s" % (res["rank"], res["stderr"]) for res in results if res["stderr"].strip()]
+    assert not bad, "\n".join(bad[:12] + errs)
+
+
+@pytest.mark.parametrize("p", [2, 3, 4])
+def test_peer_schedule_all_dtypes(gpu, p):
+    cases = []
+    for dtype in ALL_DTYPES:
+        for n in (1, 7, 4099, 1000003):
+            cases.append({"dtype": dtype, "n": n, "seed": 100 * dtype + n % 89})
+    cases.append({"dtype": F32, "n": 262147, "seed": 5, "inplace": True})
+    cases.append({"dtype": I64, "n": 4099, "seed": 6, "inplace": True})
+    check(run_job(p, cases))
+
+
+def test_peer_schedule_pieces_and_mismatch(gpu):
+    """A 4 MiB workspace: the 64 MiB buckets go through in many pieces."""
+    p = 3
+    cases = [
+        {"dtype": F32, "n": 1000, "seed": 1},
+        {"dtype": F32, "n": 1 << 24, "seed": 2},
+        {"dtype": F32, "n": 5000, "seed": 3, "count_per_rank": [5000, 5000, 5001], "expect_error": ERR_MISMATCH},
+        {"dtype": I64, "n": 3 << 20, "seed": 4},             # the job still works after the refused call
+        {"dtype": F32, "n": (1 << 24) + 3, "seed": 7, "inplace": True},
+    ]
+    results = run_job(p, cases, TIPS_PEER_WS_MIB="4")
+    check(results)
+    for res in results:
+        assert "rank 2" in res["results"][2]["error"] or "5001" in res["results"][2]["error"]

@@ -19,7 +19,7 @@ OP_SUM, OP_MAX, OP_MIN = 0, 1, 2
 REQ_ALLREDUCE, REQ_ALLGATHER, REQ_BROADCAST = 0, 1, 2
 MAX_DIMS = 8
 REQUEST_WORDS = 3 + MAX_DIMS
-ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_ONESHOT = -1, 0, 1, 2, 3
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_ONESHOT, ALGO_PEER = -1, 0, 1, 2, 3, 4
 
 STATUS_NAMES = {
     0: "TIPS_OK",

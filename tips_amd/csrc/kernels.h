@@ -25,6 +25,19 @@ struct CopyTile {
 constexpr int64_t kCopyTileBytes = 64 * 1024;
 hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t s);
 
+// Peer transfers of the xGMI peer schedule (peer.cc): up to kMaxXferSegs byte
+// segments {src, dst, bytes} copied by one launch, segments interleaved over
+// the workgroups so every xGMI link carries traffic at once. src/dst may be
+// IPC-mapped peer memory. Passed by value (kernel argument), no descriptor upload.
+struct XferSeg {
+  const char* src;
+  char* dst;
+  int64_t bytes;
+};
+constexpr int kMaxXferSegs = 16;
+constexpr int64_t kXferTileBytes = 16 * 1024;  // per workgroup: 256 lanes x 4 x 16 B
+hipError_t launch_xfer(const XferSeg* segs, int nseg, hipStream_t s);
+
 // Tuning/sweep entry for the multi-input sum (f32, nsrc 2/4/8); variants in kernels.hip.
 hipError_t launch_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, int variant,
                                    hipStream_t s);

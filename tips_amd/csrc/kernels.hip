@@ -435,6 +435,44 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __re
 }
 
 // ---------------------------------------------------------------------------
+// Peer transfer (xGMI peer schedule, peer.cc)
+
+struct XferList {
+  XferSeg s[kMaxXferSegs];
+};
+
+// Workgroup b copies tile b / nseg of segment b % nseg: consecutive workgroups
+// (and so every XCD) cover all segments, i.e. all peers' links, at once. Each
+// lane issues its four 16-B loads before any store: a remote access over xGMI
+// takes microseconds, so bytes in flight, not instructions, set the rate. The
+// descriptors cover exactly the tile's 16-B-multiple prefix; the < 16 bytes
+// past it (a ragged last chunk) go bytewise.
+__global__ __launch_bounds__(kBlock) void xfer_kernel(XferList L, int nseg) {
+  constexpr int U = (int)(kXferTileBytes / (kBlock * 16));
+  const int seg = (int)(blockIdx.x % (unsigned)nseg);
+  const int64_t off = (int64_t)(blockIdx.x / (unsigned)nseg) * kXferTileBytes;
+  const XferSeg sg = L.s[seg];
+  if (off >= sg.bytes) return;
+  const int64_t len = sg.bytes - off < kXferTileBytes ? sg.bytes - off : kXferTileBytes;
+  const char* src = sg.src + off;
+  char* dst = sg.dst + off;
+  const int tid = threadIdx.x;
+  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+    const int len16 = (int)(len & ~(int64_t)15);
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, len16, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, len16, 0x00020000);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (u * kBlock + tid) * 16, 0, 0);
+    if (len16 + tid < len) dst[len16 + tid] = src[len16 + tid];
+  } else {
+    for (int64_t i = tid; i < len; i += kBlock) dst[i] = src[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 
 namespace {
@@ -719,6 +757,23 @@ hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t 
   if (ntiles <= 0) return hipSuccess;
   const unsigned grid = (unsigned)((ntiles + 7) / 8 * 8);
   hipLaunchKernelGGL(copy_tiles_kernel, dim3(grid), dim3(kBlock), 0, s, tiles_dev, ntiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_xfer(const XferSeg* segs, int nseg, hipStream_t s) {
+  if (nseg < 0 || nseg > kMaxXferSegs) return hipErrorInvalidValue;
+  XferList L{};
+  int64_t max_tiles = 0;
+  int m = 0;
+  for (int i = 0; i < nseg; i++) {
+    if (segs[i].bytes <= 0) continue;
+    L.s[m++] = segs[i];
+    max_tiles = std::max<int64_t>(max_tiles, (segs[i].bytes + kXferTileBytes - 1) / kXferTileBytes);
+  }
+  if (m == 0) return hipSuccess;
+  const int64_t grid = max_tiles * m;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(xfer_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, L, m);
   return hipGetLastError();
 }
 

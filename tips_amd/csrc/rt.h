@@ -137,6 +137,8 @@ struct FusionPlan {
   std::vector<int> unfused;  // indices allreduced in place
 };
 
+struct PeerState;  // peer.cc
+
 struct State {
   std::mutex mu;
   bool initialized = false;
@@ -155,6 +157,8 @@ struct State {
   int algo = TIPS_ALGO_AUTO;
   int sim_transport = 0;  // simulators: 0 = device copies, 1 = RCCL send/recv to self
   std::unordered_map<uint64_t, FusionPlan> plans;
+  uint64_t peer_key = 0;      // names the node-local control block of the peer schedule (hash of the unique id)
+  PeerState* peer = nullptr;  // peer schedule: IPC workspaces + shared-memory barrier, created on first use
 };
 
 State& S();
@@ -172,6 +176,9 @@ int ensure_comm(State& st);
 
 // schedules.cc: device-resident allreduce, caller holds st.mu
 int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream);
+// peer.cc: allreduce over IPC-mapped peer memory (1 < p <= kMaxSrcs, one node), caller holds st.mu
+int peer_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t stream);
+void peer_release(State& st);  // collective (shutdown)
 // host_staging.cc: host-resident allreduce over pipelined pieces, caller holds st.mu
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
 // fusion.cc

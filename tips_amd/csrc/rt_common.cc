@@ -93,6 +93,7 @@ int resolve_algo(int algo, int p, int64_t bytes) {
       if (!strcmp(e, "direct")) algo = TIPS_ALGO_DIRECT;
       if (!strcmp(e, "rccl")) algo = TIPS_ALGO_RCCL;
       if (!strcmp(e, "oneshot")) algo = TIPS_ALGO_ONESHOT;
+      if (!strcmp(e, "peer")) algo = TIPS_ALGO_PEER;
     }
   }
   if (algo != TIPS_ALGO_AUTO) return algo;

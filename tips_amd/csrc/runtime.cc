@@ -57,7 +57,12 @@ int tips_init_rank(int rank, int size, int device, const void* unique_id, int64_
       return fail(TIPS_ERR_INVALID_ARG, "unique id must be %zu bytes", sizeof(ncclUniqueId));
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof id);
-    NCCL_TRY(ncclCommInitRank(&st.comm, size, id, rank));
+    // TIPS_NO_RCCL=1: no communicator (only the peer schedule, which needs none, can run). Lets
+    // several ranks share one GPU, which RCCL refuses: the peer schedule's multi-process tests.
+    if (!env_i64("TIPS_NO_RCCL", 0)) NCCL_TRY(ncclCommInitRank(&st.comm, size, id, rank));
+    uint64_t h = 1469598103934665603ull;  // FNV-1a of the id: the peer schedule's node-local block name
+    for (size_t i = 0; i < sizeof id; i++) h = (h ^ ((const unsigned char*)unique_id)[i]) * 1099511628211ull;
+    st.peer_key = h ? h : 1;
   }
   st.rank = rank;
   st.size = size;
@@ -98,6 +103,8 @@ void tips_shutdown(void) {
   if (st.device >= 0) (void)hipSetDevice(st.device);
   if (st.comm_stream) (void)hipStreamSynchronize(st.comm_stream);
   if (st.comp_stream) (void)hipStreamSynchronize(st.comp_stream);
+  peer_release(st);  // collective: no rank frees its IPC workspace while a peer may still read it
+  st.peer_key = 0;
   if (st.comm) {
     (void)ncclCommDestroy(st.comm);
     st.comm = nullptr;
@@ -145,7 +152,7 @@ int tips_size(void) { return S().initialized ? S().size : -1; }
 int tips_rank(void) { return S().initialized ? S().rank : -1; }
 
 int tips_set_algorithm(int algo) {
-  if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_ONESHOT) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
+  if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_PEER) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   st.algo = algo;

@@ -240,9 +240,9 @@ class registered_host_buffer(object):
 
 
 def set_algorithm(algo):
-    """Select 'auto', 'ring', 'direct', 'oneshot' or 'rccl'; returns the previous selection's name."""
+    """Select 'auto', 'ring', 'direct', 'oneshot', 'peer' or 'rccl'; returns the previous selection's name."""
     names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL,
-             "oneshot": _lib.ALGO_ONESHOT}
+             "oneshot": _lib.ALGO_ONESHOT, "peer": _lib.ALGO_PEER}
     inv = {v: k for k, v in names.items()}
     prev = _lib.lib().tips_get_algorithm()
     _lib.call("tips_set_algorithm", names[algo])
