@@ -17,7 +17,13 @@ $(LIB): $(SRCS) $(HDRS)
 oracle:
 	$(MAKE) -C oracle
 
-tools: tools/sum_sweep tools/cpu_sum_bench
+tools: tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
+
+tools/peer_mem_probe: tools/peer_mem_probe.cc $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../tips_amd/lib'
+
+tools/ipc_probe: tools/ipc_probe.cc
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -o $@ $<
 
 tools/cpu_sum_bench: tools/cpu_sum_bench.c
 	gcc -O3 -fopenmp -o $@ $<
@@ -26,7 +32,7 @@ tools/sum_sweep: tools/sum_sweep.cc $(LIB)
 	$(HIPCC) -O2 -std=c++17 -o $@ $< -Itips_amd -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../tips_amd/lib'
 
 clean:
-	rm -f $(LIB) tools/sum_sweep tools/cpu_sum_bench
+	rm -f $(LIB) tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle tools clean

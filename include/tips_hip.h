@@ -256,6 +256,11 @@ TIPS_API int tips_sum_variant(void* dst, const void* a, const void* b, int64_t c
 TIPS_API int tips_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, int variant,
                                     void* stream);
 
+/* The peer schedule's transfer kernel on its own (tests, tools/peer_mem_probe.cc):
+ * copies bytes[i] from srcs[i] to dsts[i] for n <= 16 segments in one launch,
+ * any alignment; pointers may be IPC-mapped peer memory. */
+TIPS_API int tips_xfer(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, void* stream);
+
 /* Pipeline shape the ring/direct schedules use for a bucket: depth = K
  * sub-chunks per chunk, sub_elems = elements in a (first) sub-chunk, i.e. the
  * size of one reduce-kernel launch (TIPS_PIPELINE_DEPTH, TIPS_MIN_SUBCHUNK_BYTES). */

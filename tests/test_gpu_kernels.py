@@ -148,3 +148,31 @@ def test_count_beyond_int32(gpu):
     torch.cuda.synchronize()
     assert torch.equal(c, a + b)
     assert torch.equal(c[-13:], a[-13:] + b[-13:])
+
+
+@pytest.mark.parametrize("nseg", [1, 3, 7, 16])
+@pytest.mark.parametrize("shift", [0, 1, 4, 16])
+def test_xfer_segments(gpu, nseg, shift):
+    """The peer schedule's transfer kernel: ragged segment sizes (0, < 16 B, tile multiples and
+    not), 16-B-aligned and misaligned pointers; every byte copied, nothing written outside."""
+    import torch
+    from tips_amd import _lib
+    rng = np.random.default_rng(nseg * 100 + shift)
+    sizes = [int(x) for x in rng.choice([0, 1, 15, 16, 17, 4096, 16384, 16385, 65536 + 48, 1000003], size=nseg)]
+    src = torch.from_numpy(rng.integers(0, 256, size=sum(sizes) + 64 * nseg + 64, dtype=np.uint8)).cuda()
+    dst = torch.full((sum(sizes) + 64 * nseg + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    offs, o = [], shift
+    for k in sizes:
+        offs.append(o)
+        o += k + 48 + shift
+    pd, _k1 = _lib.ptr_array([dst.data_ptr() + x for x in offs])
+    ps, _k2 = _lib.ptr_array([src.data_ptr() + x for x in offs])
+    pb, _k3 = _lib.i64_array(sizes)
+    _lib.call("tips_xfer", pd, ps, pb, nseg, stream())
+    torch.cuda.synchronize()
+    d, s = dst.cpu().numpy(), src.cpu().numpy()
+    mask = np.zeros(len(d), dtype=bool)
+    for x, k in zip(offs, sizes):
+        assert np.array_equal(d[x:x + k], s[x:x + k])
+        mask[x:x + k] = True
+    assert np.all(d[~mask] == 0xAB)

@@ -206,6 +206,18 @@ int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, 
   return 0;
 }
 
+int tips_xfer(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, void* stream) {
+  if (n < 0 || n > tips::kMaxXferSegs || (n > 0 && (!dsts || !srcs || !bytes)))
+    return fail(TIPS_ERR_INVALID_ARG, "tips_xfer takes 0..%d segments", tips::kMaxXferSegs);
+  tips::XferSeg segs[tips::kMaxXferSegs];
+  for (int i = 0; i < n; i++) {
+    if (bytes[i] < 0 || (bytes[i] > 0 && (!dsts[i] || !srcs[i]))) return fail(TIPS_ERR_INVALID_ARG, "bad segment %d", i);
+    segs[i] = {(const char*)srcs[i], (char*)dsts[i], bytes[i]};
+  }
+  HIP_TRY(tips::launch_xfer(segs, n, (hipStream_t)stream));
+  return 0;
+}
+
 int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream) {
   TRY(check_dtype(dtype));
   if (op != TIPS_OP_SUM) return fail(TIPS_ERR_UNSUPPORTED, "only SUM is implemented (op %d)", op);
