@@ -286,6 +286,66 @@ def all_ranks_ok(dist, ok):
     return bool(t.item())
 
 
+def link_probe(dist, rank, world, mib=256, iters=5, backend="nccl", device="cuda"):
+    """What one xGMI link and all of them carry, measured with RCCL point-to-point through a torch
+    "nccl" group (independent of libtips_hip): rank 0 -> 1 one way, 0 <-> 1 both ways, and every
+    rank exchanging mib / (world - 1) with every peer at once. Host-timed (barrier, synchronize on
+    both sides), median of `iters` after one warm-up, max over ranks. GB/s = bytes each rank sends
+    (and receives) per second. Grounds the xGMI roofline the allreduce lines are priced against."""
+    import torch
+    pg = dist.new_group(backend=backend)
+    dist.all_reduce(torch.zeros(1, device=device), group=pg)  # every rank creates the communicator
+    n = mib << 20
+    a = torch.empty(n, dtype=torch.uint8, device=device)
+    b = torch.empty(n, dtype=torch.uint8, device=device)
+    sync = torch.cuda.synchronize if device == "cuda" else (lambda: None)
+
+    def run(ops_fn):
+        ts = []
+        for _ in range(iters + 1):
+            dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            ops = ops_fn()
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+            sync()
+            ts.append(max_over_ranks(dist, time.perf_counter() - t0))
+        return sorted(ts[1:])[iters // 2]
+
+    def uni():
+        if rank == 0:
+            return [dist.P2POp(dist.isend, a, 1, group=pg)]
+        return [dist.P2POp(dist.irecv, b, 0, group=pg)] if rank == 1 else []
+
+    def bi():
+        if rank in (0, 1):
+            return [dist.P2POp(dist.isend, a, 1 - rank, group=pg), dist.P2POp(dist.irecv, b, 1 - rank, group=pg)]
+        return []
+
+    part = n // (world - 1) // 4096 * 4096
+
+    def all_pairs():
+        ops = []
+        for d in range(1, world):
+            to, frm = (rank + d) % world, (rank - d) % world
+            k = d - 1
+            ops.append(dist.P2POp(dist.isend, a[k * part:(k + 1) * part], to, group=pg))
+            ops.append(dist.P2POp(dist.irecv, b[k * part:(k + 1) * part], frm, group=pg))
+        return ops
+
+    out = {"bytes": n, "method": "%s p2p via a torch %s group, host-timed, median of %d" % (
+        "RCCL" if backend == "nccl" else backend, backend, iters)}
+    out["one_link_one_way_GBps"] = round(n / run(uni) / 1e9, 1)
+    out["one_link_both_ways_GBps_per_direction"] = round(n / run(bi) / 1e9, 1)
+    if world > 2:
+        out["all_links_GBps_per_rank_per_direction"] = round(part * (world - 1) / run(all_pairs) / 1e9, 1)
+    del a, b
+    dist.destroy_process_group(pg)
+    return out
+
+
 _RESULT = {}  # rank 0's finished result line, if the main measurement completed
 
 
@@ -504,23 +564,42 @@ def bench_allreduce(args):
         kc = max(3, steps // 4)
         # (oneshot targets small buckets only). peer = the same exchange by our own kernels over
         # IPC-mapped peer memory; measured here (the driver's 8-GPU run) before it can be a default.
-        for name in ("ring", "direct", "rccl", "peer"):
-            if algo_names[name] == algo or (name == "peer" and workload != "bucket"):
+        # The _k entries re-run a schedule at another sub-chunk pipeline depth (read per call).
+        variants = [("ring", "ring", {}), ("direct", "direct", {}), ("rccl", "rccl", {}), ("peer", "peer", {}),
+                    ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
+                    ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
+                    ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})]
+        for label, name, env in variants:
+            if (label == name and algo_names[name] == algo) or (name == "peer" and workload != "bucket") or \
+                    (env and workload != "bucket"):
                 continue
+            saved = {k: os.environ.get(k) for k in env}
             try:
+                os.environ.update(env)
                 _lib.call("tips_set_algorithm", algo_names[name])
                 for _ in range(2):
                     step()
                 torch.cuda.synchronize()
                 tc = timed(kc)
-                compare[name] = round(total_elems * 4 / (tc / kc) / GIB, 2)
+                compare[label] = round(total_elems * 4 / (tc / kc) / GIB, 2)
                 good, msg = parity(algo_names[name])
-                compare_check[name] = msg if all_ranks_ok(dist, good) else "FAIL on some rank (%s here)" % msg
+                compare_check[label] = msg if all_ranks_ok(dist, good) else "FAIL on some rank (%s here)" % msg
             except Exception as e:  # noqa: BLE001 - a comparison point never costs the main line
-                compare[name] = None
-                compare_check[name] = "error: %s" % (e,)
+                compare[label] = None
+                compare_check[label] = "error: %s" % (e,)
+            finally:
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
         _lib.call("tips_set_algorithm", algo_names[args.algo])
     line["compare_check"] = compare_check
+    if world > 1 and not args.no_compare and not os.environ.get("TIPS_NO_RCCL"):
+        try:
+            line["xgmi_probe"] = link_probe(dist, rank, world)
+        except Exception as e:  # noqa: BLE001
+            line["xgmi_probe"] = {"error": str(e)}
     line["compare_algbw_gib_s"] = compare
     if rank == 0:
         print(json.dumps(line), flush=True)

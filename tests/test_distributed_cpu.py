@@ -39,6 +39,38 @@ def _worker(rank, world, port, q):
     q.put((rank, uid, t, ok_all, ok_one_bad))
 
 
+def _probe_worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    out = bench.link_probe(dist, rank, world, mib=4, iters=3, backend="gloo", device="cpu")
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_link_probe_shapes(world):
+    """bench.link_probe's three patterns (one way, both ways, all pairs) complete and report on
+    every rank; on the GPU node the same code runs over a torch nccl (RCCL) group."""
+    import torch.multiprocessing as tmp
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_probe_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, out in res:
+        assert out["one_link_one_way_GBps"] > 0 and out["one_link_both_ways_GBps_per_direction"] > 0
+        assert ("all_links_GBps_per_rank_per_direction" in out) == (world > 2)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_gloo_plumbing(world):
     import torch.multiprocessing as tmp
