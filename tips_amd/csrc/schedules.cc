@@ -179,9 +179,11 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
     if (in != out) HIP_TRY(hipMemcpyAsync(out, in, (size_t)(n * es), hipMemcpyDeviceToDevice, stream));
     return 0;
   }
+  if (algo == TIPS_ALGO_PEER && st.size <= tips::kMaxSrcs)
+    return peer_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
+  TRY(ensure_comm(st));  // every other schedule moves its bytes over RCCL (no half-built group on failure)
   if (st.size > tips::kMaxSrcs && (algo == TIPS_ALGO_DIRECT || algo == TIPS_ALGO_ONESHOT || algo == TIPS_ALGO_PEER))
     return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
-  if (algo == TIPS_ALGO_PEER) return peer_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
   if (algo == TIPS_ALGO_ONESHOT) return oneshot_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
   if (algo == TIPS_ALGO_DIRECT) return direct_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
   return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
