@@ -433,18 +433,36 @@ def bench_allreduce(args):
     cp, _keep2 = _lib.i64_array(sizes)
 
     names = [("grad.%d" % i).encode() for i in range(len(sizes))]
+    view_ptrs = [v.data_ptr() for v in views]
+    host_t = {"enqueue": 0.0, "wait": 0.0}
+    per_call = [False]
+    import ctypes
+    name_arr = (ctypes.c_char_p * len(names))(*names)
+    vp_arr = pp
+    h_arr = (ctypes.c_int64 * len(sizes))()
 
     def step():
         if workload == "bucket":
             rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), sizes[0], _lib.FLOAT32, _lib.OP_SUM, sp)
-        elif workload == "negotiated1000":
-            hs = [L.tips_enqueue_allreduce(nm, v.data_ptr(), v.data_ptr(), v.numel(), _lib.FLOAT32, sp)
-                  for nm, v in zip(names, views)]
+        elif workload == "negotiated1000" and per_call[0]:  # one ctypes call per tensor (Python-bound)
+            t0 = time.perf_counter()
+            hs = [L.tips_enqueue_allreduce(nm, p_, p_, k, _lib.FLOAT32, sp) for nm, p_, k in zip(names, view_ptrs, sizes)]
+            t1 = time.perf_counter()
             rc = next((int(h) for h in hs if h < 0), 0)
             for h in hs:
                 if h > 0:
                     w = L.tips_wait(h)
                     rc = rc or (w if w < 0 else 0)
+            host_t["enqueue"] += t1 - t0
+            host_t["wait"] += time.perf_counter() - t1
+        elif workload == "negotiated1000":  # the same 1000 named requests, one library call each way
+            t0 = time.perf_counter()
+            rc = L.tips_enqueue_allreduce_n(name_arr, vp_arr, vp_arr, cp, len(sizes), _lib.FLOAT32, sp, h_arr)
+            t1 = time.perf_counter()
+            if rc == 0:
+                rc = L.tips_wait_n(h_arr, len(sizes))
+            host_t["enqueue"] += t1 - t0
+            host_t["wait"] += time.perf_counter() - t1
         else:
             rc = L.tips_fused_allreduce(pp, cp, len(sizes), _lib.FLOAT32, sp)
         if rc:
@@ -464,7 +482,9 @@ def bench_allreduce(args):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    host_t.update(enqueue=0.0, wait=0.0)
     t = timed(steps)
+    host_split = dict(host_t)
     ms = t / steps * 1e3
 
     # parity: one fresh call, then fold all ranks' seeded inputs on this device (rank order) and compare
@@ -554,6 +574,16 @@ def bench_allreduce(args):
     }
     if workload == "negotiated1000":
         line["per_tensor_us"] = round(ms * 1e3 / len(sizes), 2)
+        line["host_us_per_tensor"] = {k: round(v / steps / len(sizes) * 1e6, 2) for k, v in host_split.items()}
+        line["api"] = "tips_enqueue_allreduce_n + tips_wait_n (1000 named requests, one call each way)"
+        per_call[0] = True  # the same requests through one ctypes call per tensor, for comparison
+        for _ in range(2):
+            step()
+        host_t.update(enqueue=0.0, wait=0.0)
+        tpc = timed(steps)
+        line["per_call_api_per_tensor_us"] = round(tpc / steps / len(sizes) * 1e6, 2)
+        line["per_call_api_host_us_per_tensor"] = {k: round(v / steps / len(sizes) * 1e6, 2) for k, v in host_t.items()}
+        per_call[0] = False
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True
 

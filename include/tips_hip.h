@@ -202,6 +202,13 @@ TIPS_API int64_t tips_enqueue_allreduce(const char* name, const void* in, void* 
 TIPS_API int tips_poll(int64_t handle);
 /* Blocks until the request is reduced (TIPS_OK, handle released) or failed (< 0). */
 TIPS_API int tips_wait(int64_t handle);
+/* n named requests in one call (what a framework's gradient hook hands over at once):
+ * handles[i] = tips_enqueue_allreduce(names[i], ins[i], outs[i], counts[i], dtype, stream).
+ * Returns TIPS_OK, or the first failure (its handles[i] < 0; the others are enqueued). */
+TIPS_API int tips_enqueue_allreduce_n(const char* const* names, const void* const* ins, void* const* outs,
+                                      const int64_t* counts, int n, int dtype, void* stream, int64_t* handles);
+/* tips_wait on each of n handles (handles <= 0 are skipped): TIPS_OK or the first failure. */
+TIPS_API int tips_wait_n(const int64_t* handles, int n);
 /* The negotiation protocol with an executor that only logs (no GPU): each
  * rank enqueues the newline-separated "name dtype count" lines of `requests`
  * ("@sleep ms" pauses, "@wait" blocks until every earlier request is

@@ -21,6 +21,38 @@ sys.path.insert(0, os.path.dirname(HERE))
 os.environ["TIPS_NO_RCCL"] = "1"
 
 
+def named_case(c, rank, size, L, _lib, sp):
+    """Named requests (tips_enqueue_allreduce) enqueued in a different order on every rank; the
+    negotiation orders them and the executor fuses each ready run into one allreduce (readiness
+    batching). Every output is checked against the oracle's fold of all ranks' inputs."""
+    import numpy as np
+    import oracle_bind
+    from gpu_util import from_dev, rand, same_bits, to_dev
+    tensors = c["named"]  # [[dtype, n], ...]
+    order = list(range(len(tensors)))
+    np.random.default_rng(c["seed"] * 31 + rank).shuffle(order)
+    ins, outs, handles = {}, {}, {}
+    for i in order:
+        dtype, n = tensors[i]
+        all_in = [rand(dtype, n, np.random.default_rng(c["seed"] + 1000 * i + r)) for r in range(size)]
+        x = to_dev(all_in[rank])
+        y = x if (i % 3 == 0) else x.new_empty(x.shape)
+        ins[i], outs[i] = all_in, y
+        handles[i] = L.tips_enqueue_allreduce(("t%d" % i).encode(), x.data_ptr(), y.data_ptr(), n, dtype, sp)
+        ins[i] = (all_in, x)
+    bad = []
+    for i in range(len(tensors)):
+        rc = L.tips_wait(handles[i]) if handles[i] > 0 else int(handles[i])
+        dtype, n = tensors[i]
+        if rc != 0:
+            bad.append("t%d rc %d %s" % (i, rc, _lib.last_error()))
+            continue
+        exp = oracle_bind.fold(ins[i][0], code=dtype, wide_acc=True)
+        if not same_bits(from_dev(outs[i], dtype), exp, dtype):
+            bad.append("t%d (dtype %d, n %d) differs" % (i, dtype, n))
+    return {"case": {"named": len(tensors), "seed": c["seed"]}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5])}
+
+
 def main():
     rank, size, uid, cases = int(sys.argv[1]), int(sys.argv[2]), bytes.fromhex(sys.argv[3]), json.loads(sys.argv[4])
     import ctypes
@@ -41,6 +73,9 @@ def main():
     sp = torch.cuda.current_stream().cuda_stream
     results = []
     for c in cases:
+        if c.get("named"):
+            results.append(named_case(c, rank, size, L, _lib, sp))
+            continue
         dtype, n, seed = c["dtype"], c["n"], c["seed"]
         if c.get("count_per_rank"):  # deliberately inconsistent counts: every rank must fail, none hang
             n = c["count_per_rank"][rank]

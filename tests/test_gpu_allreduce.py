@@ -396,6 +396,22 @@ def test_named_async_allreduce_single_rank(gpu):
         gpu.allreduce_async(torch.zeros(3), "host")
 
 
+def test_named_async_many_single_rank(gpu, monkeypatch):
+    """allreduce_async_many / synchronize_many (tips_enqueue_allreduce_n / tips_wait_n): 500
+    named tensors in one call, fused per readiness list (1 MiB threshold: some batches, some
+    singles, some empty tensors); mixed dtypes in one call are refused."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(1 << 20))
+    rng = np.random.default_rng(3)
+    ts = [torch.randn(int(rng.choice([0, 1, 33, 4099, 70000, 300000])), device="cuda") for _ in range(500)]
+    hs = gpu.allreduce_async_many(ts, ["many.%d" % i for i in range(len(ts))])
+    outs = gpu.synchronize_many(hs)
+    for o, t in zip(outs, ts):
+        assert torch.equal(o, t)
+    with pytest.raises(ValueError):
+        gpu.allreduce_async_many([ts[0], ts[1].double()], ["a", "b"])
+
+
 def test_sparse_allreduce_single_rank(gpu):
     """The reference's IndexedSlices branch (allgather of values and indices, __init__.py:59-74) through
     tips_allgatherv on one rank: device and host, IndexedSlices and torch sparse COO."""

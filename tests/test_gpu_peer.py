@@ -82,3 +82,20 @@ def test_peer_schedule_pieces_and_mismatch(gpu):
     check(results)
     for res in results:
         assert "rank 2" in res["results"][2]["error"] or "5001" in res["results"][2]["error"]
+
+
+def test_named_requests_batched_across_processes(gpu):
+    """The negotiated path with readiness batching, 3 processes: 300 named tensors of mixed dtypes
+    and sizes (some at and above a 1 MiB fusion threshold, some empty, a third in place),
+    enqueued in a different order on every rank; every result bit-exact against the fold."""
+    import numpy as np
+    from gpu_util import F16, F64, I32
+    rng = np.random.default_rng(11)
+    dts = [F32, F32, F32, F64, I32, F16]
+    tensors = []
+    for i in range(300):
+        n = int(rng.choice([0, 1, 7, 300, 4099, 65536, 262144, 300000]))
+        tensors.append([int(dts[int(rng.integers(len(dts)))]), n])
+    port = str(29700 + os.getpid() % 200)
+    check(run_job(3, [{"named": tensors, "seed": 5}], TIPS_FUSION_THRESHOLD=str(1 << 20), MASTER_ADDR="127.0.0.1",
+                  MASTER_PORT=port, TIPS_ALGO="peer"))

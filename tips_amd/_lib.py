@@ -84,6 +84,10 @@ _SIGNATURES = [
     ("tips_enqueue_allreduce", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_poll", ctypes.c_int, [ctypes.c_int64]),
+    ("tips_enqueue_allreduce_n", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_char_p), _c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+      _c_i64_p]),
+    ("tips_wait_n", ctypes.c_int, [_c_i64_p, ctypes.c_int]),
     ("tips_wait", ctypes.c_int, [ctypes.c_int64]),
     ("tips_negotiation_selftest", ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),

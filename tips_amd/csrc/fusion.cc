@@ -6,6 +6,8 @@
 // threshold (TIPS_FUSION_THRESHOLD, 64 MiB) by copy_tiles_kernel, each bucket
 // is allreduced once, and the sums are unpacked in place. Pack/unpack
 // descriptors are built once per distinct tensor list and cached in HBM.
+#include <string.h>
+
 #include <algorithm>
 
 #include "rt.h"
@@ -95,6 +97,98 @@ int build_plan(State& st, FusionPlan& pl, int64_t threshold) {
 }
 
 }  // namespace
+
+int64_t fusion_threshold_bytes() {
+  return round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_FUSION_THRESHOLD", 64 << 20)), kAlignBytes);
+}
+
+// Readiness batching. The tensors differ from cycle to cycle, so no plan is cached:
+// descriptors are written to a page-locked slot and copied to HBM on the stream.
+// A ring of slots lets the host fill the next one while earlier batches still run.
+struct BatchFusion {
+  static constexpr int kSlots = 4;
+  struct Slot {
+    CopyTile* host = nullptr;  // hipHostMalloc
+    size_t cap = 0;            // tiles
+    DevBuf dev;
+    hipEvent_t done = nullptr;  // after the unpack that last read dev
+    bool used = false;
+  } slot[kSlots];
+  int next = 0;
+  DevBuf bucket;
+};
+
+void batch_release(State& st) {
+  BatchFusion* b = st.batch;
+  if (!b) return;
+  for (auto& sl : b->slot) {
+    if (sl.done) (void)hipEventSynchronize(sl.done), (void)hipEventDestroy(sl.done);
+    if (sl.host) (void)hipHostFree(sl.host);
+    sl.dev.release();
+  }
+  b->bucket.release();
+  delete b;
+  st.batch = nullptr;
+}
+
+int batch_fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStream_t stream) {
+  if (!st.batch) st.batch = new BatchFusion();
+  BatchFusion& bf = *st.batch;
+  const int64_t es = tips::dtype_size(dtype);
+  const int64_t tile = kDefaultCopyTile;
+  std::vector<CopyTile> tiles;  // pack tiles, then unpack tiles (bucket offsets, rebased below)
+  int64_t off = 0;
+  for (int i = 0; i < n; i++) {
+    const int64_t bytes = items[i].count * es;
+    off = round_up(off, kAlignBytes);
+    for (int64_t t = 0; t < bytes; t += tile)
+      tiles.push_back(CopyTile{(const char*)items[i].in + t, (char*)(uintptr_t)(off + t), std::min(tile, bytes - t)});
+    off += bytes;
+  }
+  const int64_t total = round_up(off, kAlignBytes);
+  if (total == 0) return 0;
+  if ((size_t)total > bf.bucket.bytes)  // the old bucket is freed: no queued batch may still use it
+    for (auto& sl : bf.slot)
+      if (sl.used) HIP_TRY(hipEventSynchronize(sl.done));
+  TRY(bf.bucket.ensure((size_t)total));  // (padding between tensors is reduced too, never unpacked)
+  const size_t npack = tiles.size();
+  for (size_t k = 0; k < npack; k++) tiles[k].dst = (char*)bf.bucket.p + (uintptr_t)tiles[k].dst;
+  // unpack mirrors pack: bucket -> out
+  {
+    int64_t o = 0;
+    for (int i = 0; i < n; i++) {
+      const int64_t bytes = items[i].count * es;
+      o = round_up(o, kAlignBytes);
+      for (int64_t t = 0; t < bytes; t += tile)
+        tiles.push_back(CopyTile{(const char*)bf.bucket.p + o + t, (char*)items[i].out + t, std::min(tile, bytes - t)});
+      o += bytes;
+    }
+  }
+  BatchFusion::Slot& sl = bf.slot[bf.next];
+  bf.next = (bf.next + 1) % BatchFusion::kSlots;
+  if (sl.used) HIP_TRY(hipEventSynchronize(sl.done));  // the kernels that last read this slot are done
+  if (tiles.size() > sl.cap) {
+    if (sl.host) HIP_TRY(hipHostFree(sl.host));
+    sl.host = nullptr;
+    sl.cap = 0;
+    const size_t cap = std::max<size_t>(tiles.size(), 4096);
+    HIP_TRY(hipHostMalloc((void**)&sl.host, cap * sizeof(CopyTile), hipHostMallocDefault));
+    sl.cap = cap;
+  }
+  if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  const size_t dbytes = tiles.size() * sizeof(CopyTile);
+  TRY(sl.dev.ensure(dbytes));
+  memcpy(sl.host, tiles.data(), dbytes);
+  HIP_TRY(hipMemcpyAsync(sl.dev.p, sl.host, dbytes, hipMemcpyHostToDevice, stream));
+  CopyTile* dev = (CopyTile*)sl.dev.p;
+  HIP_TRY(tips::launch_copy_tiles(dev, (int)npack, stream));
+  TRY(allreduce_device(st, bf.bucket.p, bf.bucket.p, total / es, dtype, stream));
+  HIP_TRY(tips::launch_copy_tiles(dev + npack, (int)(tiles.size() - npack), stream));
+  HIP_TRY(hipEventRecord(sl.done, stream));
+  sl.used = true;
+  return 0;
+}
+
 }  // namespace rt
 }  // namespace tips
 

@@ -35,6 +35,14 @@ namespace {
 
 using namespace tips::net;
 
+// One completion event shared by the requests of a fused batch.
+struct GroupEv {
+  hipEvent_t ev = nullptr;
+  ~GroupEv() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
+};
+
 struct Req {
   int64_t handle = 0;
   std::string name;
@@ -44,6 +52,7 @@ struct Req {
   int dtype = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
+  std::shared_ptr<GroupEv> gev;  // set when the request ran inside a fused batch (then ev is unused)
   int state = 0;  // 0 queued, 1 announced, 2 launched (ev recorded), 3 done (dry run), -1 error
   std::string err;
 };
@@ -227,9 +236,9 @@ class Negotiator {
     r->dtype = dtype;
     r->stream = s;
     if (!dry_) {  // device-resident tensors only: the negotiated path runs on the caller's stream
-      State& st = S();
-      std::lock_guard<std::mutex> lk(st.mu);
-      TRY(set_device(st));
+      // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
+      // st.device is fixed from init on)
+      TRY(set_device(S()));
       if (count > 0 && !(is_device_ptr(in) && is_device_ptr(out)))
         return fail(TIPS_ERR_INVALID_ARG, "named allreduce needs device pointers");
       {
@@ -267,13 +276,15 @@ class Negotiator {
     if (r->state < 0) {
       rc = fail(TIPS_ERR_MISMATCH, "%s", r->err.c_str());
     } else if (r->state == 2) {
-      hipError_t e = block ? hipEventSynchronize(r->ev) : hipEventQuery(r->ev);
+      hipEvent_t ev = r->gev ? r->gev->ev : r->ev;
+      hipError_t e = block ? hipEventSynchronize(ev) : hipEventQuery(ev);
       if (e == hipErrorNotReady) return 0;
       if (e != hipSuccess) rc = fail(TIPS_ERR_HIP, "request %s: %s", r->name.c_str(), hipGetErrorString(e));
     }
     std::lock_guard<std::mutex> l(m_);
     if (r->ev) ev_pool_.push_back(r->ev);  // reused by the next request
     r->ev = nullptr;
+    r->gev.reset();
     by_handle_.erase(h);
     return rc;
   }
@@ -300,6 +311,8 @@ class Negotiator {
     for (auto& kv : by_handle_)  // never polled to completion
       if (kv.second->ev) ev_pool_.push_back(kv.second->ev);
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
+    join_ev_.release();
+    if (neg_stream_) (void)hipStreamDestroy(neg_stream_);
   }
 
   bool running() {
@@ -318,12 +331,21 @@ class Negotiator {
  private:
   void loop() {
     const auto cycle = std::chrono::microseconds(std::max<int64_t>(50, env_i64("TIPS_CYCLE_TIME_US", 1000)));
+    const auto linger = std::chrono::microseconds(std::max<int64_t>(0, env_i64("TIPS_BATCH_LINGER_US", 30)));
     while (true) {
       std::vector<std::shared_ptr<Req>> batch;
       bool stopping;
       {
         std::unique_lock<std::mutex> l(m_);
         cv_.wait_for(l, cycle, [&] { return !fresh_.empty() || want_stop_; });
+        // Linger while requests keep arriving (a gradient list is enqueued in a burst), so one
+        // cycle announces - and one fused batch reduces - the whole burst instead of its first
+        // few tensors. Bounded by the cycle time; TIPS_BATCH_LINGER_US = 0 turns it off.
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!fresh_.empty() && !want_stop_ && linger.count() > 0 && std::chrono::steady_clock::now() - t0 < cycle) {
+          const size_t seen = fresh_.size();
+          if (!cv_.wait_for(l, linger, [&] { return fresh_.size() != seen || want_stop_; })) break;
+        }
         batch.assign(fresh_.begin(), fresh_.end());
         fresh_.clear();
         for (auto& r : batch) r->state = 1;
@@ -342,15 +364,19 @@ class Negotiator {
       Reader rd(resp);
       const bool shutdown = rd.get<uint8_t>() != 0;
       const uint32_t n = rd.get<uint32_t>();
+      std::vector<Decision> ds;
       for (uint32_t i = 0; i < n && rd.ok; i++) {
-        const bool ok = rd.get<uint8_t>() != 0;
-        const std::string name = rd.str(), err = rd.str();
-        execute(name, ok, err);
+        Decision d;
+        d.ok = rd.get<uint8_t>() != 0;
+        d.name = rd.str();
+        d.err = rd.str();
+        ds.push_back(std::move(d));
       }
       if (!rd.ok) {
         set_loop_error("negotiation: malformed response");
         break;
       }
+      execute(ds);
       if (shutdown) break;
     }
     std::lock_guard<std::mutex> l(m_);
@@ -426,33 +452,100 @@ class Negotiator {
     return true;
   }
 
-  void execute(const std::string& name, bool ok, const std::string& err) {
-    std::shared_ptr<Req> r;
+  // PerformCollectiveOp for one cycle's ready list, in rank 0's order. Readiness
+  // batching: a run of consecutive ready requests of one dtype, each under the fusion
+  // threshold and together within it, is reduced as ONE fused allreduce (pack, one
+  // bucket exchange, unpack; fusion.cc) instead of one exchange per tensor. Every rank
+  // received the same list, so every rank forms the same batches.
+  void execute(const std::vector<Decision>& ds) {
+    const size_t n = ds.size();
+    std::vector<std::shared_ptr<Req>> reqs(n);
     {
       std::lock_guard<std::mutex> l(m_);
-      auto it = by_name_.find(name);
-      if (it == by_name_.end()) return;  // (cannot happen: every rank announced it)
-      r = it->second;
-      by_name_.erase(it);
-      if (dry_) log_.push_back(name + (ok ? " OK" : " ERR " + err));
+      for (size_t i = 0; i < n; i++) {
+        auto it = by_name_.find(ds[i].name);
+        if (it == by_name_.end()) continue;  // (cannot happen: every rank announced it)
+        reqs[i] = it->second;
+        by_name_.erase(it);
+        if (dry_) log_.push_back(ds[i].name + (ds[i].ok ? " OK" : " ERR " + ds[i].err));
+      }
     }
-    int state = ok ? (dry_ ? 3 : 2) : -1;
-    std::string msg = err;
-    if (ok && !dry_) {  // PerformCollectiveOp: the device allreduce, on the request's stream
+    std::vector<int> state(n, 0);
+    std::vector<std::string> msg(n);
+    for (size_t i = 0; i < n; i++) {
+      state[i] = ds[i].ok ? (dry_ ? 3 : 2) : -1;
+      msg[i] = ds[i].err;
+    }
+    if (!dry_) {
       State& st = S();
       std::lock_guard<std::mutex> lk(st.mu);
-      int rc = set_device(st);
-      if (rc == 0) rc = allreduce_device(st, r->in, r->out, r->count, r->dtype, r->stream);
-      if (rc == 0 && hipEventRecord(r->ev, r->stream) != hipSuccess) rc = fail(TIPS_ERR_HIP, "hipEventRecord failed");
-      if (rc != 0) {
-        state = -1;
-        msg = last_error();
+      int rc0 = set_device(st);
+      const bool fuse = env_i64("TIPS_NEGOTIATED_FUSION", 1) != 0;
+      const int64_t threshold = fusion_threshold_bytes();
+      for (size_t i = 0; i < n;) {
+        if (!reqs[i] || state[i] != 2) {
+          i++;
+          continue;
+        }
+        const int dtype = reqs[i]->dtype;
+        const int64_t es = tips::dtype_size(dtype);
+        size_t j = i;
+        int64_t bytes = 0;
+        while (fuse && j < n && reqs[j] && state[j] == 2 && reqs[j]->dtype == dtype && reqs[j]->count * es < threshold &&
+               round_up(bytes, kAlignBytes) + reqs[j]->count * es <= threshold) {
+          bytes = round_up(bytes, kAlignBytes) + reqs[j]->count * es;
+          j++;
+        }
+        int rc = rc0;
+        if (j - i >= 2) {
+          if (rc == 0) rc = run_batch(st, reqs, i, j);
+        } else {
+          j = i + 1;
+          auto& r = reqs[i];
+          if (rc == 0) rc = allreduce_device(st, r->in, r->out, r->count, r->dtype, r->stream);
+          if (rc == 0 && hipEventRecord(r->ev, r->stream) != hipSuccess) rc = fail(TIPS_ERR_HIP, "hipEventRecord failed");
+        }
+        if (rc != 0)
+          for (size_t k = i; k < j; k++) {
+            state[k] = -1;
+            msg[k] = last_error();
+          }
+        i = j;
       }
     }
     std::lock_guard<std::mutex> l(m_);
-    r->state = state;
-    r->err = msg;
+    for (size_t i = 0; i < n; i++)
+      if (reqs[i]) {
+        reqs[i]->state = state[i];
+        reqs[i]->err = msg[i];
+      }
     cv_.notify_all();
+  }
+
+  // reqs[i, j): one fused allreduce on their stream (or, if they came on several, on a
+  // negotiation stream joined with each of them both ways); one shared completion event.
+  int run_batch(State& st, std::vector<std::shared_ptr<Req>>& reqs, size_t i, size_t j) {
+    std::vector<hipStream_t> streams;
+    for (size_t k = i; k < j; k++)
+      if (std::find(streams.begin(), streams.end(), reqs[k]->stream) == streams.end()) streams.push_back(reqs[k]->stream);
+    hipStream_t s = streams[0];
+    if (streams.size() > 1) {
+      if (!neg_stream_) HIP_TRY(hipStreamCreateWithFlags(&neg_stream_, hipStreamNonBlocking));
+      s = neg_stream_;
+      TRY(join_ev_.ensure(streams.size()));
+      for (size_t k = 0; k < streams.size(); k++) TRY(join(s, streams[k], join_ev_.ev[k]));
+    }
+    std::vector<BatchItem> items;
+    items.reserve(j - i);
+    for (size_t k = i; k < j; k++) items.push_back(BatchItem{reqs[k]->in, reqs[k]->out, reqs[k]->count});
+    TRY(batch_fused_allreduce(st, items.data(), (int)items.size(), reqs[i]->dtype, s));
+    auto g = std::make_shared<GroupEv>();
+    HIP_TRY(hipEventCreateWithFlags(&g->ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(g->ev, s));
+    if (streams.size() > 1)
+      for (hipStream_t u : streams) HIP_TRY(hipStreamWaitEvent(u, g->ev, 0));  // results in stream order for each owner
+    for (size_t k = i; k < j; k++) reqs[k]->gev = g;
+    return 0;
   }
 
   void set_loop_error(const std::string& e) {
@@ -476,6 +569,8 @@ class Negotiator {
   std::vector<std::string> log_;
   std::vector<hipEvent_t> ev_pool_;
   std::string loop_err_;
+  hipStream_t neg_stream_ = nullptr;  // fused batches whose requests came on several streams
+  EventPool join_ev_;
 };
 
 std::mutex g_neg_mu;
@@ -549,6 +644,37 @@ int tips_wait(int64_t handle) {
   }
   const int rc = n->poll(handle, true);
   return rc == 1 ? 0 : rc;
+}
+
+int tips_enqueue_allreduce_n(const char* const* names, const void* const* ins, void* const* outs, const int64_t* counts,
+                             int n, int dtype, void* stream, int64_t* handles) {
+  if (n < 0 || (n > 0 && (!names || !ins || !outs || !counts || !handles)))
+    return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce list");
+  int rc = 0;
+  std::string first_err;
+  for (int i = 0; i < n; i++) {
+    handles[i] = tips_enqueue_allreduce(names[i], ins[i], outs[i], counts[i], dtype, stream);
+    if (handles[i] < 0 && rc == 0) {
+      rc = (int)handles[i];
+      first_err = last_error();
+    }
+  }
+  return rc ? fail(rc, "%s", first_err.c_str()) : 0;
+}
+
+int tips_wait_n(const int64_t* handles, int n) {
+  if (n < 0 || (n > 0 && !handles)) return fail(TIPS_ERR_INVALID_ARG, "bad handle list");
+  int rc = 0;
+  std::string first_err;
+  for (int i = 0; i < n; i++) {
+    if (handles[i] <= 0) continue;
+    const int w = tips_wait(handles[i]);
+    if (w < 0 && rc == 0) {
+      rc = w;
+      first_err = last_error();
+    }
+  }
+  return rc ? fail(rc, "%s", first_err.c_str()) : 0;
 }
 
 int tips_negotiation_selftest(int rank, int size, const char* host, int port, const char* requests, char* out,

@@ -137,7 +137,8 @@ struct FusionPlan {
   std::vector<int> unfused;  // indices allreduced in place
 };
 
-struct PeerState;  // peer.cc
+struct PeerState;   // peer.cc
+struct BatchFusion;  // fusion.cc: readiness batching of negotiated requests
 
 struct State {
   std::mutex mu;
@@ -159,6 +160,7 @@ struct State {
   std::unordered_map<uint64_t, FusionPlan> plans;
   uint64_t peer_key = 0;      // names the node-local control block of the peer schedule (hash of the unique id)
   PeerState* peer = nullptr;  // peer schedule: IPC workspaces + shared-memory barrier, created on first use
+  BatchFusion* batch = nullptr;  // negotiated requests fused per readiness list, created on first use
 };
 
 State& S();
@@ -183,6 +185,17 @@ void peer_release(State& st);  // collective (shutdown)
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
 // fusion.cc
 void free_plan(FusionPlan& pl);
+// One fused allreduce of out-of-place tensors that became ready together (negotiate.cc's
+// readiness batching): pack in[i] -> bucket, allreduce, unpack -> out[i], on `stream`,
+// sum of padded sizes <= the fusion threshold. Caller holds st.mu.
+struct BatchItem {
+  const void* in;
+  void* out;
+  int64_t count;
+};
+int batch_fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStream_t stream);
+int64_t fusion_threshold_bytes();
+void batch_release(State& st);
 // control.cc: ConstructResponseMessage's rules over p request records (TIPS_REQUEST_WORDS each)
 int check_records(const int64_t* t, int p);
 // negotiate.cc: stop the negotiation thread (collective; call without holding st.mu)

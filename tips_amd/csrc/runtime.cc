@@ -111,6 +111,7 @@ void tips_shutdown(void) {
   }
   for (auto& kv : st.plans) free_plan(kv.second);
   st.plans.clear();
+  batch_release(st);
   st.staging.release();
   st.host_in.release();
   st.host_out.release();

@@ -203,6 +203,51 @@ def allreduce_async(tensor, name):
     return hd
 
 
+def allreduce_async_many(tensor_list, names):
+    """allreduce_async over a list in one library call (tips_enqueue_allreduce_n): what a
+    gradient hook hands over at once. Same negotiation per name; returns one Handle each."""
+    import ctypes
+    basics.init()
+    if len(tensor_list) != len(names):
+        raise ValueError("one name per tensor")
+    if not tensor_list:
+        return []
+    code = tensors.dtype_code(tensor_list[0])
+    srcs, outs = [], []
+    for t in tensor_list:
+        if not tensors.is_device(t):
+            raise ValueError("allreduce_async_many needs device tensors")
+        if tensors.dtype_code(t) != code:
+            raise ValueError("allreduce_async_many needs one dtype (call it once per dtype)")
+        srcs.append(t.contiguous())
+        outs.append(tensors.empty_like(srcs[-1]))
+    n = len(srcs)
+    nm = (ctypes.c_char_p * n)(*[x.encode() for x in names])
+    pi, _k1 = _lib.ptr_array([x.data_ptr() for x in srcs])
+    po, _k2 = _lib.ptr_array([x.data_ptr() for x in outs])
+    pc, _k3 = _lib.i64_array([x.numel() for x in srcs])
+    hs = (ctypes.c_int64 * n)()
+    _lib.call("tips_enqueue_allreduce_n", nm, pi, po, pc, n, code, tensors.stream_of(srcs[0]), hs)
+    out = []
+    for h, o, x, name in zip(hs, outs, srcs, names):
+        hd = Handle(int(h), o, name)
+        hd._keep = x
+        out.append(hd)
+    return out
+
+
+def synchronize_many(handles):
+    """synchronize() over a list in one library call (tips_wait_n); returns the outputs."""
+    import ctypes
+    pend = [h for h in handles if not h.done]
+    if pend:
+        arr = (ctypes.c_int64 * len(pend))(*[h.handle for h in pend])
+        _lib.call("tips_wait_n", arr, len(pend))
+        for h in pend:
+            h.done = True
+    return [h.output for h in handles]
+
+
 def poll(handle):
     """True once the named allreduce has completed on the device."""
     if handle.done:
