@@ -53,6 +53,43 @@ def named_case(c, rank, size, L, _lib, sp):
     return {"case": {"named": len(tensors), "seed": c["seed"]}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5])}
 
 
+def golden_case(c, rank, size, L, _lib, sp):
+    """A committed golden vector (tests/golden: inputs and the reference's MPI_Allreduce output
+    under MPICH) through the real multi-process product path: rank r reduces inputs[r]; the
+    result must meet the reference's tolerance against MPICH and be bit-exact against the
+    oracle's rank-order fold (the peer schedule's order)."""
+    import numpy as np
+    import oracle_bind
+    from conftest import golden_cases, load_golden
+    from gpu_util import F32, F64, I32, I64, from_dev, same_bits, to_dev
+    name = c["golden"]
+    ins, exp = load_golden(name)
+    dtype = {"f32": F32, "f64": F64, "i32": I32, "i64": I64}[golden_cases()[name]["dtype"]]
+    assert ins.shape[0] == size, "golden case %s is for %d ranks" % (name, ins.shape[0])
+    x = to_dev(np.ascontiguousarray(ins[rank]))
+    y = x.new_empty(x.shape)
+    rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), x.numel(), dtype, _lib.OP_SUM, sp)
+    import torch
+    torch.cuda.synchronize()
+    res = {"case": {"golden": name}, "rc": int(rc)}
+    if rc != 0:
+        res.update(ok=False, error=_lib.last_error())
+        return res
+    got = from_dev(y, dtype)
+    fold_ok = bool(same_bits(got, oracle_bind.fold([ins[r] for r in range(size)], code=dtype, wide_acc=True), dtype))
+    if exp.dtype.kind == "i":
+        ref_ok = bool(np.array_equal(got, exp))
+    elif name.startswith("signed"):
+        ref_ok = bool(np.all(np.abs(got.astype(np.float64) - exp) <= 1e-6 * np.sum(np.abs(ins.astype(np.float64)), axis=0)))
+    elif name.startswith("kat"):
+        ref_ok = bool(np.allclose(got, exp, rtol=0, atol=1e-6))
+    else:
+        ref_ok = bool((np.abs(got.astype(np.float64) - exp) / np.abs(exp)).max() <= 1e-6)
+    res.update(ok=fold_ok and ref_ok, fold_bit_exact=fold_ok, within_reference_tolerance=ref_ok,
+               bit_exact_vs_mpich=bool(np.array_equal(got.view(np.uint8), np.ascontiguousarray(exp).view(np.uint8))))
+    return res
+
+
 def main():
     rank, size, uid, cases = int(sys.argv[1]), int(sys.argv[2]), bytes.fromhex(sys.argv[3]), json.loads(sys.argv[4])
     import ctypes
@@ -75,6 +112,9 @@ def main():
     for c in cases:
         if c.get("named"):
             results.append(named_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("golden"):
+            results.append(golden_case(c, rank, size, L, _lib, sp))
             continue
         dtype, n, seed = c["dtype"], c["n"], c["seed"]
         if c.get("count_per_rank"):  # deliberately inconsistent counts: every rank must fail, none hang

@@ -17,6 +17,7 @@ import sys
 
 import pytest
 
+from conftest import golden_cases
 from gpu_util import ALL_DTYPES, F32, I64
 
 pytestmark = pytest.mark.gpu
@@ -99,3 +100,18 @@ def test_named_requests_batched_across_processes(gpu):
     port = str(29700 + os.getpid() % 200)
     check(run_job(3, [{"named": tensors, "seed": 5}], TIPS_FUSION_THRESHOLD=str(1 << 20), MASTER_ADDR="127.0.0.1",
                   MASTER_PORT=port, TIPS_ALGO="peer"))
+
+
+@pytest.mark.parametrize("p", [2, 3, 4, 5, 8])
+def test_golden_vectors_across_processes(gpu, p):
+    """Every committed golden vector for p ranks (the reference's own KATs, config 1's 1 MiB
+    bucket, the seeded i32/i64/f32/f64 sets: outputs of MPI_Allreduce under MPICH) through p real
+    processes. p = 8 is config 3's rank count. At p = 2 the sum is order-free, so the result
+    must also equal MPICH's bit for bit."""
+    names = sorted(n for n, c in golden_cases().items() if c["p"] == p)
+    assert names
+    results = run_job(p, [{"golden": n} for n in names], TIPS_PEER_WS_MIB="16")
+    check(results)
+    if p == 2:
+        for res in results:
+            assert all(c["bit_exact_vs_mpich"] for c in res["results"])
