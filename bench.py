@@ -596,6 +596,7 @@ def bench_allreduce(args):
         # IPC-mapped peer memory; measured here (the driver's 8-GPU run) before it can be a default.
         # The _k entries re-run a schedule at another sub-chunk pipeline depth (read per call).
         variants = [("ring", "ring", {}), ("direct", "direct", {}), ("rccl", "rccl", {}), ("peer", "peer", {}),
+                    ("peer_push", "peer", {"TIPS_PEER_AG": "push"}),
                     ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
                     ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
                     ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})]

@@ -58,18 +58,20 @@ def check(results):
     assert not bad, "\n".join(bad[:12] + errs)
 
 
+@pytest.mark.parametrize("ag", ["pull", "push"])
 @pytest.mark.parametrize("p", [2, 3, 4])
-def test_peer_schedule_all_dtypes(gpu, p):
+def test_peer_schedule_all_dtypes(gpu, p, ag):
     cases = []
     for dtype in ALL_DTYPES:
         for n in (1, 7, 4099, 1000003):
             cases.append({"dtype": dtype, "n": n, "seed": 100 * dtype + n % 89})
     cases.append({"dtype": F32, "n": 262147, "seed": 5, "inplace": True})
     cases.append({"dtype": I64, "n": 4099, "seed": 6, "inplace": True})
-    check(run_job(p, cases))
+    check(run_job(p, cases, TIPS_PEER_AG=ag))
 
 
-def test_peer_schedule_pieces_and_mismatch(gpu):
+@pytest.mark.parametrize("ag", ["pull", "push"])
+def test_peer_schedule_pieces_and_mismatch(gpu, ag):
     """A 4 MiB workspace: the 64 MiB buckets go through in many pieces."""
     p = 3
     cases = [
@@ -79,7 +81,7 @@ def test_peer_schedule_pieces_and_mismatch(gpu):
         {"dtype": I64, "n": 3 << 20, "seed": 4},             # the job still works after the refused call
         {"dtype": F32, "n": (1 << 24) + 3, "seed": 7, "inplace": True},
     ]
-    results = run_job(p, cases, TIPS_PEER_WS_MIB="4")
+    results = run_job(p, cases, TIPS_PEER_WS_MIB="4", TIPS_PEER_AG=ag)
     check(results)
     for res in results:
         assert "rank 2" in res["results"][2]["error"] or "5001" in res["results"][2]["error"]

@@ -48,7 +48,7 @@ constexpr int kPeerMaxRanks = tips::kMaxSrcs;
 constexpr uint64_t kPeerMagic = 0x5449505350454552ull;  // "TIPSPEER"
 constexpr int64_t kPeerSlotPad = 4096;  // slots not at power-of-two strides (as schedules.cc kSlotPad)
 
-enum Phase : int32_t { kCall = 1, kPushed = 2, kReduced = 3, kPublish = 4, kShutdown = 5 };
+enum Phase : int32_t { kCall = 1, kPushed = 2, kReduced = 3, kPublish = 4, kShutdown = 5, kGathered = 6, kUnpacked = 7 };
 
 struct Post {
   int64_t count;
@@ -286,8 +286,10 @@ void peer_release(State& st) {
 
 namespace {
 
-// One piece (<= the workspace): push, barrier, fold, barrier, pull.
-int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
+// One piece (<= the workspace): push, barrier, fold, barrier, pull; or, with the push
+// allgather (TIPS_PEER_AG=push), push, barrier, fold, barrier, push, barrier, local copy.
+int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, int dtype, hipStream_t user,
+               bool ag_push) {
   const int p = st.size, r = st.rank;
   const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
   const int64_t cap = round_up(chunk_of(n, p, align, 0).len() * es, kAlignBytes) + kPeerSlotPad;
@@ -313,22 +315,42 @@ int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, i
   q.phase = kPushed;
   TRY(barrier(st, ps, q, nullptr, peer_timeout()));
 
-  // fold: rank-order sum of chunk r (same bits as the direct schedule)
+  // fold: rank-order sum of chunk r (same bits as the direct schedule). With the push
+  // allgather it lands in out directly (the pushes below read it from there).
   const Range mine = chunk_of(n, p, align, r);
   const void* srcs[tips::kMaxSrcs];
   for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)(in + mine.b * es) : (char*)ps.ws + slot_of(r, j);
-  HIP_TRY(tips::launch_multi_sum((char*)ps.ws + red_off, srcs, p, mine.len(), dtype, user));
+  char* red = ag_push ? out + mine.b * es : (char*)ps.ws + red_off;
+  HIP_TRY(tips::launch_multi_sum(red, srcs, p, mine.len(), dtype, user));
   HIP_TRY(hipStreamSynchronize(user));
   q.phase = kReduced;
   TRY(barrier(st, ps, q, nullptr, peer_timeout()));
 
-  // pull: every rank's reduced chunk -> out, stream-ordered (the next push's sync and
-  // barrier keep the peers from overwriting red before this has read it)
+  if (!ag_push) {
+    // pull: every rank's reduced chunk -> out, stream-ordered (the next push's sync and
+    // barrier keep the peers from overwriting red before this has read it)
+    m = 0;
+    for (int d = 0; d < p; d++) {
+      const int from = mod(r + d, p);
+      const Range c = chunk_of(n, p, align, from);
+      segs[m++] = {(const char*)ps.remote[from] + red_off, out + c.b * es, c.len() * es};
+    }
+    HIP_TRY(tips::launch_xfer(segs, m, user));
+    return 0;
+  }
+  // push allgather: my reduced chunk -> every peer's slot for r (every fold has consumed
+  // the slots: barrier above), then each rank copies its slots into out
   m = 0;
-  for (int d = 0; d < p; d++) {
+  for (int d = 1; d < p; d++) segs[m++] = {red, (char*)ps.remote[mod(r + d, p)] + slot_of(mod(r + d, p), r), mine.len() * es};
+  HIP_TRY(tips::launch_xfer(segs, m, user));
+  HIP_TRY(hipStreamSynchronize(user));
+  q.phase = kGathered;
+  TRY(barrier(st, ps, q, nullptr, peer_timeout()));
+  m = 0;
+  for (int d = 1; d < p; d++) {
     const int from = mod(r + d, p);
     const Range c = chunk_of(n, p, align, from);
-    segs[m++] = {(const char*)ps.remote[from] + red_off, out + c.b * es, c.len() * es};
+    segs[m++] = {(const char*)ps.ws + slot_of(r, from), out + c.b * es, c.len() * es};
   }
   HIP_TRY(tips::launch_xfer(segs, m, user));
   return 0;
@@ -339,7 +361,7 @@ int peer_allreduce_impl(State& st, PeerState& ps, const char* in, char* out, int
   TRY(attach(st, ps));
   const int p = st.size, r = st.rank;
   const int64_t es = tips::dtype_size(dtype);
-  if (ps.pull_pending) {  // the last call's pull, on whatever stream it ran, has read the peers' red
+  if (ps.pull_pending) {  // the last call's pull (or slot copy), on whatever stream it ran, is done
     HIP_TRY(hipEventSynchronize(ps.pulled));
     ps.pull_pending = false;
   }
@@ -358,8 +380,17 @@ int peer_allreduce_impl(State& st, PeerState& ps, const char* in, char* out, int
   // piece: the largest multiple of p 256-B-aligned chunks whose p slots fit the workspace
   const int64_t per_chunk = (ps.ws_bytes / p - kPeerSlotPad) / kAlignBytes * kAlignBytes;
   const int64_t piece = per_chunk / es * p;
-  for (int64_t b = 0; b < n; b += piece)
-    TRY(peer_piece(st, ps, in + b * es, out + b * es, std::min(piece, n - b), dtype, user));
+  const char* agv = getenv("TIPS_PEER_AG");
+  const bool ag_push = agv && !strcmp(agv, "push");
+  for (int64_t b = 0; b < n; b += piece) {
+    if (b > 0 && ag_push) {  // every rank's local copy out of its slots is done before new pushes land
+      HIP_TRY(hipStreamSynchronize(user));
+      Post u = call;
+      u.phase = kUnpacked;
+      TRY(barrier(st, ps, u, nullptr, peer_timeout()));
+    }
+    TRY(peer_piece(st, ps, in + b * es, out + b * es, std::min(piece, n - b), dtype, user, ag_push));
+  }
   if (!ps.pulled) HIP_TRY(hipEventCreateWithFlags(&ps.pulled, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(ps.pulled, user));
   ps.pull_pending = true;
