@@ -479,9 +479,23 @@ def bench_allreduce(args):
         dist.barrier()
         return max_over_ranks(dist, dt)
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
+    # A schedule that fails outright on this node (an error on every rank, not a hang) must not
+    # cost the whole line: the next one is measured instead and the failure is reported.
+    fallbacks = []
+    while True:
+        try:
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            break
+        except _lib.TipsError as e:
+            nxt = {_lib.ALGO_DIRECT: _lib.ALGO_RING, _lib.ALGO_PEER: _lib.ALGO_DIRECT,
+                   _lib.ALGO_ONESHOT: _lib.ALGO_RING, _lib.ALGO_RING: _lib.ALGO_RCCL}.get(algo)
+            if workload == "negotiated1000" or nxt is None:
+                raise
+            fallbacks.append({"algorithm": inv.get(algo, str(algo)), "error": str(e)})
+            algo = nxt
+            _lib.call("tips_set_algorithm", algo)
     host_t.update(enqueue=0.0, wait=0.0)
     t = timed(steps)
     host_split = dict(host_t)
@@ -572,6 +586,8 @@ def bench_allreduce(args):
         "reduce_kernel_roofline": kernel_roof,
         "check": check if all_ok else "FAIL on some rank",
     }
+    if fallbacks:
+        line["failed_schedules"] = fallbacks
     if workload == "negotiated1000":
         line["per_tensor_us"] = round(ms * 1e3 / len(sizes), 2)
         line["host_us_per_tensor"] = {k: round(v / steps / len(sizes) * 1e6, 2) for k, v in host_split.items()}
@@ -624,7 +640,7 @@ def bench_allreduce(args):
                         os.environ.pop(k, None)
                     else:
                         os.environ[k] = v
-        _lib.call("tips_set_algorithm", algo_names[args.algo])
+        _lib.call("tips_set_algorithm", algo if fallbacks else algo_names[args.algo])
     line["compare_check"] = compare_check
     if world > 1 and not args.no_compare and not os.environ.get("TIPS_NO_RCCL"):
         try:
