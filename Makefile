@@ -8,7 +8,14 @@ SRCS     := tips_amd/csrc/kernels.hip tips_amd/csrc/runtime.cc tips_amd/csrc/rt_
 HDRS     := tips_amd/csrc/kernels.h tips_amd/csrc/rt.h tips_amd/csrc/net.h include/tips_hip.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-result -fvisibility=hidden
 
-all: $(LIB) oracle
+CRASH    := tools/lib/libcrashline.so
+
+all: $(LIB) $(CRASH) oracle
+
+# bench.py's last-words hook (not part of the product library)
+$(CRASH): tools/crash_line.c
+	@mkdir -p tools/lib
+	gcc -O2 -fPIC -shared -Wall -Wextra -std=c11 -D_POSIX_C_SOURCE=200809L -o $@ $<
 
 $(LIB): $(SRCS) $(HDRS)
 	@mkdir -p tips_amd/lib

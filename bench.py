@@ -349,6 +349,24 @@ def link_probe(dist, rank, world, mib=256, iters=5, backend="nccl", device="cuda
 _RESULT = {}  # rank 0's finished result line, if the main measurement completed
 
 
+def crash_line():
+    """rank 0's last-words hook (tools/crash_line.c): once installed, a fatal signal (a GPU fault's
+    SIGABRT, torchrun's SIGTERM after another rank died) still prints the line measured so far.
+    Returns set(text or None), or None when the helper is not built."""
+    import ctypes
+    path = os.path.join(REPO, "tools", "lib", "libcrashline.so")
+    if not os.path.exists(path):
+        return None
+    try:
+        h = ctypes.CDLL(path)
+    except OSError:
+        return None
+    h.crash_line_set.argtypes = [ctypes.c_char_p]
+    if h.crash_line_install() != 0:
+        return None
+    return lambda text: h.crash_line_set(text.encode() if text else None)
+
+
 def start_watchdog(seconds, rank):
     """A hung collective must end the run with a message, never hang the box. If the main
     measurement already finished (only the optional comparison runs hung), its line is printed."""
@@ -602,24 +620,25 @@ def bench_allreduce(args):
         per_call[0] = False
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True
+    last_words = crash_line() if rank == 0 and not args.no_compare else None
+
+    def note_progress(what):
+        """What rank 0 prints if a fatal signal ends the process during `what`."""
+        if last_words:
+            last_words(json.dumps(dict(line, compare_algbw_gib_s=compare, compare_check=compare_check,
+                                       compare_error="process ended by a signal during %s" % what)))
 
     # comparison points on the same workload: the other schedules and ncclAllReduce (optional; a hang
-    # here is caught by the watchdog, which then still prints the line above)
+    # here is caught by the watchdog, which then still prints the line above; a crash by last_words)
     compare, compare_check = {}, {}
-    if not args.no_compare:
+
+    def run_variants(variants):
         kc = max(3, steps // 4)
-        # (oneshot targets small buckets only). peer = the same exchange by our own kernels over
-        # IPC-mapped peer memory; measured here (the driver's 8-GPU run) before it can be a default.
-        # The _k entries re-run a schedule at another sub-chunk pipeline depth (read per call).
-        variants = [("ring", "ring", {}), ("direct", "direct", {}), ("rccl", "rccl", {}), ("peer", "peer", {}),
-                    ("peer_push", "peer", {"TIPS_PEER_AG": "push"}),
-                    ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
-                    ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
-                    ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})]
         for label, name, env in variants:
             if (label == name and algo_names[name] == algo) or (name == "peer" and workload != "bucket") or \
                     (env and workload != "bucket"):
                 continue
+            note_progress("comparison %r" % label)
             saved = {k: os.environ.get(k) for k in env}
             try:
                 os.environ.update(env)
@@ -641,14 +660,29 @@ def bench_allreduce(args):
                     else:
                         os.environ[k] = v
         _lib.call("tips_set_algorithm", algo if fallbacks else algo_names[args.algo])
+
+    if not args.no_compare:
+        # (oneshot targets small buckets only.) The _k entries re-run a schedule at another sub-chunk
+        # pipeline depth (read per call). RCCL-moved schedules first, then the link probe, and last
+        # the schedules whose bytes our own kernels move through IPC-mapped peer memory: peer is
+        # measured here (the driver's 8-GPU run) before it can be a default, and placed last so that
+        # a fault in it cannot cost the numbers gathered before it (last_words prints them).
+        run_variants([("ring", "ring", {}), ("direct", "direct", {}), ("rccl", "rccl", {}),
+                      ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
+                      ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
+                      ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
+        if world > 1 and not os.environ.get("TIPS_NO_RCCL"):
+            note_progress("the xGMI link probe")
+            try:
+                line["xgmi_probe"] = link_probe(dist, rank, world)
+            except Exception as e:  # noqa: BLE001
+                line["xgmi_probe"] = {"error": str(e)}
+        run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"})])
     line["compare_check"] = compare_check
-    if world > 1 and not args.no_compare and not os.environ.get("TIPS_NO_RCCL"):
-        try:
-            line["xgmi_probe"] = link_probe(dist, rank, world)
-        except Exception as e:  # noqa: BLE001
-            line["xgmi_probe"] = {"error": str(e)}
     line["compare_algbw_gib_s"] = compare
     if rank == 0:
+        if last_words:
+            last_words(None)
         print(json.dumps(line), flush=True)
     _RESULT["printed"] = True  # the watchdog must not print a second line
     dist.barrier()

@@ -100,6 +100,32 @@ def test_workload_shapes():
     assert len(f) == 1000 and sum(f) == 20680288 and min(f) == 257 and max(f) == 130946  # config 4
 
 
+@pytest.mark.parametrize("how", ["abort", "term", "cleared"])
+def test_bench_last_words(how):
+    """A fatal signal during bench.py's comparison runs still prints the line measured so far
+    (tools/crash_line.c): a GPU fault is SIGABRT, torchrun stops surviving ranks with SIGTERM. The
+    process still dies of that signal; once the final line is out the hook prints nothing."""
+    import json
+    import signal
+    import subprocess
+    lib = os.path.join(REPO, "tools", "lib", "libcrashline.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", REPO, "tools/lib/libcrashline.so"], check=True, capture_output=True)
+    prog = ("import os, signal, sys, time\nsys.path.insert(0, %r)\nimport bench\n"
+            "say = bench.crash_line()\nassert say is not None\n"
+            "say('{\"metric\": \"m\", \"value\": 2.5, \"compare_error\": \"during peer\"}')\n" % REPO)
+    if how == "cleared":
+        prog += "say(None)\n"
+    prog += "os.abort()\n" if how == "abort" else "os.kill(os.getpid(), signal.SIGTERM)\ntime.sleep(30)\n"
+    r = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True, timeout=120)
+    assert r.returncode == (-signal.SIGABRT if how == "abort" else -signal.SIGTERM), r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if how == "cleared":
+        assert lines == []
+    else:
+        assert len(lines) == 1 and json.loads(lines[0])["value"] == 2.5
+
+
 @pytest.mark.parametrize("state,code,expect", [
     ("done", 0, "compare_error"),     # main result finished, comparison runs hung -> the result is printed
     ("none", 3, "watchdog: no progress"),
