@@ -163,6 +163,34 @@ def bench_sum(args):
     ms = ev0.elapsed_time(ev1) / steps  # HIP events on the kernel's stream = avg launch duration
     ok = bool(torch.equal(c, a + b))   # one IEEE add per element: bit-exact vs torch
 
+    # The same kernel cycling over 4 operand triples (3 GiB, 12x the 256 MiB Infinity Cache): no
+    # launch can find its inputs on-die from the previous one, so this rate is HBM's alone.
+    rot = [(a, b, c)]
+    for k in range(3):
+        t3 = tuple(torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(3))
+        g.manual_seed(10 + k)
+        t3[0].uniform_(-1.0, 1.0, generator=g)
+        t3[1].uniform_(-1.0, 1.0, generator=g)
+        rot.append(t3)
+    for x_, y_, z_ in rot:
+        L.tips_bucket_sum(z_.data_ptr(), x_.data_ptr(), y_.data_ptr(), n, _lib.FLOAT32, sp)
+    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e2.record(stream)
+    for i in range(steps):
+        x_, y_, z_ = rot[i % len(rot)]
+        rc = L.tips_bucket_sum(z_.data_ptr(), x_.data_ptr(), y_.data_ptr(), n, _lib.FLOAT32, sp)
+        if rc:
+            raise _lib.TipsError("tips_bucket_sum", rc, _lib.last_error())
+    e3.record(stream)
+    torch.cuda.synchronize()
+    rot_ms = e2.elapsed_time(e3) / steps
+    ok = ok and all(bool(torch.equal(z_, x_ + y_)) for x_, y_, z_ in rot[1:])
+    rotating = {"sets": len(rot), "resident_bytes": len(rot) * 3 * n * 4, "us_per_launch": round(rot_ms * 1e3, 2),
+                "achieved_GBps": round(3 * n * 4 / (rot_ms / 1e3) / 1e9, 1),
+                "note": "tips_bucket_sum cycling over 4 (a, b, c) triples, 3 GiB resident: no operand of a launch "
+                        "can be served from the 256 MiB Infinity Cache by the previous launch"}
+    del rot
+
     # PCIe-inclusive rate (the path starts and ends in host memory): pinned H2D a,b + sum + D2H c
     ha, hb, hc = (torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(3))
     ha.copy_(a)
@@ -222,6 +250,7 @@ def bench_sum(args):
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": (tr["bytes"] if tr else None)},
         "cpu_baseline": cpu,
+        "rotating_buffers": rotating,
         "input_bucket_gib_s": round(n * 4 / t_s / GIB, 2),
         "algorithmic_bytes_per_step": moved,
         "pcie_inclusive_gib_s": round(n * 4 / t_host / GIB, 3),
@@ -604,6 +633,15 @@ def bench_allreduce(args):
         "reduce_kernel_roofline": kernel_roof,
         "check": check if all_ok else "FAIL on some rank",
     }
+    if world == 1:  # one rank: no link carries anything; the step is HBM work on this GPU
+        # bucket: the allreduce is a copy (read + write); fused: pack + unpack (2 reads + 2 writes)
+        moved = (2 if workload == "bucket" else 4) * total_elems * 4
+        line["roofline"] = {"bound": "hbm", "achieved": round(moved / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                            "unit": "GB/s", "frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                            "note": "one rank: the allreduce of a bucket is the identity; %s" % (
+                                "in -> out copy" if workload == "bucket" else
+                                "algorithmic bytes = pack + unpack of every tensor (2 reads + 2 writes)")}
+        del line["xgmi"]
     if fallbacks:
         line["failed_schedules"] = fallbacks
     if workload == "negotiated1000":

@@ -247,7 +247,10 @@ TIPS_API int tips_set_sim_transport(int transport);
 
 /* Explicit variant of the 2-input sum kernel, for the gfx950 tuning sweep
  * (tools/sum_sweep.cc): mode 0 = grid-stride over `blocks` workgroups,
- * mode 1 = one tile per workgroup; unroll = 16-B vectors per lane in flight;
+ * mode 1 = one tile per workgroup, mode 2 = the same in XCD-contiguous order,
+ * mode 3 = buffer-op forms (nt = cache-policy pair), mode 4 = LDS-staged
+ * through direct-to-LDS loads (unroll 1/2/4, 256 threads);
+ * unroll = 16-B vectors per lane in flight;
  * nt: 0 plain, 1 non-temporal loads+stores, 2 nt loads only, 3 nt stores only;
  * threads = workgroup size. Non-default variants exist for f32 only
  * (others return TIPS_ERR_HIP). tips_bucket_sum uses the default chosen

@@ -66,7 +66,8 @@ SWEEP_VARIANTS = ([(m, u, t, 256) for m in (0, 1) for u in (1, 2, 4, 8) for t in
                      (1, 1, 2, 256), (1, 8, 2, 256), (1, 2, 2, 512), (1, 2, 2, 128), (1, 1, 2, 512), (0, 2, 2, 256),
                      (0, 4, 2, 256), (2, 1, 2, 256), (2, 2, 2, 256), (2, 1, 2, 512), (2, 4, 1, 256)]
                   + [(3, 1, i, 256) for i in range(10)]
-                  + [(3, u, 1, t) for u, t in ((2, 256), (4, 256), (1, 512), (2, 128), (1, 1024), (1, 128), (2, 512))])
+                  + [(3, u, 1, t) for u, t in ((2, 256), (4, 256), (1, 512), (2, 128), (1, 1024), (1, 128), (2, 512))]
+                  + [(4, u, 0, 256) for u in (1, 2, 4)])
 
 
 @pytest.mark.parametrize("mode,unroll,nt,threads", SWEEP_VARIANTS)

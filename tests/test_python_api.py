@@ -137,3 +137,24 @@ def test_allreduce_grads_routes_sparse_to_allgather(monkeypatch):
     assert out[0] is None
     assert torch.equal(out[1].to_dense(), 2 * dense)
     assert np.array_equal(out[2].indices, [3, 3])
+
+
+def test_allreduce_grads_sparse_as_dense(monkeypatch):
+    """sparse_as_dense (reference __init__.py:205-210): IndexedSlices (numpy or torch) and torch sparse
+    gradients are densified (repeated rows summed) and then take the dense allreduce."""
+    import torch
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    monkeypatch.setattr(tips_amd, "allreduce", lambda t, **kw: t * 2)
+    sl = tips_amd.IndexedSlices(np.ones((3, 2), np.float32), np.array([1, 3, 1]), dense_shape=(4, 2))
+    tsl = tips_amd.IndexedSlices(torch.ones(2, 2), torch.tensor([0, 0]), dense_shape=(3, 2))
+    dense = torch.zeros(4, 2)
+    dense[2, 1] = 3.0
+    out = tips_amd.allreduce_grads([sl, tsl, dense.to_sparse(), None], sparse_as_dense=True, fused=False)
+    exp0 = np.zeros((4, 2), np.float32)
+    exp0[1] = 2.0
+    exp0[3] = 1.0
+    assert isinstance(out[0], np.ndarray) and np.array_equal(out[0], 2 * exp0)
+    assert torch.equal(out[1], 2 * torch.tensor([[2.0, 2.0], [0.0, 0.0], [0.0, 0.0]]))
+    assert not out[2].is_sparse and torch.equal(out[2], 2 * dense)
+    assert out[3] is None

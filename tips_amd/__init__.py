@@ -85,15 +85,39 @@ def _allreduce_cond(tensor, *args, **kwargs):
     return tensor
 
 
-def allreduce_grads(grads, compression=Compression.none, op=None, fused=True):
+def _to_dense(g):
+    """tf.convert_to_tensor of an IndexedSlices (rows summed over repeated indices), or a torch
+    sparse tensor's dense form; anything else unchanged."""
+    if isinstance(g, IndexedSlices):
+        if g.dense_shape is None:
+            raise ValueError("sparse_as_dense needs the IndexedSlices' dense_shape")
+        if _tensors.is_torch(g.values):
+            import torch
+            dense = torch.zeros(tuple(int(d) for d in g.dense_shape), dtype=g.values.dtype, device=g.values.device)
+            idx = g.indices if _tensors.is_torch(g.indices) else torch.as_tensor(g.indices)
+            return dense.index_add_(0, idx.to(dense.device, torch.int64), g.values)
+        import numpy as np
+        dense = np.zeros(tuple(int(d) for d in g.dense_shape), dtype=np.asarray(g.values).dtype)
+        np.add.at(dense, np.asarray(g.indices), np.asarray(g.values))
+        return dense
+    if _tensors.is_torch(g) and g.is_sparse:
+        return g.to_dense()
+    return g
+
+
+def allreduce_grads(grads, compression=Compression.none, op=None, fused=True, sparse_as_dense=False):
     """Allreduce a list of gradients (None entries pass through).
 
     Mirrors the per-gradient loop of _make_cached_allreduce_grads_fn
     (__init__.py:203-222), including the size()==1 identity of
-    _allreduce_cond. With fused=True, device tensors are summed through the
-    fusion buckets (one allreduce per <=64 MiB bucket instead of one per
-    gradient); outputs are new tensors, inputs are left unchanged.
+    _allreduce_cond and `sparse_as_dense` (__init__.py:205-210: sparse
+    gradients are densified first and then take the dense path). With
+    fused=True, device tensors are summed through the fusion buckets (one
+    allreduce per <=64 MiB bucket instead of one per gradient); outputs are
+    new tensors, inputs are left unchanged.
     """
+    if sparse_as_dense:
+        grads = [_to_dense(g) if g is not None else g for g in grads]
     if size() <= 1:
         return list(grads)
     out = list(grads)

@@ -221,6 +221,48 @@ __global__ __launch_bounds__(BLOCK) void sum2_buf_kernel(u32x4* __restrict__ dst
   if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<DT>(dst, a, b, tail_begin + threadIdx.x);
 }
 
+// LDS-staged 2-input sum (tuning sweep only, f32): both operand tiles go global -> LDS with
+// gfx950's direct-to-LDS loads (global_load_lds_dwordx4 nt: no VGPR destination, each
+// wave-instruction lands 1 KiB at a wave-uniform LDS base + lane x 16 B), then LDS -> VGPRs
+// (ds_read_b128), add, sc1 buffer store as the shipped kernel. It measures what an LDS hop
+// costs a stream that reads every byte once. Partial last tile: plain loads.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+template <int U>
+__global__ __launch_bounds__(256) void sum2_lds_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
+                                                       const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
+                                                       int64_t n) {
+  __shared__ u32x4 stage[2 * 256 * U];  // one array: [a tile | b tile]
+  constexpr int64_t kTile = 256 * U;
+  const int tid = threadIdx.x, wbase = tid & ~63;
+  const int64_t first = xcd_tile(blockIdx.x, gridDim.x) * kTile;
+  if (first + kTile <= nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a + first + u * 256 + tid), (lds_ptr_t)(stage + u * 256 + wbase),
+                                       16, 0, 2);
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(b + first + u * 256 + tid),
+                                       (lds_ptr_t)(stage + kTile + u * 256 + wbase), 16, 0, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, (int)(kTile * 16),
+                                                                  0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(add16<kF32>(stage[u * 256 + tid], stage[kTile + u * 256 + tid]), rd,
+                                             (u * 256 + tid) * 16, 0, 16);
+  } else if (first < nvec) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = first + u * 256 + tid;
+      if (i < nvec) dst[i] = add16<kF32>(a[i], b[i]);
+    }
+  }
+  if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
+}
+
 // Unaligned fallback (any pointer not 16-B aligned): one element per lane.
 template <int DT>
 __global__ __launch_bounds__(kBlock) void sum2_scalar_kernel(void* dst, const void* a, const void* b, int64_t n) {
@@ -506,6 +548,28 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((sum2_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, a, b, n);
     return hipGetLastError();
+  }
+  if (mode == 4) {  // LDS-staged (direct-to-LDS loads), f32, 256 threads; unroll = 16-B vectors per lane
+    if constexpr (DT == kF32) {
+      const int64_t nvec = n / 4;
+      auto grid_for = [&](int64_t tile) { return (unsigned)std::max<int64_t>(8, ((nvec + tile - 1) / tile + 7) / 8 * 8); };
+      if (threads == 256 && unroll == 1) {
+        hipLaunchKernelGGL((sum2_lds_kernel<1>), dim3(grid_for(256)), dim3(256), 0, s, (u32x4*)dst, (const u32x4*)a,
+                           (const u32x4*)b, nvec, nvec * 4, n);
+        return hipGetLastError();
+      }
+      if (threads == 256 && unroll == 2) {
+        hipLaunchKernelGGL((sum2_lds_kernel<2>), dim3(grid_for(512)), dim3(256), 0, s, (u32x4*)dst, (const u32x4*)a,
+                           (const u32x4*)b, nvec, nvec * 4, n);
+        return hipGetLastError();
+      }
+      if (threads == 256 && unroll == 4) {
+        hipLaunchKernelGGL((sum2_lds_kernel<4>), dim3(grid_for(1024)), dim3(256), 0, s, (u32x4*)dst, (const u32x4*)a,
+                           (const u32x4*)b, nvec, nvec * 4, n);
+        return hipGetLastError();
+      }
+    }
+    return hipErrorInvalidValue;
   }
 #define TIPS_SUM2_CASE(M, U, NTV, L, S_, B)                      \
   if (mode == M && unroll == U && nt == NTV && threads == B) \

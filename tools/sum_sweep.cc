@@ -70,6 +70,8 @@ int main(int argc, char** argv) {
   const int bufshape[][2] = {{2, 256}, {4, 256}, {1, 512}, {2, 128}, {1, 1024}, {1, 128}, {2, 512}};
   for (auto& t : bufshape)
     vs.push_back({"buf_ntsc1_u" + std::to_string(t[0]) + "_t" + std::to_string(t[1]), 3, t[0], 1, 0, t[1], {}});
+  for (int u : {1, 2, 4})  // LDS-staged through direct-to-LDS loads (mode 4)
+    vs.push_back({"lds_glds_u" + std::to_string(u) + "_t256", 4, u, 0, 0, 256, {}});
   for (auto& t : xcd)
     vs.push_back({"xcd_u" + std::to_string(t[0]) + ntn[t[1]] + "_t" + std::to_string(t[2]), 2, t[0], t[1], 0, t[2], {}});
   for (int u : {1, 2, 4, 8})
