@@ -36,6 +36,8 @@ GIB = float(1 << 30)
 # the exact instantiation tips_bucket_sum launches for f32 (kernels.hip kDef*): PMC traffic is only
 # reported from a profile of this kernel
 DEFAULT_SUM_KERNEL = "sum2_buf_kernel<0, 2, 16, 1, 256>"
+# N == 1 cycles over this many (a, b, c) triples of config 2's size (3 GiB at 4): see bench_sum
+ROTATING_SETS = 4
 
 
 def parse():
@@ -48,6 +50,8 @@ def parse():
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N=1: time the headline kernel only (no same-buffer, PCIe or host-memory legs), as under rocprofv3")
     ap.add_argument("--workload", default="auto", choices=["auto", "sum", "bucket", "fused1000", "resnet50", "negotiated1000"],
                     help="auto: config 2 (sum) at N=1, config 3 (bucket allreduce) at N>1")
     return ap.parse_args()
@@ -134,105 +138,98 @@ def bench_sum(args):
     L = _lib.lib()
     torch.cuda.set_device(0)
     g = torch.Generator(device="cuda")
-    a = torch.empty(n, dtype=torch.float32, device="cuda")
-    b = torch.empty(n, dtype=torch.float32, device="cuda")
-    c = torch.empty(n, dtype=torch.float32, device="cuda")
-    g.manual_seed(1)
-    a.uniform_(-1.0, 1.0, generator=g)
-    g.manual_seed(2)
-    b.uniform_(-1.0, 1.0, generator=g)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
+    # ROTATING_SETS (a, b, c) triples, 768 MiB each: step i sums triple i % ROTATING_SETS, so 2.25 GiB
+    # of other traffic separates two uses of a buffer and no launch finds its operands in the
+    # 256 MiB Infinity Cache: the timed rate is HBM's. Triple 0 is config 2's seeded pair (seeds 1, 2).
+    sets = []
+    for k in range(ROTATING_SETS):
+        x_, y_, z_ = (torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(3))
+        g.manual_seed(1 if k == 0 else 10 + 2 * k)
+        x_.uniform_(-1.0, 1.0, generator=g)
+        g.manual_seed(2 if k == 0 else 11 + 2 * k)
+        y_.uniform_(-1.0, 1.0, generator=g)
+        sets.append((x_, y_, z_))
+    a, b, c = sets[0]
 
-    def step():
-        rc = L.tips_bucket_sum(c.data_ptr(), a.data_ptr(), b.data_ptr(), n, _lib.FLOAT32, sp)
-        if rc:
-            raise _lib.TipsError("tips_bucket_sum", rc, _lib.last_error())
-
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    ms = ev0.elapsed_time(ev1) / steps  # HIP events on the kernel's stream = avg launch duration
-    ok = bool(torch.equal(c, a + b))   # one IEEE add per element: bit-exact vs torch
-
-    # The same kernel cycling over 4 operand triples (3 GiB, 12x the 256 MiB Infinity Cache): no
-    # launch can find its inputs on-die from the previous one, so this rate is HBM's alone.
-    rot = [(a, b, c)]
-    for k in range(3):
-        t3 = tuple(torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(3))
-        g.manual_seed(10 + k)
-        t3[0].uniform_(-1.0, 1.0, generator=g)
-        t3[1].uniform_(-1.0, 1.0, generator=g)
-        rot.append(t3)
-    for x_, y_, z_ in rot:
-        L.tips_bucket_sum(z_.data_ptr(), x_.data_ptr(), y_.data_ptr(), n, _lib.FLOAT32, sp)
-    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e2.record(stream)
-    for i in range(steps):
-        x_, y_, z_ = rot[i % len(rot)]
+    def step(i=0):
+        x_, y_, z_ = sets[i % len(sets)]
         rc = L.tips_bucket_sum(z_.data_ptr(), x_.data_ptr(), y_.data_ptr(), n, _lib.FLOAT32, sp)
         if rc:
             raise _lib.TipsError("tips_bucket_sum", rc, _lib.last_error())
-    e3.record(stream)
-    torch.cuda.synchronize()
-    rot_ms = e2.elapsed_time(e3) / steps
-    ok = ok and all(bool(torch.equal(z_, x_ + y_)) for x_, y_, z_ in rot[1:])
-    rotating = {"sets": len(rot), "resident_bytes": len(rot) * 3 * n * 4, "us_per_launch": round(rot_ms * 1e3, 2),
-                "achieved_GBps": round(3 * n * 4 / (rot_ms / 1e3) / 1e9, 1),
-                "note": "tips_bucket_sum cycling over 4 (a, b, c) triples, 3 GiB resident: no operand of a launch "
-                        "can be served from the 256 MiB Infinity Cache by the previous launch"}
-    del rot
 
-    # PCIe-inclusive rate (the path starts and ends in host memory): pinned H2D a,b + sum + D2H c
-    ha, hb, hc = (torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(3))
-    ha.copy_(a)
-    hb.copy_(b)
-    torch.cuda.synchronize()
-    reps = 3
-    t1 = time.perf_counter()
-    for _ in range(reps):
-        a.copy_(ha, non_blocking=True)
-        b.copy_(hb, non_blocking=True)
-        step()
-        hc.copy_(c, non_blocking=True)
-    torch.cuda.synchronize()
-    t_host = (time.perf_counter() - t1) / reps
+    def timed(k, same_buffers):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(k):
+            step(0 if same_buffers else i)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / k, time.perf_counter() - t0  # HIP events on the kernel's stream
 
-    # host-memory leg of the drop-in path: tips_allreduce on host buffers (1 rank: H2D, device copy, D2H)
-    host_rates = {}
-    import numpy as np
-    pinned_in = torch.empty(n, dtype=torch.float32, pin_memory=True)
-    pinned_out = torch.empty(n, dtype=torch.float32, pin_memory=True)
-    pageable_in = np.random.default_rng(1).random(n, dtype=np.float32)
-    pageable_out = np.empty_like(pageable_in)
-    tips_amd.init()
-    reg_in = np.random.default_rng(2).random(n, dtype=np.float32)
-    reg_out = np.empty_like(reg_in)
-    _lib.call("tips_host_register", reg_in.ctypes.data, reg_in.nbytes)
-    _lib.call("tips_host_register", reg_out.ctypes.data, reg_out.nbytes)
-    for label, src, dst in (("pageable_numpy", pageable_in.ctypes.data, pageable_out.ctypes.data),
-                            ("pinned", pinned_in.data_ptr(), pinned_out.data_ptr()),
-                            ("registered_numpy", reg_in.ctypes.data, reg_out.ctypes.data)):
-        _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)  # warm (allocates staging)
-        ts = []
-        for _ in range(5):
-            t2 = time.perf_counter()
-            _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)
-            ts.append(time.perf_counter() - t2)
-        host_rates[label] = round(n * 4 / sorted(ts)[2] / GIB, 3)  # median of 5 calls
-        host_rates[label + "_calls_ms"] = [round(t * 1e3, 3) for t in ts]
-    host_ok = bool(np.array_equal(pageable_out, pageable_in)) and bool(np.array_equal(reg_out, reg_in))
-    _lib.call("tips_host_unregister", reg_in.ctypes.data)
-    _lib.call("tips_host_unregister", reg_out.ctypes.data)
-    del pinned_in, pinned_out, pageable_in, pageable_out, reg_in, reg_out
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ms, wall = timed(steps, same_buffers=False)
+    ok = all(bool(torch.equal(z_, x_ + y_)) for x_, y_, z_ in sets)  # one IEEE add per element: bit-exact
+
+    same = None
+    if not args.no_extras:
+        # the same kernel re-reading ONE triple (the literal config-2 loop): part of each launch's
+        # operands is still in the Infinity Cache from the launch before, so this is not an HBM rate
+        step(0)
+        ms_same, _ = timed(steps, same_buffers=True)
+        same = {"us_per_launch": round(ms_same * 1e3, 2), "achieved_GBps": round(3 * n * 4 / (ms_same / 1e3) / 1e9, 1),
+                "note": "tips_bucket_sum on the same (a, b, c) every launch: the 256 MiB Infinity Cache serves part "
+                        "of the 768 MiB working set from the previous launch, so this exceeds the HBM-only rate above"}
+    del sets[1:]  # (the PCIe leg below uses triple 0)
+
+    t_host, host_rates, host_ok = None, {}, True
+    if not args.no_extras:  # (skipped under rocprofv3: its kernel stats then hold only the timed launches)
+        # PCIe-inclusive rate (the path starts and ends in host memory): pinned H2D a,b + sum + D2H c
+        ha, hb, hc = (torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(3))
+        ha.copy_(a)
+        hb.copy_(b)
+        torch.cuda.synchronize()
+        reps = 3
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            a.copy_(ha, non_blocking=True)
+            b.copy_(hb, non_blocking=True)
+            step()
+            hc.copy_(c, non_blocking=True)
+        torch.cuda.synchronize()
+        t_host = (time.perf_counter() - t1) / reps
+
+        # host-memory leg of the drop-in path: tips_allreduce on host buffers (1 rank: H2D, device copy, D2H)
+        host_rates = {}
+        import numpy as np
+        pinned_in = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        pinned_out = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        pageable_in = np.random.default_rng(1).random(n, dtype=np.float32)
+        pageable_out = np.empty_like(pageable_in)
+        tips_amd.init()
+        reg_in = np.random.default_rng(2).random(n, dtype=np.float32)
+        reg_out = np.empty_like(reg_in)
+        _lib.call("tips_host_register", reg_in.ctypes.data, reg_in.nbytes)
+        _lib.call("tips_host_register", reg_out.ctypes.data, reg_out.nbytes)
+        for label, src, dst in (("pageable_numpy", pageable_in.ctypes.data, pageable_out.ctypes.data),
+                                ("pinned", pinned_in.data_ptr(), pinned_out.data_ptr()),
+                                ("registered_numpy", reg_in.ctypes.data, reg_out.ctypes.data)):
+            _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)  # warm (allocates staging)
+            ts = []
+            for _ in range(5):
+                t2 = time.perf_counter()
+                _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)
+                ts.append(time.perf_counter() - t2)
+            host_rates[label] = round(n * 4 / sorted(ts)[2] / GIB, 3)  # median of 5 calls
+            host_rates[label + "_calls_ms"] = [round(t * 1e3, 3) for t in ts]
+        host_ok = bool(np.array_equal(pageable_out, pageable_in)) and bool(np.array_equal(reg_out, reg_in))
+        _lib.call("tips_host_unregister", reg_in.ctypes.data)
+        _lib.call("tips_host_unregister", reg_out.ctypes.data)
+        del pinned_in, pinned_out, pageable_in, pageable_out, reg_in, reg_out
 
     moved = 3 * n * 4
     t_s = ms / 1e3
@@ -242,18 +239,21 @@ def bench_sum(args):
         "metric": METRIC, "value": round(moved / t_s / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
         "warmup": warmup, "ms_per_step": round(ms, 6), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: fp32 U[-1,1), torch cuda generator seeds 1 and 2, resident in HBM",
+        "data": "synthetic: fp32 U[-1,1), torch cuda generator seeds 1 and 2 (+ %d more seeded pairs), resident in HBM"
+                % (ROTATING_SETS - 1),
         "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
-                   "bucket_bytes": n * 4, "elements": n, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, XCD-contiguous order, buffer_load/store_dwordx4)",
+                   "bucket_bytes": n * 4, "elements": n, "rotating_sets": ROTATING_SETS,
+                   "timing": "HIP events over the timed launches; launch i sums triple i %% %d (HBM-only: no launch "
+                             "finds its operands in the 256 MiB Infinity Cache)" % ROTATING_SETS, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, XCD-contiguous order, buffer_load/store_dwordx4)",
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": (tr["bytes"] if tr else None)},
         "cpu_baseline": cpu,
-        "rotating_buffers": rotating,
+        "same_buffers_repeated": same,
         "input_bucket_gib_s": round(n * 4 / t_s / GIB, 2),
         "algorithmic_bytes_per_step": moved,
-        "pcie_inclusive_gib_s": round(n * 4 / t_host / GIB, 3),
+        "pcie_inclusive_gib_s": round(n * 4 / t_host / GIB, 3) if t_host else None,
         "pcie_inclusive_note": "pinned H2D of a and b + kernel + D2H of c, bucket bytes / wall time",
         "host_allreduce_gib_s": host_rates,
         "host_allreduce_note": "tips_allreduce(host in, host out) on one rank, 256 MiB: staged H2D + device + D2H, "

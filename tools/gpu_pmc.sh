@@ -8,6 +8,6 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o bench \
-    -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 2 ${BENCH_ARGS:-} > "$OUT/pmc_$c.log" 2>&1 || exit $?
+    -- python3 bench.py --no-cpu-baseline --no-extras --steps 20 --warmup 2 ${BENCH_ARGS:-} > "$OUT/pmc_$c.log" 2>&1 || exit $?
 done
 exit 0

@@ -46,7 +46,7 @@ fi
 if [ "${PROFILE:-1}" = "1" ]; then
   export TMPDIR=/tmp
   run rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_stats" -o bench \
-      -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-}
+      -- python3 bench.py --no-cpu-baseline --no-extras ${BENCH_ARGS:-}
   rc=$?; fatal $rc && exit $rc
 fi
 exit 0

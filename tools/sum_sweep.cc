@@ -49,6 +49,26 @@ int main(int argc, char** argv) {
     for (auto& x : h) x = u(g);
     CHECK(hipMemcpy(b, h.data(), bytes, hipMemcpyHostToDevice));
   }
+  // SWEEP_ROT=R: every timed launch uses the next of R (a, b, c) triples. With R >= 2 at 256 MiB no
+  // launch finds its operands in the 256 MiB Infinity Cache from an earlier one, so the rate is
+  // HBM's; R = 1 (default) re-reads the same buffers, which the Infinity Cache partly serves.
+  const char* rot_env = getenv("SWEEP_ROT");
+  const int rot = std::max(1, std::min(8, rot_env ? atoi(rot_env) : 1));
+  float *A[8] = {a}, *B[8] = {b}, *C[8] = {c};
+  for (int r = 1; r < rot; r++) {
+    CHECK(hipMalloc(&A[r], bytes));
+    CHECK(hipMalloc(&B[r], bytes));
+    CHECK(hipMalloc(&C[r], bytes));
+    CHECK(hipMemcpy(A[r], a, bytes, hipMemcpyDeviceToDevice));
+    CHECK(hipMemcpy(B[r], b, bytes, hipMemcpyDeviceToDevice));
+  }
+  int next_set = 0;
+  auto rotate = [&]() {
+    const int r = next_set++ % rot;
+    a = A[r];
+    b = B[r];
+    c = C[r];
+  };
   std::vector<Variant> vs;
   vs.push_back({"memcpy_d2d", -1, 0, 0, 0, 0, {}});
   vs.push_back({"default", -3, 0, 0, 0, 0, {}});
@@ -70,6 +90,9 @@ int main(int argc, char** argv) {
   const int bufshape[][2] = {{2, 256}, {4, 256}, {1, 512}, {2, 128}, {1, 1024}, {1, 128}, {2, 512}};
   for (auto& t : bufshape)
     vs.push_back({"buf_ntsc1_u" + std::to_string(t[0]) + "_t" + std::to_string(t[1]), 3, t[0], 1, 0, t[1], {}});
+  const int ntnt[][2] = {{1, 512}, {1, 1024}, {2, 256}, {4, 256}, {2, 512}};  // buffer nt loads + nt stores
+  for (auto& t : ntnt)
+    vs.push_back({"buf_ntnt_u" + std::to_string(t[0]) + "_t" + std::to_string(t[1]), 3, t[0], 7, 0, t[1], {}});
   for (int u : {1, 2, 4})  // LDS-staged through direct-to-LDS loads (mode 4)
     vs.push_back({"lds_glds_u" + std::to_string(u) + "_t256", 4, u, 0, 0, 256, {}});
   for (auto& t : xcd)
@@ -87,10 +110,20 @@ int main(int argc, char** argv) {
       for (int pad : {0, 4096})
         vs.push_back({"multi" + std::to_string(ns) + "_v" + std::to_string(var) + "_pad" + std::to_string(pad), -5, ns,
                       var, pad, 0, {}});
-  if (argc > 4) {  // optional name filter; the references always stay
+  if (argc > 4) {  // optional name filter: comma-separated substrings (exact name with a leading '='); references stay
+    std::vector<std::string> pats;
+    for (std::string f = argv[4]; !f.empty();) {
+      const size_t k = f.find(',');
+      pats.push_back(f.substr(0, k));
+      f = (k == std::string::npos) ? "" : f.substr(k + 1);
+    }
     std::vector<Variant> keep;
-    for (auto& v : vs)
-      if (v.mode == -1 || v.mode == -3 || v.name.find(argv[4]) != std::string::npos) keep.push_back(v);
+    for (auto& v : vs) {
+      bool hit = v.mode == -1 || v.mode == -3;
+      for (auto& p : pats)
+        hit = hit || (p[0] == '=' ? v.name == p.substr(1) : v.name.find(p) != std::string::npos);
+      if (hit) keep.push_back(v);
+    }
     vs.swap(keep);
   }
   hipStream_t s;
@@ -160,9 +193,13 @@ int main(int argc, char** argv) {
   }
   for (int r = 0; r < rounds; r++) {
     for (auto& v : vs) {
+      rotate();
       run(v);  // warm
       CHECK(hipEventRecord(e0, s));
-      for (int i = 0; i < iters; i++) run(v);
+      for (int i = 0; i < iters; i++) {
+        rotate();
+        run(v);
+      }
       CHECK(hipEventRecord(e1, s));
       CHECK(hipEventSynchronize(e1));
       float ms = 0;
@@ -176,9 +213,13 @@ int main(int argc, char** argv) {
     const int64_t cnt = (int64_t)bytes / (dt == 1 || dt == 3 ? 8 : dt >= 4 ? 2 : 4);
     std::vector<double> ms;
     for (int r = 0; r < rounds; r++) {
+      rotate();
       (void)tips_bucket_sum(c, a, b, cnt, dt, s);
       CHECK(hipEventRecord(e0, s));
-      for (int i = 0; i < iters; i++) (void)tips_bucket_sum(c, a, b, cnt, dt, s);
+      for (int i = 0; i < iters; i++) {
+        rotate();
+        (void)tips_bucket_sum(c, a, b, cnt, dt, s);
+      }
       CHECK(hipEventRecord(e1, s));
       CHECK(hipEventSynchronize(e1));
       float t = 0;
