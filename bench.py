@@ -8,7 +8,9 @@ N == 1 (BASELINE.json configs[1], the config the metric's first half is
 quoted on): one step = the device-resident sum of two 256 MiB fp32 gradient
 buffers, c = a + b (tips_bucket_sum: the per-chunk MPI_SUM of
 tips/core/collective/utils.h:60-65 as a gfx950 kernel). value = algorithmic
-bytes moved (2 reads + 1 write = 805,306,368 B per step) / time, GiB/s.
+bytes moved (2 reads + 1 write = 805,306,368 B per step) / time, GiB/s. Step i
+sums the (i % 4)-th of four such buffer triples, so every launch reads its
+operands from HBM, not from the 256 MiB Infinity Cache.
 
 N > 1 (configs[2]): one step = allreduce of one 1 GiB fp32 bucket per GPU
 (tips_allreduce: RCCL send/recv over xGMI + the sum kernels).
@@ -606,7 +608,9 @@ def bench_allreduce(args):
                        "elements_per_launch": m, "launches_per_step": depth.value * (world - 1 if nsrc == 2 else 1),
                        "bound": "hbm", "achieved": round(kbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                        "unit": "GB/s", "frac": round(kbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
-                       "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": kbytes}
+                       "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": kbytes,
+                       "note": "one launch of the schedule's sub-chunk shape, timed alone on re-read buffers "
+                               "(Infinity Cache assisted: in the schedule a freshly received slot may be on-die too)"}
         del bufs, srcs, dst
 
     algbw = total_elems * 4 / (ms / 1e3)  # bytes/s per rank
@@ -715,7 +719,14 @@ def bench_allreduce(args):
                 line["xgmi_probe"] = link_probe(dist, rank, world)
             except Exception as e:  # noqa: BLE001
                 line["xgmi_probe"] = {"error": str(e)}
-        run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"})])
+        # Only in a job that spans every GPU of the node (the driver's last, N = 8, run) unless
+        # TIPS_BENCH_PEER=1: if the first cross-GPU run of these kernels faulted and took the
+        # GPUs down, no later bench run could be lost with it.
+        if world >= torch.cuda.device_count() or os.environ.get("TIPS_BENCH_PEER") == "1":
+            run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"})])
+        elif workload == "bucket":
+            compare_check["peer"] = ("skipped: the IPC peer schedules run only when the job spans all %d GPUs of "
+                                     "the node (TIPS_BENCH_PEER=1 forces them)" % torch.cuda.device_count())
     line["compare_check"] = compare_check
     line["compare_algbw_gib_s"] = compare
     if rank == 0:
