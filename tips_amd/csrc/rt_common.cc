@@ -46,7 +46,14 @@ State& S() {
 }
 
 int ensure_streams(State& st) {
-  if (!st.comm_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comm_stream, hipStreamNonBlocking));
+  if (!st.comm_stream) {
+    // The transfers get the device's highest stream priority: a sum kernel of ~10^5 workgroups
+    // on the compute stream must not keep the next sub-chunk's RCCL kernel waiting for CUs, or
+    // the transfer/sum overlap of the pipelined schedules is lost.
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&st.comm_stream, hipStreamNonBlocking, greatest));
+  }
   if (!st.comp_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comp_stream, hipStreamNonBlocking));
   if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
   if (!st.h2d_stream) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream, hipStreamNonBlocking));
