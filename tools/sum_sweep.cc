@@ -36,10 +36,27 @@ int main(int argc, char** argv) {
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
   const int iters = argc > 3 ? atoi(argv[3]) : 20;
   const size_t bytes = (size_t)n * 4;
+  // SWEEP_PAD="pb,pc": each (a, b, c) triple is carved from ONE allocation, b starting pb bytes
+  // after a's end and c pc bytes after b's end (their relative placement modulo the DRAM channel /
+  // bank interleave). Unset: three separate hipMallocs (2 MiB-aligned, the placement torch gives).
+  const char* pad_env = getenv("SWEEP_PAD");
+  int64_t pad_b = 0, pad_c = 0;
+  if (pad_env) sscanf(pad_env, "%ld,%ld", &pad_b, &pad_c);
+  auto alloc3 = [&](float** x, float** y, float** z) {
+    if (!pad_env) {
+      CHECK(hipMalloc(x, bytes));
+      CHECK(hipMalloc(y, bytes));
+      CHECK(hipMalloc(z, bytes));
+      return;
+    }
+    char* base = nullptr;
+    CHECK(hipMalloc((void**)&base, 3 * bytes + pad_b + pad_c));
+    *x = (float*)base;
+    *y = (float*)(base + bytes + pad_b);
+    *z = (float*)(base + 2 * bytes + pad_b + pad_c);
+  };
   float *a, *b, *c;
-  CHECK(hipMalloc(&a, bytes));
-  CHECK(hipMalloc(&b, bytes));
-  CHECK(hipMalloc(&c, bytes));
+  alloc3(&a, &b, &c);
   {
     std::vector<float> h(n);
     std::mt19937 g(1);
@@ -56,9 +73,7 @@ int main(int argc, char** argv) {
   const int rot = std::max(1, std::min(8, rot_env ? atoi(rot_env) : 1));
   float *A[8] = {a}, *B[8] = {b}, *C[8] = {c};
   for (int r = 1; r < rot; r++) {
-    CHECK(hipMalloc(&A[r], bytes));
-    CHECK(hipMalloc(&B[r], bytes));
-    CHECK(hipMalloc(&C[r], bytes));
+    alloc3(&A[r], &B[r], &C[r]);
     CHECK(hipMemcpy(A[r], a, bytes, hipMemcpyDeviceToDevice));
     CHECK(hipMemcpy(B[r], b, bytes, hipMemcpyDeviceToDevice));
   }
