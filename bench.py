@@ -660,6 +660,29 @@ def bench_allreduce(args):
         line["per_call_api_per_tensor_us"] = round(tpc / steps / len(sizes) * 1e6, 2)
         line["per_call_api_host_us_per_tensor"] = {k: round(v / steps / len(sizes) * 1e6, 2) for k, v in host_t.items()}
         per_call[0] = False
+    if workload == "resnet50":
+        # Config 5 host -> host through the Python surface, as the reference's op sees it: every
+        # gradient a host (numpy) array, one tips_amd.allreduce per tensor (__init__.py:212-222),
+        # each staged H2D -> device allreduce -> D2H. Bytes reduced per second of the whole step.
+        import numpy as np
+        hg = [np.random.default_rng(seed0 + rank * 1000 + i).random(k, dtype=np.float32) for i, k in enumerate(sizes)]
+        for gr in hg:
+            tips_amd.allreduce(gr)
+        hsteps = max(3, steps // 4)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(hsteps):
+            for gr in hg:  # each result consumed at once, as the optimizer would (no 100 MB of live outputs)
+                tips_amd.allreduce(gr)
+        th = max_over_ranks(dist, time.perf_counter() - t0) / hsteps
+        outs = [tips_amd.allreduce(gr) for gr in hg]
+        h_ok = world > 1 or all(np.array_equal(o, gr) for o, gr in zip(outs, hg))
+        line["host_to_host_python"] = {
+            "ms_per_step": round(th * 1e3, 3), "algbw_gib_s": round(total_elems * 4 / th / GIB, 2),
+            "us_per_tensor": round(th * 1e6 / len(sizes), 2), "steps": hsteps,
+            "check": "identity at one rank" if world == 1 and h_ok else ("FAIL" if not h_ok else "not checked"),
+            "note": "214 numpy gradients, one tips_amd.allreduce each (host staged), the reference's per-op structure"}
+        del hg, outs
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True
     last_words = crash_line() if rank == 0 and not args.no_compare else None

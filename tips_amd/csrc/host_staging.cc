@@ -11,6 +11,12 @@
 namespace tips {
 namespace rt {
 
+int ensure_bounce(State& st) {
+  if (!st.bounce_in) HIP_TRY(hipHostMalloc(&st.bounce_in, kBounceBytes, hipHostMallocDefault));
+  if (!st.bounce_out) HIP_TRY(hipHostMalloc(&st.bounce_out, kBounceBytes, hipHostMallocDefault));
+  return 0;
+}
+
 // Host-resident allreduce, pipelined over pieces so both PCIe directions and
 // the device work overlap: H2D of piece i+1 (h2d stream) || allreduce of piece
 // i (io stream) || D2H of piece i-1 (d2h stream). Each piece is a complete

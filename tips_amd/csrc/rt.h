@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <mutex>
 #include <string>
@@ -155,6 +156,8 @@ struct State {
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
+  void* bounce_in = nullptr;  // page-locked kBounceBytes each (hipHostMalloc), for small pageable host tensors
+  void* bounce_out = nullptr;
   int algo = TIPS_ALGO_AUTO;
   int sim_transport = 0;  // simulators: 0 = device copies, 1 = RCCL send/recv to self
   std::unordered_map<uint64_t, FusionPlan> plans;
@@ -204,6 +207,12 @@ int negotiation_stop();
 // ---------------------------------------------------------------------------
 // host staging: the reference's ops work on host (TF CPU) tensors (ops.cc:88-90)
 
+// Small pageable host tensors go through a page-locked bounce pair: a copy
+// from pageable memory is a synchronous, high-latency staged transfer inside
+// the HIP runtime, while a page-locked one is a plain DMA.
+constexpr size_t kBounceBytes = 256 << 10;
+int ensure_bounce(State& st);  // host_staging.cc
+
 // Runs enqueue(dev_in, dev_out, stream). Device pointers: on the caller's
 // stream, asynchronous. Host pointers: staged through HBM on the io stream and
 // synchronous on return. Caller holds st.mu.
@@ -215,10 +224,18 @@ int run_staged(State& st, const void* in, size_t in_bytes, void* out, size_t out
   if (dout) return enqueue(in, out, user);
   TRY(st.host_in.ensure(std::max<size_t>(in_bytes, 1)));
   TRY(st.host_out.ensure(std::max<size_t>(out_bytes, 1)));
-  if (in_bytes) HIP_TRY(hipMemcpyAsync(st.host_in.p, in, in_bytes, hipMemcpyHostToDevice, st.io_stream));
+  const bool bounce_in = in_bytes > 0 && in_bytes <= kBounceBytes && !is_pinned_host(in, (int64_t)in_bytes);
+  const bool bounce_out = out_bytes > 0 && out_bytes <= kBounceBytes && !is_pinned_host(out, (int64_t)out_bytes);
+  if (bounce_in || bounce_out) TRY(ensure_bounce(st));
+  if (bounce_in) memcpy(st.bounce_in, in, in_bytes);
+  if (in_bytes)
+    HIP_TRY(hipMemcpyAsync(st.host_in.p, bounce_in ? st.bounce_in : in, in_bytes, hipMemcpyHostToDevice, st.io_stream));
   TRY(enqueue(st.host_in.p, st.host_out.p, st.io_stream));
-  if (out_bytes) HIP_TRY(hipMemcpyAsync(out, st.host_out.p, out_bytes, hipMemcpyDeviceToHost, st.io_stream));
+  if (out_bytes)
+    HIP_TRY(hipMemcpyAsync(bounce_out ? st.bounce_out : out, st.host_out.p, out_bytes, hipMemcpyDeviceToHost,
+                           st.io_stream));
   HIP_TRY(hipStreamSynchronize(st.io_stream));
+  if (bounce_out) memcpy(out, st.bounce_out, out_bytes);
   return 0;
 }
 

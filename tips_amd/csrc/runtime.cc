@@ -115,6 +115,11 @@ void tips_shutdown(void) {
   st.staging.release();
   st.host_in.release();
   st.host_out.release();
+  for (void** b : {&st.bounce_in, &st.bounce_out})
+    if (*b) {
+      (void)hipHostFree(*b);
+      *b = nullptr;
+    }
   st.fusion.release();
   st.small.release();
   st.recv_ev.release();
