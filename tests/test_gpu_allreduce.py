@@ -430,3 +430,29 @@ def test_sparse_allreduce_single_rank(gpu):
         dense[[3, 17, 40], 1] = torch.tensor([1.0, -2.0, 0.5], device=dev)
         out = gpu.allreduce(dense.to_sparse())
         assert out.is_sparse and torch.equal(out.to_dense(), dense)
+
+
+@pytest.mark.parametrize("n", [1, 1000, 65535, 65536, 65537, 300000])
+def test_host_bounce_boundary(gpu, n):
+    """Host tensors on either side of the 256 KiB page-locked bounce threshold (rt.h run_staged):
+    pageable in and out, in place, one side page-locked, and the broadcast host path; at one rank
+    every result is the input, bit for bit."""
+    import torch
+    from tips_amd import _lib
+    h = np.random.default_rng(n).random(n).astype(np.float32)
+    out = np.full_like(h, -1.0)
+    _lib.call("tips_allreduce", h.ctypes.data, out.ctypes.data, n, _lib.FLOAT32, _lib.OP_SUM, None)
+    assert np.array_equal(out, h)
+    g = h.copy()
+    _lib.call("tips_allreduce", g.ctypes.data, g.ctypes.data, n, _lib.FLOAT32, _lib.OP_SUM, None)
+    assert np.array_equal(g, h)
+    pin = torch.from_numpy(h).pin_memory()
+    out2 = np.full_like(h, -1.0)
+    _lib.call("tips_allreduce", pin.data_ptr(), out2.ctypes.data, n, _lib.FLOAT32, _lib.OP_SUM, None)
+    assert np.array_equal(out2, h)
+    pout = torch.full((n,), -1.0).pin_memory()
+    _lib.call("tips_allreduce", h.ctypes.data, pout.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, None)
+    assert np.array_equal(pout.numpy(), h)
+    out3 = np.full_like(h, -1.0)
+    _lib.call("tips_broadcast", h.ctypes.data, out3.ctypes.data, n, _lib.FLOAT32, 0, None)
+    assert np.array_equal(out3, h)
