@@ -249,7 +249,8 @@ TIPS_API int tips_set_sim_transport(int transport);
  * (tools/sum_sweep.cc): mode 0 = grid-stride over `blocks` workgroups,
  * mode 1 = one tile per workgroup, mode 2 = the same in XCD-contiguous order,
  * mode 3 = buffer-op forms (nt = cache-policy pair), mode 4 = LDS-staged
- * through direct-to-LDS loads (unroll 1/2/4, 256 threads);
+ * through direct-to-LDS loads (unroll 1/2/4, 256 threads), mode 5 = persistent
+ * streaming, 256 x unroll workgroups each walking one contiguous range;
  * unroll = 16-B vectors per lane in flight;
  * nt: 0 plain, 1 non-temporal loads+stores, 2 nt loads only, 3 nt stores only;
  * threads = workgroup size. Non-default variants exist for f32 only

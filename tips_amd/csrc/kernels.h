@@ -47,7 +47,8 @@ hipError_t launch_multi_sum_variant(void* dst, const void* const* srcs, int nsrc
 //   unroll = 16-B vectors per lane in flight, nt: 0 plain, 1 non-temporal loads+stores,
 //   2 nt loads only, 3 nt stores only; threads = workgroup size. Non-default variants are f32 only.
 //   mode 3 = buffer-op forms (nt = cache-policy pair index), mode 4 = LDS-staged through gfx950's
-//   direct-to-LDS loads (unroll 1, 2 or 4; 256 threads).
+//   direct-to-LDS loads (unroll 1, 2 or 4; 256 threads), mode 5 = persistent streaming (unroll =
+//   workgroups per CU: 1, 2, 4 or 8).
 hipError_t launch_sum2_variant(void* dst, const void* a, const void* b, int64_t n, int dtype, int mode, int unroll,
                                int nt, int blocks, int threads, hipStream_t s);
 

@@ -263,6 +263,45 @@ __global__ __launch_bounds__(256) void sum2_lds_kernel(u32x4* __restrict__ dst, 
   if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
 }
 
+// Persistent streaming 2-input sum (tuning sweep only, f32): gridDim = 256 CUs x WPC
+// workgroups, each owning one contiguous range of the bucket (XCD-contiguous order), walked
+// 4 KiB per operand at a time with the next tile's loads issued before the current tile's add
+// and sc1 store (2-deep software pipeline). Tests whether long sequential runs per CU beat one
+// short tile per workgroup on DRAM efficiency.
+__global__ __launch_bounds__(256) void sum2_stream_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
+                                                          const u32x4* __restrict__ b, int64_t nvec,
+                                                          int64_t tail_begin, int64_t n) {
+  const int64_t G = gridDim.x;
+  const int64_t per = ((nvec + G - 1) / G + 255) / 256 * 256;
+  const int64_t beg = xcd_tile(blockIdx.x, gridDim.x) * per;
+  const int64_t end = beg + per < nvec ? beg + per : nvec;
+  const int tid = threadIdx.x;
+  if (beg < end) {
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + beg), (short)0,
+                                                                  (int)((end - beg) * 16), 0x00020000);
+    const int64_t iters = (end - beg + 255) / 256;
+    int64_t i = beg + tid;
+    u32x4 x0 = {}, y0 = {};
+    if (i < end) {
+      x0 = ld16<true>(a + i);
+      y0 = ld16<true>(b + i);
+    }
+    for (int64_t k = 0; k < iters; k++) {
+      const int64_t j = i + 256;
+      u32x4 x1 = {}, y1 = {};
+      if (j < end) {
+        x1 = ld16<true>(a + j);
+        y1 = ld16<true>(b + j);
+      }
+      if (i < end) __builtin_amdgcn_raw_buffer_store_b128(add16<kF32>(x0, y0), rd, (int)((i - beg) * 16), 0, 16);
+      x0 = x1;
+      y0 = y1;
+      i = j;
+    }
+  }
+  if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
+}
+
 // Unaligned fallback (any pointer not 16-B aligned): one element per lane.
 template <int DT>
 __global__ __launch_bounds__(kBlock) void sum2_scalar_kernel(void* dst, const void* a, const void* b, int64_t n) {
@@ -548,6 +587,17 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((sum2_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, a, b, n);
     return hipGetLastError();
+  }
+  if (mode == 5) {  // persistent streaming, f32, 256 threads; unroll = workgroups per CU (grid = 256 x unroll)
+    if constexpr (DT == kF32) {
+      if (threads == 256 && (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8)) {
+        const int64_t nvec = n / 4;
+        hipLaunchKernelGGL(sum2_stream_kernel, dim3((unsigned)(kNumCUs * unroll)), dim3(256), 0, s, (u32x4*)dst,
+                           (const u32x4*)a, (const u32x4*)b, nvec, nvec * 4, n);
+        return hipGetLastError();
+      }
+    }
+    return hipErrorInvalidValue;
   }
   if (mode == 4) {  // LDS-staged (direct-to-LDS loads), f32, 256 threads; unroll = 16-B vectors per lane
     if constexpr (DT == kF32) {

@@ -108,6 +108,8 @@ int main(int argc, char** argv) {
   const int ntnt[][2] = {{1, 512}, {1, 1024}, {2, 256}, {4, 256}, {2, 512}};  // buffer nt loads + nt stores
   for (auto& t : ntnt)
     vs.push_back({"buf_ntnt_u" + std::to_string(t[0]) + "_t" + std::to_string(t[1]), 3, t[0], 7, 0, t[1], {}});
+  for (int w : {1, 2, 4, 8})  // persistent streaming, w workgroups per CU, 2-deep pipeline (mode 5)
+    vs.push_back({"stream_w" + std::to_string(w), 5, w, 0, 0, 256, {}});
   for (int u : {1, 2, 4})  // LDS-staged through direct-to-LDS loads (mode 4)
     vs.push_back({"lds_glds_u" + std::to_string(u) + "_t256", 4, u, 0, 0, 256, {}});
   for (auto& t : xcd)
