@@ -302,6 +302,28 @@ def resnet50_grad_sizes():
     return sizes
 
 
+def gpu_topology():
+    """rocm-smi's GPU-to-GPU link type and hop matrices (rank 0 at N > 1, before the GPU is used):
+    what the xGMI numbers of the line ran over. None if rocm-smi is missing or fails."""
+    try:
+        r = subprocess.run(["rocm-smi", "--showtopotype", "--showtopohops"], capture_output=True, text=True,
+                           timeout=30)
+    except Exception:  # noqa: BLE001
+        return None
+    out, section = {}, None
+    for ln in r.stdout.splitlines():
+        if "Link Type between two GPUs" in ln:
+            section = out.setdefault("link_type", [])
+        elif "Hops between two GPUs" in ln:
+            section = out.setdefault("hops", [])
+        elif ln.startswith("GPU") and section is not None and len(ln.split()) > 1:
+            section.append(ln.split()[1:])
+        elif ln.startswith("=") or not ln.strip():
+            if section is not None and section:
+                section = None
+    return out or None
+
+
 def max_over_ranks(dist, seconds):
     """The contract's job time: the slowest rank's timed region (gloo all-reduce MAX on the host)."""
     import torch
@@ -429,6 +451,7 @@ def bench_allreduce(args):
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "420")), rank)
+    topo = gpu_topology() if rank == 0 and world > 1 else None
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))  # (several ranks per GPU only under TIPS_NO_RCCL)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import tips_amd
@@ -646,6 +669,8 @@ def bench_allreduce(args):
                                 "in -> out copy" if workload == "bucket" else
                                 "algorithmic bytes = pack + unpack of every tensor (2 reads + 2 writes)")}
         del line["xgmi"]
+    if topo:
+        line["gpu_topology"] = topo
     if fallbacks:
         line["failed_schedules"] = fallbacks
     if workload == "negotiated1000":

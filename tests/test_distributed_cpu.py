@@ -148,3 +148,29 @@ def test_bench_watchdog(state, code, expect):
     else:
         assert len(lines) == 1 and expect in lines[0]
         json.loads(lines[0])
+
+
+def test_gpu_topology_parse(monkeypatch):
+    """bench.gpu_topology reads rocm-smi's link-type and hop matrices (the text layout of ROCm 7.2)."""
+    import subprocess
+    sys.path.insert(0, REPO)
+    import bench
+    txt = ("=== ROCm System Management Interface ===\n\n"
+           "======== Hops between two GPUs ========\n"
+           "       GPU0         GPU1         GPU2\n"
+           "GPU0   0            1            1\n"
+           "GPU1   1            0            1\n"
+           "GPU2   1            1            0\n\n"
+           "======== Link Type between two GPUs ========\n"
+           "       GPU0         GPU1         GPU2\n"
+           "GPU0   0            XGMI         XGMI\n"
+           "GPU1   XGMI         0            XGMI\n"
+           "GPU2   XGMI         XGMI         0\n\n"
+           "======== End of ROCm SMI Log ========\n")
+
+    class R:
+        stdout = txt
+    monkeypatch.setattr(subprocess, "run", lambda *a, **k: R)
+    topo = bench.gpu_topology()
+    assert topo["hops"] == [["0", "1", "1"], ["1", "0", "1"], ["1", "1", "0"]]
+    assert topo["link_type"][1] == ["XGMI", "0", "XGMI"]
