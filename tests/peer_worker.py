@@ -53,6 +53,45 @@ def named_case(c, rank, size, L, _lib, sp):
     return {"case": {"named": len(tensors), "seed": c["seed"]}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5])}
 
 
+def optimizer_case(c, rank, size, L, _lib, sp):
+    """tips_amd.DistributedOptimizer over torch.optim.SGD on a small model on the device: every
+    rank computes its own gradients from its own seeded batch, step() sums them over the ranks
+    (fusion buckets -> peer schedule) and applies SGD. Every rank recomputes all ranks' gradients
+    locally and checks the updated parameters against p - lr * sum_r grad_r (summed in rank order,
+    as the fold does), to within fp32 rounding of the SGD update."""
+    import torch
+    import tips_amd
+
+    def model():
+        torch.manual_seed(c["seed"])
+        return torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4)).cuda()
+
+    def grads_of(r):
+        m = model()
+        g = torch.Generator().manual_seed(c["seed"] * 100 + r)
+        x = torch.randn(8, 16, generator=g).cuda()
+        m(x).pow(2).sum().backward()
+        return [p.grad.detach().clone() for p in m.parameters()]
+
+    all_g = [grads_of(r) for r in range(size)]
+    m = model()
+    g = torch.Generator().manual_seed(c["seed"] * 100 + rank)
+    m(torch.randn(8, 16, generator=g).cuda()).pow(2).sum().backward()
+    lr = 0.05
+    with torch.no_grad():
+        exp = []
+        for i, p in enumerate(m.parameters()):
+            s = all_g[0][i].clone()
+            for r in range(1, size):
+                s = s + all_g[r][i]
+            exp.append(p - lr * s)
+    opt = tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=lr))
+    opt.step()
+    torch.cuda.synchronize()
+    ok = all(torch.allclose(p, e, rtol=0, atol=1e-6) for p, e in zip(m.parameters(), exp))
+    return {"case": {"optimizer": c["seed"]}, "rc": 0, "ok": bool(ok), "error": "" if ok else "parameters differ"}
+
+
 def golden_case(c, rank, size, L, _lib, sp):
     """A committed golden vector (tests/golden: inputs and the reference's MPI_Allreduce output
     under MPICH) through the real multi-process product path: rank r reduces inputs[r]; the
@@ -115,6 +154,9 @@ def main():
             continue
         if c.get("golden"):
             results.append(golden_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("optimizer"):
+            results.append(optimizer_case(c, rank, size, L, _lib, sp))
             continue
         dtype, n, seed = c["dtype"], c["n"], c["seed"]
         if c.get("count_per_rank"):  # deliberately inconsistent counts: every rank must fail, none hang

@@ -117,3 +117,11 @@ def test_golden_vectors_across_processes(gpu, p):
     if p == 2:
         for res in results:
             assert all(c["bit_exact_vs_mpich"] for c in res["results"])
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_distributed_optimizer_across_processes(gpu, p):
+    """tips_amd.DistributedOptimizer (reference __init__.py:252-456) in p real processes: each
+    rank's gradients differ, step() sums them through the fusion buckets over the peer schedule,
+    and every rank ends with the same parameters, p - lr * sum of all ranks' gradients."""
+    check(run_job(p, [{"optimizer": True, "seed": 7}], TIPS_PEER_WS_MIB="16"))

@@ -158,3 +158,58 @@ def test_allreduce_grads_sparse_as_dense(monkeypatch):
     assert torch.equal(out[1], 2 * torch.tensor([[2.0, 2.0], [0.0, 0.0], [0.0, 0.0]]))
     assert not out[2].is_sparse and torch.equal(out[2], 2 * dense)
     assert out[3] is None
+
+
+def _toy_model():
+    import torch
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.Tanh(), torch.nn.Linear(3, 2))
+
+
+def test_distributed_optimizer_sums_gradients_before_step(monkeypatch):
+    """DistributedOptimizer (reference __init__.py:252-456) over torch.optim: step() allreduces every
+    .grad first; as in the reference the reduction is a SUM even for op=Average (two fake ranks
+    holding the same gradient: the update is twice the local one)."""
+    import torch
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    monkeypatch.setattr(tips_amd, "allreduce", lambda t, **kw: t * 2)
+    ref, dist_m = _toy_model(), _toy_model()
+    x = torch.randn(5, 4)
+    for m in (ref, dist_m):
+        m(x).pow(2).sum().backward()
+    lr = 0.1
+    opt = tips_amd.DistributedOptimizer(torch.optim.SGD(dist_m.parameters(), lr=lr))
+    with torch.no_grad():
+        exp = [p - lr * 2 * p.grad for p in ref.parameters()]
+    opt.step()
+    for p, e in zip(dist_m.parameters(), exp):
+        assert torch.allclose(p, e, atol=1e-7)
+
+
+def test_distributed_optimizer_backward_passes_and_validation(monkeypatch):
+    import torch
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    calls = []
+    monkeypatch.setattr(tips_amd, "allreduce", lambda t, **kw: calls.append(1) or t)
+    m = _toy_model()
+    x = torch.randn(5, 4)
+    opt = tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), backward_passes_per_step=2,
+                                        average_aggregated_gradients=True)
+    before = [p.detach().clone() for p in m.parameters()]
+    m(x).sum().backward()
+    g1 = [p.grad.clone() for p in m.parameters()]
+    opt.step()  # first pass: accumulate only
+    assert not calls and all(torch.equal(p, b) for p, b in zip(m.parameters(), before))
+    m(x).sum().backward()  # .grad now holds both passes
+    opt.step()
+    assert len(calls) == len(before)
+    for p, b, g in zip(m.parameters(), before, g1):  # averaged over the 2 passes: (g + g) / 2 = g
+        assert torch.allclose(p, b - 0.1 * g, atol=1e-6)
+    with pytest.raises(ValueError, match="gradient_predivide_factor not supported"):
+        tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), op="Sum", gradient_predivide_factor=2.0)
+    with pytest.raises(ValueError, match="groups should be a non-negative integer"):
+        tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), groups=-1)
+    with pytest.raises(ValueError, match="doesn't inherit"):
+        tips_amd.DistributedOptimizer(object())

@@ -32,6 +32,7 @@ __all__ = [
     "set_consistency_check", "registered_host_buffer", "bucket_sum", "fused_allreduce_", "init", "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
+    "DistributedOptimizer",
 ]
 
 
@@ -143,3 +144,6 @@ def allreduce_grads(grads, compression=Compression.none, op=None, fused=True, sp
 def _fusable(g):
     """Dense device tensors go through the fusion buckets; sparse and host ones are reduced one by one."""
     return g is not None and _tensors.is_device(g) and not g.is_sparse
+
+
+from .optim import DistributedOptimizer  # noqa: E402  (uses allreduce_grads above)

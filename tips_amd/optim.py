@@ -1,0 +1,122 @@
+"""DistributedOptimizer for torch — mirrors tips.tensorflow.DistributedOptimizer
+(reference tips/tensorflow/__init__.py:252-456).
+
+The reference wraps a TF optimizer: compute_gradients() allreduces every
+gradient (_make_allreduce_grads_fn, __init__.py:189-227) before the wrapped
+optimizer applies them, optionally after backward_passes_per_step local
+accumulations (LocalGradientAggregationHelper, gradient_aggregation.py). Here
+the wrapped object is a torch.optim.Optimizer and the hook point is step():
+the parameters' .grad tensors are summed over ranks through
+tips_amd.allreduce_grads (device tensors through the fusion buckets), written
+back in place, and then the wrapped optimizer steps.
+
+As in the reference, op / prescale / postscale never reach the reduction
+(__init__.py:82-87, 194-201): the gradients are SUMMED over ranks, op=Average
+included. gradient_predivide_factor is validated as the
+reference validates it (__init__.py:408-411) and otherwise has no effect,
+for the same reason.
+"""
+import warnings
+
+Average = 'Average'
+
+
+class _DistributedOptimizer(object):
+    """Wraps a torch.optim.Optimizer; step() allreduces the gradients first (__init__.py:252-335)."""
+
+    def __init__(self, optimizer, compression, sparse_as_dense, op, backward_passes_per_step,
+                 average_aggregated_gradients, groups):
+        from . import Compression
+        self._optimizer = optimizer
+        self._compression = compression if compression is not None else Compression.none
+        self._sparse_as_dense = sparse_as_dense
+        self._op = op
+        self._passes = int(backward_passes_per_step)
+        self._average_aggregated = average_aggregated_gradients
+        self._groups = groups
+        self._calls = 0
+        if self._passes < 1:
+            raise ValueError("backward_passes_per_step must be >= 1")
+
+    # the wrapped optimizer's surface
+    @property
+    def param_groups(self):
+        return self._optimizer.param_groups
+
+    @property
+    def state(self):
+        return self._optimizer.state
+
+    def zero_grad(self, set_to_none=True):
+        return self._optimizer.zero_grad(set_to_none=set_to_none)
+
+    def state_dict(self):
+        return self._optimizer.state_dict()
+
+    def load_state_dict(self, sd):
+        return self._optimizer.load_state_dict(sd)
+
+    def _params_with_grad(self):
+        return [p for g in self._optimizer.param_groups for p in g["params"] if p.grad is not None]
+
+    def synchronize(self):
+        """Allreduce every parameter's .grad in place (compute_gradients, __init__.py:296-310)."""
+        from . import allreduce_grads
+        params = self._params_with_grad()
+        grads = [p.grad for p in params]
+        if self._passes > 1 and self._average_aggregated:
+            grads = [g / self._passes for g in grads]
+        reduced = allreduce_grads(grads, compression=self._compression, op=self._op,
+                                  sparse_as_dense=self._sparse_as_dense)
+        for p, r in zip(params, reduced):
+            if r is not p.grad:
+                p.grad = r.to(p.grad.dtype) if (not r.is_sparse and r.dtype != p.grad.dtype) else r
+
+    def step(self, closure=None):
+        """Every backward_passes_per_step-th call: allreduce the (locally accumulated) gradients,
+        then step the wrapped optimizer. Other calls only count (torch accumulates .grad across
+        backward passes when zero_grad is not called in between), as the aggregation helper
+        applies updates once per backward_passes_per_step (gradient_aggregation.py)."""
+        self._calls += 1
+        if self._calls % self._passes:
+            return None
+        self.synchronize()
+        return self._optimizer.step(closure) if closure is not None else self._optimizer.step()
+
+
+def DistributedOptimizer(optimizer,
+                         name=None,
+                         use_locking=False,
+                         device_dense='',
+                         device_sparse='',
+                         compression=None,
+                         sparse_as_dense=False,
+                         backward_passes_per_step=1,
+                         op=Average,
+                         gradient_predivide_factor=1.0,
+                         average_aggregated_gradients=False,
+                         num_groups=0,
+                         groups=None):
+    """Same arguments and validation as the reference (__init__.py:337-456); `optimizer` is a
+    torch.optim.Optimizer. name / use_locking / device_* are accepted for signature compatibility."""
+    if gradient_predivide_factor != 1.0:
+        if op != Average:
+            raise ValueError('gradient_predivide_factor not supported with op != Average')
+    if num_groups != 0:
+        warnings.warn('Parameter `num_groups` has been replaced by `groups` '
+                      'and will be removed in v0.23.0.', DeprecationWarning)
+        if groups is None:
+            groups = num_groups
+    if groups is not None:
+        if not (isinstance(groups, list) or groups > 0):
+            raise ValueError('groups should be a non-negative integer or '
+                             'a list of list of tf.Variable.')
+    try:
+        import torch
+        ok = isinstance(optimizer, torch.optim.Optimizer)
+    except ImportError:  # pragma: no cover - torch is in the image
+        ok = False
+    if not ok:
+        raise ValueError('Provided optimizer doesn\'t inherit from torch.optim.Optimizer: %s' % optimizer)
+    return _DistributedOptimizer(optimizer, compression, sparse_as_dense, op, backward_passes_per_step,
+                                 average_aggregated_gradients, groups)
