@@ -92,6 +92,34 @@ def optimizer_case(c, rank, size, L, _lib, sp):
     return {"case": {"optimizer": c["seed"]}, "rc": 0, "ok": bool(ok), "error": "" if ok else "parameters differ"}
 
 
+def tape_case(c, rank, size, L, _lib, sp):
+    """tips_amd.DistributedGradientTape on the device: every rank differentiates its own seeded
+    loss; gradient() returns the sum over ranks (fusion buckets -> peer schedule), which must equal
+    the rank-order sum of all ranks' local gradients bit for bit (the peer fold's order)."""
+    import torch
+    import tips_amd
+    torch.manual_seed(c["seed"])
+    w = torch.randn(1000, device="cuda", requires_grad=True)
+    b = torch.randn(37, device="cuda", requires_grad=True)
+
+    def local(r):
+        g = torch.Generator().manual_seed(c["seed"] * 100 + r)
+        x, y = torch.randn(1000, generator=g).cuda(), torch.randn(37, generator=g).cuda()
+        return (w * x).pow(2).sum() + (b * y).sum()
+
+    all_g = [torch.autograd.grad(local(r), [w, b]) for r in range(size)]
+    exp = []
+    for i in range(2):
+        s = all_g[0][i].clone()
+        for r in range(1, size):
+            s = s + all_g[r][i]
+        exp.append(s)
+    got = tips_amd.DistributedGradientTape().gradient(local(rank), [w, b])
+    torch.cuda.synchronize()
+    ok = all(torch.equal(g, e) for g, e in zip(got, exp))
+    return {"case": {"tape": c["seed"]}, "rc": 0, "ok": bool(ok), "error": "" if ok else "gradients differ"}
+
+
 def golden_case(c, rank, size, L, _lib, sp):
     """A committed golden vector (tests/golden: inputs and the reference's MPI_Allreduce output
     under MPICH) through the real multi-process product path: rank r reduces inputs[r]; the
@@ -154,6 +182,9 @@ def main():
             continue
         if c.get("golden"):
             results.append(golden_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("tape"):
+            results.append(tape_case(c, rank, size, L, _lib, sp))
             continue
         if c.get("optimizer"):
             results.append(optimizer_case(c, rank, size, L, _lib, sp))

@@ -125,3 +125,11 @@ def test_distributed_optimizer_across_processes(gpu, p):
     rank's gradients differ, step() sums them through the fusion buckets over the peer schedule,
     and every rank ends with the same parameters, p - lr * sum of all ranks' gradients."""
     check(run_job(p, [{"optimizer": True, "seed": 7}], TIPS_PEER_WS_MIB="16"))
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_distributed_gradient_tape_across_processes(gpu, p):
+    """tips_amd.DistributedGradientTape (reference __init__.py:460-569) in p real processes:
+    gradient() returns every rank's gradients summed over the ranks, bit-exact against the
+    rank-order sum (the peer schedule's fold order)."""
+    check(run_job(p, [{"tape": True, "seed": 11}], TIPS_PEER_WS_MIB="16"))

@@ -213,3 +213,34 @@ def test_distributed_optimizer_backward_passes_and_validation(monkeypatch):
         tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), groups=-1)
     with pytest.raises(ValueError, match="doesn't inherit"):
         tips_amd.DistributedOptimizer(object())
+
+
+def test_distributed_gradient_tape(monkeypatch):
+    """DistributedGradientTape (reference __init__.py:460-569): gradient() differentiates, then sums
+    the gradients over the ranks (a SUM for op=Average too); an unused source stays None; a single
+    source gives a single gradient; a wrapped tape object supplies the gradients; the reference's
+    argument validation."""
+    import torch
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    monkeypatch.setattr(tips_amd, "allreduce", lambda t, **kw: t * 2)
+    w = torch.randn(3, requires_grad=True)
+    unused = torch.randn(2, requires_grad=True)
+    x = torch.randn(3)
+    tape = tips_amd.DistributedGradientTape()
+    gw, gu = tape.gradient((w * x).sum(), [w, unused])
+    assert torch.equal(gw, 2 * x) and gu is None
+    assert torch.equal(tape.gradient((w * w).sum(), w), 4 * w.detach())
+
+    class Tape(object):
+        def gradient(self, target, sources, output_gradients=None):
+            return [torch.ones_like(s) for s in sources]
+    assert torch.equal(tips_amd.DistributedGradientTape(Tape()).gradient(None, [w])[0], 2 * torch.ones(3))
+    with pytest.raises(ValueError, match="gradient_predivide_factor not supported"):
+        tips_amd.DistributedGradientTape(op="Sum", gradient_predivide_factor=2.0)
+    with pytest.raises(ValueError, match="groups should be a non-negative integer"):
+        tips_amd.DistributedGradientTape(groups=0)
+    with pytest.warns(DeprecationWarning):
+        tips_amd.DistributedGradientTape(num_groups=2)
+    with pytest.raises(ValueError, match="gradient"):
+        tips_amd.DistributedGradientTape(object())

@@ -32,7 +32,7 @@ __all__ = [
     "set_consistency_check", "registered_host_buffer", "bucket_sum", "fused_allreduce_", "init", "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
-    "DistributedOptimizer",
+    "DistributedOptimizer", "DistributedGradientTape",
 ]
 
 
@@ -146,4 +146,4 @@ def _fusable(g):
     return g is not None and _tensors.is_device(g) and not g.is_sparse
 
 
-from .optim import DistributedOptimizer  # noqa: E402  (uses allreduce_grads above)
+from .optim import DistributedGradientTape, DistributedOptimizer  # noqa: E402  (uses allreduce_grads above)

@@ -1,5 +1,6 @@
-"""DistributedOptimizer for torch — mirrors tips.tensorflow.DistributedOptimizer
-(reference tips/tensorflow/__init__.py:252-456).
+"""DistributedOptimizer and DistributedGradientTape for torch — mirror
+tips.tensorflow.DistributedOptimizer / DistributedGradientTape
+(reference tips/tensorflow/__init__.py:252-456, 460-569).
 
 The reference wraps a TF optimizer: compute_gradients() allreduces every
 gradient (_make_allreduce_grads_fn, __init__.py:189-227) before the wrapped
@@ -84,6 +85,69 @@ class _DistributedOptimizer(object):
         return self._optimizer.step(closure) if closure is not None else self._optimizer.step()
 
 
+def _validate(op, gradient_predivide_factor, num_groups, groups):
+    """The argument checks DistributedOptimizer and DistributedGradientTape share
+    (__init__.py:408-423, 540-556), with the reference's messages; returns `groups`."""
+    if gradient_predivide_factor != 1.0:
+        if op != Average:
+            raise ValueError('gradient_predivide_factor not supported with op != Average')
+    if num_groups != 0:
+        warnings.warn('Parameter `num_groups` has been replaced by `groups` '
+                      'and will be removed in v0.23.0.', DeprecationWarning)
+        if groups is None:
+            groups = num_groups
+    if groups is not None:
+        if not (isinstance(groups, list) or groups > 0):
+            raise ValueError('groups should be a non-negative integer or '
+                             'a list of list of tf.Variable.')
+    return groups
+
+
+class _DistributedGradientTape(object):
+    """gradient() computes the gradients, then sums them over the ranks
+    (_DistributedGradientTape.gradient, __init__.py:485-488)."""
+
+    def __init__(self, tape, compression, sparse_as_dense, op):
+        from . import Compression
+        self._tape = tape
+        self._compression = compression if compression is not None else Compression.none
+        self._sparse_as_dense = sparse_as_dense
+        self._op = op
+
+    def gradient(self, target, sources, output_gradients=None):
+        from . import allreduce_grads
+        single = not isinstance(sources, (list, tuple))
+        srcs = [sources] if single else list(sources)
+        if self._tape is not None:
+            grads = self._tape.gradient(target, srcs, output_gradients)
+        else:
+            import torch
+            grads = torch.autograd.grad(target, srcs, grad_outputs=output_gradients, allow_unused=True)
+        reduced = allreduce_grads(list(grads), compression=self._compression, op=self._op,
+                                  sparse_as_dense=self._sparse_as_dense)
+        return reduced[0] if single else reduced
+
+
+def DistributedGradientTape(gradtape=None,
+                            device_dense='',
+                            device_sparse='',
+                            compression=None,
+                            sparse_as_dense=False,
+                            op=Average,
+                            gradient_predivide_factor=1.0,
+                            num_groups=0,
+                            groups=None):
+    """Same arguments and validation as the reference (__init__.py:490-569). torch has no tape
+    object: with gradtape=None, gradient(target, sources, output_gradients) differentiates with
+    torch.autograd.grad (allow_unused: a source the target does not depend on gets None, as
+    tf.GradientTape returns); any object with that gradient() method can be wrapped instead.
+    As for the optimizer, the gradients are SUMMED over ranks for op=Average too (__init__.py:82-87)."""
+    _validate(op, gradient_predivide_factor, num_groups, groups)
+    if gradtape is not None and not callable(getattr(gradtape, 'gradient', None)):
+        raise ValueError('gradtape must have a gradient(target, sources, output_gradients) method: %s' % gradtape)
+    return _DistributedGradientTape(gradtape, compression, sparse_as_dense, op)
+
+
 def DistributedOptimizer(optimizer,
                          name=None,
                          use_locking=False,
@@ -99,18 +163,7 @@ def DistributedOptimizer(optimizer,
                          groups=None):
     """Same arguments and validation as the reference (__init__.py:337-456); `optimizer` is a
     torch.optim.Optimizer. name / use_locking / device_* are accepted for signature compatibility."""
-    if gradient_predivide_factor != 1.0:
-        if op != Average:
-            raise ValueError('gradient_predivide_factor not supported with op != Average')
-    if num_groups != 0:
-        warnings.warn('Parameter `num_groups` has been replaced by `groups` '
-                      'and will be removed in v0.23.0.', DeprecationWarning)
-        if groups is None:
-            groups = num_groups
-    if groups is not None:
-        if not (isinstance(groups, list) or groups > 0):
-            raise ValueError('groups should be a non-negative integer or '
-                             'a list of list of tf.Variable.')
+    groups = _validate(op, gradient_predivide_factor, num_groups, groups)
     try:
         import torch
         ok = isinstance(optimizer, torch.optim.Optimizer)
