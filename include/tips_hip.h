@@ -248,7 +248,8 @@ TIPS_API int tips_set_sim_transport(int transport);
 /* Explicit variant of the 2-input sum kernel, for the gfx950 tuning sweep
  * (tools/sum_sweep.cc): mode 0 = grid-stride over `blocks` workgroups,
  * mode 1 = one tile per workgroup, mode 2 = the same in XCD-contiguous order,
- * mode 3 = buffer-op forms (nt = cache-policy pair), mode 4 = LDS-staged
+ * mode 3 = buffer-op forms (nt = cache-policy pair; blocks = bytes of LDS
+ * reserved per workgroup, 0-65536, to cap workgroups per CU), mode 4 = LDS-staged
  * through direct-to-LDS loads (unroll 1/2/4, 256 threads), mode 5 = persistent
  * streaming, 256 x unroll workgroups each walking one contiguous range;
  * unroll = 16-B vectors per lane in flight;

@@ -65,7 +65,7 @@ SWEEP_VARIANTS = ([(m, u, t, 256) for m in (0, 1) for u in (1, 2, 4, 8) for t in
                      (1, 4, 3, 512), (1, 16, 1, 256), (1, 16, 1, 128), (1, 8, 1, 128), (1, 4, 1, 128), (1, 8, 1, 64),
                      (1, 1, 2, 256), (1, 8, 2, 256), (1, 2, 2, 512), (1, 2, 2, 128), (1, 1, 2, 512), (0, 2, 2, 256),
                      (0, 4, 2, 256), (2, 1, 2, 256), (2, 2, 2, 256), (2, 1, 2, 512), (2, 4, 1, 256)]
-                  + [(3, 1, i, 256) for i in range(10)]
+                  + [(3, 1, i, 256) for i in range(14)]
                   + [(3, u, 1, t) for u, t in ((2, 256), (4, 256), (1, 512), (2, 128), (1, 1024), (1, 128), (2, 512))]
                   + [(4, u, 0, 256) for u in (1, 2, 4)]
                   + [(5, w, 0, 256) for w in (1, 2, 4, 8)]

@@ -628,9 +628,13 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     const int64_t ve = 16 / (int64_t)dtype_size(DT);
     const int64_t nvec = n / ve;
     auto grid_for = [&](int64_t tile) { return (unsigned)std::max<int64_t>(8, ((nvec + tile - 1) / tile + 7) / 8 * 8); };
+    // blocks > 0: that many bytes of (unused) LDS reserved per workgroup, capping workgroups per CU
+    // at 160 KiB / blocks (the occupancy sweep); 0 = no cap
+    if (blocks < 0 || blocks > 65536) return hipErrorInvalidValue;
+    const unsigned shmem = (unsigned)blocks;
 #define TIPS_BUF_CASE(I, L, S_, U, B)                                                                          \
   if (nt == I && unroll == U && threads == B) {                                                            \
-    hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_, U, B>), dim3(grid_for((int64_t)U * B)), dim3(B), 0, s,     \
+    hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_, U, B>), dim3(grid_for((int64_t)U * B)), dim3(B), shmem, s, \
                        (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);                 \
     return hipGetLastError();                                                                              \
   }
@@ -657,6 +661,10 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
       TIPS_BUF_CASE(7, 2, 2, 2, 256)
       TIPS_BUF_CASE(7, 2, 2, 4, 256)
       TIPS_BUF_CASE(7, 2, 2, 2, 512)
+      TIPS_BUF_CASE(10, 2, 18, 1, 256)  // nt loads; stores nt sc1, sc0 nt sc1, sc0, sc0 nt
+      TIPS_BUF_CASE(11, 2, 19, 1, 256)
+      TIPS_BUF_CASE(12, 2, 1, 1, 256)
+      TIPS_BUF_CASE(13, 2, 3, 1, 256)
     }
 #undef TIPS_BUF_CASE
     return hipErrorInvalidValue;

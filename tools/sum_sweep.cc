@@ -102,6 +102,10 @@ int main(int argc, char** argv) {
                         "ld_sc0nt/st_plain", "ld_sc1/st_plain", "ld_ntsc1/st_sc1", "ld_nt/st_nt",
                         "ld_plain/st_sc1",   "ld_sc0nt/st_sc0sc1"};
   for (int i = 0; i < 10; i++) vs.push_back({std::string("buf_") + cpol[i], 3, 1, i, 0, 256, {}});
+  const char* stpol[] = {"ld_nt/st_ntsc1", "ld_nt/st_sc0ntsc1", "ld_nt/st_sc0", "ld_nt/st_sc0nt"};
+  for (int i = 0; i < 4; i++) vs.push_back({std::string("buf_") + stpol[i], 3, 1, 10 + i, 0, 256, {}});
+  for (int kib : {20, 24, 32, 40, 54, 64})  // the default with k KiB of LDS reserved: 160 / k workgroups per CU
+    vs.push_back({"buf_ntsc1_occ_lds" + std::to_string(kib) + "k", 3, 1, 1, kib * 1024, 256, {}});
   const int bufshape[][2] = {{2, 256}, {4, 256}, {1, 512}, {2, 128}, {1, 1024}, {1, 128}, {2, 512}};
   for (auto& t : bufshape)
     vs.push_back({"buf_ntsc1_u" + std::to_string(t[0]) + "_t" + std::to_string(t[1]), 3, t[0], 1, 0, t[1], {}});
