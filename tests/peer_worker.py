@@ -120,6 +120,76 @@ def tape_case(c, rank, size, L, _lib, sp):
     return {"case": {"tape": c["seed"]}, "rc": 0, "ok": bool(ok), "error": "" if ok else "gradients differ"}
 
 
+def collectives_case(c, rank, size, L, _lib, sp):
+    """broadcast_op / allgather_op / broadcast_variables and the consistency-checked allreduce
+    over the peer transport (tips_broadcast, tips_allgatherv and the record exchange routed to
+    peer.cc when the peer schedule is selected). Broadcast: every dtype, device and host, and one
+    bucket larger than the workspace (pieces); the result must equal the root's tensor bit for
+    bit. Allgather: ragged first dimensions, one rank contributing zero rows. A root that differs
+    between ranks must fail on every rank with TIPS_ERR_MISMATCH and leave the job usable."""
+    import numpy as np
+    import torch
+    import tips_amd
+    seed = c["seed"]
+    root = seed % size
+    bad = []
+
+    def tensor(r, dtype, n, salt=0):
+        g = torch.Generator().manual_seed(seed * 1000 + 17 * salt + r)
+        return (torch.randn(n, generator=g) * 100).to(dtype)
+
+    sizes = [(torch.float32, 4099), (torch.float64, 1), (torch.int32, 70001), (torch.int64, 3), (torch.float16, 513),
+             (torch.bfloat16, 1000), (torch.float32, c.get("big", 0))]
+    for k, (dt, n) in enumerate(sizes):
+        if n == 0:
+            continue
+        y = tips_amd.broadcast_op(tensor(rank, dt, n, k).cuda(), root)
+        torch.cuda.synchronize()
+        if not torch.equal(y.cpu(), tensor(root, dt, n, k)):
+            bad.append("broadcast %s x %d differs" % (dt, n))
+    h = tips_amd.broadcast_op(tensor(rank, torch.float32, 777, 50).numpy(), root)
+    if not np.array_equal(h, tensor(root, torch.float32, 777, 50).numpy()):
+        bad.append("host broadcast differs")
+    v = [tensor(rank, torch.float32, 300, 60).cuda(), tensor(rank, torch.int64, 5, 61).cuda()]
+    tips_amd.broadcast_variables(v, root)
+    torch.cuda.synchronize()
+    if not (torch.equal(v[0].cpu(), tensor(root, torch.float32, 300, 60))
+            and torch.equal(v[1].cpu(), tensor(root, torch.int64, 5, 61))):
+        bad.append("broadcast_variables differs")
+    rows = [(seed + 3 * r) % 5 if r != 1 else 0 for r in range(size)]
+    parts = [tensor(r, torch.float32, rows[r] * 7, 70).reshape(rows[r], 7) for r in range(size)]
+    g = tips_amd.allgather_op(parts[rank].cuda())
+    torch.cuda.synchronize()
+    if not torch.equal(g.cpu(), torch.cat(parts)):
+        bad.append("allgather differs (rows %s)" % rows)
+    gi = tips_amd.allgather_op(np.arange(rank + 1, dtype=np.int64) + 10 * rank)
+    if not np.array_equal(gi, np.concatenate([np.arange(r + 1, dtype=np.int64) + 10 * r for r in range(size)])):
+        bad.append("host allgather differs")
+    tips_amd.set_consistency_check(True)
+    try:
+        x = tensor(rank, torch.float32, 1000, 80).cuda()
+        y = tips_amd.allreduce(x)
+        torch.cuda.synchronize()
+        exp = tensor(0, torch.float32, 1000, 80)
+        for r in range(1, size):
+            exp = exp + tensor(r, torch.float32, 1000, 80)
+        if not torch.equal(y.cpu(), exp):
+            bad.append("checked allreduce differs")
+    finally:
+        tips_amd.set_consistency_check(False)
+    try:
+        tips_amd.broadcast_op(tensor(rank, torch.float32, 64, 90).cuda(), rank % 2)
+        bad.append("a root differing between ranks was accepted")
+    except tips_amd.TipsError as e:
+        if e.code != -7:  # TIPS_ERR_MISMATCH
+            bad.append("mismatched root: %s" % e)
+    y = tips_amd.broadcast_op(tensor(rank, torch.float32, 64, 91).cuda(), root)
+    torch.cuda.synchronize()
+    if not torch.equal(y.cpu(), tensor(root, torch.float32, 64, 91)):
+        bad.append("broadcast after the refused call differs")
+    return {"case": {"collectives": seed}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:6])}
+
+
 def golden_case(c, rank, size, L, _lib, sp):
     """A committed golden vector (tests/golden: inputs and the reference's MPI_Allreduce output
     under MPICH) through the real multi-process product path: rank r reduces inputs[r]; the
@@ -182,6 +252,9 @@ def main():
             continue
         if c.get("golden"):
             results.append(golden_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("collectives"):
+            results.append(collectives_case(c, rank, size, L, _lib, sp))
             continue
         if c.get("tape"):
             results.append(tape_case(c, rank, size, L, _lib, sp))

@@ -133,3 +133,12 @@ def test_distributed_gradient_tape_across_processes(gpu, p):
     gradient() returns every rank's gradients summed over the ranks, bit-exact against the
     rank-order sum (the peer schedule's fold order)."""
     check(run_job(p, [{"tape": True, "seed": 11}], TIPS_PEER_WS_MIB="16"))
+
+
+@pytest.mark.parametrize("p", [2, 3, 4])
+def test_broadcast_allgather_over_peer(gpu, p):
+    """broadcast_op / allgather_op / broadcast_variables / the checked allreduce over the peer
+    transport in p real processes (peer.cc peer_broadcast / peer_allgatherv): every dtype, host
+    and device, a 6 MiB broadcast through a 4 MiB workspace (two pieces), ragged allgather with an
+    empty rank, and a mismatched root refused on every rank without breaking the job."""
+    check(run_job(p, [{"collectives": True, "seed": 5 + p, "big": 1536 * 1024}], TIPS_PEER_WS_MIB="4"))

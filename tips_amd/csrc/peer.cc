@@ -48,12 +48,16 @@ constexpr int kPeerMaxRanks = tips::kMaxSrcs;
 constexpr uint64_t kPeerMagic = 0x5449505350454552ull;  // "TIPSPEER"
 constexpr int64_t kPeerSlotPad = 4096;  // slots not at power-of-two strides (as schedules.cc kSlotPad)
 
-enum Phase : int32_t { kCall = 1, kPushed = 2, kReduced = 3, kPublish = 4, kShutdown = 5, kGathered = 6, kUnpacked = 7 };
+enum Phase : int32_t {
+  kCall = 1, kPushed = 2, kReduced = 3, kPublish = 4, kShutdown = 5, kGathered = 6, kUnpacked = 7,
+  kBcastCall = 8, kGatherCall = 9, kStaged = 10, kPulled = 11
+};
 
 struct Post {
   int64_t count;
   int32_t dtype;
   int32_t phase;
+  int64_t aux;  // broadcast: the root rank
   int64_t ws_bytes;
   hipIpcMemHandle_t handle;
 };
@@ -397,7 +401,146 @@ int peer_allreduce_impl(State& st, PeerState& ps, const char* in, char* out, int
   return 0;
 }
 
+// Entry of a broadcast / allgatherv call: the last call's pull is done, then the call barrier
+// (every rank's post in all[]).
+int peer_enter(State& st, PeerState& ps, const Post& call, Post* all) {
+  TRY(attach(st, ps));
+  if (ps.pull_pending) {
+    HIP_TRY(hipEventSynchronize(ps.pulled));
+    ps.pull_pending = false;
+  }
+  TRY(barrier(st, ps, call, all, peer_timeout()));
+  return 0;
+}
+
+int peer_leave(PeerState& ps, hipStream_t user) {
+  if (!ps.pulled) HIP_TRY(hipEventCreateWithFlags(&ps.pulled, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(ps.pulled, user));
+  ps.pull_pending = true;
+  return 0;
+}
+
+// Broadcast (MPI_Bcast of BroadcastCpu, reference tips/core/collective/utils.h:118-134): per
+// piece of up to the workspace, the root stages its bytes in its own workspace, barrier, every
+// other rank reads them from there into out in one xfer launch (all its peers' links idle but
+// the root's: a broadcast is bounded by the root's outgoing links, which the p-1 readers share).
+int peer_broadcast_impl(State& st, PeerState& ps, const char* in, char* out, int64_t bytes, int root, hipStream_t user,
+                        bool* clean) {
+  const int p = st.size, r = st.rank;
+  Post call{};
+  call.count = bytes;
+  call.aux = root;
+  call.phase = kBcastCall;
+  Post all[kPeerMaxRanks];
+  TRY(peer_enter(st, ps, call, all));
+  for (int j = 0; j < p; j++)
+    if (all[j].count != bytes || all[j].aux != root)
+      return fail(TIPS_ERR_MISMATCH, "peer broadcast: rank %d broadcasts %lld B from root %lld, rank %d %lld B from root %d",
+                  j, (long long)all[j].count, (long long)all[j].aux, r, (long long)bytes, root);
+  *clean = false;
+  TRY(setup_ws(st, ps));
+  const int64_t piece = ps.ws_bytes / kAlignBytes * kAlignBytes;
+  Post q = call;
+  for (int64_t b = 0; b < bytes; b += piece) {
+    const int64_t len = std::min(piece, bytes - b);
+    if (b > 0) {  // every reader has its copy of the previous piece before the root overwrites it
+      HIP_TRY(hipStreamSynchronize(user));
+      q.phase = kPulled;
+      TRY(barrier(st, ps, q, nullptr, peer_timeout()));
+    }
+    if (r == root) {
+      tips::XferSeg segs[2] = {{in + b, (char*)ps.ws, len}, {in + b, out + b, in == out ? 0 : len}};
+      HIP_TRY(tips::launch_xfer(segs, 2, user));
+      HIP_TRY(hipStreamSynchronize(user));
+    }
+    q.phase = kStaged;
+    TRY(barrier(st, ps, q, nullptr, peer_timeout()));
+    if (r != root) {
+      tips::XferSeg seg = {(const char*)ps.remote[root], out + b, len};
+      HIP_TRY(tips::launch_xfer(&seg, 1, user));
+    }
+  }
+  return peer_leave(ps, user);
+}
+
+// Allgatherv (MPI_Allgatherv of AllgathervCpu, utils.h:83-116): per piece, every rank stages
+// its next bytes in its own workspace and copies them to its place in out, barrier, then one
+// xfer launch reads every peer's piece into out (one segment per peer: all links at once).
+// Barrier 0 checks every rank's byte count against the counts the caller passed.
+int peer_allgatherv_impl(State& st, PeerState& ps, const char* in, char* out, const int64_t* bytes, const int64_t* displ,
+                         hipStream_t user, bool* clean) {
+  const int p = st.size, r = st.rank;
+  Post call{};
+  call.count = bytes[r];
+  call.phase = kGatherCall;
+  Post all[kPeerMaxRanks];
+  TRY(peer_enter(st, ps, call, all));
+  int64_t longest = 0;
+  for (int j = 0; j < p; j++) {
+    if (all[j].count != bytes[j])
+      return fail(TIPS_ERR_MISMATCH, "peer allgatherv: rank %d contributes %lld B, rank %d expects %lld B from it", j,
+                  (long long)all[j].count, r, (long long)bytes[j]);
+    longest = std::max(longest, bytes[j]);
+  }
+  *clean = false;
+  TRY(setup_ws(st, ps));
+  const int64_t piece = ps.ws_bytes / kAlignBytes * kAlignBytes;
+  Post q = call;
+  for (int64_t b = 0; b < longest; b += piece) {
+    auto len_of = [&](int j) { return std::max<int64_t>(0, std::min(piece, bytes[j] - b)); };
+    if (b > 0) {
+      HIP_TRY(hipStreamSynchronize(user));
+      q.phase = kPulled;
+      TRY(barrier(st, ps, q, nullptr, peer_timeout()));
+    }
+    const bool self_in_place = (in + b == out + displ[r] + b);
+    tips::XferSeg mine[2] = {{in + b, (char*)ps.ws, len_of(r)}, {in + b, out + displ[r] + b, self_in_place ? 0 : len_of(r)}};
+    HIP_TRY(tips::launch_xfer(mine, 2, user));
+    HIP_TRY(hipStreamSynchronize(user));
+    q.phase = kStaged;
+    TRY(barrier(st, ps, q, nullptr, peer_timeout()));
+    tips::XferSeg segs[tips::kMaxXferSegs];
+    int m = 0;
+    for (int d = 1; d < p; d++) {
+      const int from = mod(r + d, p);
+      segs[m++] = {(const char*)ps.remote[from], out + displ[from] + b, len_of(from)};
+    }
+    HIP_TRY(tips::launch_xfer(segs, m, user));
+  }
+  return peer_leave(ps, user);
+}
+
+PeerState& peer_state(State& st) {
+  if (!st.peer) st.peer = new PeerState();
+  return *st.peer;
+}
+
+int refuse_if_broken(PeerState& ps) {
+  if (ps.broken)
+    return fail(TIPS_ERR_HIP, "peer schedule: an earlier call failed part-way and left the ranks out of step; "
+                              "shut down and re-initialise");
+  return 0;
+}
+
 }  // namespace
+
+int peer_broadcast(State& st, const char* in, char* out, int64_t bytes, int root, hipStream_t user) {
+  PeerState& ps = peer_state(st);
+  TRY(refuse_if_broken(ps));
+  bool clean = true;
+  const int rc = peer_broadcast_impl(st, ps, in, out, bytes, root, user, &clean);
+  if (rc && !clean) ps.broken = true;
+  return rc;
+}
+
+int peer_allgatherv(State& st, const char* in, char* out, const int64_t* bytes, const int64_t* displ, hipStream_t user) {
+  PeerState& ps = peer_state(st);
+  TRY(refuse_if_broken(ps));
+  bool clean = true;
+  const int rc = peer_allgatherv_impl(st, ps, in, out, bytes, displ, user, &clean);
+  if (rc && !clean) ps.broken = true;
+  return rc;
+}
 
 // device-resident allreduce over IPC-mapped peer memory, caller holds st.mu, 1 < p <= 16
 int peer_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {

@@ -184,6 +184,9 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
 // peer.cc: allreduce over IPC-mapped peer memory (1 < p <= kMaxSrcs, one node), caller holds st.mu
 int peer_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t stream);
 void peer_release(State& st);  // collective (shutdown)
+// peer.cc: broadcast / allgatherv over the same workspaces (byte counts; displ = byte offsets in out)
+int peer_broadcast(State& st, const char* in, char* out, int64_t bytes, int root, hipStream_t stream);
+int peer_allgatherv(State& st, const char* in, char* out, const int64_t* bytes, const int64_t* displ, hipStream_t stream);
 // host_staging.cc: host-resident allreduce over pipelined pieces, caller holds st.mu
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
 // fusion.cc
