@@ -266,14 +266,20 @@ def main():
         if c.get("count_per_rank"):  # deliberately inconsistent counts: every rank must fail, none hang
             n = c["count_per_rank"][rank]
         ins = [rand(dtype, n, np.random.default_rng(seed + r)) for r in range(size)]
-        x = to_dev(ins[rank])
-        y = x if c.get("inplace") else torch.empty_like(x)
-        rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, sp)
+        if c.get("host"):  # host buffers: staged through the device (bounce / pipelined pieces)
+            x = ins[rank].copy()
+            y = x if c.get("inplace") else np.empty_like(x)
+            rc = L.tips_allreduce(x.ctypes.data, y.ctypes.data, n, dtype, _lib.OP_SUM, None)
+        else:
+            x = to_dev(ins[rank])
+            y = x if c.get("inplace") else torch.empty_like(x)
+            rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, sp)
         torch.cuda.synchronize()
         res = {"case": c, "rc": int(rc)}
         if rc == 0:
             exp = oracle_bind.fold(ins, code=dtype, wide_acc=True)
-            res["ok"] = bool(same_bits(from_dev(y, dtype), exp, dtype))
+            got = y if c.get("host") else from_dev(y, dtype)
+            res["ok"] = bool(same_bits(got, exp, dtype))
         else:
             res["error"] = _lib.last_error()
             res["ok"] = bool(c.get("expect_error")) and rc == c["expect_error"]

@@ -142,3 +142,14 @@ def test_broadcast_allgather_over_peer(gpu, p):
     and device, a 6 MiB broadcast through a 4 MiB workspace (two pieces), ragged allgather with an
     empty rank, and a mismatched root refused on every rank without breaking the job."""
     check(run_job(p, [{"collectives": True, "seed": 5 + p, "big": 1536 * 1024}], TIPS_PEER_WS_MIB="4"))
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_host_buffers_across_processes(gpu, p):
+    """Host-memory allreduce in p real processes over the peer schedule: small pageable buffers
+    through the page-locked bounce pair, large ones as pipelined pieces (1 MiB pieces here, so a
+    5 MB bucket is 5 pieces, each H2D -> peer allreduce -> D2H on its own stream), in and out of
+    place, every dtype; bit-exact against the oracle's fold."""
+    cases = [{"dtype": d, "n": n, "seed": 40 + d, "host": True, "inplace": inplace}
+             for d in ALL_DTYPES for n, inplace in ((1000, False), (1310721, False), (1310721, True))]
+    check(run_job(p, cases, TIPS_PEER_WS_MIB="16", TIPS_HOST_PIECE_BYTES=str(1 << 20)))
