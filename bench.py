@@ -777,6 +777,11 @@ def bench_allreduce(args):
                                      "the node (TIPS_BENCH_PEER=1 forces them)" % torch.cuda.device_count())
     line["compare_check"] = compare_check
     line["compare_algbw_gib_s"] = compare
+    ring_algbw = algbw if algo == _lib.ALGO_RING else (compare.get("ring") or 0) * GIB
+    if world > 1 and workload == "bucket" and ring_algbw:  # the north star's ring target: >= 70 % of one xGMI link
+        rb = ring_algbw * 2 * (world - 1) / world
+        line["ring_xgmi"] = {"busbw_GBps": round(rb / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS,
+                             "frac_of_one_link": round(rb / 1e9 / XGMI_LINK_GBPS, 4), "target_frac": 0.70}
     if rank == 0:
         if last_words:
             last_words(None)
