@@ -2,10 +2,10 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 LIB      := tips_amd/lib/libtips_hip.so
-SRCS     := tips_amd/csrc/kernels.hip tips_amd/csrc/runtime.cc tips_amd/csrc/rt_common.cc tips_amd/csrc/schedules.cc \
+SRCS     := tips_amd/csrc/kernels.hip tips_amd/csrc/runtime.cc tips_amd/csrc/rt_common.cc tips_amd/csrc/plan.cc tips_amd/csrc/schedules.cc \
             tips_amd/csrc/fusion.cc tips_amd/csrc/host_staging.cc tips_amd/csrc/control.cc tips_amd/csrc/negotiate.cc tips_amd/csrc/peer.cc \
             tips_amd/csrc/bootstrap.cc
-HDRS     := tips_amd/csrc/kernels.h tips_amd/csrc/rt.h tips_amd/csrc/net.h include/tips_hip.h
+HDRS     := tips_amd/csrc/kernels.h tips_amd/csrc/rt.h tips_amd/csrc/net.h tips_amd/csrc/plan.h include/tips_hip.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-result -fvisibility=hidden
 
 CRASH    := tools/lib/libcrashline.so
@@ -17,9 +17,16 @@ $(CRASH): tools/crash_line.c
 	@mkdir -p tools/lib
 	gcc -O2 -fPIC -shared -Wall -Wextra -std=c11 -D_POSIX_C_SOURCE=200809L -o $@ $<
 
-$(LIB): $(SRCS) $(HDRS)
+OBJS     := $(patsubst tips_amd/csrc/%,build/obj/%.o,$(SRCS))
+
+# one object per source (parallel, incremental); every object depends on every internal header
+build/obj/%.o: tips_amd/csrc/% $(HDRS)
+	@mkdir -p build/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
 	@mkdir -p tips_amd/lib
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lrccl
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -lrccl
 
 oracle:
 	$(MAKE) -C oracle
@@ -39,6 +46,7 @@ tools/sum_sweep: tools/sum_sweep.cc $(LIB)
 	$(HIPCC) -O2 -std=c++17 -o $@ $< -Itips_amd -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../tips_amd/lib'
 
 clean:
+	rm -rf build/obj
 	rm -f $(LIB) tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
 	$(MAKE) -C oracle clean
 

@@ -281,6 +281,19 @@ TIPS_API int tips_schedule_shape(int64_t count, int p, int dtype, int* depth, in
 /* Chunk partition the ring uses (element offsets), for tests. */
 TIPS_API int tips_chunk_bounds(int64_t count, int p, int dtype, int c, int64_t* begin, int64_t* end);
 
+/* The op plan rank `rank` of `p` issues for an allreduce of `count` elements with
+ * schedule `algo` (TIPS_ALGO_RING / DIRECT / ONESHOT) and `depth` sub-chunks per
+ * chunk (<= 0: the runtime's choice). The RCCL executor and the single-GPU
+ * simulators run exactly these plans (tips_amd/csrc/plan.cc); this dump is for
+ * host-side checks (pairing, stream hazards, a CPU interpreter). Pure host
+ * function. Writes the plan as int64 words into out[0..cap) when it fits and
+ * returns the number of words (< 0 = error). Layout:
+ *   {nsteps, staging_bytes, K}, then per step {wait_sum, nxfer, nsum},
+ *   nxfer x {send, peer, buf, byte_off, bytes}, nsum x {dst_buf, dst_off, count,
+ *   nsrc, nsrc x {buf, byte_off}}; buf 0 = in, 1 = out, 2 = staging. */
+TIPS_API int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, int depth, int64_t* out,
+                                    int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,219 @@
+"""Host-side checkers of the schedules' op plans (tips_schedule_plan, tips_amd/csrc/plan.cc).
+
+The RCCL executor and the single-GPU simulator both run these plans, so what is
+checked here is what runs on an 8-GPU node:
+
+- pairing():  in every step, the k-th send from r to q has the k-th receive on q
+  from r, with equal bytes, and no receive is left over. Every rank issues the
+  same number of steps, each one ncclGroupStart/End, so with pairing inside a
+  step no group can wait on a partner that never comes (deadlock freedom).
+- hazards():  a happens-before model of the executor's streams and events
+  (schedules.cc run_plan: prologue, per-step comm waits, recv / sum events,
+  epilogue), for two back-to-back calls issued from two DIFFERENT user streams.
+  Every pair of accesses to one buffer range where one is a write must be ordered
+  (a data race otherwise), and every access of a call must be ordered before the
+  user's next work on that call's stream.
+- interpret(): executes p ranks' plans on numpy buffers, with the oracle's sum2 /
+  rank-order fold as the arithmetic, so the plans' index arithmetic can be compared
+  bit for bit with oracle_ring / oracle_fold on a host without a GPU.
+"""
+import ctypes
+
+import numpy as np
+
+IN, OUT, STG = 0, 1, 2
+RING, DIRECT, ONESHOT = 0, 1, 3
+
+
+def dump(algo, p, rank, n, dtype, depth=0):
+    from tips_amd import _lib
+    L = _lib.lib()
+    need = L.tips_schedule_plan(algo, p, rank, n, dtype, depth, None, 0)
+    assert need > 0, _lib.last_error()
+    buf = (ctypes.c_int64 * need)()
+    assert L.tips_schedule_plan(algo, p, rank, n, dtype, depth, buf, need) == need
+    return parse(list(buf))
+
+
+def parse(w):
+    nsteps, staging, K = w[0], w[1], w[2]
+    i = 3
+    steps = []
+    for _ in range(nsteps):
+        wait_sum, nx, ns = w[i:i + 3]
+        i += 3
+        xfers = []
+        for _ in range(nx):
+            send, peer, buf, off, nb = w[i:i + 5]
+            i += 5
+            xfers.append(dict(send=bool(send), peer=peer, buf=buf, off=off, bytes=nb))
+        sums = []
+        for _ in range(ns):
+            dbuf, doff, count, nsrc = w[i:i + 4]
+            i += 4
+            srcs = [(w[i + 2 * j], w[i + 2 * j + 1]) for j in range(nsrc)]
+            i += 2 * nsrc
+            sums.append(dict(dst=(dbuf, doff), count=count, srcs=srcs))
+        steps.append(dict(wait_sum=wait_sum, xfers=xfers, sums=sums))
+    assert i == len(w)
+    return dict(steps=steps, staging=staging, K=K)
+
+
+def pairing(plans):
+    """Raise AssertionError unless every send pairs with a receive of equal bytes in the same step."""
+    p = len(plans)
+    nsteps = len(plans[0]["steps"])
+    assert all(len(pl["steps"]) == nsteps for pl in plans), "ranks issue different numbers of groups"
+    for i in range(nsteps):
+        recvs = {}  # (receiver, sender) -> list of byte counts, in issue order
+        sends = {}
+        for r in range(p):
+            for x in plans[r]["steps"][i]["xfers"]:
+                assert 0 <= x["peer"] < p and x["peer"] != r, (i, r, x)
+                assert x["bytes"] > 0, (i, r, x)
+                if x["send"]:
+                    sends.setdefault((x["peer"], r), []).append(x["bytes"])
+                else:
+                    recvs.setdefault((r, x["peer"]), []).append(x["bytes"])
+        assert sends == recvs, "step %d: sends %s vs receives %s" % (i, sends, recvs)
+
+
+def _ranges_overlap(a, b):
+    return a[0] < b[1] and b[0] < a[1]
+
+
+def hazards(plan, es, nbytes, inplace=False):
+    """Happens-before check of one rank's plan over two calls from different user streams.
+    Returns a list of race descriptions (empty = race-free). nbytes = bucket bytes."""
+    ops = []     # (stream, accesses) ; accesses = [(buffer_id, lo, hi, is_write)]
+    preds = []   # explicit cross-stream predecessors (event waits) per op
+    last = {}    # stream -> index of its last op
+    pending_waits = {}  # stream -> list of op indices the next op on that stream must follow
+
+    def add(stream, acc=()):
+        idx = len(ops)
+        ops.append((stream, list(acc)))
+        pr = []
+        if stream in last:
+            pr.append(last[stream])
+        pr += pending_waits.pop(stream, [])
+        preds.append(pr)
+        last[stream] = idx
+        return idx
+
+    def record(stream):  # an event recorded on `stream` covers its last op (a marker op keeps it explicit)
+        return add(stream)
+
+    def wait(stream, ev_op):
+        pending_waits.setdefault(stream, []).append(ev_op)
+
+    def buf_id(call, buf):
+        if buf == STG:
+            return "stg"
+        if inplace:
+            return ("io", call)
+        return ("in" if buf == IN else "out", call)
+
+    ends = []
+    for call, user in ((0, "U0"), (1, "U1")):
+        add(user, [(buf_id(call, IN), 0, nbytes, True)] + ([] if inplace else [(buf_id(call, OUT), 0, nbytes, True)]))
+        ev_start = record(user)
+        wait("C", ev_start)
+        ev_prev = record("P")
+        wait("C", ev_prev)
+        wait("P", ev_start)
+        sum_ev = {}
+        for i, s in enumerate(plan["steps"]):
+            if s["wait_sum"] >= 0 and s["wait_sum"] in sum_ev:
+                wait("C", sum_ev[s["wait_sum"]])
+            if s["xfers"]:
+                acc = [(buf_id(call, x["buf"]), x["off"], x["off"] + x["bytes"], not x["send"]) for x in s["xfers"]]
+                add("C", acc)
+            if s["sums"]:
+                rev = record("C")
+                wait("P", rev)
+                for u in s["sums"]:
+                    acc = [(buf_id(call, u["dst"][0]), u["dst"][1], u["dst"][1] + u["count"] * es, True)]
+                    acc += [(buf_id(call, b), o, o + u["count"] * es, False) for b, o in u["srcs"]]
+                    add("P", acc)
+                sum_ev[i] = record("P")
+        e1 = record("C")
+        wait(user, e1)
+        e2 = record("P")
+        wait(user, e2)
+        # the user's next work on this stream reads and writes this call's buffers
+        ends.append(add(user, [(buf_id(call, IN), 0, nbytes, True), (buf_id(call, OUT), 0, nbytes, True)]))
+
+    # reachability: bitset of ancestors per op (ops are created in topological order)
+    anc = []
+    for i in range(len(ops)):
+        a = 0
+        for q in preds[i]:
+            a |= anc[q] | (1 << q)
+        anc.append(a)
+
+    def ordered(i, j):
+        return bool(anc[j] >> i & 1) or bool(anc[i] >> j & 1)
+
+    races = []
+    flat = [(i, a) for i, (_, acc) in enumerate(ops) for a in acc]
+    by_buf = {}
+    for i, a in flat:
+        by_buf.setdefault(a[0], []).append((i, a))
+    for buf, lst in by_buf.items():
+        for x in range(len(lst)):
+            i, a = lst[x]
+            for y in range(x + 1, len(lst)):
+                j, b = lst[y]
+                if i == j or not (a[3] or b[3]) or not _ranges_overlap(a[1:3], b[1:3]):
+                    continue
+                if not ordered(i, j):
+                    races.append("%s [%d,%d)%s on %s vs [%d,%d)%s on %s" % (
+                        buf, a[1], a[2], "w" if a[3] else "r", ops[i][0], b[1], b[2], "w" if b[3] else "r", ops[j][0]))
+                    if len(races) > 20:
+                        return races
+    return races
+
+
+def interpret(plans, ins, dtype, inplace=False):
+    """Execute p ranks' plans on host buffers: step by step, transfers first (paired as
+    pairing() checks), then the step's sums with the oracle's arithmetic. Returns p outputs."""
+    import oracle_bind
+    p = len(plans)
+    ins = [np.ascontiguousarray(x).copy() for x in ins]
+    es = ins[0].itemsize
+    nbytes = ins[0].nbytes
+    outs = ins if inplace else [np.zeros_like(x) for x in ins]
+    stg = [np.zeros(max(1, pl["staging"]), np.uint8) for pl in plans]
+
+    def raw(r, buf):
+        if buf == STG:
+            return stg[r]
+        return (ins if buf == IN else outs)[r].view(np.uint8)
+
+    def view(r, buf, off, count):
+        return raw(r, buf)[off:off + count * es].view(ins[0].dtype)
+
+    for i in range(len(plans[0]["steps"])):
+        moves = []
+        for r in range(p):
+            nth = {}
+            for x in plans[r]["steps"][i]["xfers"]:
+                if not x["send"]:
+                    continue
+                q = x["peer"]
+                k = nth.get(q, 0)
+                nth[q] = k + 1
+                rv = [y for y in plans[q]["steps"][i]["xfers"] if not y["send"] and y["peer"] == r][k]
+                moves.append((raw(r, x["buf"])[x["off"]:x["off"] + x["bytes"]].copy(), q, rv))
+        for data, q, rv in moves:  # all of a step's sends read before any of its receives land
+            raw(q, rv["buf"])[rv["off"]:rv["off"] + rv["bytes"]] = data
+        for r in range(p):
+            for u in plans[r]["steps"][i]["sums"]:
+                srcs = [view(r, b, o, u["count"]).copy() for b, o in u["srcs"]]
+                if len(srcs) == 2:
+                    res = oracle_bind.sum2(srcs[0], srcs[1], code=dtype)
+                else:
+                    res = oracle_bind.fold(srcs, code=dtype, wide_acc=True)
+                view(r, u["dst"][0], u["dst"][1], u["count"])[:] = res
+    return outs

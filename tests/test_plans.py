@@ -1,0 +1,96 @@
+"""The schedules' op plans on the CPU (no GPU): tips_schedule_plan dumps exactly what the RCCL
+executor issues on an 8-GPU node and what the single-GPU simulator runs (plan.cc), so these
+checks cover the multi-GPU default path itself, not a twin of it:
+
+- every send pairs with a receive of equal bytes in the same group (no deadlock), for
+  p = 2..16, ragged sizes and pipeline depths K = 1..6;
+- the executor's streams and events order every conflicting access, across two calls from
+  different user streams (no data race, staging reuse included);
+- the plans, interpreted on host buffers with the oracle's arithmetic, give oracle_ring's /
+  oracle_fold's bits (the reference's AllreduceCpu<T> SUM, utils.h:52-67).
+"""
+import numpy as np
+import pytest
+
+import plan_util as pu
+from gpu_util import BF16, F16, F32, F64, I32, I64, rand
+
+ES = {F32: 4, F64: 8, I32: 4, I64: 8, F16: 2, BF16: 2}
+SIZES = [1, 7, 64, 65, 1000, 4099, 65536 + 3, 262147]
+
+
+@pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
+@pytest.mark.parametrize("p", range(2, 17))
+def test_send_recv_pairing(algo, p):
+    for n in SIZES:
+        for K in (range(1, 7) if algo != pu.ONESHOT else (1,)):
+            for dtype in (F32, F16):
+                plans = [pu.dump(algo, p, r, n, dtype, K) for r in range(p)]
+                try:
+                    pu.pairing(plans)
+                except AssertionError as e:
+                    raise AssertionError("algo %d p %d n %d K %d dtype %d: %s" % (algo, p, n, K, dtype, e))
+
+
+def test_bucket_bytes_conserved():
+    """Config 3's shape (p = 8, 1 GiB f32): each rank sends 2(p-1)/p of the bucket in the ring and
+    in direct (the bandwidth-optimal volume), (p-1) buckets in one-shot; every chunk byte is summed once."""
+    n, p = 268435456, 8
+    for algo in (pu.RING, pu.DIRECT):
+        for r in (0, 3, 7):
+            pl = pu.dump(algo, p, r, n, F32)
+            sent = sum(x["bytes"] for s in pl["steps"] for x in s["xfers"] if x["send"])
+            got = sum(x["bytes"] for s in pl["steps"] for x in s["xfers"] if not x["send"])
+            assert sent == got == 2 * (p - 1) * n * 4 // p
+            summed = sum(u["count"] for s in pl["steps"] for u in s["sums"])
+            assert summed == (n // p) * ((p - 1) if algo == pu.RING else 1)
+    pl = pu.dump(pu.ONESHOT, 4, 1, 1000, F32)
+    assert sum(x["bytes"] for s in pl["steps"] for x in s["xfers"] if x["send"]) == 3 * 4000
+
+
+@pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
+@pytest.mark.parametrize("p,n,K", [(2, 4099, 1), (2, 262147, 4), (3, 1000, 3), (4, 65539, 6), (5, 7, 2),
+                                   (8, 262147, 4), (8, 1 << 20, 2), (16, 100003, 3)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_stream_event_hazards(algo, p, n, K, inplace):
+    """No two conflicting accesses are unordered by the executor's streams and events, over two
+    back-to-back calls issued from different user streams (the one-shot fold used to run on the
+    caller's stream, unordered against the next call's receives into the same staging slots)."""
+    for r in sorted({0, 1, p - 1}):
+        pl = pu.dump(algo, p, r, n, F32, K)
+        races = pu.hazards(pl, 4, n * 4, inplace=inplace)
+        assert not races, "rank %d: %s" % (r, races[:5])
+
+
+def test_hazard_checker_catches_a_missing_wait():
+    """The checker itself: drop the ring's comm-stream wait on the previous step's sum and it must
+    report the send reading `out` before the sum wrote it."""
+    pl = pu.dump(pu.RING, 4, 0, 100000, F32, 2)
+    for s in pl["steps"]:
+        s["wait_sum"] = -1
+    assert pu.hazards(pl, 4, 400000)
+
+
+@pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
+@pytest.mark.parametrize("dtype", [F32, I32, F64, BF16])
+@pytest.mark.parametrize("p,n,K", [(2, 4099, 1), (3, 1000, 3), (4, 65539, 4), (5, 7, 2), (8, 100003, 3),
+                                   (16, 20011, 2)])
+def test_interpreted_plans_match_oracle(oracle, algo, dtype, p, n, K):
+    rng = np.random.default_rng(p * 1000 + n + dtype)
+    ins = [rand(dtype, n, rng) for _ in range(p)]
+    plans = [pu.dump(algo, p, r, n, dtype, K) for r in range(p)]
+    outs = pu.interpret(plans, ins, dtype, inplace=(n % 2 == 1))
+    exp = oracle.ring(ins, code=dtype)[0] if algo == pu.RING else oracle.fold(ins, code=dtype, wide_acc=True)
+    for o in outs:
+        assert np.array_equal(o.view(np.uint8), exp.view(np.uint8))
+
+
+def test_plan_argument_errors():
+    from tips_amd import _lib
+    L = _lib.lib()
+    assert L.tips_schedule_plan(pu.DIRECT, 17, 0, 100, F32, 1, None, 0) == -1  # fold takes <= 16 sources
+    assert L.tips_schedule_plan(pu.RING, 1, 0, 100, F32, 1, None, 0) == -1
+    assert L.tips_schedule_plan(pu.RING, 4, 4, 100, F32, 1, None, 0) == -1
+    assert L.tips_schedule_plan(2, 4, 0, 100, F32, 1, None, 0) == -1  # ncclAllReduce has no plan
+    assert L.tips_schedule_plan(pu.RING, 4, 0, 100, 42, 1, None, 0) == -1
+    assert L.tips_schedule_plan(pu.RING, 32, 5, 100, F32, 2, None, 0) > 0  # the ring takes any p

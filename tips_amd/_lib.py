@@ -111,6 +111,8 @@ _SIGNATURES = [
      [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), _c_i64_p]),
     ("tips_chunk_bounds", ctypes.c_int,
      [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p]),
+    ("tips_schedule_plan", ctypes.c_int64,
+     [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _c_i64_p, ctypes.c_int64]),
     ("tips_bootstrap_broadcast", ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
 ]

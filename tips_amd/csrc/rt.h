@@ -153,7 +153,7 @@ struct State {
   EventPool fuse_ev;
   int64_t fusion_threshold = 0;  // the fusion slots' size; plans hold addresses into them
   int64_t fusion_tile_env = 0;   // TIPS_COPY_TILE_BYTES the cached plans were built with
-  hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr;
+  hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr, ev_comp_prev = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
   void* bounce_in = nullptr;  // page-locked kBounceBytes each (hipHostMalloc), for small pageable host tensors

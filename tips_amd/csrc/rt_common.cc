@@ -63,6 +63,7 @@ int ensure_streams(State& st) {
   if (!st.ev_start) HIP_TRY(hipEventCreateWithFlags(&st.ev_start, hipEventDisableTiming));
   if (!st.ev_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
   if (!st.ev_comp_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_done, hipEventDisableTiming));
+  if (!st.ev_comp_prev) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_prev, hipEventDisableTiming));
   return 0;
 }
 

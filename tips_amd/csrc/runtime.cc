@@ -124,7 +124,7 @@ void tips_shutdown(void) {
   st.small.release();
   st.recv_ev.release();
   st.sum_ev.release();
-  for (hipEvent_t* e : {&st.ev_start, &st.ev_done, &st.ev_comp_done})
+  for (hipEvent_t* e : {&st.ev_start, &st.ev_done, &st.ev_comp_done, &st.ev_comp_prev})
     if (*e) {
       (void)hipEventDestroy(*e);
       *e = nullptr;

@@ -1,166 +1,96 @@
-// schedules.cc — the allreduce schedules over RCCL point-to-point (xGMI) and
-// their single-GPU simulators.
+// schedules.cc — the allreduce schedules' executors: over RCCL point-to-point
+// (xGMI, one rank per GPU) and, for tests, for p virtual ranks on one GPU.
 //
 // Replaces what MPI_Allreduce does inside libmpi for AllreduceCpu<T>
 // (reference tips/core/collective/utils.h:60-65): the reduce-scatter +
 // allgather exchange and, at each step, the local MPI_SUM — here the gfx950
-// kernels of kernels.hip. One comm stream carries every RCCL call of a rank
-// (one ordered channel, as the reference's single MPI_COMM_WORLD); sums run on
-// a separate compute stream so sub-chunk k+1's transfer overlaps sub-chunk k's
-// sum.
+// kernels of kernels.hip. Both executors run the same per-rank op plans
+// (plan.cc): the simulator is not a second implementation of the schedules.
+// One comm stream carries every RCCL call of a rank (one ordered channel, as
+// the reference's single MPI_COMM_WORLD); sums run on a separate compute
+// stream, so sub-chunk k+1's transfer overlaps sub-chunk k's sum.
 #include <string.h>
 
 #include <algorithm>
 #include <tuple>
 
+#include "plan.h"
 #include "rt.h"
 
 namespace tips {
 namespace rt {
 namespace {
 
-// Staging slots that feed one multi_sum launch sit one slot plus 4 KiB apart:
-// sources at power-of-two strides read ~7 % slower (profiles/r01_sum_sweep_multi_pad.jsonl).
-constexpr int64_t kSlotPad = 4096;
-
-// The sum kernel launch used by every schedule (ring step: out = local + received).
-int sum2(void* dst, const void* a, const void* b, int64_t n, int dtype, hipStream_t s) {
-  HIP_TRY(tips::launch_sum2(dst, a, b, n, dtype, s));
-  return 0;
-}
-
-// ---------------------------------------------------------------------------
-// Ring allreduce over RCCL send/recv. Own rank only.
-
-int ring_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
-  const int p = st.size, r = st.rank, next = mod(r + 1, p), prev = mod(r - 1, p);
-  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
-  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
-  const int K = pipeline_depth(max_chunk * es);
-  TRY(st.staging.ensure((size_t)(2 * max_chunk * es)));
-  TRY(st.recv_ev.ensure(2 * K));
-  TRY(st.sum_ev.ensure(2 * K));
-  char* stg[2] = {(char*)st.staging.p, (char*)st.staging.p + max_chunk * es};
-  TRY(join(st.comm_stream, user, st.ev_start));
-  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
-
-  // reduce-scatter: at step s send chunk (r-s), receive chunk (r-s-1) and add it in
-  for (int s = 0; s < p - 1; s++) {
-    const Range sc = chunk_of(n, p, align, mod(r - s, p)), rc = chunk_of(n, p, align, mod(r - s - 1, p));
-    const char* src = (s == 0) ? in : out;
-    for (int k = 0; k < K; k++) {
-      const Range ss = sub_of(sc, K, align, k), rs = sub_of(rc, K, align, k);
-      if (s > 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((s - 1) & 1) * K + k], 0));
-      char* land = stg[s & 1] + (rs.b - rc.b) * es;
-      if (ss.len() > 0 || rs.len() > 0) {
-        NCCL_TRY(ncclGroupStart());
-        if (ss.len() > 0) NCCL_TRY(ncclSend(src + ss.b * es, ss.len() * es, ncclInt8, next, st.comm, st.comm_stream));
-        if (rs.len() > 0) NCCL_TRY(ncclRecv(land, rs.len() * es, ncclInt8, prev, st.comm, st.comm_stream));
-        NCCL_TRY(ncclGroupEnd());
-      }
-      hipEvent_t rev = st.recv_ev.ev[(s & 1) * K + k];
-      HIP_TRY(hipEventRecord(rev, st.comm_stream));
-      HIP_TRY(hipStreamWaitEvent(st.comp_stream, rev, 0));
-      TRY(sum2(out + rs.b * es, in + rs.b * es, land, rs.len(), dtype, st.comp_stream));
-      HIP_TRY(hipEventRecord(st.sum_ev.ev[(s & 1) * K + k], st.comp_stream));
-    }
+int launch_psum(const PSum& s, char* const* base, int dtype, hipStream_t stream) {
+  void* dst = base[s.dst.buf] + s.dst.off;
+  if (s.nsrc == 2) {
+    HIP_TRY(tips::launch_sum2(dst, base[s.src[0].buf] + s.src[0].off, base[s.src[1].buf] + s.src[1].off, s.count,
+                              dtype, stream));
+    return 0;
   }
-  // allgather: rank r owns chunk (r+1); at step s forward chunk (r+1-s), receive chunk (r-s)
-  for (int s = 0; s < p - 1; s++) {
-    const Range sc = chunk_of(n, p, align, mod(r + 1 - s, p)), rc = chunk_of(n, p, align, mod(r - s, p));
-    for (int k = 0; k < K; k++) {
-      const Range ss = sub_of(sc, K, align, k), rs = sub_of(rc, K, align, k);
-      if (s == 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((p - 2) & 1) * K + k], 0));
-      if (ss.len() > 0 || rs.len() > 0) {
-        NCCL_TRY(ncclGroupStart());
-        if (ss.len() > 0) NCCL_TRY(ncclSend(out + ss.b * es, ss.len() * es, ncclInt8, next, st.comm, st.comm_stream));
-        if (rs.len() > 0) NCCL_TRY(ncclRecv(out + rs.b * es, rs.len() * es, ncclInt8, prev, st.comm, st.comm_stream));
-        NCCL_TRY(ncclGroupEnd());
-      }
-    }
-  }
-  TRY(join(user, st.comm_stream, st.ev_done));
-  TRY(join(user, st.comp_stream, st.ev_comp_done));
-  return 0;
-}
-
-// ---------------------------------------------------------------------------
-// Direct (all-pairs) allreduce: rank r owns chunk r. Every
-// peer's slice of chunk r arrives over its own xGMI link at once; one p-input
-// kernel folds them in rank order; then chunk r goes to every peer at once.
-
-int direct_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
-  const int p = st.size, r = st.rank;
-  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
-  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
-  const int K = pipeline_depth(max_chunk * es);
-  const int64_t stride = max_chunk * es + kSlotPad;
-  TRY(st.staging.ensure((size_t)((p - 1) * stride)));
-  TRY(st.recv_ev.ensure(K));
-  TRY(st.sum_ev.ensure(K));
-  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * stride; };
-  const Range mine = chunk_of(n, p, align, r);
-  TRY(join(st.comm_stream, user, st.ev_start));
-  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
-  for (int k = 0; k < K; k++) {
-    const Range ms = sub_of(mine, K, align, k);
-    NCCL_TRY(ncclGroupStart());
-    for (int d = 1; d < p; d++) {
-      const int to = mod(r + d, p), from = mod(r - d, p);
-      const Range ts = sub_of(chunk_of(n, p, align, to), K, align, k);
-      if (ts.len() > 0) NCCL_TRY(ncclSend(in + ts.b * es, ts.len() * es, ncclInt8, to, st.comm, st.comm_stream));
-      if (ms.len() > 0)
-        NCCL_TRY(ncclRecv(slot(from) + (ms.b - mine.b) * es, ms.len() * es, ncclInt8, from, st.comm, st.comm_stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    HIP_TRY(hipEventRecord(st.recv_ev.ev[k], st.comm_stream));
-    HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[k], 0));
-    const void* srcs[tips::kMaxSrcs];
-    for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)(in + ms.b * es) : slot(j) + (ms.b - mine.b) * es;
-    HIP_TRY(tips::launch_multi_sum(out + ms.b * es, srcs, p, ms.len(), dtype, st.comp_stream));
-    HIP_TRY(hipEventRecord(st.sum_ev.ev[k], st.comp_stream));
-  }
-  for (int k = 0; k < K; k++) {
-    const Range ms = sub_of(mine, K, align, k);
-    HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[k], 0));
-    NCCL_TRY(ncclGroupStart());
-    for (int d = 1; d < p; d++) {
-      const int to = mod(r + d, p), from = mod(r - d, p);
-      const Range fs = sub_of(chunk_of(n, p, align, from), K, align, k);
-      if (ms.len() > 0) NCCL_TRY(ncclSend(out + ms.b * es, ms.len() * es, ncclInt8, to, st.comm, st.comm_stream));
-      if (fs.len() > 0) NCCL_TRY(ncclRecv(out + fs.b * es, fs.len() * es, ncclInt8, from, st.comm, st.comm_stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-  }
-  TRY(join(user, st.comm_stream, st.ev_done));
-  TRY(join(user, st.comp_stream, st.ev_comp_done));
-  return 0;
-}
-
-// One-shot (small buckets): every rank sends its whole bucket to
-// every peer in one grouped step (all xGMI links at once) and folds the p
-// buckets locally in rank order with one multi_sum launch. (p-1)·S bytes per
-// rank instead of 2(p-1)/p·S, but 1 exchange + 1 kernel instead of 2(p-1)
-// pipelined steps: latency-optimal. Same bits as direct (rank-order fold).
-int oneshot_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
-  const int p = st.size, r = st.rank;
-  const int64_t bytes = n * tips::dtype_size(dtype);
-  const int64_t stride = (bytes + kAlignBytes - 1) / kAlignBytes * kAlignBytes + kSlotPad;
-  TRY(st.staging.ensure((size_t)((p - 1) * stride)));
-  auto slot = [&](int j) { return (char*)st.staging.p + (int64_t)(j < r ? j : j - 1) * stride; };
-  TRY(join(st.comm_stream, user, st.ev_start));
-  NCCL_TRY(ncclGroupStart());
-  for (int d = 1; d < p; d++) {
-    const int to = mod(r + d, p), from = mod(r - d, p);
-    NCCL_TRY(ncclSend(in, (size_t)bytes, ncclInt8, to, st.comm, st.comm_stream));
-    NCCL_TRY(ncclRecv(slot(from), (size_t)bytes, ncclInt8, from, st.comm, st.comm_stream));
-  }
-  NCCL_TRY(ncclGroupEnd());
-  TRY(join(user, st.comm_stream, st.ev_done));  // the fold runs on the caller's stream
   const void* srcs[tips::kMaxSrcs];
-  for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)in : slot(j);
-  HIP_TRY(tips::launch_multi_sum(out, srcs, p, n, dtype, user));
+  for (int j = 0; j < s.nsrc; j++) srcs[j] = base[s.src[j].buf] + s.src[j].off;
+  HIP_TRY(tips::launch_multi_sum(dst, srcs, s.nsrc, s.count, dtype, stream));
   return 0;
+}
+
+// Stream prologue shared by both executors: the comm stream waits for the caller's stream (the
+// inputs are ready) and for every sum already queued on the compute stream (the previous call's
+// sums have read the staging slots this call's receives overwrite, whatever stream that call
+// came on); the compute stream waits for the caller's stream.
+int prologue(State& st, hipStream_t user) {
+  TRY(join(st.comm_stream, user, st.ev_start));
+  TRY(join(st.comm_stream, st.comp_stream, st.ev_comp_prev));
+  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
+  return 0;
+}
+
+int epilogue(State& st, hipStream_t user) {
+  TRY(join(user, st.comm_stream, st.ev_done));
+  TRY(join(user, st.comp_stream, st.ev_comp_done));
+  return 0;
+}
+
+// One rank's plan over RCCL: each step's transfers are one ncclGroupStart/End on the comm
+// stream, followed by an event the compute stream waits on before the step's sums; a step's
+// wait_sum makes the comm stream wait for an earlier step's sums (what it sends, they wrote).
+int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t user) {
+  const size_t nsteps = pl.steps.size();
+  TRY(st.staging.ensure((size_t)std::max<int64_t>(pl.staging_bytes, 1)));
+  TRY(st.recv_ev.ensure(nsteps));
+  TRY(st.sum_ev.ensure(nsteps));
+  char* base[3] = {(char*)in, out, (char*)st.staging.p};
+  TRY(prologue(st, user));
+  for (size_t i = 0; i < nsteps; i++) {
+    const PStep& s = pl.steps[i];
+    if (s.wait_sum >= 0 && !pl.steps[s.wait_sum].sums.empty())
+      HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[s.wait_sum], 0));
+    if (!s.xfers.empty()) {
+      NCCL_TRY(ncclGroupStart());
+      for (const PXfer& x : s.xfers) {
+        char* ptr = base[x.at.buf] + x.at.off;
+        if (x.send) {
+          NCCL_TRY(ncclSend(ptr, (size_t)x.bytes, ncclInt8, x.peer, st.comm, st.comm_stream));
+        } else {
+          NCCL_TRY(ncclRecv(ptr, (size_t)x.bytes, ncclInt8, x.peer, st.comm, st.comm_stream));
+        }
+      }
+      NCCL_TRY(ncclGroupEnd());
+    }
+    if (!s.sums.empty()) {
+      HIP_TRY(hipEventRecord(st.recv_ev.ev[i], st.comm_stream));
+      HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[i], 0));
+      for (const PSum& ps : s.sums) TRY(launch_psum(ps, base, pl.dtype, st.comp_stream));
+      HIP_TRY(hipEventRecord(st.sum_ev.ev[i], st.comp_stream));
+    }
+  }
+  return epilogue(st, user);
+}
+
+int plan_allreduce(State& st, int algo, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
+  Plan pl;
+  TRY(build_schedule_plan(algo, st.size, st.rank, n, dtype, plan_depth(st.size, n, dtype), &pl));
+  return run_plan(st, pl, in, out, user);
 }
 
 }  // namespace
@@ -182,17 +112,19 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
   if (algo == TIPS_ALGO_PEER && st.size <= tips::kMaxSrcs)
     return peer_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
   TRY(ensure_comm(st));  // every other schedule moves its bytes over RCCL (no half-built group on failure)
-  if (st.size > tips::kMaxSrcs && (algo == TIPS_ALGO_DIRECT || algo == TIPS_ALGO_ONESHOT || algo == TIPS_ALGO_PEER))
-    return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
-  if (algo == TIPS_ALGO_ONESHOT) return oneshot_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
-  if (algo == TIPS_ALGO_DIRECT) return direct_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
-  return ring_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
+  int a = algo;
+  if (st.size > tips::kMaxSrcs && (a == TIPS_ALGO_DIRECT || a == TIPS_ALGO_ONESHOT || a == TIPS_ALGO_PEER))
+    a = TIPS_ALGO_RING;
+  if (a != TIPS_ALGO_DIRECT && a != TIPS_ALGO_ONESHOT) a = TIPS_ALGO_RING;
+  return plan_allreduce(st, a, (const char*)in, (char*)out, n, dtype, stream);
 }
 
-// Peer transfers of the single-GPU simulators, batched per pipeline step:
-// device-to-device copies, or (sim_transport 1) the same bytes as grouped
-// ncclSend/ncclRecv pairs to this rank itself, so the RCCL p2p calls the real
-// schedules make (byte counts, grouping, stream order) run on a 1-GPU box.
+namespace {
+
+// Peer transfers of the single-GPU simulator, batched per plan step: device-to-device
+// copies, or (sim_transport 1) the same bytes as grouped ncclSend/ncclRecv pairs to this rank
+// itself, so the RCCL p2p calls the real schedules make (byte counts, grouping, stream order)
+// run on a 1-GPU box.
 struct SimXfer {
   State& st;
   std::vector<std::tuple<void*, const void*, size_t>> ops;
@@ -230,6 +162,99 @@ int sim_prepare(State& st) {
   return 0;
 }
 
+// Runs the p ranks' plans on this GPU, step by step in lockstep. Step i's transfers pair the
+// k-th send from r to q with the k-th receive on q from r in q's step i (what RCCL's grouped
+// p2p does); a send or receive without its partner is reported as the deadlock it would be.
+// All virtual ranks share the comm and compute streams, so every event wait of the real
+// executor holds here too (with more ordering, never less).
+int simulate_plans(State& st, std::vector<Plan>& plans, void* const* outs, const void* const* ins, int dtype,
+                   hipStream_t user) {
+  const int p = (int)plans.size();
+  const size_t nsteps = plans[0].steps.size();
+  for (auto& pl : plans)
+    if (pl.steps.size() != nsteps) return fail(TIPS_ERR_INVALID_ARG, "plans of one schedule differ in step count");
+  const int64_t stg = round_up(std::max<int64_t>(plans[0].staging_bytes, 1), 4096);
+  TRY(st.staging.ensure((size_t)(stg * p)));
+  TRY(st.recv_ev.ensure(nsteps));
+  TRY(st.sum_ev.ensure(nsteps));
+  auto base = [&](int r, int buf) -> char* {
+    return buf == kBufIn ? (char*)ins[r] : buf == kBufOut ? (char*)outs[r] : (char*)st.staging.p + r * stg;
+  };
+  SimXfer xf(st);
+  TRY(prologue(st, user));
+  std::vector<char> has_sums(nsteps, 0);
+  for (size_t i = 0; i < nsteps; i++) {
+    bool sums = false;
+    std::vector<int> waited;  // one shared event per earlier step covers every rank's sums of it
+    for (int r = 0; r < p; r++) {
+      const PStep& s = plans[r].steps[i];
+      sums = sums || !s.sums.empty();
+      if (s.wait_sum >= 0 && has_sums[s.wait_sum] &&
+          std::find(waited.begin(), waited.end(), s.wait_sum) == waited.end()) {
+        HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[s.wait_sum], 0));
+        waited.push_back(s.wait_sum);
+      }
+    }
+    for (int r = 0; r < p; r++) {
+      std::vector<int> nth(p, 0);  // sends from r to q seen so far in this step
+      for (const PXfer& x : plans[r].steps[i].xfers) {
+        if (!x.send) continue;
+        if (x.peer < 0 || x.peer >= p || x.peer == r) return fail(TIPS_ERR_INVALID_ARG, "plan: bad peer %d", x.peer);
+        int seen = 0;
+        const PXfer* match = nullptr;
+        for (const PXfer& y : plans[x.peer].steps[i].xfers)
+          if (!y.send && y.peer == r && seen++ == nth[x.peer]) {
+            match = &y;
+            break;
+          }
+        nth[x.peer]++;
+        if (!match || match->bytes != x.bytes)
+          return fail(TIPS_ERR_INVALID_ARG, "plan deadlock: step %zu, rank %d sends %lld B to %d without a matching receive",
+                      i, r, (long long)x.bytes, x.peer);
+        xf.add(base(x.peer, match->at.buf) + match->at.off, base(r, x.at.buf) + x.at.off, x.bytes);
+      }
+    }
+    size_t nrecv = 0, nsend = 0;
+    for (int r = 0; r < p; r++)
+      for (const PXfer& x : plans[r].steps[i].xfers) (x.send ? nsend : nrecv)++;
+    if (nrecv != nsend) return fail(TIPS_ERR_INVALID_ARG, "plan deadlock: step %zu has %zu receives for %zu sends", i, nrecv, nsend);
+    TRY(xf.flush());
+    if (sums) {
+      HIP_TRY(hipEventRecord(st.recv_ev.ev[i], st.comm_stream));
+      HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[i], 0));
+      for (int r = 0; r < p; r++) {
+        char* b[3] = {base(r, kBufIn), base(r, kBufOut), base(r, kBufStaging)};
+        for (const PSum& ps : plans[r].steps[i].sums) TRY(launch_psum(ps, b, dtype, st.comp_stream));
+      }
+      HIP_TRY(hipEventRecord(st.sum_ev.ev[i], st.comp_stream));
+      has_sums[i] = 1;
+    }
+  }
+  return epilogue(st, user);
+}
+
+int simulate(int algo, void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
+  TRY(check_dtype(dtype));
+  const int pmax = algo == TIPS_ALGO_RING ? 64 : tips::kMaxSrcs;
+  if (p < 1 || p > pmax || n < 0 || !outs || !ins) return fail(TIPS_ERR_INVALID_ARG, "bad simulate args");
+  if (n == 0) return 0;
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  TRY(sim_prepare(st));
+  hipStream_t user = (hipStream_t)stream;
+  if (p == 1) {
+    if (outs[0] != ins[0])
+      HIP_TRY(hipMemcpyAsync(outs[0], ins[0], (size_t)(n * tips::dtype_size(dtype)), hipMemcpyDeviceToDevice, user));
+    return 0;
+  }
+  std::vector<Plan> plans(p);
+  const int K = plan_depth(p, n, dtype);
+  for (int r = 0; r < p; r++) TRY(build_schedule_plan(algo, p, r, n, dtype, K, &plans[r]));
+  return simulate_plans(st, plans, outs, ins, dtype, user);
+}
+
+}  // namespace
+
 }  // namespace rt
 }  // namespace tips
 
@@ -256,158 +281,37 @@ int tips_schedule_shape(int64_t count, int p, int dtype, int* depth, int64_t* su
   return 0;
 }
 
+int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, int depth, int64_t* out, int64_t cap) {
+  TRY(check_dtype(dtype));
+  if (cap < 0 || (cap > 0 && !out)) return fail(TIPS_ERR_INVALID_ARG, "bad plan buffer");
+  Plan pl;
+  TRY(build_schedule_plan(algo, p, rank, count, dtype, depth > 0 ? depth : plan_depth(p, count, dtype), &pl));
+  std::vector<int64_t> w = {(int64_t)pl.steps.size(), pl.staging_bytes, pl.K};
+  for (const PStep& s : pl.steps) {
+    w.insert(w.end(), {(int64_t)s.wait_sum, (int64_t)s.xfers.size(), (int64_t)s.sums.size()});
+    for (const PXfer& x : s.xfers) w.insert(w.end(), {(int64_t)x.send, (int64_t)x.peer, (int64_t)x.at.buf, x.at.off, x.bytes});
+    for (const PSum& u : s.sums) {
+      w.insert(w.end(), {(int64_t)u.dst.buf, u.dst.off, u.count, (int64_t)u.nsrc});
+      for (int j = 0; j < u.nsrc; j++) w.insert(w.end(), {(int64_t)u.src[j].buf, u.src[j].off});
+    }
+  }
+  if ((int64_t)w.size() <= cap) std::copy(w.begin(), w.end(), out);
+  return (int64_t)w.size();
+}
+
 // ---------------------------------------------------------------------------
-// single-GPU schedule simulators (test harnesses)
+// single-GPU schedule simulators (test harnesses): the plans of all p ranks, on one device
 
 int tips_ring_simulate(void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
-  TRY(check_dtype(dtype));
-  if (p < 1 || p > 64 || n < 0 || !outs || !ins) return fail(TIPS_ERR_INVALID_ARG, "bad simulate args");
-  if (n == 0) return 0;
-  State& st = S();
-  std::lock_guard<std::mutex> lk(st.mu);
-  TRY(sim_prepare(st));
-  SimXfer xf(st);
-  hipStream_t user = (hipStream_t)stream;
-  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
-  if (p == 1) {
-    if (outs[0] != ins[0]) HIP_TRY(hipMemcpyAsync(outs[0], ins[0], (size_t)(n * es), hipMemcpyDeviceToDevice, user));
-    return 0;
-  }
-  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
-  const int K = pipeline_depth(max_chunk * es);
-  TRY(st.staging.ensure((size_t)(2 * p * max_chunk * es)));
-  TRY(st.recv_ev.ensure(2 * K));
-  TRY(st.sum_ev.ensure(2 * K));
-  auto stg = [&](int r, int par) { return (char*)st.staging.p + ((int64_t)r * 2 + par) * max_chunk * es; };
-  TRY(join(st.comm_stream, user, st.ev_start));
-  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
-  for (int s = 0; s < p - 1; s++) {
-    for (int k = 0; k < K; k++) {
-      if (s > 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((s - 1) & 1) * K + k], 0));
-      for (int r = 0; r < p; r++) {  // virtual rank r receives from r-1
-        const int prev = mod(r - 1, p);
-        const Range rc = chunk_of(n, p, align, mod(r - s - 1, p));
-        const Range rs = sub_of(rc, K, align, k);
-        if (rs.len() == 0) continue;
-        const char* src = (s == 0) ? (const char*)ins[prev] : (const char*)outs[prev];
-        xf.add(stg(r, s & 1) + (rs.b - rc.b) * es, src + rs.b * es, rs.len() * es);
-      }
-      TRY(xf.flush());
-      hipEvent_t rev = st.recv_ev.ev[(s & 1) * K + k];
-      HIP_TRY(hipEventRecord(rev, st.comm_stream));
-      HIP_TRY(hipStreamWaitEvent(st.comp_stream, rev, 0));
-      for (int r = 0; r < p; r++) {
-        const Range rc = chunk_of(n, p, align, mod(r - s - 1, p));
-        const Range rs = sub_of(rc, K, align, k);
-        TRY(sum2((char*)outs[r] + rs.b * es, (const char*)ins[r] + rs.b * es, stg(r, s & 1) + (rs.b - rc.b) * es,
-                 rs.len(), dtype, st.comp_stream));
-      }
-      HIP_TRY(hipEventRecord(st.sum_ev.ev[(s & 1) * K + k], st.comp_stream));
-    }
-  }
-  for (int s = 0; s < p - 1; s++) {
-    for (int k = 0; k < K; k++) {
-      if (s == 0) HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[((p - 2) & 1) * K + k], 0));
-      for (int r = 0; r < p; r++) {
-        const int prev = mod(r - 1, p);
-        const Range rs = sub_of(chunk_of(n, p, align, mod(r - s, p)), K, align, k);
-        if (rs.len() == 0) continue;
-        xf.add((char*)outs[r] + rs.b * es, (const char*)outs[prev] + rs.b * es, rs.len() * es);
-      }
-      TRY(xf.flush());
-    }
-  }
-  TRY(join(user, st.comm_stream, st.ev_done));
-  TRY(join(user, st.comp_stream, st.ev_comp_done));
-  return 0;
+  return simulate(TIPS_ALGO_RING, outs, ins, p, n, dtype, stream);
 }
 
 int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
-  TRY(check_dtype(dtype));
-  if (p < 1 || p > tips::kMaxSrcs || n < 0 || !outs || !ins) return fail(TIPS_ERR_INVALID_ARG, "bad simulate args");
-  if (n == 0) return 0;
-  State& st = S();
-  std::lock_guard<std::mutex> lk(st.mu);
-  TRY(sim_prepare(st));
-  SimXfer xf(st);
-  hipStream_t user = (hipStream_t)stream;
-  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
-  if (p == 1) {
-    if (outs[0] != ins[0]) HIP_TRY(hipMemcpyAsync(outs[0], ins[0], (size_t)(n * es), hipMemcpyDeviceToDevice, user));
-    return 0;
-  }
-  const int64_t max_chunk = chunk_of(n, p, align, 0).len();
-  const int K = pipeline_depth(max_chunk * es);
-  // staging[r][j]: slice of chunk r sent by virtual rank j
-  TRY(st.staging.ensure((size_t)((int64_t)p * p * max_chunk * es)));
-  TRY(st.recv_ev.ensure(K));
-  TRY(st.sum_ev.ensure(K));
-  auto slot = [&](int r, int j) { return (char*)st.staging.p + ((int64_t)r * p + j) * max_chunk * es; };
-  TRY(join(st.comm_stream, user, st.ev_start));
-  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
-  for (int k = 0; k < K; k++) {
-    for (int r = 0; r < p; r++) {
-      const Range mine = chunk_of(n, p, align, r), ms = sub_of(mine, K, align, k);
-      if (ms.len() == 0) continue;
-      for (int j = 0; j < p; j++)
-        if (j != r) xf.add(slot(r, j) + (ms.b - mine.b) * es, (const char*)ins[j] + ms.b * es, ms.len() * es);
-    }
-    TRY(xf.flush());
-    HIP_TRY(hipEventRecord(st.recv_ev.ev[k], st.comm_stream));
-    HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[k], 0));
-    for (int r = 0; r < p; r++) {
-      const Range mine = chunk_of(n, p, align, r), ms = sub_of(mine, K, align, k);
-      const void* srcs[tips::kMaxSrcs];
-      for (int j = 0; j < p; j++)
-        srcs[j] = (j == r) ? (const void*)((const char*)ins[r] + ms.b * es) : slot(r, j) + (ms.b - mine.b) * es;
-      HIP_TRY(tips::launch_multi_sum((char*)outs[r] + ms.b * es, srcs, p, ms.len(), dtype, st.comp_stream));
-    }
-    HIP_TRY(hipEventRecord(st.sum_ev.ev[k], st.comp_stream));
-  }
-  for (int k = 0; k < K; k++) {
-    HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[k], 0));
-    for (int r = 0; r < p; r++) {
-      const Range ms = sub_of(chunk_of(n, p, align, r), K, align, k);
-      if (ms.len() == 0) continue;
-      for (int j = 0; j < p; j++)
-        if (j != r) xf.add((char*)outs[j] + ms.b * es, (const char*)outs[r] + ms.b * es, ms.len() * es);
-    }
-    TRY(xf.flush());
-  }
-  TRY(join(user, st.comm_stream, st.ev_done));
-  TRY(join(user, st.comp_stream, st.ev_comp_done));
-  return 0;
+  return simulate(TIPS_ALGO_DIRECT, outs, ins, p, n, dtype, stream);
 }
 
 int tips_oneshot_simulate(void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
-  TRY(check_dtype(dtype));
-  if (p < 1 || p > tips::kMaxSrcs || n < 0 || !outs || !ins) return fail(TIPS_ERR_INVALID_ARG, "bad simulate args");
-  if (n == 0) return 0;
-  State& st = S();
-  std::lock_guard<std::mutex> lk(st.mu);
-  TRY(sim_prepare(st));
-  SimXfer xf(st);
-  hipStream_t user = (hipStream_t)stream;
-  const int64_t bytes = n * tips::dtype_size(dtype);
-  if (p == 1) {
-    if (outs[0] != ins[0]) HIP_TRY(hipMemcpyAsync(outs[0], ins[0], (size_t)bytes, hipMemcpyDeviceToDevice, user));
-    return 0;
-  }
-  // staging[r][j]: rank j's bucket as received by virtual rank r
-  TRY(st.staging.ensure((size_t)((int64_t)p * p * bytes)));
-  auto slot = [&](int r, int j) { return (char*)st.staging.p + ((int64_t)r * p + j) * bytes; };
-  TRY(join(st.comm_stream, user, st.ev_start));
-  for (int r = 0; r < p; r++)
-    for (int j = 0; j < p; j++)
-      if (j != r) xf.add(slot(r, j), ins[j], bytes);
-  TRY(xf.flush());
-  TRY(join(user, st.comm_stream, st.ev_done));
-  for (int r = 0; r < p; r++) {
-    const void* srcs[tips::kMaxSrcs];
-    for (int j = 0; j < p; j++) srcs[j] = (j == r) ? ins[r] : (const void*)slot(r, j);
-    HIP_TRY(tips::launch_multi_sum(outs[r], srcs, p, n, dtype, user));
-  }
-  return 0;
+  return simulate(TIPS_ALGO_ONESHOT, outs, ins, p, n, dtype, stream);
 }
 
 }  // extern "C"
