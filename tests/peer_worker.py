@@ -1,12 +1,18 @@
 """One rank of the peer schedule's multi-process test (tests/test_gpu_peer.py).
 
 Run as: python peer_worker.py RANK SIZE UID_HEX CASES_JSON
-Every rank of the job runs on GPU 0 of the test box (TIPS_NO_RCCL=1: no RCCL
-communicator, which would refuse two ranks on one device). The ranks share
-nothing but the IPC workspaces and the node-local control block, exactly as
-on an 8-GPU node, so this exercises the whole peer path: the shared-memory
-barriers, the handle exchange, the workspace growth, the push / fold / pull
-kernels and the cross-rank count check. Each case's inputs are seeded per
+Every rank of the job runs on GPU 0 of the test box. Two transports:
+- TIPS_WORKER_ALGO=peer (default): TIPS_NO_RCCL=1, no RCCL communicator. The
+  ranks share nothing but the IPC workspaces and the node-local control block,
+  exactly as on an 8-GPU node, so this exercises the whole peer path: the
+  shared-memory barriers, the handle exchange, the push / fold / pull kernels
+  and the cross-rank count check.
+- TIPS_WORKER_ALGO=ring|direct|oneshot|auto: a real RCCL communicator per
+  process (tips_init: unique id over the TCP bootstrap, ncclCommInitRank). RCCL
+  refuses two ranks on one GPU of one host, so each process claims its own host
+  (NCCL_HOSTID=rank) and RCCL connects them with its socket transport over
+  loopback: slow, but the per-rank RCCL executor (schedules.cc run_plan) runs
+  exactly as on the node - same plans, groups, streams and events. Each case's inputs are seeded per
 rank; every rank regenerates all ranks' inputs and checks its result bit-exact
 against the oracle's rank-order fold (oracle/oracle.c: oracle_fold).
 Prints one JSON line: {"rank": r, "results": [...]}.
@@ -18,7 +24,17 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
-os.environ["TIPS_NO_RCCL"] = "1"
+ALGO_NAMES = {"ring": 0, "direct": 1, "rccl": 2, "oneshot": 3, "peer": 4, "auto": -1}
+JOB_ALGO = ALGO_NAMES["peer"]  # the job's schedule (main sets it from TIPS_WORKER_ALGO)
+
+
+def expected(ins, dtype, algo):
+    """The bits the schedule must produce: the ring's chunk-rotated fold (oracle_ring) or the
+    rank-order fold (oracle_fold, wide accumulation) of direct / one-shot / peer."""
+    import oracle_bind
+    if algo == ALGO_NAMES["ring"]:
+        return oracle_bind.ring(ins, code=dtype)[0]
+    return oracle_bind.fold(ins, code=dtype, wide_acc=True)
 
 
 def named_case(c, rank, size, L, _lib, sp):
@@ -47,7 +63,7 @@ def named_case(c, rank, size, L, _lib, sp):
         if rc != 0:
             bad.append("t%d rc %d %s" % (i, rc, _lib.last_error()))
             continue
-        exp = oracle_bind.fold(ins[i][0], code=dtype, wide_acc=True)
+        exp = expected(ins[i][0], dtype, c.get("expect_algo", JOB_ALGO))
         if not same_bits(from_dev(outs[i], dtype), exp, dtype):
             bad.append("t%d (dtype %d, n %d) differs" % (i, dtype, n))
     return {"case": {"named": len(tensors), "seed": c["seed"]}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5])}
@@ -213,7 +229,7 @@ def golden_case(c, rank, size, L, _lib, sp):
         res.update(ok=False, error=_lib.last_error())
         return res
     got = from_dev(y, dtype)
-    fold_ok = bool(same_bits(got, oracle_bind.fold([ins[r] for r in range(size)], code=dtype, wide_acc=True), dtype))
+    fold_ok = bool(same_bits(got, expected([ins[r] for r in range(size)], dtype, c.get("expect_algo", JOB_ALGO)), dtype))
     if exp.dtype.kind == "i":
         ref_ok = bool(np.array_equal(got, exp))
     elif name.startswith("signed"):
@@ -241,12 +257,25 @@ def main():
     oracle_bind.load()
     L = _lib.lib()
     torch.cuda.set_device(0)
-    idbuf = ctypes.create_string_buffer(uid, len(uid))
-    _lib.call("tips_init_rank", rank, size, 0, idbuf, len(uid))
-    _lib.call("tips_set_algorithm", _lib.ALGO_PEER)
+    global JOB_ALGO
+    algo = JOB_ALGO = ALGO_NAMES[os.environ.get("TIPS_WORKER_ALGO", "peer")]
+    if algo == ALGO_NAMES["peer"]:
+        os.environ["TIPS_NO_RCCL"] = "1"
+        idbuf = ctypes.create_string_buffer(uid, len(uid))
+        _lib.call("tips_init_rank", rank, size, 0, idbuf, len(uid))
+    else:  # real RCCL: rank 0's ncclGetUniqueId over the TCP bootstrap (MASTER_ADDR / MASTER_PORT)
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(size), LOCAL_RANK="0", NCCL_HOSTID="tips-rank-%d" % rank)
+        L.tips_init()
+        if not L.tips_is_initialize():
+            print(json.dumps({"rank": rank, "results": [{"case": "init", "ok": False, "error": _lib.last_error()}]}))
+            return
+    _lib.call("tips_set_algorithm", algo)
     sp = torch.cuda.current_stream().cuda_stream
     results = []
     for c in cases:
+        case_algo = ALGO_NAMES[c["algo"]] if c.get("algo") else algo
+        JOB_ALGO = case_algo
+        _lib.call("tips_set_algorithm", case_algo)
         if c.get("named"):
             results.append(named_case(c, rank, size, L, _lib, sp))
             continue
@@ -277,7 +306,7 @@ def main():
         torch.cuda.synchronize()
         res = {"case": c, "rc": int(rc)}
         if rc == 0:
-            exp = oracle_bind.fold(ins, code=dtype, wide_acc=True)
+            exp = expected(ins, dtype, c.get("expect_algo", case_algo))
             got = y if c.get("host") else from_dev(y, dtype)
             res["ok"] = bool(same_bits(got, exp, dtype))
         else:

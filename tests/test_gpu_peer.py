@@ -28,7 +28,8 @@ ERR_MISMATCH = -7
 
 def run_job(p, cases, timeout=300, **extra_env):
     uid = os.urandom(128).hex()
-    env = dict(os.environ, TIPS_NO_RCCL="1", TIPS_PEER_TIMEOUT_S="60", TIPS_VERBOSE="1", **extra_env)
+    env = dict(os.environ, TIPS_NO_RCCL="1", TIPS_PEER_TIMEOUT_S="60", TIPS_VERBOSE="1")
+    env.update(extra_env)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "peer_worker.py"), str(r), str(p), uid,
                                json.dumps(cases)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
              for r in range(p)]
@@ -47,7 +48,8 @@ def run_job(p, cases, timeout=300, **extra_env):
         assert rc == 0, "rank %d exited %d:\n%s" % (r, rc, e[-3000:])
         line = [ln for ln in o.splitlines() if ln.startswith("{")][-1]
         res = json.loads(line)
-        res["stderr"] = e[-2000:]
+        res["stderr"] = e[-20000:]
+        res["stdout"] = o[-20000:]
         results.append(res)
     return results
 
