@@ -206,6 +206,70 @@ def collectives_case(c, rank, size, L, _lib, sp):
     return {"case": {"collectives": seed}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:6])}
 
 
+def workload_sizes(name):
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    return bench.fused1000_sizes() if name == "config4" else bench.resnet50_grad_sizes()
+
+
+def fused_case(c, rank, size, L, _lib, sp):
+    """BASELINE config 4 (1000 fp32 grads, 2^U(8,17) elements) or config 5 (the 214 ResNet-50
+    gradients) through the fusion buckets, as the named API would run them every step:
+    mode "inplace" (tips_fused_allreduce), "oop" (tips_fused_allreduce_oop), "grads"
+    (tips_amd.allreduce_grads, the reference's per-gradient loop fused, __init__.py:203-222) or
+    "optimizer" (DistributedOptimizer.step over SGD(lr=1): p - sum of all ranks' gradients).
+    Every tensor is checked bit-exact against the oracle's rank-order fold of all ranks' inputs
+    (the fold order of every schedule but the ring; run these with direct / peer / AUTO at p > 2)."""
+    import numpy as np
+    import torch
+    import oracle_bind
+    import tips_amd
+    sizes = workload_sizes(c["fused"])
+    mode = c.get("mode", "inplace")
+    g = torch.Generator(device="cuda")
+
+    def inputs(r):
+        g.manual_seed(c["seed"] * 100 + r)
+        return torch.empty(sum(sizes), dtype=torch.float32, device="cuda").uniform_(-1.0, 1.0, generator=g)
+
+    mine = inputs(rank)
+    views = list(torch.split(mine, sizes))
+    before = mine.clone()
+    if mode == "inplace":
+        tips_amd.fused_allreduce_(views)
+        got = views
+    elif mode == "oop":
+        got = tips_amd.fused_allreduce(views)
+    elif mode == "grads":
+        got = tips_amd.allreduce_grads(views)
+    else:
+        params = [torch.nn.Parameter(torch.zeros(k, device="cuda")) for k in sizes]
+        for p, v in zip(params, views):
+            p.grad = v.clone()
+        opt = tips_amd.DistributedOptimizer(torch.optim.SGD(params, lr=1.0))
+        opt.step()
+        got = [0.0 - p.detach() for p in params]  # p = 0 - 1.0 * sum exactly (0 - p: no -0.0 where sum == +0)
+    torch.cuda.synchronize()
+    allin = np.stack([inputs(r).cpu().numpy() for r in range(size)])
+    exp = oracle_bind.fold([allin[r] for r in range(size)], code=0, wide_acc=True)
+    got_flat = torch.cat([t.reshape(-1) for t in got]).cpu().numpy()
+    bad = []
+    if not np.array_equal(got_flat.view(np.uint32), exp.view(np.uint32)):
+        off, wrong = 0, []
+        for i, k in enumerate(sizes):
+            if not np.array_equal(got_flat[off:off + k].view(np.uint32), exp[off:off + k].view(np.uint32)):
+                d = np.nonzero(got_flat[off:off + k].view(np.uint32) != exp[off:off + k].view(np.uint32))[0]
+                j = off + int(d[0])
+                own = "own input" if got_flat[j] == allin[rank][j] else "not own input"
+                wrong.append("tensor %d (%d elems): %d differ from element %d to %d (got %r, expected %r, %s)" % (
+                    i, k, d.size, int(d[0]), int(d[-1]), float(got_flat[j]), float(exp[j]), own))
+            off += k
+        bad.append("%d of %d tensors differ: %s" % (len(wrong), len(sizes), "; ".join(wrong[:3])))
+    if mode in ("oop", "grads") and not torch.equal(mine, before):
+        bad.append("inputs modified by an out-of-place call")
+    return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": not bad, "error": "; ".join(bad)}
+
+
 def golden_case(c, rank, size, L, _lib, sp):
     """A committed golden vector (tests/golden: inputs and the reference's MPI_Allreduce output
     under MPICH) through the real multi-process product path: rank r reduces inputs[r]; the
@@ -278,6 +342,9 @@ def main():
         _lib.call("tips_set_algorithm", case_algo)
         if c.get("named"):
             results.append(named_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("fused"):
+            results.append(fused_case(c, rank, size, L, _lib, sp))
             continue
         if c.get("golden"):
             results.append(golden_case(c, rank, size, L, _lib, sp))

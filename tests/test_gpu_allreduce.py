@@ -456,3 +456,68 @@ def test_host_bounce_boundary(gpu, n):
     out3 = np.full_like(h, -1.0)
     _lib.call("tips_broadcast", h.ctypes.data, out3.ctypes.data, n, _lib.FLOAT32, 0, None)
     assert np.array_equal(out3, h)
+
+
+@pytest.mark.parametrize("workload", ["config4", "config5"])
+def test_fusion_workloads_single_rank(gpu, workload):
+    """Configs 4 and 5's tensor lists through the fusion path on one rank (pack -> bucket ->
+    unpack moves every byte: the identity), in place and out of place, twice (the second call hits
+    the descriptor cache); allreduce_grads and DistributedOptimizer.step() are the identity at one
+    rank, as the reference's _allreduce_cond (__init__.py:94-103)."""
+    import sys
+    import torch
+    from conftest import REPO
+    sys.path.insert(0, REPO)
+    import bench
+    sizes = bench.fused1000_sizes() if workload == "config4" else bench.resnet50_grad_sizes()
+    flat = torch.randn(sum(sizes), device="cuda")
+    views = list(torch.split(flat, sizes))
+    ref = flat.clone()
+    for _ in range(2):
+        outs = gpu.fused_allreduce(views)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat(outs), ref) and torch.equal(flat, ref)
+        gpu.fused_allreduce_(views)
+        torch.cuda.synchronize()
+        assert torch.equal(flat, ref)
+    assert all(a is b for a, b in zip(gpu.allreduce_grads(views), views))
+    params = [torch.nn.Parameter(torch.zeros(k, device="cuda")) for k in sizes[:50]]
+    for p, v in zip(params, views):
+        p.grad = v.clone()
+    gpu.DistributedOptimizer(torch.optim.SGD(params, lr=1.0)).step()
+    assert all(torch.equal(0.0 - p.detach(), v) for p, v in zip(params, views))
+
+
+def test_fusion_concurrent_streams(gpu, monkeypatch):
+    """Fused calls and negotiated batches issued from two torch streams at once, with distinct data,
+    share the library's fusion slots: every output must still be bit-exact (at one rank, the
+    input). A 1 MiB threshold makes every call span several buckets, so a call that packed or
+    unpacked another call's slot would show."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(1 << 20))
+    rng = np.random.default_rng(8)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    lists = []
+    for k in range(6):
+        sizes = [int(x) for x in rng.integers(1, 200000, size=20)]
+        lists.append([torch.full((n,), float(100 * k + i), device="cuda") for i, n in enumerate(sizes)])
+    expect = [[t.clone() for t in lst] for lst in lists]
+    torch.cuda.synchronize()
+    outs, handles = [], []
+    for rep in range(3):
+        for k, lst in enumerate(lists):
+            with torch.cuda.stream(s1 if k % 2 == 0 else s2):
+                if k % 3 == 0:
+                    outs.append((expect[k], gpu.fused_allreduce(lst)))
+                elif k % 3 == 1:
+                    gpu.fused_allreduce_(lst)
+                    outs.append((expect[k], lst))
+                else:
+                    names = ["c%d.%d.%d" % (rep, k, i) for i in range(len(lst))]
+                    handles.append((expect[k], gpu.allreduce_async_many(lst, names)))
+    for exp, hs in handles:
+        outs.append((exp, gpu.synchronize_many(hs)))
+    torch.cuda.synchronize()
+    for exp, got in outs:
+        for e, o in zip(exp, got):
+            assert torch.equal(o, e)

@@ -155,3 +155,14 @@ def test_host_buffers_across_processes(gpu, p):
     cases = [{"dtype": d, "n": n, "seed": 40 + d, "host": True, "inplace": inplace}
              for d in ALL_DTYPES for n, inplace in ((1000, False), (1310721, False), (1310721, True))]
     check(run_job(p, cases, TIPS_PEER_WS_MIB="16", TIPS_HOST_PIECE_BYTES=str(1 << 20)))
+
+
+@pytest.mark.parametrize("workload", ["config4", "config5"])
+def test_fusion_workloads_8_processes(gpu, workload):
+    """BASELINE configs 4 and 5 at their own workloads (the 1000-gradient 2^U(8,17) list; the 214
+    ResNet-50 gradients) in 8 real processes over the peer schedule: fused in place, fused out of
+    place, allreduce_grads and DistributedOptimizer.step(); every tensor bit-exact against the
+    oracle's rank-order fold of the 8 ranks' gradients (reference per-gradient loop:
+    tips/tensorflow/__init__.py:203-222)."""
+    cases = [{"fused": workload, "seed": 3, "mode": m} for m in ("inplace", "oop", "grads", "optimizer")]
+    check(run_job(8, cases, timeout=600, TIPS_PEER_WS_MIB="64"))

@@ -69,3 +69,12 @@ def test_rccl_transport_is_real(gpu):
     log = "".join(res["stderr"] + res["stdout"] for res in results)  # (NCCL_DEBUG prints to stdout)
     assert "NET/Socket" in log, log[-3000:]
     assert "Duplicate GPU" not in log
+
+
+@pytest.mark.parametrize("workload,p", [("config4", 8), ("config5", 8), ("config5", 3)])
+def test_fusion_workloads_over_rccl(gpu, workload, p):
+    """Configs 4 and 5 through the fusion buckets over real RCCL ranks with the default (AUTO)
+    schedule: direct for every bucket at p > 2, one-shot for buckets of 256 KiB or less; in place,
+    out of place, allreduce_grads and DistributedOptimizer.step(), bit-exact against the fold."""
+    cases = [{"fused": workload, "seed": 4, "mode": m} for m in ("inplace", "oop", "grads", "optimizer")]
+    check(run_job(p, cases, timeout=600, **rccl_env("auto")))

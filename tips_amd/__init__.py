@@ -8,8 +8,8 @@ libtips_hip.so (include/tips_hip.h); there is no CPU fallback.
 """
 from .basics import TipsBasics, init, is_initialized, rank, shutdown, size
 from .compression import Compression, Compressor, FP16Compressor, NoneCompressor
-from .ops import (Handle, allgather_op, allreduce_async, allreduce_async_many, synchronize_many, allreduce_op, broadcast_op, poll, synchronize, broadcast_variables, bucket_sum, fused_allreduce_,
-                  rank_op, registered_host_buffer, set_algorithm, set_consistency_check, size_op)
+from .ops import (Handle, allgather_op, allreduce_async, allreduce_async_many, synchronize_many, allreduce_op, broadcast_op, poll, synchronize, broadcast_variables, bucket_sum, fused_allreduce,
+                  fused_allreduce_, rank_op, registered_host_buffer, set_algorithm, set_consistency_check, size_op)
 from ._lib import TipsError, TipsLibraryError
 from . import tensors as _tensors
 
@@ -29,7 +29,8 @@ class IndexedSlices(object):
 
 __all__ = [
     "allreduce", "IndexedSlices", "allreduce_async", "allreduce_async_many", "synchronize_many", "poll", "synchronize", "Handle", "allreduce_grads", "allreduce_op", "allgather_op", "broadcast_op", "broadcast_variables",
-    "set_consistency_check", "registered_host_buffer", "bucket_sum", "fused_allreduce_", "init", "shutdown",
+    "set_consistency_check", "registered_host_buffer", "bucket_sum", "fused_allreduce", "fused_allreduce_", "init",
+    "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
     "DistributedOptimizer", "DistributedGradientTape",
@@ -126,15 +127,13 @@ def allreduce_grads(grads, compression=Compression.none, op=None, fused=True, sp
         groups = {}
         for i, g in enumerate(grads):
             if _fusable(g):
-                groups.setdefault(g.dtype, []).append(i)
-        for idx in groups.values():
-            clones = []
-            for i in idx:
-                c, ctx = compression.compress(grads[i])
-                clones.append((i, c.contiguous().clone(), ctx))
-            fused_allreduce_([c for _, c, _ in clones])
-            for i, c, ctx in clones:
-                out[i] = compression.decompress(c, ctx)
+                c, ctx = compression.compress(g)
+                groups.setdefault(c.dtype, []).append((i, c.contiguous(), ctx))
+        for members in groups.values():
+            # out of place: pack reads each gradient, unpack writes a new tensor (no clone)
+            sums = fused_allreduce([c for _, c, _ in members])
+            for (i, _, ctx), s in zip(members, sums):
+                out[i] = compression.decompress(s, ctx)
     for i, g in enumerate(grads):
         if g is not None and (not fused or not _fusable(g)):
             out[i] = allreduce(g, compression=compression, op=op)

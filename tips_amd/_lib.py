@@ -81,6 +81,8 @@ _SIGNATURES = [
     ("tips_host_register", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     ("tips_host_unregister", ctypes.c_int, [ctypes.c_void_p]),
     ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_fused_allreduce_oop", ctypes.c_int,
+     [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_enqueue_allreduce", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_poll", ctypes.c_int, [ctypes.c_int64]),

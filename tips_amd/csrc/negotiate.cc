@@ -538,7 +538,7 @@ class Negotiator {
     std::vector<BatchItem> items;
     items.reserve(j - i);
     for (size_t k = i; k < j; k++) items.push_back(BatchItem{reqs[k]->in, reqs[k]->out, reqs[k]->count});
-    TRY(batch_fused_allreduce(st, items.data(), (int)items.size(), reqs[i]->dtype, s));
+    TRY(fused_allreduce(st, items.data(), (int)items.size(), reqs[i]->dtype, s));
     auto g = std::make_shared<GroupEv>();
     HIP_TRY(hipEventCreateWithFlags(&g->ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(g->ev, s));

@@ -122,24 +122,8 @@ struct EventPool {
   }
 };
 
-// fusion plan: cached per (dtype, tensor list)
-struct FusionBucket {
-  char* buf = nullptr;        // the fusion slot this bucket packs into (slot b % 2)
-  int64_t bytes = 0;          // padded bucket size
-  int ntiles = 0;
-  CopyTile* pack = nullptr;   // device descriptor arrays
-  CopyTile* unpack = nullptr;
-};
-struct FusionPlan {
-  int dtype;
-  std::vector<void*> ptrs;
-  std::vector<int64_t> counts;
-  std::vector<FusionBucket> buckets;
-  std::vector<int> unfused;  // indices allreduced in place
-};
-
 struct PeerState;   // peer.cc
-struct BatchFusion;  // fusion.cc: readiness batching of negotiated requests
+struct FusionCache;  // fusion.cc: pack/unpack descriptor tables of recent tensor lists
 
 struct State {
   std::mutex mu;
@@ -151,8 +135,7 @@ struct State {
   EventPool pipe_ev;
   hipStream_t fuse_stream = nullptr, bucket_stream = nullptr;  // fusion: pack/unpack || bucket allreduce
   EventPool fuse_ev;
-  int64_t fusion_threshold = 0;  // the fusion slots' size; plans hold addresses into them
-  int64_t fusion_tile_env = 0;   // TIPS_COPY_TILE_BYTES the cached plans were built with
+  int64_t fusion_threshold = 0;  // the fusion slots' size (2 slots of it in `fusion`)
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr, ev_comp_prev = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
@@ -160,10 +143,9 @@ struct State {
   void* bounce_out = nullptr;
   int algo = TIPS_ALGO_AUTO;
   int sim_transport = 0;  // simulators: 0 = device copies, 1 = RCCL send/recv to self
-  std::unordered_map<uint64_t, FusionPlan> plans;
   uint64_t peer_key = 0;      // names the node-local control block of the peer schedule (hash of the unique id)
   PeerState* peer = nullptr;  // peer schedule: IPC workspaces + shared-memory barrier, created on first use
-  BatchFusion* batch = nullptr;  // negotiated requests fused per readiness list, created on first use
+  FusionCache* fusion_cache = nullptr;  // created on first use
 };
 
 State& S();
@@ -189,19 +171,18 @@ int peer_broadcast(State& st, const char* in, char* out, int64_t bytes, int root
 int peer_allgatherv(State& st, const char* in, char* out, const int64_t* bytes, const int64_t* displ, hipStream_t stream);
 // host_staging.cc: host-resident allreduce over pipelined pieces, caller holds st.mu
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
-// fusion.cc
-void free_plan(FusionPlan& pl);
-// One fused allreduce of out-of-place tensors that became ready together (negotiate.cc's
-// readiness batching): pack in[i] -> bucket, allreduce, unpack -> out[i], on `stream`,
-// sum of padded sizes <= the fusion threshold. Caller holds st.mu.
+// fusion.cc: allreduce n same-dtype device tensors, in[i] -> out[i] (in == out allowed), packed
+// into buckets of at most the fusion threshold: pack -> one allreduce per bucket -> unpack.
+// Stream-ordered after `stream` and before its later work; all device work runs on the fusion
+// streams, so calls from different streams never share a bucket unordered. Caller holds st.mu.
 struct BatchItem {
   const void* in;
   void* out;
   int64_t count;
 };
-int batch_fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStream_t stream);
+int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStream_t stream);
 int64_t fusion_threshold_bytes();
-void batch_release(State& st);
+void fusion_release(State& st);  // (shutdown)
 // control.cc: ConstructResponseMessage's rules over p request records (TIPS_REQUEST_WORDS each)
 int check_records(const int64_t* t, int p);
 // negotiate.cc: stop the negotiation thread (collective; call without holding st.mu)

@@ -109,9 +109,7 @@ void tips_shutdown(void) {
     (void)ncclCommDestroy(st.comm);
     st.comm = nullptr;
   }
-  for (auto& kv : st.plans) free_plan(kv.second);
-  st.plans.clear();
-  batch_release(st);
+  fusion_release(st);
   st.staging.release();
   st.host_in.release();
   st.host_out.release();

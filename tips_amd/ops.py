@@ -142,18 +142,43 @@ def fused_allreduce_(tensor_list):
     basics.init()
     if not tensor_list:
         return tensor_list
-    code = tensors.dtype_code(tensor_list[0])
-    for t in tensor_list:
-        if not tensors.is_device(t):
-            raise ValueError("fused_allreduce_ needs device tensors")
-        if tensors.dtype_code(t) != code:
-            raise TypeError("fused_allreduce_ needs one dtype per call")
-        if not t.is_contiguous():
-            raise ValueError("fused_allreduce_ needs contiguous tensors")
+    code = _check_fusable(tensor_list, "fused_allreduce_")
     pp, _keep1 = _lib.ptr_array([t.data_ptr() for t in tensor_list])
     cp, _keep2 = _lib.i64_array([t.numel() for t in tensor_list])
     _lib.call("tips_fused_allreduce", pp, cp, len(tensor_list), code, tensors.stream_of(tensor_list[0]))
     return tensor_list
+
+
+def fused_allreduce(tensor_list, out_list=None):
+    """Out-of-place SUM of a list of same-dtype device tensors through the fusion buckets
+    (tips_fused_allreduce_oop): returns new tensors (or fills `out_list`), inputs unchanged.
+    Pack reads each input once and unpack writes each output once: 4 x the bytes in HBM
+    traffic, no extra copy."""
+    basics.init()
+    if not tensor_list:
+        return []
+    code = _check_fusable(tensor_list, "fused_allreduce")
+    outs = [tensors.empty_like(t) for t in tensor_list] if out_list is None else list(out_list)
+    if len(outs) != len(tensor_list) or any(o.shape != t.shape or o.dtype != t.dtype or not o.is_contiguous()
+                                            for o, t in zip(outs, tensor_list)):
+        raise ValueError("out_list must hold one contiguous tensor of each input's shape and dtype")
+    pi, _keep1 = _lib.ptr_array([t.data_ptr() for t in tensor_list])
+    po, _keep2 = _lib.ptr_array([o.data_ptr() for o in outs])
+    cp, _keep3 = _lib.i64_array([t.numel() for t in tensor_list])
+    _lib.call("tips_fused_allreduce_oop", pi, po, cp, len(tensor_list), code, tensors.stream_of(tensor_list[0]))
+    return outs
+
+
+def _check_fusable(tensor_list, what):
+    code = tensors.dtype_code(tensor_list[0])
+    for t in tensor_list:
+        if not tensors.is_device(t):
+            raise ValueError("%s needs device tensors" % what)
+        if tensors.dtype_code(t) != code:
+            raise TypeError("%s needs one dtype per call" % what)
+        if not t.is_contiguous():
+            raise ValueError("%s needs contiguous tensors" % what)
+    return code
 
 
 def bucket_sum(a, b, out=None):
