@@ -206,6 +206,14 @@ TIPS_API int tips_fused_allreduce_oop(const void* const* ins, void* const* outs,
  * requests are ordered by rank 0. */
 TIPS_API int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype,
                                         void* stream);
+/* The same with the tensor's shape (ndim <= TIPS_MAX_DIMS; ndim 0 = a scalar, announced as
+ * shape [1] as CreateNoEmptyTfShape does, coordinator.cc:212-221): rank 0 validates shapes
+ * with ConstructResponseMessage's rule and text (coordinator.cc:129-146), so a [2,4] request
+ * on one rank and [4,2] on another fails on every rank with "Mismatched allreduce tensor
+ * shapes: [2,4] vs [4,2]" although the element counts agree. tips_enqueue_allreduce
+ * announces shape [count]. */
+TIPS_API int64_t tips_enqueue_allreduce_shaped(const char* name, const void* in, void* out, const int64_t* shape,
+                                               int ndim, int dtype, void* stream);
 /* 1 = done (handle released), 0 = pending, < 0 = error (message in tips_last_error). */
 TIPS_API int tips_poll(int64_t handle);
 /* Blocks until the request is reduced (TIPS_OK, handle released) or failed (< 0). */
@@ -215,6 +223,11 @@ TIPS_API int tips_wait(int64_t handle);
  * Returns TIPS_OK, or the first failure (its handles[i] < 0; the others are enqueued). */
 TIPS_API int tips_enqueue_allreduce_n(const char* const* names, const void* const* ins, void* const* outs,
                                       const int64_t* counts, int n, int dtype, void* stream, int64_t* handles);
+/* Shaped form of tips_enqueue_allreduce_n: tensor i has ndims[i] dims, taken in order from the
+ * concatenated dims array (sum of ndims entries). */
+TIPS_API int tips_enqueue_allreduce_shaped_n(const char* const* names, const void* const* ins, void* const* outs,
+                                             const int* ndims, const int64_t* dims, int n, int dtype, void* stream,
+                                             int64_t* handles);
 /* tips_wait on each of n handles (handles <= 0 are skipped): TIPS_OK or the first failure. */
 TIPS_API int tips_wait_n(const int64_t* handles, int n);
 /* The negotiation protocol with an executor that only logs (no GPU): each

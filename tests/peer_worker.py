@@ -206,6 +206,32 @@ def collectives_case(c, rank, size, L, _lib, sp):
     return {"case": {"collectives": seed}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:6])}
 
 
+def shapes_case(c, rank, size, L, _lib, sp):
+    """Named requests with shapes (tips_amd.allreduce_async -> tips_enqueue_allreduce_shaped): a
+    tensor that is [2,4] on even ranks and [4,2] on odd ones (equal counts) must fail on EVERY rank
+    with the reference's text (coordinator.cc:142-143), while its neighbours still reduce."""
+    import torch
+    import tips_amd
+    x = torch.arange(8, dtype=torch.float32, device="cuda") + rank
+    good = tips_amd.allreduce_async(x.reshape(2, 4), "shapes.good")
+    bad = tips_amd.allreduce_async(x.reshape(2, 4) if rank % 2 == 0 else x.reshape(4, 2), "shapes.bad")
+    s = tips_amd.allreduce_async(x[3], "shapes.scalar")
+    errs = []
+    out = tips_amd.synchronize(good)
+    exp = sum(torch.arange(8, dtype=torch.float32) + r for r in range(size)).reshape(2, 4)
+    if not torch.equal(out.cpu(), exp):
+        errs.append("good tensor differs")
+    try:
+        tips_amd.synchronize(bad)
+        errs.append("mismatched shapes were accepted")
+    except tips_amd.TipsError as e:
+        if e.code != -7 or "Mismatched allreduce tensor shapes: [2,4] vs [4,2]" not in str(e):
+            errs.append("wrong error: %s" % e)
+    if float(tips_amd.synchronize(s).item()) != float(sum(3 + r for r in range(size))):
+        errs.append("scalar differs")
+    return {"case": {"shapes": True}, "rc": 0, "ok": not errs, "error": "; ".join(errs)}
+
+
 def workload_sizes(name):
     sys.path.insert(0, os.path.dirname(HERE))
     import bench
@@ -339,12 +365,18 @@ def main():
     for c in cases:
         case_algo = ALGO_NAMES[c["algo"]] if c.get("algo") else algo
         JOB_ALGO = case_algo
-        _lib.call("tips_set_algorithm", case_algo)
+        if os.environ.get("TIPS_WORKER_SET_ALGO", "1") == "1":
+            _lib.call("tips_set_algorithm", case_algo)
+        else:  # the selection comes from TIPS_ALGO alone (equivalent to tips_set_algorithm)
+            _lib.call("tips_set_algorithm", ALGO_NAMES["auto"])
         if c.get("named"):
             results.append(named_case(c, rank, size, L, _lib, sp))
             continue
         if c.get("fused"):
             results.append(fused_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("shapes"):
+            results.append(shapes_case(c, rank, size, L, _lib, sp))
             continue
         if c.get("golden"):
             results.append(golden_case(c, rank, size, L, _lib, sp))

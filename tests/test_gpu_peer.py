@@ -166,3 +166,19 @@ def test_fusion_workloads_8_processes(gpu, workload):
     tips/tensorflow/__init__.py:203-222)."""
     cases = [{"fused": workload, "seed": 3, "mode": m} for m in ("inplace", "oop", "grads", "optimizer")]
     check(run_job(8, cases, timeout=600, TIPS_PEER_WS_MIB="64"))
+
+
+def test_peer_selected_by_env_alone(gpu):
+    """TIPS_ALGO=peer without tips_set_algorithm routes every collective - allreduce, broadcast,
+    allgatherv and the consistency check's record exchange - over the peer workspaces: the job has
+    no RCCL communicator (TIPS_NO_RCCL=1), so any RCCL fallback would fail."""
+    check(run_job(3, [{"collectives": True, "seed": 9, "big": 1 << 20}, {"dtype": F32, "n": 5000, "seed": 2}],
+                  TIPS_PEER_WS_MIB="4", TIPS_ALGO="peer", TIPS_WORKER_SET_ALGO="0"))
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_named_shape_validation_across_processes(gpu, p):
+    """allreduce_async carries the tensor's shape: [2,4] against [4,2] fails on every rank with
+    TIPS_ERR_MISMATCH and the reference's message, the job keeps working (coordinator.cc:129-146)."""
+    port = str(29600 + os.getpid() % 100 + p)
+    check(run_job(p, [{"shapes": True}], MASTER_ADDR="127.0.0.1", MASTER_PORT=port, TIPS_PEER_WS_MIB="4"))

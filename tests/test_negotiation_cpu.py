@@ -96,3 +96,26 @@ def test_readiness_order():
     for _, rc, log, err in res:
         assert rc == 0, err
         assert lines(log) == ["b OK", "a OK"]
+
+
+def test_shape_mismatch_with_equal_counts_fails_everywhere():
+    """The negotiated path carries each tensor's shape (tips_enqueue_allreduce_shaped): [2,4] on
+    rank 0 and [4,2] on rank 1 have equal element counts, and must still fail on every rank with
+    ConstructResponseMessage's text (reference coordinator.cc:129-146, message at :142-143)."""
+    res = run(["w 0 8 2,4\nv 0 6 3,2\nok 0 8 2,4", "ok 0 8 2,4\nv 0 6 3,2\nw 0 8 4,2"])
+    logs = [dict(l.split(" ", 1) for l in lines(log)) for _, _, log, _ in res]
+    for rank, rc, _, err in res:
+        assert rc == 0, err
+    for got in logs:
+        assert got["w"] == "ERR Mismatched allreduce tensor shapes: [2,4] vs [4,2]"
+        assert got["v"] == "OK" and got["ok"] == "OK"
+
+
+def test_shape_rank_and_scalar():
+    """Shapes of different rank fail with the reference's TensorShape text; a scalar announces [1]."""
+    res = run(["a 0 4 4\nb 0 1 1\nc 1 4 4", "a 0 4 4,1\nb 0 1\nc 1 4 2,2"])
+    for _, _, log, _ in res:
+        got = dict(l.split(" ", 1) for l in lines(log))
+        assert got["a"] == "ERR Mismatched allreduce tensor shapes: [4] vs [4,1]"
+        assert got["b"] == "OK"
+        assert got["c"] == "ERR Mismatched allreduce tensor shapes: [4] vs [2,2]"

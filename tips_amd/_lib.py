@@ -85,6 +85,11 @@ _SIGNATURES = [
      [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_enqueue_allreduce", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_enqueue_allreduce_shaped", ctypes.c_int64,
+     [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_enqueue_allreduce_shaped_n", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_char_p), _c_void_pp, _c_void_pp, ctypes.POINTER(ctypes.c_int), _c_i64_p, ctypes.c_int,
+      ctypes.c_int, ctypes.c_void_p, _c_i64_p]),
     ("tips_poll", ctypes.c_int, [ctypes.c_int64]),
     ("tips_enqueue_allreduce_n", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_char_p), _c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,

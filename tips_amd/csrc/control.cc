@@ -25,7 +25,7 @@ int exchange_i64(State& st, const int64_t* mine, int words, std::vector<int64_t>
   int64_t* d = (int64_t*)st.small.p;
   HIP_TRY(hipMemcpyAsync(d + (size_t)words * st.size, mine, sizeof(int64_t) * words, hipMemcpyHostToDevice,
                          st.io_stream));
-  if (st.algo == TIPS_ALGO_PEER && st.size <= tips::kMaxSrcs) {
+  if (peer_selected(st)) {
     std::vector<int64_t> b(st.size, (int64_t)sizeof(int64_t) * words), disp(st.size);
     for (int r = 0; r < st.size; r++) disp[r] = (int64_t)sizeof(int64_t) * words * r;
     TRY(peer_allgatherv(st, (const char*)(d + (size_t)words * st.size), (char*)d, b.data(), disp.data(), st.io_stream));
@@ -148,7 +148,7 @@ int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root
       if (i != o) HIP_TRY(hipMemcpyAsync(o, i, bytes, hipMemcpyDeviceToDevice, s));
       return 0;
     }
-    if (st.algo == TIPS_ALGO_PEER && st.size <= tips::kMaxSrcs)
+    if (peer_selected(st))
       return peer_broadcast(st, (const char*)i, (char*)o, (int64_t)bytes, root, s);
     TRY(ensure_comm(st));
     NCCL_TRY(ncclBroadcast(i, o, bytes, ncclInt8, root, st.comm, s));
@@ -181,7 +181,7 @@ int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* cou
                         HIP_TRY(hipMemcpyAsync(ob + disp[st.rank] * es, i, (size_t)(count * es),
                                                hipMemcpyDeviceToDevice, s));
                       if (st.size == 1) return 0;
-                      if (st.algo == TIPS_ALGO_PEER && st.size <= tips::kMaxSrcs) {
+                      if (peer_selected(st)) {
                         std::vector<int64_t> b(st.size), d(st.size);
                         for (int r = 0; r < st.size; r++) b[r] = counts[r] * es, d[r] = disp[r] * es;
                         return peer_allgatherv(st, (const char*)i, ob, b.data(), d.data(), s);

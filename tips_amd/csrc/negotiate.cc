@@ -49,6 +49,7 @@ struct Req {
   const void* in = nullptr;
   void* out = nullptr;
   int64_t count = 0;
+  std::vector<int64_t> shape;  // dims (the reference's TensorShape; [count] for unshaped requests)
   int dtype = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
@@ -98,11 +99,13 @@ struct Reader {
   }
 };
 
-// announce (rank -> rank 0): u8 shutdown, u32 n, n x {i32 dtype, i64 count, str name}
+// announce (rank -> rank 0): u8 shutdown, u32 n, n x {i32 dtype, i64 count, u32 ndim, ndim x i64 dim, str name}
+//   (the fields of the reference's RequestMessage, collective_messages.fbs: dtype, name, shape)
 // response (rank 0 -> all):  u8 shutdown, u32 n, n x {u8 ok, str name, str error}
 struct Announce {
   int dtype;
   int64_t count;
+  std::vector<int64_t> shape;
   std::string name;
 };
 
@@ -144,8 +147,8 @@ struct Table {
       int64_t* rec = &r.rec[(size_t)rank * TIPS_REQUEST_WORDS];
       rec[0] = TIPS_REQ_ALLREDUCE;
       rec[1] = a.dtype;
-      rec[2] = 1;  // the C-ABI carries element counts: shape [count]
-      rec[3] = a.count;
+      rec[2] = (int64_t)a.shape.size();  // (<= TIPS_MAX_DIMS: checked at enqueue and on decode)
+      for (size_t d = 0; d < a.shape.size(); d++) rec[3 + d] = a.shape[d];
     }
     if (!r.queued && (!r.dup.empty() || r.nseen == p)) {
       r.queued = true;
@@ -227,19 +230,27 @@ class Negotiator {
     return 0;
   }
 
-  int64_t enqueue(const std::string& name, const void* in, void* out, int64_t count, int dtype, hipStream_t s) {
+  int64_t enqueue(const std::string& name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
+                  hipStream_t s) {
+    if (ndim < 0 || ndim > TIPS_MAX_DIMS) return fail(TIPS_ERR_INVALID_ARG, "bad ndim %d", ndim);
     auto r = std::make_shared<Req>();
     r->name = name;
     r->in = in;
     r->out = out;
-    r->count = count;
+    r->count = 1;
+    for (int d = 0; d < ndim; d++) {
+      if (shape[d] < 0) return fail(TIPS_ERR_INVALID_ARG, "negative dimension");
+      r->shape.push_back(shape[d]);
+      r->count *= shape[d];
+    }
+    if (ndim == 0) r->shape.push_back(1);  // a scalar travels as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
     r->dtype = dtype;
     r->stream = s;
     if (!dry_) {  // device-resident tensors only: the negotiated path runs on the caller's stream
       // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
       // st.device is fixed from init on)
       TRY(set_device(S()));
-      if (count > 0 && !(is_device_ptr(in) && is_device_ptr(out)))
+      if (r->count > 0 && !(is_device_ptr(in) && is_device_ptr(out)))
         return fail(TIPS_ERR_INVALID_ARG, "named allreduce needs device pointers");
       {
         std::lock_guard<std::mutex> l(m_);
@@ -251,8 +262,13 @@ class Negotiator {
       if (!r->ev) HIP_TRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
     }
     std::lock_guard<std::mutex> l(m_);
-    if (!running_) return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
-    if (by_name_.count(name)) return fail(TIPS_ERR_INVALID_ARG, "a request named %s is already pending", name.c_str());
+    auto refuse = [&](int code, const std::string& msg) -> int64_t {  // the event goes back to the pool
+      if (r->ev) ev_pool_.push_back(r->ev);
+      r->ev = nullptr;
+      return fail(code, "%s", msg.c_str());
+    };
+    if (!running_) return refuse(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
+    if (by_name_.count(name)) return refuse(TIPS_ERR_INVALID_ARG, "a request named " + name + " is already pending");
     r->handle = ++next_handle_;
     by_name_[name] = r;
     by_handle_[r->handle] = r;
@@ -357,6 +373,8 @@ class Negotiator {
       for (auto& r : batch) {
         w.put<int32_t>(r->dtype);
         w.put<int64_t>(r->count);
+        w.put<uint32_t>((uint32_t)r->shape.size());
+        for (int64_t d : r->shape) w.put<int64_t>(d);
         w.str(r->name);
       }
       std::string resp;
@@ -431,6 +449,9 @@ class Negotiator {
         Announce a;
         a.dtype = rd.get<int32_t>();
         a.count = rd.get<int64_t>();
+        const uint32_t ndim = rd.get<uint32_t>();
+        if (ndim > TIPS_MAX_DIMS) rd.ok = false;
+        for (uint32_t d = 0; d < ndim && rd.ok; d++) a.shape.push_back(rd.get<int64_t>());
         a.name = rd.str();
         if (rd.ok) table_.announce(r, a);
       }
@@ -603,30 +624,53 @@ using namespace tips::rt;
 
 extern "C" {
 
-int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype, void* stream) {
-  TRY(check_dtype(dtype));
-  if (!name || !*name || count < 0 || (count > 0 && (!in || !out)))
-    return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
-  Negotiator* n = nullptr;
-  {
-    std::lock_guard<std::mutex> l(g_neg_mu);
-    if (!g_neg) {
-      State& st = S();
-      int rank, size;
-      {
-        std::lock_guard<std::mutex> lk(st.mu);
-        if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
-        rank = st.rank;
-        size = st.size;
+namespace {
+
+Negotiator* negotiator() {  // started by the first named request (collective)
+  std::lock_guard<std::mutex> l(g_neg_mu);
+  if (!g_neg) {
+    State& st = S();
+    int rank, size;
+    {
+      std::lock_guard<std::mutex> lk(st.mu);
+      if (!st.initialized) {
+        fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+        return nullptr;
       }
-      auto neg = std::make_unique<Negotiator>();
-      TRY(neg->start(rank, size, master_addr(), negotiation_port(), false,
-                     (int)env_i64("TIPS_NEGOTIATION_TIMEOUT", 600)));
-      g_neg = std::move(neg);
+      rank = st.rank;
+      size = st.size;
     }
-    n = g_neg.get();
+    auto neg = std::make_unique<Negotiator>();
+    if (neg->start(rank, size, master_addr(), negotiation_port(), false, (int)env_i64("TIPS_NEGOTIATION_TIMEOUT", 600)))
+      return nullptr;
+    g_neg = std::move(neg);
   }
-  return n->enqueue(name, in, out, count, dtype, (hipStream_t)stream);
+  return g_neg.get();
+}
+
+int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
+                      void* stream) {
+  TRY(check_dtype(dtype));
+  if (!name || !*name || ndim < 0 || ndim > TIPS_MAX_DIMS || (ndim > 0 && !shape))
+    return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
+  int64_t count = 1;
+  for (int d = 0; d < ndim; d++) count *= shape[d] < 0 ? 0 : shape[d];
+  if (count > 0 && (!in || !out)) return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
+  Negotiator* n = negotiator();
+  if (!n) return TIPS_ERR_NOT_INITIALIZED;
+  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream);
+}
+
+}  // namespace
+
+int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype, void* stream) {
+  if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
+  return enqueue_named(name, in, out, &count, 1, dtype, stream);  // shape [count]
+}
+
+int64_t tips_enqueue_allreduce_shaped(const char* name, const void* in, void* out, const int64_t* shape, int ndim,
+                                      int dtype, void* stream) {
+  return enqueue_named(name, in, out, shape, ndim, dtype, stream);
 }
 
 int tips_poll(int64_t handle) {
@@ -662,6 +706,29 @@ int tips_enqueue_allreduce_n(const char* const* names, const void* const* ins, v
   return rc ? fail(rc, "%s", first_err.c_str()) : 0;
 }
 
+int tips_enqueue_allreduce_shaped_n(const char* const* names, const void* const* ins, void* const* outs,
+                                    const int* ndims, const int64_t* dims, int n, int dtype, void* stream,
+                                    int64_t* handles) {
+  if (n < 0 || (n > 0 && (!names || !ins || !outs || !ndims || !handles)))
+    return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce list");
+  int rc = 0;
+  std::string first_err;
+  int64_t off = 0;
+  for (int i = 0; i < n; i++) {
+    if (ndims[i] < 0 || ndims[i] > TIPS_MAX_DIMS || (ndims[i] > 0 && !dims)) {
+      handles[i] = fail(TIPS_ERR_INVALID_ARG, "bad ndim %d for %s", ndims[i], names[i] ? names[i] : "?");
+    } else {
+      handles[i] = enqueue_named(names[i], ins[i], outs[i], dims ? dims + off : nullptr, ndims[i], dtype, stream);
+      off += ndims[i];
+    }
+    if (handles[i] < 0 && rc == 0) {
+      rc = (int)handles[i];
+      first_err = last_error();
+    }
+  }
+  return rc ? fail(rc, "%s", first_err.c_str()) : 0;
+}
+
 int tips_wait_n(const int64_t* handles, int n) {
   if (n < 0 || (n > 0 && !handles)) return fail(TIPS_ERR_INVALID_ARG, "bad handle list");
   int rc = 0;
@@ -686,12 +753,14 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   std::vector<int64_t> handles;
   const char* p = requests;
   const auto t0 = std::chrono::steady_clock::now();
-  while (*p) {  // lines: "name dtype count", "@sleep ms", "@wait" (all so far resolved), "@mark" (log "# mark us")
+  // lines: "name dtype count [d0,d1,...]" (shape: default [count]), "@sleep ms", "@wait" (all so far
+  // resolved), "@mark" (log "# mark us")
+  while (*p) {
     const char* e = strchr(p, '\n');
     std::string line(p, e ? (size_t)(e - p) : strlen(p));
     p = e ? e + 1 : p + line.size();
     if (line.empty()) continue;
-    char nm[256];
+    char nm[256], dims[256] = "";
     long long dt = 0, cnt = 0;
     if (line.rfind("@sleep ", 0) == 0) {
       std::this_thread::sleep_for(std::chrono::milliseconds(atoi(line.c_str() + 7)));
@@ -701,8 +770,15 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
     } else if (line == "@mark") {
       const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
       neg.note("# mark " + std::to_string((long long)us.count()));
-    } else if (sscanf(line.c_str(), "%255s %lld %lld", nm, &dt, &cnt) == 3) {
-      const int64_t h = neg.enqueue(nm, nullptr, nullptr, cnt, (int)dt, nullptr);
+    } else if (sscanf(line.c_str(), "%255s %lld %lld %255s", nm, &dt, &cnt, dims) >= 3) {
+      std::vector<int64_t> shape;
+      for (const char* q = dims; *q;) {
+        shape.push_back(strtoll(q, nullptr, 10));
+        q = strchr(q, ',');
+        q = q ? q + 1 : "";
+      }
+      if (shape.empty()) shape.push_back(cnt);
+      const int64_t h = neg.enqueue(nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr);
       if (h < 0) return (int)h;
       handles.push_back(h);
     }

@@ -159,6 +159,11 @@ bool is_pinned_host(const void* p, int64_t bytes);
 int check_dtype(int dtype);
 int set_device(State& st);
 int resolve_algo(int algo, int p, int64_t bytes);
+// The peer transport is selected (tips_set_algorithm or TIPS_ALGO=peer) and can serve this job:
+// the broadcast / allgatherv / record exchange then go over the IPC workspaces, not RCCL.
+inline bool peer_selected(const State& st) {
+  return st.size > 1 && st.size <= tips::kMaxSrcs && resolve_algo(st.algo, st.size, 0) == TIPS_ALGO_PEER;
+}
 int ensure_comm(State& st);
 
 // schedules.cc: device-resident allreduce, caller holds st.mu

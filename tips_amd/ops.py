@@ -219,8 +219,10 @@ def allreduce_async(tensor, name):
     code = tensors.dtype_code(tensor)
     src = tensor.contiguous()
     out = tensors.empty_like(src)
-    h = _lib.lib().tips_enqueue_allreduce(name.encode(), src.data_ptr(), out.data_ptr(), src.numel(), code,
-                                          tensors.stream_of(src))
+    shape = _shape(src)  # validated across ranks with ConstructResponseMessage's rule (coordinator.cc:129-146)
+    sp, _keep = _lib.i64_array(shape or [1])
+    h = _lib.lib().tips_enqueue_allreduce_shaped(name.encode(), src.data_ptr(), out.data_ptr(), sp, len(shape), code,
+                                                 tensors.stream_of(src))
     if h < 0:
         raise _lib.TipsError("tips_enqueue_allreduce", int(h), _lib.last_error())
     hd = Handle(int(h), out, name)
@@ -250,9 +252,11 @@ def allreduce_async_many(tensor_list, names):
     nm = (ctypes.c_char_p * n)(*[x.encode() for x in names])
     pi, _k1 = _lib.ptr_array([x.data_ptr() for x in srcs])
     po, _k2 = _lib.ptr_array([x.data_ptr() for x in outs])
-    pc, _k3 = _lib.i64_array([x.numel() for x in srcs])
+    shapes = [_shape(x) for x in srcs]
+    nd = (ctypes.c_int * n)(*[len(s) for s in shapes])
+    pd, _k3 = _lib.i64_array([d for s in shapes for d in s] or [0])
     hs = (ctypes.c_int64 * n)()
-    _lib.call("tips_enqueue_allreduce_n", nm, pi, po, pc, n, code, tensors.stream_of(srcs[0]), hs)
+    _lib.call("tips_enqueue_allreduce_shaped_n", nm, pi, po, nd, pd, n, code, tensors.stream_of(srcs[0]), hs)
     out = []
     for h, o, x, name in zip(hs, outs, srcs, names):
         hd = Handle(int(h), o, name)
