@@ -70,7 +70,10 @@ enum tips_algorithm {
   TIPS_ALGO_RCCL = 2,   /* ncclAllReduce, kept as a comparison point only */
   TIPS_ALGO_ONESHOT = 3, /* whole bucket to every peer in one step + one p-input fold (small buckets) */
   TIPS_ALGO_PEER = 4,    /* direct's exchange by our own kernels through IPC-mapped peer memory (no RCCL):
-                            push + rank-order fold + pull, phases ordered by a node-local shared-memory barrier */
+                            push + rank-order fold + pull, phases ordered by a node-local shared-memory barrier.
+                            Host-synchronous: a device-pointer call under PEER returns only after its push and
+                            fold have run on every rank (each phase ends in a stream synchronize + barrier); only
+                            the final pull is left queued on the caller's stream. */
 };
 
 /* ---- lifecycle: same names and types as tips/core/operations.h:7-21 ---- */
@@ -125,7 +128,8 @@ TIPS_API int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_
 /* Replaces AllreduceCpu<T> (tips/core/collective/utils.h:52-67) and the
  * MPIAllreduce op's data path (tips/tensorflow/ops.cc:86-115):
  * out = SUM over ranks of in, out-of-place (in == out allowed).
- * Device pointers: stream-ordered, returns after enqueue.
+ * Device pointers: stream-ordered, returns after enqueue (TIPS_ALGO_PEER excepted: it
+ * blocks the host through its push and fold phases, see enum tips_algorithm).
  * Host pointers (both): staged through HBM, returns when out is written.
  * op must be TIPS_OP_SUM. */
 TIPS_API int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream);

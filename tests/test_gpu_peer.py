@@ -182,3 +182,17 @@ def test_named_shape_validation_across_processes(gpu, p):
     TIPS_ERR_MISMATCH and the reference's message, the job keeps working (coordinator.cc:129-146)."""
     port = str(29600 + os.getpid() % 100 + p)
     check(run_job(p, [{"shapes": True}], MASTER_ADDR="127.0.0.1", MASTER_PORT=port, TIPS_PEER_WS_MIB="4"))
+
+
+def test_stale_mapping_refused_on_every_rank(gpu):
+    """Every rank reads each peer's workspace header back through its IPC mapping and checks the
+    nonce the owner published: a header that does not match (here rank 1 writes a wrong nonce, as a
+    stale import would show another buffer's) fails the call on EVERY rank with TIPS_ERR_HIP
+    instead of reducing through the mapping; a clean job right after works."""
+    ERR_HIP = -3
+    results = run_job(3, [{"dtype": F32, "n": 1000, "seed": 1, "expect_error": ERR_HIP}], TIPS_PEER_WS_MIB="4",
+                      TIPS_PEER_TEST_CORRUPT_RANK="1")
+    check(results)
+    for res in results:
+        assert "stale or foreign IPC mapping" in res["results"][0]["error"]
+    check(run_job(3, [{"dtype": F32, "n": 1000, "seed": 1}], TIPS_PEER_WS_MIB="4"))

@@ -46,20 +46,35 @@ namespace {
 
 constexpr int kPeerMaxRanks = tips::kMaxSrcs;
 constexpr uint64_t kPeerMagic = 0x5449505350454552ull;  // "TIPSPEER"
-constexpr int64_t kPeerSlotPad = 4096;  // slots not at power-of-two strides (as schedules.cc kSlotPad)
+constexpr int64_t kPeerSlotPad = 4096;  // slots not at power-of-two strides (as plan.cc kSlotPad)
+constexpr int64_t kWsHeader = 4096;     // each workspace starts with its WsHeader; slots follow
 
 enum Phase : int32_t {
   kCall = 1, kPushed = 2, kReduced = 3, kPublish = 4, kShutdown = 5, kGathered = 6, kUnpacked = 7,
-  kBcastCall = 8, kGatherCall = 9, kStaged = 10, kPulled = 11
+  kBcastCall = 8, kGatherCall = 9, kStaged = 10, kPulled = 11, kVerified = 12
 };
 
 struct Post {
   int64_t count;
   int32_t dtype;
   int32_t phase;
-  int64_t aux;  // broadcast: the root rank
+  int64_t aux;  // broadcast: the root rank; kVerified: -1 if every header checked out, else the failing owner
   int64_t ws_bytes;
+  uint64_t nonce;  // kPublish: the nonce the owner wrote at its workspace head
   hipIpcMemHandle_t handle;
+};
+
+// Written by the owner at the head of its workspace before it publishes the IPC handle, and read
+// back by every peer THROUGH its mapping: a mapping that shows another buffer (a stale import
+// was once seen on this ROCm's dmabuf IPC) fails the job instead of summing
+// wrong data.
+struct WsHeader {
+  uint64_t magic;
+  uint64_t key;    // the job's unique-id hash
+  int64_t rank;    // owner
+  int64_t bytes;   // workspace size
+  uint64_t nonce;  // per allocation
+  uint64_t pad[3];
 };
 
 struct alignas(64) PeerRank {
@@ -96,8 +111,10 @@ struct PeerState {
   PeerCtl* ctl = nullptr;
   uint64_t epoch = 0;
   void* ws = nullptr;        // this rank's workspace (uncached device memory, IPC-exported)
-  int64_t ws_bytes = 0;
-  void* remote[kPeerMaxRanks] = {};  // peers' workspaces, IPC-opened (remote[rank] = ws)
+  int64_t ws_bytes = 0;      // data bytes after the header
+  void* remote[kPeerMaxRanks] = {};  // peers' workspaces as IPC-opened (remote[rank] = ws)
+  char* rdata[kPeerMaxRanks] = {};   // their data regions (after the WsHeader): what the schedule uses
+  void* hdr_dev = nullptr;           // p headers read back through the mappings
   hipEvent_t pulled = nullptr;        // after the last call's pull (which reads the peers' red)
   bool pull_pending = false;
   bool broken = false;  // a failure past barrier 0 leaves the ranks out of step: refuse further calls
@@ -238,7 +255,7 @@ int setup_ws(State& st, PeerState& ps) {
   std::vector<void*> refused;
   int rc = 0;
   for (int attempt = 0;; attempt++) {
-    rc = alloc_ws(&ps.ws, bytes);
+    rc = alloc_ws(&ps.ws, bytes + kWsHeader);
     if (rc) break;
     hipError_t he = hipIpcGetMemHandle(&mine.handle, ps.ws);
     if (he == hipSuccess) break;
@@ -254,18 +271,55 @@ int setup_ws(State& st, PeerState& ps) {
   for (void* q : refused) (void)hipFree(q);
   if (rc) return rc;
   ps.ws_bytes = bytes;
+  // the header: this job's key, the owner, the size and a nonce that no earlier buffer carried
+  WsHeader h{};
+  h.magic = kPeerMagic;
+  h.key = st.peer_key;
+  h.rank = st.rank;
+  h.bytes = bytes;
+  h.nonce = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 6364136223846793005ull ^
+            (uint64_t)(uintptr_t)ps.ws ^ ((uint64_t)getpid() << 32) ^ (uint64_t)st.rank;
+  mine.nonce = h.nonce;
+  if (env_i64("TIPS_PEER_TEST_CORRUPT_RANK", -1) == st.rank) h.nonce ^= 1;  // test hook: a header peers must refuse
+  HIP_TRY(hipMemcpy(ps.ws, &h, sizeof h, hipMemcpyHostToDevice));
   Post all[kPeerMaxRanks];
   TRY(barrier(st, ps, mine, all, peer_timeout()));
   for (int j = 0; j < st.size; j++) {
     if (j == st.rank) {
       ps.remote[j] = ps.ws;
-      continue;
+    } else {
+      if (all[j].ws_bytes != bytes)
+        return fail(TIPS_ERR_MISMATCH, "peer schedule: rank %d workspace %lld B, rank %d %lld B (TIPS_PEER_WS_MIB must match)",
+                    j, (long long)all[j].ws_bytes, st.rank, (long long)bytes);
+      HIP_TRY(hipIpcOpenMemHandle(&ps.remote[j], all[j].handle, hipIpcMemLazyEnablePeerAccess));
     }
-    if (all[j].ws_bytes != bytes)
-      return fail(TIPS_ERR_MISMATCH, "peer schedule: rank %d workspace %lld B, rank %d %lld B (TIPS_PEER_WS_MIB must match)",
-                  j, (long long)all[j].ws_bytes, st.rank, (long long)bytes);
-    HIP_TRY(hipIpcOpenMemHandle(&ps.remote[j], all[j].handle, hipIpcMemLazyEnablePeerAccess));
+    ps.rdata[j] = (char*)ps.remote[j] + kWsHeader;
   }
+  // every peer's header, read through the mapping by a kernel (uncached memory: what the owner
+  // wrote, not a stale line), checked against what the owner published at the barrier
+  const int p = st.size;
+  if (!ps.hdr_dev) HIP_TRY(hipMalloc(&ps.hdr_dev, sizeof(WsHeader) * kPeerMaxRanks));
+  tips::XferSeg segs[tips::kMaxXferSegs];
+  for (int j = 0; j < p; j++) segs[j] = {(const char*)ps.remote[j], (char*)ps.hdr_dev + j * sizeof(WsHeader), (int64_t)sizeof(WsHeader)};
+  HIP_TRY(tips::launch_xfer(segs, p, st.io_stream));
+  WsHeader seen[kPeerMaxRanks];
+  HIP_TRY(hipMemcpyAsync(seen, ps.hdr_dev, sizeof(WsHeader) * p, hipMemcpyDeviceToHost, st.io_stream));
+  HIP_TRY(hipStreamSynchronize(st.io_stream));
+  int bad = -1;
+  for (int j = 0; j < p && bad < 0; j++)
+    if (seen[j].magic != kPeerMagic || seen[j].key != st.peer_key || seen[j].rank != j || seen[j].bytes != bytes ||
+        seen[j].nonce != all[j].nonce)
+      bad = j;
+  Post v{};
+  v.phase = kVerified;
+  v.aux = bad < 0 ? -1 : bad;
+  TRY(barrier(st, ps, v, all, peer_timeout()));
+  for (int j = 0; j < p; j++)
+    if (all[j].aux >= 0)
+      return fail(TIPS_ERR_HIP,
+                  "peer schedule: rank %d's mapping of rank %lld's workspace does not show the header rank %lld wrote "
+                  "(stale or foreign IPC mapping); refusing to reduce through it",
+                  j, (long long)all[j].aux, (long long)all[j].aux);
   return 0;
 }
 
@@ -283,6 +337,7 @@ void peer_release(State& st) {
     munmap(ps->ctl, sizeof(PeerCtl));
   }
   if (ps->ws) (void)hipFree(ps->ws);
+  if (ps->hdr_dev) (void)hipFree(ps->hdr_dev);
   if (ps->pulled) (void)hipEventDestroy(ps->pulled);
   delete ps;
   st.peer = nullptr;
@@ -309,7 +364,7 @@ int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, i
   for (int d = 1; d < p; d++) {
     const int to = mod(r + d, p);
     const Range c = chunk_of(n, p, align, to);
-    segs[m++] = {in + c.b * es, (char*)ps.remote[to] + slot_of(to, r), c.len() * es};
+    segs[m++] = {in + c.b * es, ps.rdata[to] + slot_of(to, r), c.len() * es};
   }
   HIP_TRY(tips::launch_xfer(segs, m, user));
   HIP_TRY(hipStreamSynchronize(user));  // also: our previous pull has read the peers' red
@@ -323,8 +378,8 @@ int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, i
   // allgather it lands in out directly (the pushes below read it from there).
   const Range mine = chunk_of(n, p, align, r);
   const void* srcs[tips::kMaxSrcs];
-  for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)(in + mine.b * es) : (char*)ps.ws + slot_of(r, j);
-  char* red = ag_push ? out + mine.b * es : (char*)ps.ws + red_off;
+  for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)(in + mine.b * es) : ps.rdata[r] + slot_of(r, j);
+  char* red = ag_push ? out + mine.b * es : ps.rdata[r] + red_off;
   HIP_TRY(tips::launch_multi_sum(red, srcs, p, mine.len(), dtype, user));
   HIP_TRY(hipStreamSynchronize(user));
   q.phase = kReduced;
@@ -337,7 +392,7 @@ int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, i
     for (int d = 0; d < p; d++) {
       const int from = mod(r + d, p);
       const Range c = chunk_of(n, p, align, from);
-      segs[m++] = {(const char*)ps.remote[from] + red_off, out + c.b * es, c.len() * es};
+      segs[m++] = {ps.rdata[from] + red_off, out + c.b * es, c.len() * es};
     }
     HIP_TRY(tips::launch_xfer(segs, m, user));
     return 0;
@@ -345,7 +400,7 @@ int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, i
   // push allgather: my reduced chunk -> every peer's slot for r (every fold has consumed
   // the slots: barrier above), then each rank copies its slots into out
   m = 0;
-  for (int d = 1; d < p; d++) segs[m++] = {red, (char*)ps.remote[mod(r + d, p)] + slot_of(mod(r + d, p), r), mine.len() * es};
+  for (int d = 1; d < p; d++) segs[m++] = {red, ps.rdata[mod(r + d, p)] + slot_of(mod(r + d, p), r), mine.len() * es};
   HIP_TRY(tips::launch_xfer(segs, m, user));
   HIP_TRY(hipStreamSynchronize(user));
   q.phase = kGathered;
@@ -354,7 +409,7 @@ int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, i
   for (int d = 1; d < p; d++) {
     const int from = mod(r + d, p);
     const Range c = chunk_of(n, p, align, from);
-    segs[m++] = {(const char*)ps.ws + slot_of(r, from), out + c.b * es, c.len() * es};
+    segs[m++] = {ps.rdata[r] + slot_of(r, from), out + c.b * es, c.len() * es};
   }
   HIP_TRY(tips::launch_xfer(segs, m, user));
   return 0;
@@ -449,14 +504,14 @@ int peer_broadcast_impl(State& st, PeerState& ps, const char* in, char* out, int
       TRY(barrier(st, ps, q, nullptr, peer_timeout()));
     }
     if (r == root) {
-      tips::XferSeg segs[2] = {{in + b, (char*)ps.ws, len}, {in + b, out + b, in == out ? 0 : len}};
+      tips::XferSeg segs[2] = {{in + b, ps.rdata[r], len}, {in + b, out + b, in == out ? 0 : len}};
       HIP_TRY(tips::launch_xfer(segs, 2, user));
       HIP_TRY(hipStreamSynchronize(user));
     }
     q.phase = kStaged;
     TRY(barrier(st, ps, q, nullptr, peer_timeout()));
     if (r != root) {
-      tips::XferSeg seg = {(const char*)ps.remote[root], out + b, len};
+      tips::XferSeg seg = {ps.rdata[root], out + b, len};
       HIP_TRY(tips::launch_xfer(&seg, 1, user));
     }
   }
@@ -494,7 +549,7 @@ int peer_allgatherv_impl(State& st, PeerState& ps, const char* in, char* out, co
       TRY(barrier(st, ps, q, nullptr, peer_timeout()));
     }
     const bool self_in_place = (in + b == out + displ[r] + b);
-    tips::XferSeg mine[2] = {{in + b, (char*)ps.ws, len_of(r)}, {in + b, out + displ[r] + b, self_in_place ? 0 : len_of(r)}};
+    tips::XferSeg mine[2] = {{in + b, ps.rdata[r], len_of(r)}, {in + b, out + displ[r] + b, self_in_place ? 0 : len_of(r)}};
     HIP_TRY(tips::launch_xfer(mine, 2, user));
     HIP_TRY(hipStreamSynchronize(user));
     q.phase = kStaged;
@@ -503,7 +558,7 @@ int peer_allgatherv_impl(State& st, PeerState& ps, const char* in, char* out, co
     int m = 0;
     for (int d = 1; d < p; d++) {
       const int from = mod(r + d, p);
-      segs[m++] = {(const char*)ps.remote[from], out + displ[from] + b, len_of(from)};
+      segs[m++] = {ps.rdata[from], out + displ[from] + b, len_of(from)};
     }
     HIP_TRY(tips::launch_xfer(segs, m, user));
   }
