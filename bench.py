@@ -422,10 +422,18 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         calls = {"optimizer": lambda i: opts[i].synchronize(), "allreduce_grads": lambda i: tips_amd.allreduce_grads(grads[i])}
         what = "DistributedOptimizer.synchronize() / tips_amd.allreduce_grads"
     else:
-        calls = {"optimizer": lambda i: tips_amd.fused_allreduce_(grads[i]),
+        from tips_amd.ops import FusedList
+        fls = [FusedList([p_.numel() for p_ in ps]) for ps in params]
+        flats = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads]  # the optimizer's bucket views
+        views = [list(torch.split(f, sizes)) for f in flats]
+        fvs = [FusedList(sizes) for _ in flats]
+        calls = {"optimizer": lambda i: fvs[i].allreduce_(views[i]),
+                 "packed_separate_grads": lambda i: fls[i].allreduce_(grads[i]),
                  "allreduce_grads": lambda i: tips_amd.fused_allreduce(grads[i])}
         what = ("one rank: both API calls are the identity (reference _allreduce_cond); timed is what each runs at "
-                "N > 1: fused_allreduce_(grads) in place / fused_allreduce(grads) out of place")
+                "N > 1: the optimizer's FusedList.allreduce_ over its gradient bucket views (one contiguous run, "
+                "reduced where it lies: no device work at all on one rank), the same over separately allocated "
+                "gradients (pack + unpack), and allreduce_grads' fused_allreduce(grads) out of place")
     out = {"calls": what, "bytes_per_rank": sum(sizes) * 4, "fixed_view_ms": round(fixed_ms, 4)}
     ref = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads] if world == 1 else None
     for name, fn in calls.items():
@@ -440,11 +448,13 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         t = max_over_ranks(dist, time.perf_counter() - t0) / steps
         leg = {"ms_per_step": round(t * 1e3, 4), "vs_fixed_view": round(t * 1e3 / fixed_ms, 3)}
         if world == 1:
-            moved = 4 * sum(sizes) * 4
-            leg.update(hbm_achieved_GBps=round(moved / t / 1e9, 1), algorithmic_hbm_bytes=moved)
+            moved = 0 if name == "optimizer" else 4 * sum(sizes) * 4  # bucket views: nothing to pack
+            leg["algorithmic_hbm_bytes"] = moved
+            if moved:
+                leg["hbm_achieved_GBps"] = round(moved / t / 1e9, 1)
             got = fn(0)
             torch.cuda.synchronize()
-            got = grads[0] if name == "optimizer" else got
+            got = {"optimizer": views[0], "packed_separate_grads": grads[0]}.get(name, got)
             leg["check"] = "identity, bit-exact" if torch.equal(torch.cat([g.reshape(-1) for g in got]), ref[0]) else "FAIL"
         out[name] = leg
     del params, grads, opts
@@ -522,6 +532,11 @@ def bench_allreduce(args):
     _lib.call("tips_set_algorithm", algo_names[args.algo])
 
     workload = args.workload if args.workload != "auto" else "bucket"
+    measure_pack = world == 1 and workload in ("fused1000", "resnet50")
+    if measure_pack:
+        # one rank: the library does no bucket work at all (the allreduce is the identity); pack and
+        # unpack the buckets anyway, as at N > 1, so this line measures the fusion's per-step HBM cost
+        os.environ["TIPS_FUSION_MEASURE_PACK"] = "1"
     steps = args.steps if args.steps is not None else 20
     warmup = args.warmup if args.warmup is not None else 5
     g = torch.Generator(device="cuda")
@@ -544,11 +559,17 @@ def bench_allreduce(args):
     # the schedule the (largest) reduced buffer gets: the bucket itself, or a <= 64 MiB fusion bucket
     algo = L.tips_resolve_algorithm(world, sizes[0] * 4 if workload == "bucket" else
                                     max(sizes) * 4 if workload == "negotiated1000" else 64 << 20)
-    # every tensor at a 256-B aligned offset of one flat buffer (what a caching allocator hands out)
+    # every tensor at a 256-B aligned offset of one flat buffer, 256 B apart at least (separate
+    # allocations of a caching allocator never touch): the fusion path packs them. (Back-to-back
+    # tensors - a flat gradient buffer's views - are reduced where they lie instead; that path is
+    # the gradient_api "optimizer" leg.)
     offs, total = [], 0
+    gap = 64 if workload in ("fused1000", "resnet50") else 0  # (the bucket / named workloads: no gap)
     for k in sizes:
         offs.append(total)
-        total += (k + 63) // 64 * 64
+        total += (k + 63) // 64 * 64 + gap
+    if workload == "bucket":
+        total = sizes[0]  # the parity check compares the whole output buffer
     total_elems = sum(sizes)
 
     def fill(t, r):
@@ -717,6 +738,8 @@ def bench_allreduce(args):
         "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
                    "algorithm": inv.get(algo, str(algo)) if world > 1 else "none (1 rank)",
                    "rotating_sets": rot,
+                   "fusion_one_rank": ("TIPS_FUSION_MEASURE_PACK=1: buckets packed and unpacked as at N > 1 (the "
+                                       "default one-rank path does no bucket work)") if measure_pack else None,
                    "parallelism": "dp%d (one process per GPU, %s)" % (
                        world, "our kernels through IPC-mapped peer memory over xGMI" if algo == _lib.ALGO_PEER
                        else "ncclAllReduce" if algo == _lib.ALGO_RCCL else "RCCL p2p over xGMI")

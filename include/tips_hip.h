@@ -293,6 +293,13 @@ TIPS_API int tips_sum_variant(void* dst, const void* a, const void* b, int64_t c
 TIPS_API int tips_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, int variant,
                                     void* stream);
 
+/* Tuning entry for the fusion pack / unpack kernel (tools/copy_sweep.py): `tiles` is a device
+ * array of ntiles {const char* src; char* dst; int64_t bytes} records (24 B each), every
+ * bytes <= max_tile_bytes. variant 0 = the shipped kernel (one tile per workgroup); 1-8 = the
+ * grouped kernel (G tiles per workgroup, cache policies: kernels.hip copy_variant_u),
+ * max_tile_bytes <= 16384 for those. */
+TIPS_API int tips_copy_tiles_variant(const void* tiles, int ntiles, int variant, int64_t max_tile_bytes, void* stream);
+
 /* The peer schedule's transfer kernel on its own (tests, tools/peer_mem_probe.cc):
  * copies bytes[i] from srcs[i] to dsts[i] for n <= 16 segments in one launch,
  * any alignment; pointers may be IPC-mapped peer memory. */

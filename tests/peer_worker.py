@@ -261,9 +261,12 @@ def fused_case(c, rank, size, L, _lib, sp):
     mine = inputs(rank)
     views = list(torch.split(mine, sizes))
     before = mine.clone()
-    if mode == "inplace":
+    if mode == "inplace":  # views of one flat buffer: one contiguous run, reduced where it lies
         tips_amd.fused_allreduce_(views)
         got = views
+    elif mode == "inplace_separate":  # separately allocated tensors: packed into the buckets
+        got = [v.clone() for v in views]
+        tips_amd.fused_allreduce_(got)
     elif mode == "oop":
         got = tips_amd.fused_allreduce(views)
     elif mode == "grads":

@@ -173,25 +173,61 @@ def test_rccl_allreduce_single_rank(gpu):
         gpu.set_algorithm(prev)
 
 
+@pytest.mark.parametrize("measure_pack", ["1", "0"])
 @pytest.mark.parametrize("threshold", [4096, 64 << 20])
-def test_fused_pack_unpack_round_trip(gpu, monkeypatch, threshold):
-    """One rank: fused allreduce == identity, so pack -> bucket -> unpack must move every byte exactly,
-    across many buckets, odd sizes, misaligned views and tensors larger than the threshold."""
+def test_fused_pack_unpack_round_trip(gpu, monkeypatch, threshold, measure_pack):
+    """One rank: fused allreduce == identity. With TIPS_FUSION_MEASURE_PACK=1 the buckets are packed
+    and unpacked as at N > 1, so pack -> bucket -> unpack must move every byte exactly, across many
+    buckets, odd sizes, misaligned views and tensors larger than the threshold; without it, in place
+    is no work and out of place one copy."""
     import torch
     monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(threshold))
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", measure_pack)
     rng = np.random.default_rng(20261015)
     sizes = [int(round(2 ** rng.uniform(0, 14))) for _ in range(300)] + [5000, 1]
-    base = torch.randn(sum(sizes) + 1, device="cuda")
-    views, off = [], 1  # offset 1: misaligned views
+    base = torch.randn(sum(sizes) + len(sizes) + 1, device="cuda")
+    views, off = [], 1  # offset 1: misaligned views; a 1-element gap after each (no contiguous runs)
     for s in sizes:
         views.append(base[off:off + s])
-        off += s
+        off += s + 1
     before = [v.clone() for v in views]
+    gaps = base.clone()
     gpu.fused_allreduce_(views)
     gpu.fused_allreduce_(views)  # second call hits the plan cache
     torch.cuda.synchronize()
     for v, b in zip(views, before):
         assert torch.equal(v, b)
+    assert torch.equal(base, gaps)
+    # out of place into separate tensors: at one rank every byte must travel pack -> bucket -> unpack
+    for _ in range(2):
+        outs = gpu.fused_allreduce(views)
+        torch.cuda.synchronize()
+        for o, b in zip(outs, before):
+            assert torch.equal(o, b)
+
+
+def test_fused_contiguous_runs(gpu, monkeypatch):
+    """Tensors that follow each other in memory (a flat buffer's views) form one run, reduced where
+    it lies without packing (fusion.cc build_entry): in place it must leave the bytes around the run
+    alone; out of place into the views of another flat buffer it is one in -> out allreduce. Mixed
+    with separate tensors and a gap that splits two runs."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_DIRECT_BYTES", str(1 << 16))
+    sizes = [1000, 3, 70000, 257, 20000]
+    flat = torch.randn(sum(sizes) + 10, device="cuda")
+    guard = flat[-10:].clone()
+    run = list(torch.split(flat[:sum(sizes)], sizes))
+    other = [torch.randn(n, device="cuda") for n in (5, 9999)]
+    lst = run[:2] + other[:1] + run[2:] + other[1:]
+    before = [t.clone() for t in lst]
+    gpu.fused_allreduce_(lst)
+    outs_flat = torch.empty(sum(t.numel() for t in lst), device="cuda")
+    outs = list(torch.split(outs_flat, [t.numel() for t in lst]))
+    gpu.fused_allreduce(lst, out_list=outs)
+    torch.cuda.synchronize()
+    for t, b, o in zip(lst, before, outs):
+        assert torch.equal(t, b) and torch.equal(o, b)
+    assert torch.equal(flat[-10:], guard)
 
 
 def test_allreduce_grads_identity_single_rank(gpu):
@@ -458,8 +494,9 @@ def test_host_bounce_boundary(gpu, n):
     assert np.array_equal(out3, h)
 
 
+@pytest.mark.parametrize("measure_pack", ["1", "0"])
 @pytest.mark.parametrize("workload", ["config4", "config5"])
-def test_fusion_workloads_single_rank(gpu, workload):
+def test_fusion_workloads_single_rank(gpu, monkeypatch, workload, measure_pack):
     """Configs 4 and 5's tensor lists through the fusion path on one rank (pack -> bucket ->
     unpack moves every byte: the identity), in place and out of place, twice (the second call hits
     the descriptor cache); allreduce_grads and DistributedOptimizer.step() are the identity at one
@@ -469,6 +506,7 @@ def test_fusion_workloads_single_rank(gpu, workload):
     from conftest import REPO
     sys.path.insert(0, REPO)
     import bench
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", measure_pack)
     sizes = bench.fused1000_sizes() if workload == "config4" else bench.resnet50_grad_sizes()
     flat = torch.randn(sum(sizes), device="cuda")
     views = list(torch.split(flat, sizes))
@@ -495,6 +533,7 @@ def test_fusion_concurrent_streams(gpu, monkeypatch):
     unpacked another call's slot would show."""
     import torch
     monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(1 << 20))
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", "1")  # one rank still packs into the shared slots
     rng = np.random.default_rng(8)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     lists = []

@@ -114,6 +114,8 @@ _SIGNATURES = [
     ("tips_multi_sum_variant", ctypes.c_int,
      [ctypes.c_void_p, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_xfer", ctypes.c_int, [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_copy_tiles_variant", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]),
     ("tips_schedule_shape", ctypes.c_int,
      [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), _c_i64_p]),
     ("tips_chunk_bounds", ctypes.c_int,

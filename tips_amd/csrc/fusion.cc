@@ -45,13 +45,14 @@ struct Bucket {
 
 struct Entry {
   uint64_t key = 0;
+  bool identity = false;  // one rank: only the out-of-place copies (dev[0..ntiles)), no buckets
   int dtype = 0;
   int64_t tile = 0;
   std::vector<const void*> ins;
   std::vector<void*> outs;
   std::vector<int64_t> counts;
   std::vector<Bucket> buckets;
-  std::vector<int> unfused;  // indices reduced on their own (at least a bucket in size)
+  std::vector<BatchItem> direct;  // runs reduced where they lie, without packing (see build_entry)
   CopyTile* dev = nullptr;   // descriptor table in HBM
   size_t ntiles = 0;
   uint64_t stamp = 0;        // last use (LRU)
@@ -102,17 +103,28 @@ void free_entry(State& st, Entry* e) {
 }
 
 // Build a tensor list's buckets and descriptors; upload the table on fuse_stream.
+//
+// Tensors that follow each other in memory with no gap - in both their inputs and their
+// outputs - form one run and are handled as one segment (a flat gradient buffer's views are one
+// run). A run is reduced where it lies, with no pack and no unpack, when it is a single tensor of
+// at least the threshold or several tensors of at least TIPS_FUSION_DIRECT_BYTES (4 MiB) together:
+// only its own bytes are touched, so nothing outside the tensors changes. Every other run is
+// packed into the current bucket at a 256-B aligned offset.
 int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, int n, int64_t threshold) {
   const int64_t es = tips::dtype_size(e->dtype), tile = e->tile;
+  const int64_t direct_min = std::min(threshold, std::max<int64_t>(kAlignBytes, env_i64("TIPS_FUSION_DIRECT_BYTES", 4 << 20)));
   std::vector<CopyTile> pack, unpack;
   std::vector<int64_t> sizes;  // per bucket
   std::vector<int64_t> first;  // per bucket: first tile index into pack / unpack
-  for (int i = 0; i < n; i++) {
-    const int64_t bytes = items[i].count * es;
-    if (bytes == 0) continue;
-    if (bytes >= threshold) {  // already bucket-sized: reduced on its own, no packing
-      e->unfused.push_back(i);
-      continue;
+  auto place = [&](const char* in, char* out, int64_t bytes, int members) {
+    if (e->identity) {  // one rank: in place nothing, out of place a copy
+      for (int64_t t = 0; in != out && t < bytes; t += tile)
+        pack.push_back(CopyTile{in + t, out + t, std::min(tile, bytes - t)});
+      return;
+    }
+    if (bytes >= threshold || (members > 1 && bytes >= direct_min)) {
+      e->direct.push_back(BatchItem{in, out, bytes / es});
+      return;
     }
     int64_t off = sizes.empty() ? 0 : round_up(sizes.back(), kAlignBytes);
     if (sizes.empty() || off + bytes > threshold) {
@@ -123,11 +135,32 @@ int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, in
     char* slot = (char*)st.fusion.p + (int64_t)((sizes.size() - 1) % 2) * threshold;
     for (int64_t t = 0; t < bytes; t += tile) {
       const int64_t tb = std::min(tile, bytes - t);
-      pack.push_back(CopyTile{(const char*)items[i].in + t, slot + off + t, tb});
-      unpack.push_back(CopyTile{slot + off + t, (char*)items[i].out + t, tb});
+      pack.push_back(CopyTile{in + t, slot + off + t, tb});
+      unpack.push_back(CopyTile{slot + off + t, out + t, tb});
     }
     sizes.back() = off + bytes;
+  };
+  const char* run_in = nullptr;
+  char* run_out = nullptr;
+  int64_t run_bytes = 0;
+  int members = 0;
+  for (int i = 0; i < n; i++) {
+    const int64_t bytes = items[i].count * es;
+    if (bytes == 0) continue;
+    const char* in = (const char*)items[i].in;
+    char* out = (char*)items[i].out;
+    if (members > 0 && in == run_in + run_bytes && out == run_out + run_bytes) {
+      run_bytes += bytes;
+      members++;
+      continue;
+    }
+    if (members > 0) place(run_in, run_out, run_bytes, members);
+    run_in = in;
+    run_out = out;
+    run_bytes = bytes;
+    members = 1;
   }
+  if (members > 0) place(run_in, run_out, run_bytes, members);
   const int64_t npack = (int64_t)pack.size();
   for (size_t b = 0; b < sizes.size(); b++) {
     const int64_t end = b + 1 < sizes.size() ? first[b + 1] : npack;
@@ -200,16 +233,23 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
   const int64_t threshold = fusion_threshold_bytes(), tile = copy_tile_bytes();
   const int64_t es = tips::dtype_size(dtype);
   TRY(ensure_slots(st, fc, threshold));
-  TRY(join(st.fuse_stream, user, st.ev_start));  // inputs ready; the bucket stream waits for it too
-  HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
-
-  const uint64_t key = key_of(items, n, dtype, tile);
+  // One rank: the allreduce of anything is the identity (as allreduce_device's), so a tensor
+  // reduced in place needs no work and one out of place a copy - no bucket. TIPS_FUSION_MEASURE_PACK=1
+  // keeps the buckets anyway, to measure on one GPU what packing costs a step at N > 1.
+  const bool identity = st.size == 1 && !env_i64("TIPS_FUSION_MEASURE_PACK", 0);
+  const uint64_t key = key_of(items, n, dtype, tile) ^ (identity ? 0x9e3779b97f4a7c15ull : 0);
   Entry* e = nullptr;
   for (Entry* c : fc.entries)
-    if (c->key == key && same_list(*c, items, n, dtype, tile)) {
+    if (c->key == key && c->identity == identity && same_list(*c, items, n, dtype, tile)) {
       e = c;
       break;
     }
+  if (e && identity && e->ntiles == 0) {  // every tensor in place: nothing to do
+    e->stamp = ++fc.clock;
+    return 0;
+  }
+  TRY(join(st.fuse_stream, user, st.ev_start));  // inputs ready (the bucket stream waits for it too)
+  if (st.size > 1) HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
   if (!e) {
     if (fc.entries.size() >= kMaxEntries) {  // evict the least recently used list
       auto lru = std::min_element(fc.entries.begin(), fc.entries.end(),
@@ -219,6 +259,7 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
     }
     e = new Entry();
     e->key = key;
+    e->identity = identity;
     e->dtype = dtype;
     e->tile = tile;
     for (int i = 0; i < n; i++) {
@@ -237,23 +278,32 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
 
   const int B = (int)e->buckets.size();
   auto pack = [&](int b) -> int {
-    HIP_TRY(tips::launch_copy_tiles(e->dev + e->buckets[b].pack0, (int)e->buckets[b].npack, st.fuse_stream));
+    HIP_TRY(tips::launch_pack_tiles(e->dev + e->buckets[b].pack0, (int)e->buckets[b].npack, e->tile, st.fuse_stream));
     return 0;
   };
   auto unpack = [&](int b) -> int {
-    HIP_TRY(tips::launch_copy_tiles(e->dev + e->buckets[b].unpack0, (int)e->buckets[b].npack, st.fuse_stream));
+    HIP_TRY(tips::launch_pack_tiles(e->dev + e->buckets[b].unpack0, (int)e->buckets[b].npack, e->tile, st.fuse_stream));
     return 0;
   };
-  if (st.size == 1) {  // the allreduce of a bucket is the identity: pack, unpack, in stream order
+  if (identity) {  // one rank: the out-of-place tensors' copies, one launch
+    if (e->ntiles) HIP_TRY(tips::launch_pack_tiles(e->dev, (int)e->ntiles, e->tile, st.fuse_stream));
+    TRY(join(user, st.fuse_stream, st.ev_done));
+    return 0;
+  }
+  if (st.size == 1) {  // TIPS_FUSION_MEASURE_PACK: pack, (identity), unpack, in stream order
     for (int b = 0; b < B; b++) {
       TRY(pack(b));
       TRY(unpack(b));
     }
-    for (int i : e->unfused) TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, st.fuse_stream));
+    for (const BatchItem& d : e->direct) TRY(allreduce_device(st, d.in, d.out, d.count, dtype, st.fuse_stream));
+    TRY(join(user, st.fuse_stream, st.ev_done));
+    return 0;
   } else {
-    // fuse stream:   pack(0) pack(1) | unpack(0) pack(2) | unpack(1) pack(3) | ... unpack(B-1)
-    // bucket stream: allreduce(b) after pack(b); unpack(b) after allreduce(b); pack(b+2) reuses
-    // slot b % 2 after unpack(b) in fuse-stream order
+    // bucket stream: the direct runs first (nothing to pack: their exchange starts at once and
+    //                overlaps pack(0)), then allreduce(b) after pack(b)
+    // fuse stream:   pack(0) pack(1) | unpack(0) pack(2) | unpack(1) pack(3) | ... unpack(B-1);
+    //                unpack(b) after allreduce(b); pack(b+2) reuses slot b % 2 after unpack(b)
+    for (const BatchItem& d : e->direct) TRY(allreduce_device(st, d.in, d.out, d.count, dtype, st.bucket_stream));
     TRY(st.fuse_ev.ensure(2 * (size_t)B));
     hipEvent_t* packed = st.fuse_ev.ev.data();
     hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
@@ -272,8 +322,6 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
         HIP_TRY(hipEventRecord(packed[b + 2], st.fuse_stream));
       }
     }
-    for (int i : e->unfused)
-      TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, st.bucket_stream));
   }
   TRY(join(user, st.fuse_stream, st.ev_done));
   TRY(join(user, st.bucket_stream, st.ev_comp_done));

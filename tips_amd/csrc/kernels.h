@@ -24,6 +24,15 @@ struct CopyTile {
 };
 constexpr int64_t kCopyTileBytes = 64 * 1024;
 hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t s);
+// The fusion pack / unpack launcher: copy_tiles_g_kernel, one tile of <= 16 KiB per workgroup
+// held in registers (nt loads, sc1 stores, 16-B vectors + bytewise tail): 0-9 % faster than
+// copy_tiles_kernel on the configs' tensor lists (tools/copy_sweep.py); larger tiles fall back.
+hipError_t launch_pack_tiles(const CopyTile* tiles_dev, int ntiles, int64_t max_tile_bytes, hipStream_t s);
+// Tuning sweep (tools/copy_sweep.py): 0 = the shipped kernel; 1-8 = copy_tiles_g_kernel with G
+// tiles per workgroup and load / store cache policies (kernels.hip); tiles of at most
+// max_tile_bytes (<= 16 KiB for variants 1-8).
+hipError_t launch_copy_tiles_variant(const CopyTile* tiles_dev, int ntiles, int variant, int64_t max_tile_bytes,
+                                     hipStream_t s);
 
 // Peer transfers of the xGMI peer schedule (peer.cc): up to kMaxXferSegs byte
 // segments {src, dst, bytes} copied by one launch, segments interleaved over

@@ -515,6 +515,42 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __re
   }
 }
 
+// Grouped variant (tuning sweep, tools/copy_sweep.py): each workgroup copies G consecutive tiles
+// of at most 256 x U x 16 B. The G descriptors are read up front (independent scalar loads, one
+// latency for all), then every lane issues its G x U 16-B loads before the first store, so one
+// workgroup keeps G tiles in flight and the descriptor latency is paid once per G tiles. A tile
+// whose ends are 16-B aligned moves its whole 16-B vectors through buffer ops (range = those
+// vectors, so lanes past them fall off) and its < 16 trailing bytes bytewise; a misaligned tile
+// goes bytewise whole.
+template <int G, int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __restrict__ tiles, int ntiles) {
+  const int64_t t0 = xcd_tile(blockIdx.x, gridDim.x) * G;
+  if (t0 >= ntiles) return;
+  const int tid = threadIdx.x;
+  CopyTile d[G];
+  int vec[G];  // bytes moved as 16-B vectors
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    d[g] = (t0 + g < ntiles) ? tiles[t0 + g] : CopyTile{nullptr, nullptr, 0};
+    const bool al = ((reinterpret_cast<uintptr_t>(d[g].src) | reinterpret_cast<uintptr_t>(d[g].dst)) & 15) == 0;
+    vec[g] = al ? (int)(d[g].bytes & ~(int64_t)15) : 0;
+  }
+  u32x4 v[G][U];
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)d[g].src, (short)0, vec[g], 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) v[g][u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, LAUX);
+  }
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(d[g].dst, (short)0, vec[g], 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(v[g][u], rd, (u * kBlock + tid) * 16, 0, SAUX);
+    for (int64_t i = vec[g] + tid; i < d[g].bytes; i += kBlock) d[g].dst[i] = d[g].src[i];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Peer transfer (xGMI peer schedule, peer.cc)
 
@@ -885,6 +921,48 @@ hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t 
   const unsigned grid = (unsigned)((ntiles + 7) / 8 * 8);
   hipLaunchKernelGGL(copy_tiles_kernel, dim3(grid), dim3(kBlock), 0, s, tiles_dev, ntiles);
   return hipGetLastError();
+}
+
+namespace {
+
+template <int G, int U, int LAUX, int SAUX>
+hipError_t run_copy_g(const CopyTile* tiles, int ntiles, hipStream_t s) {
+  const int64_t groups = (ntiles + G - 1) / G;
+  const unsigned grid = (unsigned)std::max<int64_t>(8, (groups + 7) / 8 * 8);
+  hipLaunchKernelGGL((copy_tiles_g_kernel<G, U, LAUX, SAUX>), dim3(grid), dim3(kBlock), 0, s, tiles, ntiles);
+  return hipGetLastError();
+}
+
+template <int U>
+hipError_t copy_variant_u(const CopyTile* tiles, int ntiles, int variant, hipStream_t s) {
+  switch (variant) {
+    case 1: return run_copy_g<1, U, 2, 16>(tiles, ntiles, s);
+    case 2: return run_copy_g<2, U, 2, 16>(tiles, ntiles, s);
+    case 3: return run_copy_g<4, U, 2, 16>(tiles, ntiles, s);
+    case 4: return run_copy_g<8, U, 2, 16>(tiles, ntiles, s);
+    case 5: return run_copy_g<2, U, 0, 16>(tiles, ntiles, s);  // plain loads
+    case 6: return run_copy_g<2, U, 2, 2>(tiles, ntiles, s);   // nt stores
+    case 7: return run_copy_g<2, U, 2, 0>(tiles, ntiles, s);   // plain stores
+    case 8: return run_copy_g<4, U, 0, 0>(tiles, ntiles, s);   // plain both
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_copy_tiles_variant(const CopyTile* tiles_dev, int ntiles, int variant, int64_t max_tile_bytes,
+                                     hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  if (variant == 0) return launch_copy_tiles(tiles_dev, ntiles, s);
+  if (max_tile_bytes <= 4096) return copy_variant_u<1>(tiles_dev, ntiles, variant, s);
+  if (max_tile_bytes <= 8192) return copy_variant_u<2>(tiles_dev, ntiles, variant, s);
+  if (max_tile_bytes <= 16384) return copy_variant_u<4>(tiles_dev, ntiles, variant, s);
+  return hipErrorInvalidValue;  // the grouped kernel holds a tile in registers: at most 16 KiB
+}
+
+hipError_t launch_pack_tiles(const CopyTile* tiles_dev, int ntiles, int64_t max_tile_bytes, hipStream_t s) {
+  if (max_tile_bytes > 16384) return launch_copy_tiles(tiles_dev, ntiles, s);
+  return launch_copy_tiles_variant(tiles_dev, ntiles, 1, max_tile_bytes, s);
 }
 
 hipError_t launch_xfer(const XferSeg* segs, int nseg, hipStream_t s) {

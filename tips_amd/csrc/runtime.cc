@@ -210,6 +210,14 @@ int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, 
   return 0;
 }
 
+int tips_copy_tiles_variant(const void* tiles, int ntiles, int variant, int64_t max_tile_bytes, void* stream) {
+  if (ntiles < 0 || (ntiles > 0 && !tiles) || max_tile_bytes < 1 || max_tile_bytes > tips::kCopyTileBytes)
+    return fail(TIPS_ERR_INVALID_ARG, "bad copy-tile arguments");
+  HIP_TRY(tips::launch_copy_tiles_variant((const tips::CopyTile*)tiles, ntiles, variant, max_tile_bytes,
+                                          (hipStream_t)stream));
+  return 0;
+}
+
 int tips_xfer(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, void* stream) {
   if (n < 0 || n > tips::kMaxXferSegs || (n > 0 && (!dsts || !srcs || !bytes)))
     return fail(TIPS_ERR_INVALID_ARG, "tips_xfer takes 0..%d segments", tips::kMaxXferSegs);

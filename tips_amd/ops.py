@@ -169,6 +169,39 @@ def fused_allreduce(tensor_list, out_list=None):
     return outs
 
 
+class FusedList(object):
+    """A list of device tensors reduced in place together, step after step (a model's gradients).
+
+    fused_allreduce_ validates every tensor and rebuilds the pointer arrays on each call; for a
+    list that keeps the same tensors (or a new tensor at the same address) that host work is
+    repeated for nothing, and for 1000 gradients it costs more than the pack + unpack kernels
+    themselves. This keeps the validated arrays and, per call, only re-reads the data pointers:
+    when they are unchanged the cached arrays go straight to tips_fused_allreduce.
+
+    `counts` fixes the element count of each position (a parameter's gradient always has the
+    parameter's shape, which torch enforces on assignment); a list whose counts differ is refused."""
+
+    def __init__(self, counts):
+        self._counts = [int(c) for c in counts]
+        self._ptrs = None
+        self._arrays = None
+        self._cp = _lib.i64_array(self._counts)
+
+    def allreduce_(self, tensor_list):
+        if not tensor_list:
+            return tensor_list
+        ptrs = [t.data_ptr() for t in tensor_list]
+        if ptrs != self._ptrs:
+            basics.init()
+            code = _check_fusable(tensor_list, "fused_allreduce_")
+            if [t.numel() for t in tensor_list] != self._counts:
+                raise ValueError("FusedList: the tensors' element counts changed")
+            self._ptrs, self._arrays = ptrs, (code,) + _lib.ptr_array(ptrs)
+        code, pp = self._arrays[0], self._arrays[1]
+        _lib.call("tips_fused_allreduce", pp, self._cp[0], len(ptrs), code, tensors.stream_of(tensor_list[0]))
+        return tensor_list
+
+
 def _check_fusable(tensor_list, what):
     code = tensors.dtype_code(tensor_list[0])
     for t in tensor_list:

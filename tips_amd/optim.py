@@ -36,6 +36,9 @@ class _DistributedOptimizer(object):
         self._average_aggregated = average_aggregated_gradients
         self._groups = groups
         self._calls = 0
+        self._fused = {}  # (dtype, device, parameter ids) -> (ops.FusedList, flat buffer, offsets)
+        import os
+        self._bucket_view = os.environ.get("TIPS_GRAD_BUCKET_VIEW", "1") != "0"
         if self._passes < 1:
             raise ValueError("backward_passes_per_step must be >= 1")
 
@@ -67,7 +70,8 @@ class _DistributedOptimizer(object):
         fusion buckets (tips_fused_allreduce: pack, one allreduce per bucket, unpack straight
         back into .grad - 4 x the gradient bytes of HBM traffic, no copies). The others go
         through allreduce_grads and are replaced by its outputs."""
-        from . import Compression, _fusable, allreduce_grads, fused_allreduce_, size
+        from . import Compression, _fusable, allreduce_grads, size
+        from .ops import FusedList
         params = self._params_with_grad()
         if self._passes > 1 and self._average_aggregated:
             for p in params:
@@ -79,11 +83,42 @@ class _DistributedOptimizer(object):
             g = p.grad
             if (self._compression is Compression.none and _fusable(g) and g.is_contiguous()
                     and not self._sparse_as_dense):
-                inplace.setdefault(g.dtype, []).append(g)
+                inplace.setdefault((g.dtype, g.device), []).append(p)
             else:
                 rest.append(p)
-        for group in inplace.values():
-            fused_allreduce_(group)
+        for (dt, dev), group in inplace.items():
+            # one FusedList per (dtype, device, parameter list): validated arrays reused while the
+            # .grad tensors stay where they are (ops.FusedList)
+            key = (dt, dev, tuple(id(p) for p in group))
+            ent = self._fused.get(key)
+            if ent is None:
+                if len(self._fused) > 8:
+                    self._fused.clear()
+                numels = [p.numel() for p in group]
+                flat, offs = None, []
+                if self._bucket_view:
+                    import torch
+                    flat = torch.empty(sum(numels), dtype=dt, device=dev)
+                    o = 0
+                    for n in numels:
+                        offs.append(o)
+                        o += n
+                ent = self._fused[key] = (FusedList(numels), flat, offs)
+            fl, flat, offs = ent
+            if flat is not None:
+                # Gradient bucket views: every .grad becomes a view of one flat buffer, back to back,
+                # so the fused allreduce finds ONE contiguous run and reduces it where it lies - no
+                # pack, no unpack (fusion.cc build_entry). A .grad that is not (or no longer) its
+                # view - the first step, or after zero_grad(set_to_none=True) - is copied in once;
+                # with set_to_none=False autograd accumulates straight into the views.
+                base, es = flat.data_ptr(), flat.element_size()
+                for p, o in zip(group, offs):
+                    g = p.grad
+                    if g.data_ptr() != base + o * es:
+                        v = flat[o:o + g.numel()].view_as(g)
+                        v.copy_(g)
+                        p.grad = v
+            fl.allreduce_([p.grad for p in group])
         if rest:
             reduced = allreduce_grads([p.grad for p in rest], compression=self._compression, op=self._op,
                                       sparse_as_dense=self._sparse_as_dense)
