@@ -47,8 +47,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--algo", default=os.environ.get("TIPS_ALGO", "auto"),
-                    choices=["auto", "ring", "direct", "rccl", "oneshot", "peer"])
+    ap.add_argument("--algo", default=os.environ.get("TIPS_ALGO", "tune"),
+                    choices=["auto", "ring", "direct", "rccl", "oneshot", "peer", "tune"],
+                    help="N>1 schedule; tune (default): the library times ring / direct at several pipeline "
+                         "depths on the first call of a size class and keeps the fastest (TIPS_ALGO_TUNE)")
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
@@ -527,7 +529,7 @@ def bench_allreduce(args):
     tips_amd.init()  # unique id through the gloo group, one RCCL communicator per GPU
     L = _lib.lib()
     algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL,
-                  "oneshot": _lib.ALGO_ONESHOT, "peer": _lib.ALGO_PEER}
+                  "oneshot": _lib.ALGO_ONESHOT, "peer": _lib.ALGO_PEER, "tune": _lib.ALGO_TUNE}
     inv = {v: k for k, v in algo_names.items()}
     _lib.call("tips_set_algorithm", algo_names[args.algo])
 
@@ -651,13 +653,21 @@ def bench_allreduce(args):
             torch.cuda.synchronize()
             break
         except _lib.TipsError as e:
-            nxt = {_lib.ALGO_DIRECT: _lib.ALGO_RING, _lib.ALGO_PEER: _lib.ALGO_DIRECT,
+            nxt = {_lib.ALGO_DIRECT: _lib.ALGO_RING, _lib.ALGO_PEER: _lib.ALGO_DIRECT, _lib.ALGO_TUNE: _lib.ALGO_DIRECT,
                    _lib.ALGO_ONESHOT: _lib.ALGO_RING, _lib.ALGO_RING: _lib.ALGO_RCCL}.get(algo)
             if workload == "negotiated1000" or nxt is None:
                 raise
             fallbacks.append({"algorithm": inv.get(algo, str(algo)), "error": str(e)})
             algo = nxt
             _lib.call("tips_set_algorithm", algo)
+    tuned = None
+    if algo == _lib.ALGO_TUNE:  # the warm-up measured the schedules; report (and check) the one kept
+        import ctypes
+        ta, td = ctypes.c_int(), ctypes.c_int()
+        qbytes = sizes[0] * 4 if workload == "bucket" else max(sizes) * 4 if workload == "negotiated1000" else 64 << 20
+        if L.tips_tuned_choice(qbytes, ctypes.byref(ta), ctypes.byref(td)) == 1:
+            tuned = {"algorithm": inv.get(ta.value, str(ta.value)), "pipeline_depth": td.value}
+            algo = ta.value
     host_t.update(enqueue=0.0, wait=0.0)
     t = timed(steps)
     host_split = dict(host_t)
@@ -729,7 +739,7 @@ def bench_allreduce(args):
 
     algbw = total_elems * 4 / (ms / 1e3)  # bytes/s per rank
     busbw = algbw * 2 * (world - 1) / world
-    links = 1 if algo == _lib.ALGO_RING else world - 1
+    links = 1 if algo == _lib.ALGO_RING else max(1, world - 1)
     line = {
         "metric": METRIC, "value": round(world * total_elems * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
         "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4),
@@ -737,6 +747,7 @@ def bench_allreduce(args):
         "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % seed0,
         "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
                    "algorithm": inv.get(algo, str(algo)) if world > 1 else "none (1 rank)",
+                   "selection": ("TIPS_ALGO_TUNE: measured on the first call, kept: %s" % tuned) if tuned else args.algo,
                    "rotating_sets": rot,
                    "fusion_one_rank": ("TIPS_FUSION_MEASURE_PACK=1: buckets packed and unpacked as at N > 1 (the "
                                        "default one-rank path does no bucket work)") if measure_pack else None,

@@ -74,6 +74,11 @@ enum tips_algorithm {
                             Host-synchronous: a device-pointer call under PEER returns only after its push and
                             fold have run on every rank (each phase ends in a stream synchronize + barrier); only
                             the final pull is left queued on the caller's stream. */
+  TIPS_ALGO_TUNE = 5,    /* measured choice: on the first call of each bucket-size class (a power of two), every
+                            rank times ring and direct at several pipeline depths on scratch copies of the call's
+                            input, the ranks agree on the slowest rank's times (one small ncclAllReduce MAX) and
+                            all keep the fastest for that class; small buckets take AUTO's one-shot. The peer
+                            schedule joins the candidates with TIPS_TUNE_PEER=1. tips_tuned_choice reports it. */
 };
 
 /* ---- lifecycle: same names and types as tips/core/operations.h:7-21 ---- */
@@ -249,6 +254,10 @@ TIPS_API int tips_set_algorithm(int algo);
 TIPS_API int tips_get_algorithm(void);
 /* The algorithm the current selection resolves to for a bucket of `bytes` on `nranks`. */
 TIPS_API int tips_resolve_algorithm(int nranks, int64_t bytes);
+/* Under TIPS_ALGO_TUNE: the schedule and pipeline depth this job measured for buckets of
+ * `bytes`' size class. Returns 1 (and fills algo / depth) once that class has been tuned,
+ * 0 before; < 0 on error. */
+TIPS_API int tips_tuned_choice(int64_t bytes, int* algo, int* depth);
 
 /* ---- single-GPU harnesses (tests and benchmarks) ---- */
 

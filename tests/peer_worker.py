@@ -24,7 +24,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
-ALGO_NAMES = {"ring": 0, "direct": 1, "rccl": 2, "oneshot": 3, "peer": 4, "auto": -1}
+ALGO_NAMES = {"ring": 0, "direct": 1, "rccl": 2, "oneshot": 3, "peer": 4, "auto": -1, "tune": 5}
 JOB_ALGO = ALGO_NAMES["peer"]  # the job's schedule (main sets it from TIPS_WORKER_ALGO)
 
 
@@ -407,6 +407,14 @@ def main():
             rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, sp)
         torch.cuda.synchronize()
         res = {"case": c, "rc": int(rc)}
+        if rc == 0 and case_algo == ALGO_NAMES["tune"]:  # the bits of whichever schedule the job measured fastest
+            ta, td = ctypes.c_int(), ctypes.c_int()
+            if L.tips_tuned_choice(n * x.itemsize if c.get("host") else n * x.element_size(), ctypes.byref(ta),
+                                   ctypes.byref(td)) == 1:
+                case_algo = ta.value
+                res["tuned"] = [ta.value, td.value]
+            elif n * (x.itemsize if c.get("host") else x.element_size()) <= (256 << 10):
+                case_algo = ALGO_NAMES["oneshot"]
         if rc == 0:
             exp = expected(ins, dtype, c.get("expect_algo", case_algo))
             got = y if c.get("host") else from_dev(y, dtype)

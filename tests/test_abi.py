@@ -82,7 +82,10 @@ def test_algorithm_resolution():
     assert L.tips_resolve_algorithm(32, small) == _lib.ALGO_RING  # more ranks than the fold takes sources
     L.tips_set_algorithm(_lib.ALGO_RING)
     assert L.tips_resolve_algorithm(8, small) == _lib.ALGO_RING
-    assert L.tips_set_algorithm(5) == -1
+    L.tips_set_algorithm(_lib.ALGO_TUNE)  # measured per size class; small buckets stay one-shots
+    assert L.tips_resolve_algorithm(8, big) == _lib.ALGO_TUNE
+    assert L.tips_resolve_algorithm(8, small) == _lib.ALGO_ONESHOT
+    assert L.tips_set_algorithm(6) == -1
     L.tips_set_algorithm(prev)
 
 

@@ -78,3 +78,19 @@ def test_fusion_workloads_over_rccl(gpu, workload, p):
     out of place, allreduce_grads and DistributedOptimizer.step(), bit-exact against the fold."""
     cases = [{"fused": workload, "seed": 4, "mode": m} for m in ("inplace", "inplace_separate", "oop", "grads", "optimizer")]
     check(run_job(p, cases, timeout=600, **rccl_env("auto")))
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_tuned_schedule_across_processes(gpu, p):
+    """TIPS_ALGO=tune over real RCCL ranks: the first call of each size class times ring and
+    direct at several pipeline depths on scratch copies, the ranks agree on one choice, and every
+    call (in place too: the tuning never touches the caller's buffers) gives the bits of the chosen
+    schedule; small buckets take the one-shot."""
+    cases = [{"dtype": F32, "n": 3 << 20, "seed": 1}, {"dtype": F32, "n": (3 << 20) + 5, "seed": 2, "inplace": True},
+             {"dtype": BF16, "n": 1 << 20, "seed": 3}, {"dtype": I64, "n": 1000, "seed": 4},
+             {"dtype": F32, "n": 3 << 20, "seed": 5}]
+    results = run_job(p, cases, **rccl_env("tune"))
+    check(results)
+    picks = [tuple(c.get("tuned", ())) for c in results[0]["results"]]
+    for res in results[1:]:
+        assert [tuple(c.get("tuned", ())) for c in res["results"]] == picks, "ranks disagree on the tuned schedule"

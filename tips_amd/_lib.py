@@ -19,7 +19,7 @@ OP_SUM, OP_MAX, OP_MIN = 0, 1, 2
 REQ_ALLREDUCE, REQ_ALLGATHER, REQ_BROADCAST = 0, 1, 2
 MAX_DIMS = 8
 REQUEST_WORDS = 3 + MAX_DIMS
-ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_ONESHOT, ALGO_PEER = -1, 0, 1, 2, 3, 4
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_RCCL, ALGO_ONESHOT, ALGO_PEER, ALGO_TUNE = -1, 0, 1, 2, 3, 4, 5
 
 STATUS_NAMES = {
     0: "TIPS_OK",
@@ -101,6 +101,7 @@ _SIGNATURES = [
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),
     ("tips_get_algorithm", ctypes.c_int, []),
     ("tips_resolve_algorithm", ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),
+    ("tips_tuned_choice", ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     ("tips_ring_simulate", ctypes.c_int,
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_oneshot_simulate", ctypes.c_int,

@@ -116,6 +116,22 @@ int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, in
   std::vector<CopyTile> pack, unpack;
   std::vector<int64_t> sizes;  // per bucket
   std::vector<int64_t> first;  // per bucket: first tile index into pack / unpack
+  // Balanced buckets: B = the fewest buckets of at most `threshold` that hold the packed bytes,
+  // at least 2 once there are 32 MiB (so pack(1) overlaps the exchange of bucket 0), filled up to
+  // total / B each instead of greedily to the threshold. A greedy split of config 4 leaves a
+  // 15 MiB tail bucket (a launch that small ramps up and drains at 4.3 TB/s) and exposes a
+  // full 64 MiB pack before the first exchange.
+  int64_t target = threshold;
+  if (!e->identity) {
+    int64_t packed = 0;  // upper bound of the packed bytes: every tensor below the threshold
+    for (int i = 0; i < n; i++) {
+      const int64_t b = items[i].count * es;
+      if (b < threshold) packed += round_up(b, kAlignBytes);
+    }
+    int64_t nb = (packed + threshold - 1) / threshold;
+    if (nb < 2 && packed >= (32 << 20) && env_i64("TIPS_FUSION_BALANCE", 1)) nb = 2;
+    if (nb > 1 && env_i64("TIPS_FUSION_BALANCE", 1)) target = std::min(threshold, round_up((packed + nb - 1) / nb, kAlignBytes));
+  }
   auto place = [&](const char* in, char* out, int64_t bytes, int members) {
     if (e->identity) {  // one rank: in place nothing, out of place a copy
       for (int64_t t = 0; in != out && t < bytes; t += tile)
@@ -127,7 +143,8 @@ int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, in
       return;
     }
     int64_t off = sizes.empty() ? 0 : round_up(sizes.back(), kAlignBytes);
-    if (sizes.empty() || off + bytes > threshold) {
+    // a new bucket when this one would pass the threshold, or has reached its balanced share
+    if (sizes.empty() || off + bytes > threshold || off >= target) {
       sizes.push_back(0);
       first.push_back((int64_t)pack.size());
       off = 0;

@@ -8,8 +8,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -146,6 +148,8 @@ struct State {
   uint64_t peer_key = 0;      // names the node-local control block of the peer schedule (hash of the unique id)
   PeerState* peer = nullptr;  // peer schedule: IPC workspaces + shared-memory barrier, created on first use
   FusionCache* fusion_cache = nullptr;  // created on first use
+  // TIPS_ALGO_TUNE: (ranks, dtype, size class) -> (schedule, pipeline depth), the same on every rank
+  std::map<std::tuple<int, int, int>, std::pair<int, int>> tuned;
 };
 
 State& S();

@@ -102,7 +102,12 @@ int resolve_algo(int algo, int p, int64_t bytes) {
       if (!strcmp(e, "rccl")) algo = TIPS_ALGO_RCCL;
       if (!strcmp(e, "oneshot")) algo = TIPS_ALGO_ONESHOT;
       if (!strcmp(e, "peer")) algo = TIPS_ALGO_PEER;
+      if (!strcmp(e, "tune")) algo = TIPS_ALGO_TUNE;
     }
+  }
+  if (algo == TIPS_ALGO_TUNE) {  // measured per size class; small buckets stay latency-bound one-shots
+    if (p > 1 && p <= tips::kMaxSrcs && bytes <= env_i64("TIPS_ONESHOT_BYTES", 256 << 10)) return TIPS_ALGO_ONESHOT;
+    return TIPS_ALGO_TUNE;
   }
   if (algo != TIPS_ALGO_AUTO) return algo;
   // small buckets: one exchange + one kernel beats 2(p-1) pipelined steps (latency-bound);

@@ -120,6 +120,7 @@ void tips_shutdown(void) {
     }
   st.fusion.release();
   st.small.release();
+  st.tuned.clear();
   st.recv_ev.release();
   st.sum_ev.release();
   for (hipEvent_t* e : {&st.ev_start, &st.ev_done, &st.ev_comp_done, &st.ev_comp_prev})
@@ -156,7 +157,7 @@ int tips_size(void) { return S().initialized ? S().size : -1; }
 int tips_rank(void) { return S().initialized ? S().rank : -1; }
 
 int tips_set_algorithm(int algo) {
-  if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_PEER) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
+  if (algo < TIPS_ALGO_AUTO || algo > TIPS_ALGO_TUNE) return fail(TIPS_ERR_INVALID_ARG, "bad algorithm %d", algo);
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   st.algo = algo;

@@ -87,10 +87,100 @@ int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t u
   return epilogue(st, user);
 }
 
-int plan_allreduce(State& st, int algo, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
+int plan_allreduce(State& st, int algo, const char* in, char* out, int64_t n, int dtype, hipStream_t user,
+                   int depth = 0) {
   Plan pl;
-  TRY(build_schedule_plan(algo, st.size, st.rank, n, dtype, plan_depth(st.size, n, dtype), &pl));
+  TRY(build_schedule_plan(algo, st.size, st.rank, n, dtype, depth > 0 ? depth : plan_depth(st.size, n, dtype), &pl));
   return run_plan(st, pl, in, out, user);
+}
+
+// ---------------------------------------------------------------------------
+// TIPS_ALGO_TUNE: the schedule chosen by measurement, per (ranks, dtype, size class).
+
+int size_class(int64_t bytes) {
+  int c = 0;
+  while (c < 62 && (int64_t(1) << c) < bytes) c++;
+  return c;  // ceil(log2(bytes))
+}
+
+int run_choice(State& st, std::pair<int, int> c, const char* in, char* out, int64_t n, int dtype, hipStream_t s) {
+  if (c.first == TIPS_ALGO_PEER) return peer_allreduce(st, in, out, n, dtype, s);
+  return plan_allreduce(st, c.first, in, out, n, dtype, s, c.second);
+}
+
+// Every rank runs the same candidates in the same order (collectives), on scratch copies of the
+// call's input (the caller's buffers are not touched: in-place calls stay correct), times each with
+// events on `user` (best of 2 after a warm-up), and the ranks agree on the slowest rank's time per
+// candidate with one small ncclAllReduce(MAX): every rank then keeps the same fastest candidate.
+int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, std::pair<int, int>* best) {
+  const int p = st.size;
+  const int64_t bytes = n * tips::dtype_size(dtype);
+  const int K = plan_depth(p, n, dtype);
+  std::vector<std::pair<int, int>> cand;
+  if (p <= tips::kMaxSrcs) {
+    cand.push_back({TIPS_ALGO_DIRECT, K});
+    cand.push_back({TIPS_ALGO_DIRECT, 1});
+    if (K < 16) cand.push_back({TIPS_ALGO_DIRECT, std::min(16, 2 * K)});
+  }
+  cand.push_back({TIPS_ALGO_RING, K});
+  if (K < 16) cand.push_back({TIPS_ALGO_RING, std::min(16, 2 * K)});
+  if (p <= tips::kMaxSrcs && env_i64("TIPS_TUNE_PEER", 0)) cand.push_back({TIPS_ALGO_PEER, 0});
+  HIP_TRY(hipStreamSynchronize(user));
+  void *sin = nullptr, *sout = nullptr;
+  HIP_TRY(hipMalloc(&sin, (size_t)bytes));
+  int rc = 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<double> ms(cand.size(), 1e30);
+  do {
+    if (hipMalloc(&sout, (size_t)bytes) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess || hipMemcpyAsync(sin, in, (size_t)bytes, hipMemcpyDeviceToDevice, user) != hipSuccess) {
+      rc = fail(TIPS_ERR_HIP, "tune: scratch setup failed");
+      break;
+    }
+    for (size_t c = 0; c < cand.size() && rc == 0; c++) {
+      for (int it = 0; it < 3 && rc == 0; it++) {
+        if (it > 0 && hipEventRecord(e0, user) != hipSuccess) rc = fail(TIPS_ERR_HIP, "tune: event");
+        if (rc == 0) rc = run_choice(st, cand[c], (const char*)sin, (char*)sout, n, dtype, user);
+        if (rc == 0 && it > 0) {
+          float t = 0;
+          if (hipEventRecord(e1, user) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+              hipEventElapsedTime(&t, e0, e1) != hipSuccess)
+            rc = fail(TIPS_ERR_HIP, "tune: timing");
+          ms[c] = std::min(ms[c], (double)t);
+        }
+      }
+    }
+    if (rc) break;
+    // the slowest rank's time per candidate, on every rank
+    double* d = nullptr;
+    if (hipMalloc(&d, sizeof(double) * cand.size()) != hipSuccess) {
+      rc = fail(TIPS_ERR_HIP, "tune: hipMalloc");
+      break;
+    }
+    const size_t nb = sizeof(double) * cand.size();
+    if (hipMemcpyAsync(d, ms.data(), nb, hipMemcpyHostToDevice, st.comm_stream) != hipSuccess ||
+        ncclAllReduce(d, d, cand.size(), ncclFloat64, ncclMax, st.comm, st.comm_stream) != ncclSuccess ||
+        hipMemcpyAsync(ms.data(), d, nb, hipMemcpyDeviceToHost, st.comm_stream) != hipSuccess ||
+        hipStreamSynchronize(st.comm_stream) != hipSuccess)
+      rc = fail(TIPS_ERR_RCCL, "tune: agreeing on the timings failed");
+    (void)hipFree(d);
+  } while (0);
+  HIP_TRY(hipStreamSynchronize(user));
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(sin);
+  if (sout) (void)hipFree(sout);
+  if (rc) return rc;
+  size_t b = 0;
+  for (size_t c = 1; c < cand.size(); c++)
+    if (ms[c] < ms[b]) b = c;
+  *best = cand[b];
+  if (getenv("TIPS_VERBOSE") && st.rank == 0) {
+    fprintf(stderr, "[tips] tune p=%d bytes=%lld:", p, (long long)bytes);
+    for (size_t c = 0; c < cand.size(); c++) fprintf(stderr, " algo%d/K%d=%.3fms", cand[c].first, cand[c].second, ms[c]);
+    fprintf(stderr, " -> algo%d/K%d\n", best->first, best->second);
+  }
+  return 0;
 }
 
 }  // namespace
@@ -112,6 +202,16 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
   if (algo == TIPS_ALGO_PEER && st.size <= tips::kMaxSrcs)
     return peer_allreduce(st, (const char*)in, (char*)out, n, dtype, stream);
   TRY(ensure_comm(st));  // every other schedule moves its bytes over RCCL (no half-built group on failure)
+  if (algo == TIPS_ALGO_TUNE) {
+    const auto key = std::make_tuple(st.size, dtype, size_class(n * es));
+    auto it = st.tuned.find(key);
+    if (it == st.tuned.end()) {
+      std::pair<int, int> best;
+      TRY(tune(st, (const char*)in, n, dtype, stream, &best));
+      it = st.tuned.emplace(key, best).first;
+    }
+    return run_choice(st, it->second, (const char*)in, (char*)out, n, dtype, stream);
+  }
   int a = algo;
   if (st.size > tips::kMaxSrcs && (a == TIPS_ALGO_DIRECT || a == TIPS_ALGO_ONESHOT || a == TIPS_ALGO_PEER))
     a = TIPS_ALGO_RING;
@@ -278,6 +378,19 @@ int tips_schedule_shape(int64_t count, int p, int dtype, int* depth, int64_t* su
   const Range c0 = chunk_of(count, p, align, 0);
   *depth = pipeline_depth(c0.len() * es);
   *sub_elems = sub_of(c0, *depth, align, 0).len();
+  return 0;
+}
+
+int tips_tuned_choice(int64_t bytes, int* algo, int* depth) {
+  if (bytes < 0 || !algo || !depth) return fail(TIPS_ERR_INVALID_ARG, "bad tuned-choice query");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  for (const auto& kv : st.tuned)  // any dtype of this job's size class
+    if (std::get<0>(kv.first) == st.size && std::get<2>(kv.first) == size_class(bytes)) {
+      *algo = kv.second.first;
+      *depth = kv.second.second;
+      return 1;
+    }
   return 0;
 }
 
