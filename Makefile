@@ -10,7 +10,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals
 
 CRASH    := tools/lib/libcrashline.so
 
-all: $(LIB) $(CRASH) oracle
+REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe
+
+all: $(LIB) $(CRASH) $(REPRO) oracle
 
 # bench.py's last-words hook (not part of the product library)
 $(CRASH): tools/crash_line.c
@@ -27,6 +29,17 @@ build/obj/%.o: tips_amd/csrc/% $(HDRS)
 $(LIB): $(OBJS)
 	@mkdir -p tips_amd/lib
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -lrccl
+
+# replayed-plan checks through the C-ABI on /opt/rocm's runtime (tests/test_gpu_graphs.py)
+tools/_bin/graph_repro: tools/graph_repro.cc $(LIB) include/tips_hip.h
+	@mkdir -p tools/_bin
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Iinclude -o $@ $< -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib'
+
+tools/_bin/graph_probe: tools/graph_probe.cc
+	@mkdir -p tools/_bin
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -o $@ $< -lrccl
+
+repro: $(REPRO)
 
 oracle:
 	$(MAKE) -C oracle
@@ -47,7 +60,7 @@ tools/sum_sweep: tools/sum_sweep.cc $(LIB)
 
 clean:
 	rm -rf build/obj
-	rm -f $(LIB) tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
+	rm -f $(LIB) $(REPRO) tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle tools clean
+.PHONY: all oracle tools repro clean

@@ -258,6 +258,14 @@ TIPS_API int tips_resolve_algorithm(int nranks, int64_t bytes);
  * `bytes`' size class. Returns 1 (and fills algo / depth) once that class has been tuned,
  * 0 before; < 0 on error. */
 TIPS_API int tips_tuned_choice(int64_t bytes, int* algo, int* depth);
+/* Replayed plans (TIPS_GRAPHS): a ring / direct / one-shot call of at most TIPS_GRAPH_MAX_BYTES
+ * (64 MiB) made again on the same buffers (same addresses and allocations) is captured once into a
+ * HIP graph and replayed with one launch; streams, events and results are those of the eager
+ * steps. Off by default; TIPS_GRAPHS=1 turns it on where the loaded HIP runtime and RCCL are
+ * ROCm >= 7.2 (RCCL >= 2.27). Reports this process's captures, replays and cached graphs.
+ * Returns 0 (graphs on), 1 (a failed capture turned them off for the job), 2 (off: not asked
+ * for, or an older runtime), < 0 on error. */
+TIPS_API int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached);
 
 /* ---- single-GPU harnesses (tests and benchmarks) ---- */
 

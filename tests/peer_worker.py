@@ -299,6 +299,56 @@ def fused_case(c, rank, size, L, _lib, sp):
     return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": not bad, "error": "; ".join(bad)}
 
 
+def graphs_case(c, rank, size, L, _lib, sp):
+    """The call pattern TIPS_GRAPHS replays: the same buffers reduced round after round with new
+    data in them. Buffers under the replay limit (captured on their second call, replayed from the
+    third) interleave with one over it (always eager), in place and out of place, one of them called
+    from a second stream; after round 3 one buffer pair is freed and the allocator emptied, so
+    its successor is a new allocation (possibly at the same address: a new graph key). Every
+    result is checked bit-exact against the schedule's oracle; reports capture / replay counts."""
+    import ctypes
+    import numpy as np
+    import torch
+    from gpu_util import from_dev, rand, same_bits, to_dev
+    s2 = torch.cuda.Stream()
+    specs = c["bufs"]  # [[dtype, n, inplace, second_stream], ...]
+    bufs = []
+    for dtype, n, inplace, _ in specs:
+        x = to_dev(rand(dtype, n, np.random.default_rng(0)))
+        bufs.append((x, x if inplace else torch.empty_like(x)))
+    bad = []
+    for rnd in range(c.get("rounds", 6)):
+        if rnd == 3:
+            dtype, n, inplace, _ = specs[0]
+            del bufs[0]
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            x = to_dev(rand(dtype, n, np.random.default_rng(1)))
+            bufs.insert(0, (x, x if inplace else torch.empty_like(x)))
+        for i, (dtype, n, inplace, second) in enumerate(specs):
+            x, y = bufs[i]
+            ins = [rand(dtype, n, np.random.default_rng(c["seed"] + 1000 * rnd + 100 * i + r)) for r in range(size)]
+            x.copy_(to_dev(ins[rank]))
+            if second:
+                s2.wait_stream(torch.cuda.current_stream())
+                stream = s2.cuda_stream
+            else:
+                stream = sp
+            rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, stream)
+            if second:
+                torch.cuda.current_stream().wait_stream(s2)
+            if rc != 0:
+                bad.append("round %d buf %d rc %d %s" % (rnd, i, rc, _lib.last_error()))
+                continue
+            if not same_bits(from_dev(y, dtype), expected(ins, dtype, JOB_ALGO), dtype):
+                bad.append("round %d buf %d (dtype %d, n %d) differs" % (rnd, i, dtype, n))
+    torch.cuda.synchronize()
+    cap, rep, cached = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    off = L.tips_graph_stats(ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(cached))
+    return {"case": {"graphs": len(specs)}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5]),
+            "captured": cap.value, "replayed": rep.value, "cached": cached.value, "graphs_off": off}
+
+
 def golden_case(c, rank, size, L, _lib, sp):
     """A committed golden vector (tests/golden: inputs and the reference's MPI_Allreduce output
     under MPICH) through the real multi-process product path: rank r reduces inputs[r]; the
@@ -383,6 +433,9 @@ def main():
             continue
         if c.get("golden"):
             results.append(golden_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("bufs"):
+            results.append(graphs_case(c, rank, size, L, _lib, sp))
             continue
         if c.get("collectives"):
             results.append(collectives_case(c, rank, size, L, _lib, sp))

@@ -82,8 +82,11 @@ def _ranges_overlap(a, b):
     return a[0] < b[1] and b[0] < a[1]
 
 
-def hazards(plan, es, nbytes, inplace=False):
-    """Happens-before check of one rank's plan over two calls from different user streams.
+def hazards(plan, es, nbytes, inplace=False, modes=("eager", "eager"), replay_joins=True):
+    """Happens-before check of one rank's plan over back-to-back calls from alternating user
+    streams, each call eager (schedules.cc prologue / steps / epilogue) or a replay of the captured
+    plan (TIPS_GRAPHS: a graph launched on graph_stream, its nodes on streams of their own, ordered
+    only by the graph's edges and by graph_stream's order).
     Returns a list of race descriptions (empty = race-free). nbytes = bucket bytes."""
     ops = []     # (stream, accesses) ; accesses = [(buffer_id, lo, hi, is_write)]
     preds = []   # explicit cross-stream predecessors (event waits) per op
@@ -114,33 +117,61 @@ def hazards(plan, es, nbytes, inplace=False):
             return ("io", call)
         return ("in" if buf == IN else "out", call)
 
-    ends = []
-    for call, user in ((0, "U0"), (1, "U1")):
-        add(user, [(buf_id(call, IN), 0, nbytes, True)] + ([] if inplace else [(buf_id(call, OUT), 0, nbytes, True)]))
-        ev_start = record(user)
-        wait("C", ev_start)
-        ev_prev = record("P")
-        wait("C", ev_prev)
-        wait("P", ev_start)
+    def steps(call, C, P):
         sum_ev = {}
         for i, s in enumerate(plan["steps"]):
             if s["wait_sum"] >= 0 and s["wait_sum"] in sum_ev:
-                wait("C", sum_ev[s["wait_sum"]])
+                wait(C, sum_ev[s["wait_sum"]])
             if s["xfers"]:
                 acc = [(buf_id(call, x["buf"]), x["off"], x["off"] + x["bytes"], not x["send"]) for x in s["xfers"]]
-                add("C", acc)
+                add(C, acc)
             if s["sums"]:
-                rev = record("C")
-                wait("P", rev)
+                rev = record(C)
+                wait(P, rev)
                 for u in s["sums"]:
                     acc = [(buf_id(call, u["dst"][0]), u["dst"][1], u["dst"][1] + u["count"] * es, True)]
                     acc += [(buf_id(call, b), o, o + u["count"] * es, False) for b, o in u["srcs"]]
-                    add("P", acc)
-                sum_ev[i] = record("P")
-        e1 = record("C")
-        wait(user, e1)
-        e2 = record("P")
-        wait(user, e2)
+                    add(P, acc)
+                sum_ev[i] = record(P)
+
+    ends = []
+    graph_pending = eager_pending = False
+    for call, mode in enumerate(modes):
+        user = "U%d" % (call % 2)
+        add(user, [(buf_id(call, IN), 0, nbytes, True)] + ([] if inplace else [(buf_id(call, OUT), 0, nbytes, True)]))
+        if mode == "eager":
+            if graph_pending:  # order_after_replays
+                ev = record("G")
+                wait("C", ev)
+                wait("P", ev)
+                graph_pending = False
+            ev_start = record(user)
+            wait("C", ev_start)
+            ev_prev = record("P")
+            wait("C", ev_prev)
+            wait("P", ev_start)
+            eager_pending = True
+            steps(call, "C", "P")
+            e1 = record("C")
+            wait(user, e1)
+            e2 = record("P")
+            wait(user, e2)
+        else:  # replay
+            wait("G", record(user))
+            if eager_pending and replay_joins:  # (replay_joins=False: the checker's own test)
+                wait("G", record("C"))
+                wait("G", record("P"))
+                eager_pending = False
+            fork = add("G")  # the graph's root: after everything before it on graph_stream
+            C, P = "GC%d" % call, "GP%d" % call  # the graph's nodes run on streams of their own
+            wait(C, fork)
+            wait(P, fork)
+            steps(call, C, P)
+            wait("G", record(C))
+            wait("G", record(P))
+            add("G")  # the graph's end: before anything later on graph_stream
+            wait(user, record("G"))
+            graph_pending = True
         # the user's next work on this stream reads and writes this call's buffers
         ends.append(add(user, [(buf_id(call, IN), 0, nbytes, True), (buf_id(call, OUT), 0, nbytes, True)]))
 

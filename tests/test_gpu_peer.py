@@ -45,7 +45,7 @@ def run_job(p, cases, timeout=300, **extra_env):
                 pr.wait()
     results = []
     for r, (rc, o, e) in enumerate(outs):
-        assert rc == 0, "rank %d exited %d:\n%s" % (r, rc, e[-3000:])
+        assert rc == 0, "rank %d exited %d:\n%s\n--- stdout:\n%s" % (r, rc, e[-3000:], o[-3000:])
         line = [ln for ln in o.splitlines() if ln.startswith("{")][-1]
         res = json.loads(line)
         res["stderr"] = e[-20000:]

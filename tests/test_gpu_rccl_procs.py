@@ -80,6 +80,21 @@ def test_fusion_workloads_over_rccl(gpu, workload, p):
     check(run_job(p, cases, timeout=600, **rccl_env("auto")))
 
 
+def test_replay_gate_in_python_processes(gpu):
+    """A Python process runs on the HIP runtime and RCCL that torch bundles (ROCm 7.0.2, RCCL
+    2.26), where capturing RCCL point-to-point work crashes (tools/graph_probe.py): TIPS_GRAPHS=1
+    leaves replays off there (tips_graph_stats reports 2), and the repeated-buffer rounds run
+    eagerly, bit-exact. Replays on /opt/rocm's runtime: tests/test_gpu_graphs.py."""
+    env = rccl_env("direct")
+    env["TIPS_GRAPHS"] = "1"
+    results = run_job(2, [{"bufs": [[F32, 300007, False, False], [I64, 70001, True, False], [BF16, 4099, False, True]],
+                           "seed": 8, "rounds": 4}], **env)
+    check(results)
+    for res in results:
+        c = res["results"][0]
+        assert c["captured"] == 0 and c["replayed"] == 0 and c["graphs_off"] == 2, c
+
+
 @pytest.mark.parametrize("p", [2, 3])
 def test_tuned_schedule_across_processes(gpu, p):
     """TIPS_ALGO=tune over real RCCL ranks: the first call of each size class times ring and

@@ -62,6 +62,29 @@ def test_stream_event_hazards(algo, p, n, K, inplace):
         assert not races, "rank %d: %s" % (r, races[:5])
 
 
+@pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
+@pytest.mark.parametrize("p,n,K", [(2, 262147, 4), (3, 1000, 3), (8, 262147, 4)])
+@pytest.mark.parametrize("modes", [("eager", "replay", "replay", "eager", "replay"), ("replay", "eager", "eager"),
+                                   ("replay", "replay", "replay")])
+def test_stream_event_hazards_with_replays(algo, p, n, K, modes):
+    """TIPS_GRAPHS: replays of the captured plan (a graph on graph_stream, its nodes on streams of
+    their own) mixed with eager calls, from alternating user streams: still no unordered conflict
+    (staging shared by all calls; the joins of replay() and order_after_replays())."""
+    for r in sorted({0, p - 1}):
+        pl = pu.dump(algo, p, r, n, F32, K)
+        for inplace in (False, True):
+            races = pu.hazards(pl, 4, n * 4, inplace=inplace, modes=modes)
+            assert not races, "rank %d %s: %s" % (r, modes, races[:5])
+
+
+def test_hazard_checker_catches_a_missing_replay_join():
+    """Drop replay()'s wait for the eager work still queued on the comm / compute streams and the
+    replay's receives into staging race with the eager call's sums reading it."""
+    pl = pu.dump(pu.DIRECT, 4, 1, 100000, F32, 2)
+    assert pu.hazards(pl, 4, 400000, modes=("eager", "replay"), replay_joins=False)
+    assert not pu.hazards(pl, 4, 400000, modes=("eager", "replay"))
+
+
 def test_hazard_checker_catches_a_missing_wait():
     """The checker itself: drop the ring's comm-stream wait on the previous step's sum and it must
     report the send reading `out` before the sum wrote it."""

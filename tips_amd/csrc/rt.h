@@ -126,6 +126,7 @@ struct EventPool {
 
 struct PeerState;   // peer.cc
 struct FusionCache;  // fusion.cc: pack/unpack descriptor tables of recent tensor lists
+struct PlanGraphs;   // schedules.cc: instantiated HIP graphs of recently replayed plans
 
 struct State {
   std::mutex mu;
@@ -150,6 +151,14 @@ struct State {
   FusionCache* fusion_cache = nullptr;  // created on first use
   // TIPS_ALGO_TUNE: (ranks, dtype, size class) -> (schedule, pipeline depth), the same on every rank
   std::map<std::tuple<int, int, int>, std::pair<int, int>> tuned;
+  // schedules.cc, TIPS_GRAPHS: a plan called again on the same buffers is captured once into a HIP
+  // graph and then replayed with one launch on graph_stream, which joins the caller both ways
+  hipStream_t graph_stream = nullptr;
+  hipEvent_t ev_graph[5] = {};  // replay joins: caller in, comm in, comp in, caller out, eager after replays
+  PlanGraphs* graphs = nullptr;
+  bool graph_pending = false;  // a replay may still run on graph_stream: eager plan work waits for it
+  bool eager_pending = false;  // eager plan work was queued on comm / comp since the last replay
+  int64_t graphs_captured = 0, graphs_replayed = 0;
 };
 
 State& S();
@@ -169,9 +178,11 @@ inline bool peer_selected(const State& st) {
   return st.size > 1 && st.size <= tips::kMaxSrcs && resolve_algo(st.algo, st.size, 0) == TIPS_ALGO_PEER;
 }
 int ensure_comm(State& st);
+void rccl_env_defaults();  // before any ncclCommInitRank of ours
 
 // schedules.cc: device-resident allreduce, caller holds st.mu
 int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream);
+void graphs_release(State& st);  // schedules.cc (shutdown, before the communicator goes)
 // peer.cc: allreduce over IPC-mapped peer memory (1 < p <= kMaxSrcs, one node), caller holds st.mu
 int peer_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t stream);
 void peer_release(State& st);  // collective (shutdown)

@@ -54,6 +54,13 @@ int ensure_streams(State& st) {
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIP_TRY(hipStreamCreateWithPriority(&st.comm_stream, hipStreamNonBlocking, greatest));
   }
+  if (!st.graph_stream) {  // replayed plans carry the same RCCL kernels: the same priority
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&st.graph_stream, hipStreamNonBlocking, greatest));
+  }
+  for (hipEvent_t& e : st.ev_graph)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (!st.comp_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comp_stream, hipStreamNonBlocking));
   if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
   if (!st.h2d_stream) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream, hipStreamNonBlocking));
@@ -116,9 +123,17 @@ int resolve_algo(int algo, int p, int64_t bytes) {
   return (p <= 2 || p > tips::kMaxSrcs) ? TIPS_ALGO_RING : TIPS_ALGO_DIRECT;
 }
 
+void rccl_env_defaults() {
+  // Captured plans (TIPS_GRAPHS) key their graphs by buffer address and allocation id; RCCL's
+  // graph-time buffer registration would pin peers' mappings of a buffer past its free, so with
+  // replays on it is off unless the user sets it (read by RCCL at its first communicator).
+  if (env_i64("TIPS_GRAPHS", 0) > 0) setenv("NCCL_GRAPH_REGISTER", "0", 0);
+}
+
 int ensure_comm(State& st) {
   if (st.comm) return 0;
   if (st.size != 1) return fail(TIPS_ERR_NOT_INITIALIZED, "no RCCL communicator");
+  rccl_env_defaults();
   ncclUniqueId id;
   NCCL_TRY(ncclGetUniqueId(&id));
   NCCL_TRY(ncclCommInitRank(&st.comm, 1, id, 0));

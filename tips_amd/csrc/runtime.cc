@@ -59,6 +59,7 @@ int tips_init_rank(int rank, int size, int device, const void* unique_id, int64_
     memcpy(&id, unique_id, sizeof id);
     // TIPS_NO_RCCL=1: no communicator (only the peer schedule, which needs none, can run). Lets
     // several ranks share one GPU, which RCCL refuses: the peer schedule's multi-process tests.
+    rccl_env_defaults();
     if (!env_i64("TIPS_NO_RCCL", 0)) NCCL_TRY(ncclCommInitRank(&st.comm, size, id, rank));
     uint64_t h = 1469598103934665603ull;  // FNV-1a of the id: the peer schedule's node-local block name
     for (size_t i = 0; i < sizeof id; i++) h = (h ^ ((const unsigned char*)unique_id)[i]) * 1099511628211ull;
@@ -103,6 +104,7 @@ void tips_shutdown(void) {
   if (st.device >= 0) (void)hipSetDevice(st.device);
   if (st.comm_stream) (void)hipStreamSynchronize(st.comm_stream);
   if (st.comp_stream) (void)hipStreamSynchronize(st.comp_stream);
+  graphs_release(st);  // replayed plans hold RCCL work: gone before the communicator
   peer_release(st);  // collective: no rank frees its IPC workspace while a peer may still read it
   st.peer_key = 0;
   if (st.comm) {
@@ -123,7 +125,8 @@ void tips_shutdown(void) {
   st.tuned.clear();
   st.recv_ev.release();
   st.sum_ev.release();
-  for (hipEvent_t* e : {&st.ev_start, &st.ev_done, &st.ev_comp_done, &st.ev_comp_prev})
+  for (hipEvent_t* e : {&st.ev_start, &st.ev_done, &st.ev_comp_done, &st.ev_comp_prev, &st.ev_graph[0],
+                        &st.ev_graph[1], &st.ev_graph[2], &st.ev_graph[3], &st.ev_graph[4]})
     if (*e) {
       (void)hipEventDestroy(*e);
       *e = nullptr;
@@ -132,7 +135,7 @@ void tips_shutdown(void) {
   st.fuse_ev.release();
   st.fusion_threshold = 0;
   for (hipStream_t* s : {&st.comm_stream, &st.comp_stream, &st.io_stream, &st.h2d_stream, &st.d2h_stream,
-                         &st.fuse_stream, &st.bucket_stream})
+                         &st.fuse_stream, &st.bucket_stream, &st.graph_stream})
     if (*s) {
       (void)hipStreamDestroy(*s);
       *s = nullptr;

@@ -34,14 +34,26 @@ int launch_psum(const PSum& s, char* const* base, int dtype, hipStream_t stream)
   return 0;
 }
 
+// Eager plan work (and RCCL calls on the comm stream) after every replayed plan still in flight:
+// a replay reads and writes the same staging and issues RCCL work on the same communicator.
+int order_after_replays(State& st) {
+  if (!st.graph_pending) return 0;
+  TRY(join(st.comm_stream, st.graph_stream, st.ev_graph[4]));
+  HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_graph[4], 0));
+  st.graph_pending = false;
+  return 0;
+}
+
 // Stream prologue shared by both executors: the comm stream waits for the caller's stream (the
 // inputs are ready) and for every sum already queued on the compute stream (the previous call's
 // sums have read the staging slots this call's receives overwrite, whatever stream that call
 // came on); the compute stream waits for the caller's stream.
 int prologue(State& st, hipStream_t user) {
+  TRY(order_after_replays(st));
   TRY(join(st.comm_stream, user, st.ev_start));
   TRY(join(st.comm_stream, st.comp_stream, st.ev_comp_prev));
   HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
+  st.eager_pending = true;
   return 0;
 }
 
@@ -54,13 +66,8 @@ int epilogue(State& st, hipStream_t user) {
 // One rank's plan over RCCL: each step's transfers are one ncclGroupStart/End on the comm
 // stream, followed by an event the compute stream waits on before the step's sums; a step's
 // wait_sum makes the comm stream wait for an earlier step's sums (what it sends, they wrote).
-int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t user) {
+int issue_steps(State& st, const Plan& pl, char* const* base) {
   const size_t nsteps = pl.steps.size();
-  TRY(st.staging.ensure((size_t)std::max<int64_t>(pl.staging_bytes, 1)));
-  TRY(st.recv_ev.ensure(nsteps));
-  TRY(st.sum_ev.ensure(nsteps));
-  char* base[3] = {(char*)in, out, (char*)st.staging.p};
-  TRY(prologue(st, user));
   for (size_t i = 0; i < nsteps; i++) {
     const PStep& s = pl.steps[i];
     if (s.wait_sum >= 0 && !pl.steps[s.wait_sum].sums.empty())
@@ -84,6 +91,173 @@ int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t u
       HIP_TRY(hipEventRecord(st.sum_ev.ev[i], st.comp_stream));
     }
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// TIPS_GRAPHS: replayed plans. A plan's host cost is one ncclGroupStart/End of up to 2(p-1)
+// p2p calls per step plus its event records, waits and sum launches: ~100-250 us of HIP/RCCL API
+// time at p = 8, about what moving a 10-30 MiB bucket over xGMI takes. A plan called again on
+// the same buffers (the fusion slots, a training loop's gradient buckets) is captured once into a
+// HIP graph - the same steps, streams and events, as graph edges - and from then on replayed with
+// one hipGraphLaunch on graph_stream. Capture waits for a plan's second call, so RCCL has set up
+// its connections eagerly (outside any capture) on the first. Keys carry the buffers' allocation
+// ids, not only their addresses: a buffer freed and reallocated at the same address is a new key.
+
+}  // namespace
+
+struct PlanGraphs {
+  // (algo, K, dtype, count, in, out, staging, in allocation id, out allocation id)
+  using Key = std::tuple<int, int, int, int64_t, const void*, const void*, const void*, unsigned long long,
+                         unsigned long long>;
+  struct Ent {
+    hipGraphExec_t exec = nullptr;  // null: seen once, runs eagerly
+    uint64_t stamp = 0;
+  };
+  std::map<Key, Ent> m;
+  uint64_t clock = 0;
+  bool off = false;  // a capture failed: eager for the rest of the job
+};
+
+namespace {
+
+unsigned long long allocation_id(const void* p) {
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return id;
+}
+
+void destroy_exec(State& st, hipGraphExec_t e) {
+  if (!e) return;
+  (void)hipStreamSynchronize(st.graph_stream);  // (not while a replay of it may run)
+  (void)hipGraphExecDestroy(e);
+}
+
+// TIPS_GRAPHS=1 turns replays on where captured RCCL point-to-point work is known to replay
+// correctly: the HIP runtime and RCCL of ROCm >= 7.2 (tools/graph_repro.cc, tests/test_gpu_graphs.py).
+// The ROCm 7.0.2 runtime and RCCL 2.26 that torch bundles (what a Python process of this library
+// runs on) crash in hipStreamEndCapture once a grouped ncclSend/ncclRecv was captured on a stream
+// forked from the capture's origin (tools/graph_probe.py mode 3; mode 5, the group on the origin
+// itself, replays wrong bytes), so there every plan stays eager. Off by default: replays cut the
+// host time of a call (64 -> 27 us one-shot p = 2, 72 -> 50 us direct p = 3) but over the socket
+// transport a call's completion got slower (profiles/r02/graph_host_cost.jsonl); xGMI is
+// unmeasured. TIPS_GRAPHS=2 forces replays on any runtime (probing only).
+bool graphs_supported() {
+  static int ok = -1;
+  if (ok < 0) {
+    int rv = 0, hv = 0;
+    ok = ncclGetVersion(&rv) == ncclSuccess && hipRuntimeGetVersion(&hv) == hipSuccess && rv >= 22700 && hv >= 70200000;
+    (void)hipGetLastError();
+  }
+  return ok == 1;
+}
+
+bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
+  if (st.graphs && st.graphs->off) return false;
+  const int64_t want = env_i64("TIPS_GRAPHS", 0);
+  if (want <= 0 || (want == 1 && !graphs_supported())) return false;
+  if (pl.n * tips::dtype_size(pl.dtype) > env_i64("TIPS_GRAPH_MAX_BYTES", 64 << 20)) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(user, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return cs == hipStreamCaptureStatusNone;  // the caller's own capture takes the eager steps
+}
+
+// Captures the plan on graph_stream: comm and compute streams fork from it and join back, so the
+// graph holds exactly the eager executor's steps and edges. On failure every forked stream is
+// still joined back, so the capture ends and the streams leave capture mode.
+int capture_plan(State& st, const Plan& pl, char* const* base, hipGraphExec_t* exec) {
+  HIP_TRY(hipStreamBeginCapture(st.graph_stream, hipStreamCaptureModeRelaxed));
+  int rc = join(st.comm_stream, st.graph_stream, st.ev_start);
+  if (rc == 0 && hipStreamWaitEvent(st.comp_stream, st.ev_start, 0) != hipSuccess)
+    rc = fail(TIPS_ERR_HIP, "capture: compute stream fork failed");
+  if (rc == 0) rc = issue_steps(st, pl, base);
+  const int j1 = join(st.graph_stream, st.comm_stream, st.ev_done);
+  const int j2 = join(st.graph_stream, st.comp_stream, st.ev_comp_done);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(st.graph_stream, &g);
+  if (rc == 0) rc = j1 ? j1 : j2;
+  if (rc == 0 && (e != hipSuccess || !g)) rc = fail(TIPS_ERR_HIP, "hipStreamEndCapture failed: %s", hipGetErrorString(e));
+  if (rc == 0) {
+    const hipError_t ei = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      *exec = nullptr;
+      rc = fail(TIPS_ERR_HIP, "hipGraphInstantiate failed: %s", hipGetErrorString(ei));
+    }
+  }
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  return rc;
+}
+
+// The graph to replay for this call, or null: run eagerly (first call of a key, or graphs off).
+hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base) {
+  if (!st.graphs) st.graphs = new PlanGraphs();
+  PlanGraphs& G = *st.graphs;
+  const unsigned long long in_id = allocation_id(base[kBufIn]), out_id = allocation_id(base[kBufOut]);
+  if (!in_id || !out_id) return nullptr;
+  const PlanGraphs::Key k{pl.algo, pl.K, pl.dtype, pl.n, base[kBufIn], base[kBufOut], base[kBufStaging], in_id, out_id};
+  auto it = G.m.find(k);
+  if (it == G.m.end()) {
+    const size_t cap = (size_t)std::max<int64_t>(1, env_i64("TIPS_GRAPH_CACHE", 64));
+    while (G.m.size() >= cap) {  // least recently used out
+      auto lru = G.m.begin();
+      for (auto j = G.m.begin(); j != G.m.end(); ++j)
+        if (j->second.stamp < lru->second.stamp) lru = j;
+      destroy_exec(st, lru->second.exec);
+      G.m.erase(lru);
+    }
+    G.m[k].stamp = ++G.clock;
+    return nullptr;
+  }
+  it->second.stamp = ++G.clock;
+  if (!it->second.exec) {
+    if (capture_plan(st, pl, base, &it->second.exec) != 0) {
+      if (getenv("TIPS_VERBOSE")) fprintf(stderr, "[tips] plan capture failed, eager from now on: %s\n", last_error().c_str());
+      G.off = true;
+      return nullptr;
+    }
+    st.graphs_captured++;
+  }
+  return it->second.exec;
+}
+
+int replay(State& st, hipGraphExec_t exec, hipStream_t user) {
+  TRY(join(st.graph_stream, user, st.ev_graph[0]));
+  if (st.eager_pending) {  // earlier eager plans still own staging / the communicator's order
+    TRY(join(st.graph_stream, st.comm_stream, st.ev_graph[1]));
+    TRY(join(st.graph_stream, st.comp_stream, st.ev_graph[2]));
+    st.eager_pending = false;
+  }
+  HIP_TRY(hipGraphLaunch(exec, st.graph_stream));
+  TRY(join(user, st.graph_stream, st.ev_graph[3]));
+  st.graph_pending = true;
+  st.graphs_replayed++;
+  return 0;
+}
+
+int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t user) {
+  const size_t nsteps = pl.steps.size();
+  void* const stg_before = st.staging.p;
+  TRY(st.staging.ensure((size_t)std::max<int64_t>(pl.staging_bytes, 1)));
+  if (st.staging.p != stg_before && st.graphs) {  // graphs of the old staging can never replay again
+    for (auto& kv : st.graphs->m) destroy_exec(st, kv.second.exec);
+    st.graphs->m.clear();
+  }
+  TRY(st.recv_ev.ensure(nsteps));
+  TRY(st.sum_ev.ensure(nsteps));
+  char* base[3] = {(char*)in, out, (char*)st.staging.p};
+  if (graph_eligible(st, pl, user)) {
+    hipGraphExec_t exec = plan_graph(st, pl, base);
+    if (exec) return replay(st, exec, user);
+  }
+  TRY(prologue(st, user));
+  TRY(issue_steps(st, pl, base));
   return epilogue(st, user);
 }
 
@@ -158,6 +332,10 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, std:
       break;
     }
     const size_t nb = sizeof(double) * cand.size();
+    if ((rc = order_after_replays(st)) != 0) {
+      (void)hipFree(d);
+      break;
+    }
     if (hipMemcpyAsync(d, ms.data(), nb, hipMemcpyHostToDevice, st.comm_stream) != hipSuccess ||
         ncclAllReduce(d, d, cand.size(), ncclFloat64, ncclMax, st.comm, st.comm_stream) != ncclSuccess ||
         hipMemcpyAsync(ms.data(), d, nb, hipMemcpyDeviceToHost, st.comm_stream) != hipSuccess ||
@@ -217,6 +395,18 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
     a = TIPS_ALGO_RING;
   if (a != TIPS_ALGO_DIRECT && a != TIPS_ALGO_ONESHOT) a = TIPS_ALGO_RING;
   return plan_allreduce(st, a, (const char*)in, (char*)out, n, dtype, stream);
+}
+
+void graphs_release(State& st) {
+  if (st.graph_stream) (void)hipStreamSynchronize(st.graph_stream);
+  if (st.graphs) {
+    for (auto& kv : st.graphs->m)
+      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    delete st.graphs;
+    st.graphs = nullptr;
+  }
+  st.graph_pending = st.eager_pending = false;
+  st.graphs_captured = st.graphs_replayed = 0;
 }
 
 namespace {
@@ -392,6 +582,20 @@ int tips_tuned_choice(int64_t bytes, int* algo, int* depth) {
       return 1;
     }
   return 0;
+}
+
+int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached) {
+  if (!captured || !replayed || !cached) return fail(TIPS_ERR_INVALID_ARG, "bad graph-stats query");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  *captured = st.graphs_captured;
+  *replayed = st.graphs_replayed;
+  *cached = 0;
+  if (st.graphs)
+    for (const auto& kv : st.graphs->m) *cached += kv.second.exec != nullptr;
+  if (st.graphs && st.graphs->off) return 1;
+  const int64_t want = env_i64("TIPS_GRAPHS", 0);
+  return (want <= 0 || (want == 1 && !graphs_supported())) ? 2 : 0;
 }
 
 int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, int depth, int64_t* out, int64_t cap) {
