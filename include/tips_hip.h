@@ -258,6 +258,10 @@ TIPS_API int tips_resolve_algorithm(int nranks, int64_t bytes);
  * `bytes`' size class. Returns 1 (and fills algo / depth) once that class has been tuned,
  * 0 before; < 0 on error. */
 TIPS_API int tips_tuned_choice(int64_t bytes, int* algo, int* depth);
+/* The same, with the number of transfer lanes the choice runs on: RCCL communicators split from
+ * the job's, whose groups of consecutive plan steps are in flight together (1 = the comm stream
+ * alone). TIPS_LANES sets it (the same on every rank) for an explicitly selected schedule. */
+TIPS_API int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lanes);
 /* Replayed plans (TIPS_GRAPHS): a ring / direct / one-shot call of at most TIPS_GRAPH_MAX_BYTES
  * (64 MiB) made again on the same buffers (same addresses and allocations) is captured once into a
  * HIP graph and replayed with one launch; streams, events and results are those of the eager

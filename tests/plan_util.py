@@ -82,11 +82,15 @@ def _ranges_overlap(a, b):
     return a[0] < b[1] and b[0] < a[1]
 
 
-def hazards(plan, es, nbytes, inplace=False, modes=("eager", "eager"), replay_joins=True):
+def hazards(plan, es, nbytes, inplace=False, modes=("eager", "eager"), replay_joins=True, lanes=1,
+            cross_lane_waits=True):
     """Happens-before check of one rank's plan over back-to-back calls from alternating user
     streams, each call eager (schedules.cc prologue / steps / epilogue) or a replay of the captured
     plan (TIPS_GRAPHS: a graph launched on graph_stream, its nodes on streams of their own, ordered
     only by the graph's edges and by graph_stream's order).
+    lanes > 1: eager step i's transfers go to lane i % lanes, each lane its own stream (and RCCL
+    communicator); at entry lane 0 waits for the caller, the queued sums and every lane's queued
+    transfers, and the other lanes wait for lane 0; at exit the caller waits for every lane.
     Returns a list of race descriptions (empty = race-free). nbytes = bucket bytes."""
     ops = []     # (stream, accesses) ; accesses = [(buffer_id, lo, hi, is_write)]
     preds = []   # explicit cross-stream predecessors (event waits) per op
@@ -117,14 +121,32 @@ def hazards(plan, es, nbytes, inplace=False, modes=("eager", "eager"), replay_jo
             return ("io", call)
         return ("in" if buf == IN else "out", call)
 
-    def steps(call, C, P):
+    def conflict(a, b):  # (the executor compares addresses: in place, in and out are one buffer)
+        return any((not x["send"] or not y["send"]) and buf_id(0, x["buf"]) == buf_id(0, y["buf"]) and
+                   _ranges_overlap((x["off"], x["off"] + x["bytes"]), (y["off"], y["off"] + y["bytes"]))
+                   for x in a["xfers"] for y in b["xfers"])
+
+    def steps(call, Cs, P):
         sum_ev = {}
+        group_op = {}
+        nl = len(Cs)
         for i, s in enumerate(plan["steps"]):
+            C = Cs[i % nl]
             if s["wait_sum"] >= 0 and s["wait_sum"] in sum_ev:
                 wait(C, sum_ev[s["wait_sum"]])
+            if nl > 1 and cross_lane_waits:  # schedules.cc issue_steps: the latest conflicting step on each other lane
+                for lane in range(nl):
+                    if lane == i % nl:
+                        continue
+                    for j in range(i - 1, -1, -1):
+                        if j % nl == lane and conflict(plan["steps"][j], s):
+                            wait(C, group_op[j])
+                            break
             if s["xfers"]:
                 acc = [(buf_id(call, x["buf"]), x["off"], x["off"] + x["bytes"], not x["send"]) for x in s["xfers"]]
-                add(C, acc)
+                group_op[i] = add(C, acc)
+            else:
+                group_op[i] = record(C)
             if s["sums"]:
                 rev = record(C)
                 wait(P, rev)
@@ -149,11 +171,18 @@ def hazards(plan, es, nbytes, inplace=False, modes=("eager", "eager"), replay_jo
             wait("C", ev_start)
             ev_prev = record("P")
             wait("C", ev_prev)
+            lane_names = ["C"] + ["C%d" % l for l in range(1, lanes)]
+            for ln in lane_names[1:]:  # lane 0 after every lane's queued transfers
+                wait("C", record(ln))
+            if lanes > 1:
+                e0 = record("C")
+                for ln in lane_names[1:]:
+                    wait(ln, e0)
             wait("P", ev_start)
             eager_pending = True
-            steps(call, "C", "P")
-            e1 = record("C")
-            wait(user, e1)
+            steps(call, lane_names, "P")
+            for ln in lane_names:
+                wait(user, record(ln))
             e2 = record("P")
             wait(user, e2)
         else:  # replay
@@ -166,7 +195,7 @@ def hazards(plan, es, nbytes, inplace=False, modes=("eager", "eager"), replay_jo
             C, P = "GC%d" % call, "GP%d" % call  # the graph's nodes run on streams of their own
             wait(C, fork)
             wait(P, fork)
-            steps(call, C, P)
+            steps(call, [C], P)
             wait("G", record(C))
             wait("G", record(P))
             add("G")  # the graph's end: before anything later on graph_stream

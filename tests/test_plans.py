@@ -77,6 +77,29 @@ def test_stream_event_hazards_with_replays(algo, p, n, K, modes):
             assert not races, "rank %d %s: %s" % (r, modes, races[:5])
 
 
+@pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
+@pytest.mark.parametrize("p,n,K", [(2, 262147, 4), (3, 1000, 3), (4, 65539, 6), (8, 262147, 4), (8, 1 << 20, 2),
+                                   (16, 100003, 3)])
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_stream_event_hazards_with_lanes(algo, p, n, K, lanes):
+    """Transfer lanes: step i's group on lane i % L (its own stream and split communicator), with
+    the executor's cross-lane waits (the latest conflicting step on each other lane); calls from
+    alternating user streams, mixed with one-lane calls and replays. No unordered conflict."""
+    for r in sorted({0, 1, p - 1}):
+        pl = pu.dump(algo, p, r, n, F32, K)
+        for inplace in (False, True):
+            races = pu.hazards(pl, 4, n * 4, inplace=inplace, lanes=lanes, modes=("eager", "eager", "replay", "eager"))
+            assert not races, "rank %d: %s" % (r, races[:5])
+
+
+def test_lane_checker_needs_the_cross_lane_waits():
+    """Without the cross-lane waits, the ring's allgather forwards bytes on one lane that the
+    previous step is still receiving on the other: the checker must see the race."""
+    pl = pu.dump(pu.RING, 3, 0, 1000, F32, 3)
+    assert not pu.hazards(pl, 4, 4000, lanes=2)
+    assert pu.hazards(pl, 4, 4000, lanes=2, cross_lane_waits=False)
+
+
 def test_hazard_checker_catches_a_missing_replay_join():
     """Drop replay()'s wait for the eager work still queued on the comm / compute streams and the
     replay's receives into staging race with the eager call's sums reading it."""

@@ -102,6 +102,8 @@ _SIGNATURES = [
     ("tips_get_algorithm", ctypes.c_int, []),
     ("tips_resolve_algorithm", ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),
     ("tips_tuned_choice", ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    ("tips_tuned_schedule", ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_int)]),
     ("tips_graph_stats", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     ("tips_ring_simulate", ctypes.c_int,

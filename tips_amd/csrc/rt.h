@@ -124,6 +124,12 @@ struct EventPool {
   }
 };
 
+// A schedule as the executor runs it: algorithm, pipeline depth (sub-chunks per chunk) and
+// transfer lanes (RCCL communicators whose groups may be in flight together).
+struct Choice {
+  int algo = TIPS_ALGO_RING, depth = 0, lanes = 1;
+};
+
 struct PeerState;   // peer.cc
 struct FusionCache;  // fusion.cc: pack/unpack descriptor tables of recent tensor lists
 struct PlanGraphs;   // schedules.cc: instantiated HIP graphs of recently replayed plans
@@ -149,8 +155,14 @@ struct State {
   uint64_t peer_key = 0;      // names the node-local control block of the peer schedule (hash of the unique id)
   PeerState* peer = nullptr;  // peer schedule: IPC workspaces + shared-memory barrier, created on first use
   FusionCache* fusion_cache = nullptr;  // created on first use
-  // TIPS_ALGO_TUNE: (ranks, dtype, size class) -> (schedule, pipeline depth), the same on every rank
-  std::map<std::tuple<int, int, int>, std::pair<int, int>> tuned;
+  // TIPS_ALGO_TUNE: (ranks, dtype, size class) -> schedule, the same on every rank
+  std::map<std::tuple<int, int, int>, Choice> tuned;
+  // transfer lanes beyond the comm stream (TIPS_LANES, or tuned): RCCL communicators split from
+  // `comm`, each with its own stream at the comm stream's priority; a plan's step i moves its
+  // bytes on lane i % L, so the groups of consecutive steps can be in flight together
+  std::vector<ncclComm_t> lane_comm;
+  std::vector<hipStream_t> lane_stream;
+  EventPool lane_ev, xfer_ev;
   // schedules.cc, TIPS_GRAPHS: a plan called again on the same buffers is captured once into a HIP
   // graph and then replayed with one launch on graph_stream, which joins the caller both ways
   hipStream_t graph_stream = nullptr;
@@ -183,6 +195,7 @@ void rccl_env_defaults();  // before any ncclCommInitRank of ours
 // schedules.cc: device-resident allreduce, caller holds st.mu
 int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream);
 void graphs_release(State& st);  // schedules.cc (shutdown, before the communicator goes)
+void lanes_release(State& st);   // schedules.cc (shutdown: the split communicators and their streams)
 // peer.cc: allreduce over IPC-mapped peer memory (1 < p <= kMaxSrcs, one node), caller holds st.mu
 int peer_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t stream);
 void peer_release(State& st);  // collective (shutdown)

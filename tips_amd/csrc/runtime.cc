@@ -105,6 +105,7 @@ void tips_shutdown(void) {
   if (st.comm_stream) (void)hipStreamSynchronize(st.comm_stream);
   if (st.comp_stream) (void)hipStreamSynchronize(st.comp_stream);
   graphs_release(st);  // replayed plans hold RCCL work: gone before the communicator
+  lanes_release(st);   // (split from it)
   peer_release(st);  // collective: no rank frees its IPC workspace while a peer may still read it
   st.peer_key = 0;
   if (st.comm) {

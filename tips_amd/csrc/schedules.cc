@@ -44,48 +44,121 @@ int order_after_replays(State& st) {
   return 0;
 }
 
+// Transfer lane l: the comm stream and communicator for l = 0, a split communicator after that.
+hipStream_t lane_stream(State& st, int l) { return l == 0 ? st.comm_stream : st.lane_stream[l - 1]; }
+ncclComm_t lane_comm(State& st, int l) { return l == 0 ? st.comm : st.lane_comm[l - 1]; }
+
+// Lanes 1..L-1 exist. ncclCommSplit is collective: every rank reaches it at the same call, since
+// every rank runs the same schedule choice (TIPS_LANES is the same everywhere; the tuner agrees).
+int lanes_ensure(State& st, int L) {
+  while ((int)st.lane_comm.size() < L - 1) {
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest));
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommSplit(st.comm, 0, st.rank, &c, nullptr);
+    if (r != ncclSuccess) {
+      (void)hipStreamDestroy(s);
+      return fail(TIPS_ERR_RCCL, "ncclCommSplit for transfer lane %zu failed: %s", st.lane_comm.size() + 1,
+                  ncclGetErrorString(r));
+    }
+    st.lane_comm.push_back(c);
+    st.lane_stream.push_back(s);
+  }
+  TRY(st.lane_ev.ensure(st.lane_stream.size() + 1));
+  return 0;
+}
+
 // Stream prologue shared by both executors: the comm stream waits for the caller's stream (the
 // inputs are ready) and for every sum already queued on the compute stream (the previous call's
 // sums have read the staging slots this call's receives overwrite, whatever stream that call
 // came on); the compute stream waits for the caller's stream.
-int prologue(State& st, hipStream_t user) {
+// With transfer lanes the comm stream also waits for every lane's queued transfers (an earlier
+// call's receives into staging, on whatever lane), and lanes 1..L-1 start after the comm stream.
+int prologue(State& st, hipStream_t user, int L = 1) {
   TRY(order_after_replays(st));
   TRY(join(st.comm_stream, user, st.ev_start));
   TRY(join(st.comm_stream, st.comp_stream, st.ev_comp_prev));
+  for (size_t l = 0; l < st.lane_stream.size(); l++) TRY(join(st.comm_stream, st.lane_stream[l], st.lane_ev.ev[l + 1]));
+  if (L > 1) {
+    HIP_TRY(hipEventRecord(st.lane_ev.ev[0], st.comm_stream));
+    for (int l = 1; l < L; l++) HIP_TRY(hipStreamWaitEvent(st.lane_stream[l - 1], st.lane_ev.ev[0], 0));
+  }
   HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_start, 0));
   st.eager_pending = true;
   return 0;
 }
 
-int epilogue(State& st, hipStream_t user) {
+int epilogue(State& st, hipStream_t user, int L = 1) {
   TRY(join(user, st.comm_stream, st.ev_done));
+  for (int l = 1; l < L; l++) TRY(join(user, st.lane_stream[l - 1], st.lane_ev.ev[l]));
   TRY(join(user, st.comp_stream, st.ev_comp_done));
   return 0;
+}
+
+// Two steps' transfer groups touch a common byte range and at least one of them writes it
+// (addresses, not plan buffers: in place, in and out are one buffer).
+bool xfers_conflict(const PStep& a, const PStep& b, char* const* base) {
+  for (const PXfer& x : a.xfers)
+    for (const PXfer& y : b.xfers) {
+      if (x.send && y.send) continue;
+      const char* xp = base[x.at.buf] + x.at.off;
+      const char* yp = base[y.at.buf] + y.at.off;
+      if (xp < yp + y.bytes && yp < xp + x.bytes) return true;
+    }
+  return false;
 }
 
 // One rank's plan over RCCL: each step's transfers are one ncclGroupStart/End on the comm
 // stream, followed by an event the compute stream waits on before the step's sums; a step's
 // wait_sum makes the comm stream wait for an earlier step's sums (what it sends, they wrote).
-int issue_steps(State& st, const Plan& pl, char* const* base) {
+// With L > 1 lanes, step i's group runs on lane i % L. One comm stream ordered every group after
+// the previous one; across lanes that order is restated where it matters: a step waits for the
+// latest earlier step on each other lane whose transfers touch its bytes (the ring's allgather
+// forwards what the previous step received). Every other order comes from wait_sum and the
+// compute stream, as with one lane (tests/plan_util.py hazards(lanes=...) checks both).
+int issue_steps(State& st, const Plan& pl, char* const* base, int L = 1) {
   const size_t nsteps = pl.steps.size();
+  std::vector<std::vector<int>> deps(L > 1 ? nsteps : 0);
+  std::vector<char> needed(L > 1 ? nsteps : 0, 0);
+  if (L > 1) {
+    TRY(st.xfer_ev.ensure(nsteps));
+    for (size_t i = 0; i < nsteps; i++)
+      for (int l = 0; l < L; l++) {
+        if (l == (int)(i % L)) continue;
+        for (int j = (int)i - 1; j >= 0; j--)
+          if (j % L == l && xfers_conflict(pl.steps[j], pl.steps[i], base)) {
+            deps[i].push_back(j);
+            needed[j] = 1;
+            break;
+          }
+      }
+  }
   for (size_t i = 0; i < nsteps; i++) {
     const PStep& s = pl.steps[i];
+    const int l = (int)(i % L);
+    hipStream_t cs = lane_stream(st, l);
+    ncclComm_t cc = lane_comm(st, l);
     if (s.wait_sum >= 0 && !pl.steps[s.wait_sum].sums.empty())
-      HIP_TRY(hipStreamWaitEvent(st.comm_stream, st.sum_ev.ev[s.wait_sum], 0));
+      HIP_TRY(hipStreamWaitEvent(cs, st.sum_ev.ev[s.wait_sum], 0));
+    if (L > 1)
+      for (int j : deps[i]) HIP_TRY(hipStreamWaitEvent(cs, st.xfer_ev.ev[j], 0));
     if (!s.xfers.empty()) {
       NCCL_TRY(ncclGroupStart());
       for (const PXfer& x : s.xfers) {
         char* ptr = base[x.at.buf] + x.at.off;
         if (x.send) {
-          NCCL_TRY(ncclSend(ptr, (size_t)x.bytes, ncclInt8, x.peer, st.comm, st.comm_stream));
+          NCCL_TRY(ncclSend(ptr, (size_t)x.bytes, ncclInt8, x.peer, cc, cs));
         } else {
-          NCCL_TRY(ncclRecv(ptr, (size_t)x.bytes, ncclInt8, x.peer, st.comm, st.comm_stream));
+          NCCL_TRY(ncclRecv(ptr, (size_t)x.bytes, ncclInt8, x.peer, cc, cs));
         }
       }
       NCCL_TRY(ncclGroupEnd());
     }
+    if (L > 1 && needed[i]) HIP_TRY(hipEventRecord(st.xfer_ev.ev[i], cs));
     if (!s.sums.empty()) {
-      HIP_TRY(hipEventRecord(st.recv_ev.ev[i], st.comm_stream));
+      HIP_TRY(hipEventRecord(st.recv_ev.ev[i], cs));
       HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.recv_ev.ev[i], 0));
       for (const PSum& ps : s.sums) TRY(launch_psum(ps, base, pl.dtype, st.comp_stream));
       HIP_TRY(hipEventRecord(st.sum_ev.ev[i], st.comp_stream));
@@ -232,6 +305,7 @@ int replay(State& st, hipGraphExec_t exec, hipStream_t user) {
   if (st.eager_pending) {  // earlier eager plans still own staging / the communicator's order
     TRY(join(st.graph_stream, st.comm_stream, st.ev_graph[1]));
     TRY(join(st.graph_stream, st.comp_stream, st.ev_graph[2]));
+    for (size_t l = 0; l < st.lane_stream.size(); l++) TRY(join(st.graph_stream, st.lane_stream[l], st.lane_ev.ev[l + 1]));
     st.eager_pending = false;
   }
   HIP_TRY(hipGraphLaunch(exec, st.graph_stream));
@@ -241,7 +315,8 @@ int replay(State& st, hipGraphExec_t exec, hipStream_t user) {
   return 0;
 }
 
-int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t user) {
+int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t user, int L = 1) {
+  L = std::max(1, std::min(L, (int)pl.steps.size()));
   const size_t nsteps = pl.steps.size();
   void* const stg_before = st.staging.p;
   TRY(st.staging.ensure((size_t)std::max<int64_t>(pl.staging_bytes, 1)));
@@ -252,20 +327,20 @@ int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t u
   TRY(st.recv_ev.ensure(nsteps));
   TRY(st.sum_ev.ensure(nsteps));
   char* base[3] = {(char*)in, out, (char*)st.staging.p};
-  if (graph_eligible(st, pl, user)) {
+  if (L == 1 && graph_eligible(st, pl, user)) {
     hipGraphExec_t exec = plan_graph(st, pl, base);
     if (exec) return replay(st, exec, user);
   }
-  TRY(prologue(st, user));
-  TRY(issue_steps(st, pl, base));
-  return epilogue(st, user);
+  if (L > 1) TRY(lanes_ensure(st, L));
+  TRY(prologue(st, user, L));
+  TRY(issue_steps(st, pl, base, L));
+  return epilogue(st, user, L);
 }
 
-int plan_allreduce(State& st, int algo, const char* in, char* out, int64_t n, int dtype, hipStream_t user,
-                   int depth = 0) {
+int plan_allreduce(State& st, const Choice& c, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
   Plan pl;
-  TRY(build_schedule_plan(algo, st.size, st.rank, n, dtype, depth > 0 ? depth : plan_depth(st.size, n, dtype), &pl));
-  return run_plan(st, pl, in, out, user);
+  TRY(build_schedule_plan(c.algo, st.size, st.rank, n, dtype, c.depth > 0 ? c.depth : plan_depth(st.size, n, dtype), &pl));
+  return run_plan(st, pl, in, out, user, c.lanes);
 }
 
 // ---------------------------------------------------------------------------
@@ -277,28 +352,34 @@ int size_class(int64_t bytes) {
   return c;  // ceil(log2(bytes))
 }
 
-int run_choice(State& st, std::pair<int, int> c, const char* in, char* out, int64_t n, int dtype, hipStream_t s) {
-  if (c.first == TIPS_ALGO_PEER) return peer_allreduce(st, in, out, n, dtype, s);
-  return plan_allreduce(st, c.first, in, out, n, dtype, s, c.second);
+int run_choice(State& st, const Choice& c, const char* in, char* out, int64_t n, int dtype, hipStream_t s) {
+  if (c.algo == TIPS_ALGO_PEER) return peer_allreduce(st, in, out, n, dtype, s);
+  return plan_allreduce(st, c, in, out, n, dtype, s);
 }
 
 // Every rank runs the same candidates in the same order (collectives), on scratch copies of the
 // call's input (the caller's buffers are not touched: in-place calls stay correct), times each with
 // events on `user` (best of 2 after a warm-up), and the ranks agree on the slowest rank's time per
 // candidate with one small ncclAllReduce(MAX): every rank then keeps the same fastest candidate.
-int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, std::pair<int, int>* best) {
+int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choice* best) {
   const int p = st.size;
   const int64_t bytes = n * tips::dtype_size(dtype);
   const int K = plan_depth(p, n, dtype);
-  std::vector<std::pair<int, int>> cand;
+  const int K2 = std::min(16, 2 * K);
+  // two lanes: consecutive steps' groups in flight together, for when one communicator's
+  // point-to-point work does not fill the links (TIPS_TUNE_LANES=0 leaves them out)
+  const bool lanes = env_i64("TIPS_TUNE_LANES", 1) != 0;
+  std::vector<Choice> cand;
   if (p <= tips::kMaxSrcs) {
-    cand.push_back({TIPS_ALGO_DIRECT, K});
-    cand.push_back({TIPS_ALGO_DIRECT, 1});
-    if (K < 16) cand.push_back({TIPS_ALGO_DIRECT, std::min(16, 2 * K)});
+    cand.push_back({TIPS_ALGO_DIRECT, K, 1});
+    cand.push_back({TIPS_ALGO_DIRECT, 1, 1});
+    if (K < 16) cand.push_back({TIPS_ALGO_DIRECT, K2, 1});
+    if (lanes && K > 1) cand.push_back({TIPS_ALGO_DIRECT, K, 2});
   }
-  cand.push_back({TIPS_ALGO_RING, K});
-  if (K < 16) cand.push_back({TIPS_ALGO_RING, std::min(16, 2 * K)});
-  if (p <= tips::kMaxSrcs && env_i64("TIPS_TUNE_PEER", 0)) cand.push_back({TIPS_ALGO_PEER, 0});
+  cand.push_back({TIPS_ALGO_RING, K, 1});
+  if (K < 16) cand.push_back({TIPS_ALGO_RING, K2, 1});
+  if (lanes) cand.push_back({TIPS_ALGO_RING, K, 2});
+  if (p <= tips::kMaxSrcs && env_i64("TIPS_TUNE_PEER", 0)) cand.push_back({TIPS_ALGO_PEER, 0, 1});
   HIP_TRY(hipStreamSynchronize(user));
   void *sin = nullptr, *sout = nullptr;
   HIP_TRY(hipMalloc(&sin, (size_t)bytes));
@@ -355,8 +436,9 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, std:
   *best = cand[b];
   if (getenv("TIPS_VERBOSE") && st.rank == 0) {
     fprintf(stderr, "[tips] tune p=%d bytes=%lld:", p, (long long)bytes);
-    for (size_t c = 0; c < cand.size(); c++) fprintf(stderr, " algo%d/K%d=%.3fms", cand[c].first, cand[c].second, ms[c]);
-    fprintf(stderr, " -> algo%d/K%d\n", best->first, best->second);
+    for (size_t c = 0; c < cand.size(); c++)
+      fprintf(stderr, " algo%d/K%d/L%d=%.3fms", cand[c].algo, cand[c].depth, cand[c].lanes, ms[c]);
+    fprintf(stderr, " -> algo%d/K%d/L%d\n", best->algo, best->depth, best->lanes);
   }
   return 0;
 }
@@ -384,7 +466,7 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
     const auto key = std::make_tuple(st.size, dtype, size_class(n * es));
     auto it = st.tuned.find(key);
     if (it == st.tuned.end()) {
-      std::pair<int, int> best;
+      Choice best;
       TRY(tune(st, (const char*)in, n, dtype, stream, &best));
       it = st.tuned.emplace(key, best).first;
     }
@@ -394,7 +476,19 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
   if (st.size > tips::kMaxSrcs && (a == TIPS_ALGO_DIRECT || a == TIPS_ALGO_ONESHOT || a == TIPS_ALGO_PEER))
     a = TIPS_ALGO_RING;
   if (a != TIPS_ALGO_DIRECT && a != TIPS_ALGO_ONESHOT) a = TIPS_ALGO_RING;
-  return plan_allreduce(st, a, (const char*)in, (char*)out, n, dtype, stream);
+  // TIPS_LANES (same on every rank): transfer lanes for the explicitly chosen schedules
+  const int lanes = (int)std::max<int64_t>(1, std::min<int64_t>(8, env_i64("TIPS_LANES", 1)));
+  return plan_allreduce(st, Choice{a, 0, lanes}, (const char*)in, (char*)out, n, dtype, stream);
+}
+
+void lanes_release(State& st) {
+  for (hipStream_t s : st.lane_stream) (void)hipStreamSynchronize(s);
+  for (ncclComm_t c : st.lane_comm) (void)ncclCommDestroy(c);
+  for (hipStream_t s : st.lane_stream) (void)hipStreamDestroy(s);
+  st.lane_comm.clear();
+  st.lane_stream.clear();
+  st.lane_ev.release();
+  st.xfer_ev.release();
 }
 
 void graphs_release(State& st) {
@@ -577,11 +671,26 @@ int tips_tuned_choice(int64_t bytes, int* algo, int* depth) {
   std::lock_guard<std::mutex> lk(st.mu);
   for (const auto& kv : st.tuned)  // any dtype of this job's size class
     if (std::get<0>(kv.first) == st.size && std::get<2>(kv.first) == size_class(bytes)) {
-      *algo = kv.second.first;
-      *depth = kv.second.second;
+      *algo = kv.second.algo;
+      *depth = kv.second.depth;
       return 1;
     }
   return 0;
+}
+
+int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lanes) {
+  if (!lanes) return fail(TIPS_ERR_INVALID_ARG, "bad tuned-schedule query");
+  const int rc = tips_tuned_choice(bytes, algo, depth);
+  if (rc != 1) return rc;
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  *lanes = 1;
+  for (const auto& kv : st.tuned)
+    if (std::get<0>(kv.first) == st.size && std::get<2>(kv.first) == size_class(bytes)) {
+      *lanes = kv.second.lanes;
+      break;
+    }
+  return 1;
 }
 
 int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached) {
