@@ -663,10 +663,10 @@ def bench_allreduce(args):
     tuned = None
     if algo == _lib.ALGO_TUNE:  # the warm-up measured the schedules; report (and check) the one kept
         import ctypes
-        ta, td = ctypes.c_int(), ctypes.c_int()
+        ta, td, tl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         qbytes = sizes[0] * 4 if workload == "bucket" else max(sizes) * 4 if workload == "negotiated1000" else 64 << 20
-        if L.tips_tuned_choice(qbytes, ctypes.byref(ta), ctypes.byref(td)) == 1:
-            tuned = {"algorithm": inv.get(ta.value, str(ta.value)), "pipeline_depth": td.value}
+        if L.tips_tuned_schedule(qbytes, ctypes.byref(ta), ctypes.byref(td), ctypes.byref(tl)) == 1:
+            tuned = {"algorithm": inv.get(ta.value, str(ta.value)), "pipeline_depth": td.value, "lanes": tl.value}
             algo = ta.value
     host_t.update(enqueue=0.0, wait=0.0)
     t = timed(steps)
@@ -863,7 +863,7 @@ def bench_allreduce(args):
 
     if not args.no_compare:
         # (oneshot targets small buckets only.) The _k entries re-run a schedule at another sub-chunk
-        # pipeline depth (read per call). RCCL-moved schedules first, then the link probe, and last
+        # pipeline depth, the _l entries on more transfer lanes (both read per call). RCCL-moved schedules first, then the link probe, and last
         # the schedules whose bytes our own kernels move through IPC-mapped peer memory: peer is
         # measured here (the driver's 8-GPU run) before it can be a default, and placed last so that
         # a fault in it cannot cost the numbers gathered before it (last_words prints them).
@@ -877,6 +877,13 @@ def bench_allreduce(args):
                 line["xgmi_probe"] = link_probe(dist, rank, world)
             except Exception as e:  # noqa: BLE001
                 line["xgmi_probe"] = {"error": str(e)}
+        # two / four transfer lanes: consecutive steps' groups in flight on split communicators. After
+        # the probe: the split communicators live on to the end of the job (on the socket rehearsal
+        # their existence slowed later RCCL calls), so nothing RCCL-moved is measured after them.
+        run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
+                      ("ring_l2", "ring", {"TIPS_LANES": "2"}),
+                      ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
+                                                  "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
         # Only in a job that spans every GPU of the node (the driver's last, N = 8, run) unless
         # TIPS_BENCH_PEER=1: if the first cross-GPU run of these kernels faulted and took the
         # GPUs down, no later bench run could be lost with it.

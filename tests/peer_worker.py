@@ -461,11 +461,11 @@ def main():
         torch.cuda.synchronize()
         res = {"case": c, "rc": int(rc)}
         if rc == 0 and case_algo == ALGO_NAMES["tune"]:  # the bits of whichever schedule the job measured fastest
-            ta, td = ctypes.c_int(), ctypes.c_int()
-            if L.tips_tuned_choice(n * x.itemsize if c.get("host") else n * x.element_size(), ctypes.byref(ta),
-                                   ctypes.byref(td)) == 1:
+            ta, td, tl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            if L.tips_tuned_schedule(n * x.itemsize if c.get("host") else n * x.element_size(), ctypes.byref(ta),
+                                     ctypes.byref(td), ctypes.byref(tl)) == 1:
                 case_algo = ta.value
-                res["tuned"] = [ta.value, td.value]
+                res["tuned"] = [ta.value, td.value, tl.value]
             elif n * (x.itemsize if c.get("host") else x.element_size()) <= (256 << 10):
                 case_algo = ALGO_NAMES["oneshot"]
         if rc == 0:

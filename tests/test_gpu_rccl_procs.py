@@ -80,6 +80,24 @@ def test_fusion_workloads_over_rccl(gpu, workload, p):
     check(run_job(p, cases, timeout=600, **rccl_env("auto")))
 
 
+@pytest.mark.parametrize("algo,p,lanes", [("ring", 2, 2), ("ring", 3, 3), ("direct", 3, 2), ("direct", 4, 2)])
+def test_transfer_lanes_across_processes(gpu, algo, p, lanes):
+    """TIPS_LANES: step i's group on lane i % L, each lane a communicator split from the job's
+    (ncclCommSplit) with its own stream, plus the cross-lane waits the single comm stream gave for
+    free (the ring's allgather forwarding). Deep pipelines (sub-chunks of 4 KiB) so many groups
+    are in flight; ragged sizes, in place, every dtype; bit-exact against the schedule's oracle.
+    The one-lane calls at the end run after the lane calls on the same staging."""
+    env = rccl_env(algo)
+    env.update(TIPS_LANES=str(lanes), TIPS_PIPELINE_DEPTH="4", TIPS_MIN_SUBCHUNK_BYTES="4096")
+    cases = []
+    for dtype in ALL_DTYPES:
+        for n in (4099, 300007):
+            cases.append({"dtype": dtype, "n": n, "seed": 20 * dtype + n % 11})
+    cases.append({"dtype": F32, "n": 262147, "seed": 5, "inplace": True})
+    cases.append({"dtype": I64, "n": 70001, "seed": 6, "inplace": True})
+    check(run_job(p, cases, **env))
+
+
 def test_replay_gate_in_python_processes(gpu):
     """A Python process runs on the HIP runtime and RCCL that torch bundles (ROCm 7.0.2, RCCL
     2.26), where capturing RCCL point-to-point work crashes (tools/graph_probe.py): TIPS_GRAPHS=1

@@ -359,16 +359,19 @@ int run_choice(State& st, const Choice& c, const char* in, char* out, int64_t n,
 
 // Every rank runs the same candidates in the same order (collectives), on scratch copies of the
 // call's input (the caller's buffers are not touched: in-place calls stay correct), times each with
-// events on `user` (best of 2 after a warm-up), and the ranks agree on the slowest rank's time per
-// candidate with one small ncclAllReduce(MAX): every rank then keeps the same fastest candidate.
+// events on `user` (best of 2 runs of 2 back-to-back calls, after a warm-up), and the ranks agree
+// on the slowest rank's time per candidate with one small ncclAllReduce(MAX): every rank then keeps
+// the same fastest candidate.
 int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choice* best) {
   const int p = st.size;
   const int64_t bytes = n * tips::dtype_size(dtype);
   const int K = plan_depth(p, n, dtype);
   const int K2 = std::min(16, 2 * K);
-  // two lanes: consecutive steps' groups in flight together, for when one communicator's
-  // point-to-point work does not fill the links (TIPS_TUNE_LANES=0 leaves them out)
-  const bool lanes = env_i64("TIPS_TUNE_LANES", 1) != 0;
+  // TIPS_TUNE_LANES=1 adds two-lane candidates (consecutive steps' groups in flight together, for
+  // when one communicator's point-to-point work does not fill the links). Off by default: on the
+  // socket rehearsal the split communicator slowed every later call, chosen or not
+  // (profiles/r02/lanes_rehearsal.jsonl); the 8-GPU bench's direct_l2 / ring_l2 lines measure xGMI.
+  const bool lanes = env_i64("TIPS_TUNE_LANES", 0) != 0;
   std::vector<Choice> cand;
   if (p <= tips::kMaxSrcs) {
     cand.push_back({TIPS_ALGO_DIRECT, K, 1});
@@ -393,15 +396,20 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choi
       break;
     }
     for (size_t c = 0; c < cand.size() && rc == 0; c++) {
-      for (int it = 0; it < 3 && rc == 0; it++) {
-        if (it > 0 && hipEventRecord(e0, user) != hipSuccess) rc = fail(TIPS_ERR_HIP, "tune: event");
-        if (rc == 0) rc = run_choice(st, cand[c], (const char*)sin, (char*)sout, n, dtype, user);
-        if (rc == 0 && it > 0) {
+      // a warm-up call, then twice kBackToBack calls queued back to back (as a training step issues
+      // them: the next call's transfers behind the last one's, no host sync between), per call
+      constexpr int kBackToBack = 2;
+      if (rc == 0) rc = run_choice(st, cand[c], (const char*)sin, (char*)sout, n, dtype, user);
+      for (int it = 0; it < 2 && rc == 0; it++) {
+        if (hipEventRecord(e0, user) != hipSuccess) rc = fail(TIPS_ERR_HIP, "tune: event");
+        for (int q = 0; q < kBackToBack && rc == 0; q++)
+          rc = run_choice(st, cand[c], (const char*)sin, (char*)sout, n, dtype, user);
+        if (rc == 0) {
           float t = 0;
           if (hipEventRecord(e1, user) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
               hipEventElapsedTime(&t, e0, e1) != hipSuccess)
             rc = fail(TIPS_ERR_HIP, "tune: timing");
-          ms[c] = std::min(ms[c], (double)t);
+          ms[c] = std::min(ms[c], (double)t / kBackToBack);
         }
       }
     }
