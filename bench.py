@@ -863,10 +863,13 @@ def bench_allreduce(args):
 
     if not args.no_compare:
         # (oneshot targets small buckets only.) The _k entries re-run a schedule at another sub-chunk
-        # pipeline depth, the _l entries on more transfer lanes (both read per call). RCCL-moved schedules first, then the link probe, and last
-        # the schedules whose bytes our own kernels move through IPC-mapped peer memory: peer is
-        # measured here (the driver's 8-GPU run) before it can be a default, and placed last so that
-        # a fault in it cannot cost the numbers gathered before it (last_words prints them).
+        # pipeline depth, the _l entries on more transfer lanes (both read per call). Order:
+        # RCCL-moved schedules, the link probe, the schedules whose bytes our own kernels move
+        # through IPC-mapped peer memory (measured here, on the driver's 8-GPU run, before either
+        # can be a default), and last the transfer lanes, whose split communicators live on to the
+        # end of the job (on the socket rehearsal their existence slowed every later RCCL call).
+        # A fault or a hang in one of them costs only what comes after it: last_words / the
+        # watchdog print the numbers gathered before.
         run_variants([("ring", "ring", {}), ("direct", "direct", {}), ("rccl", "rccl", {}),
                       ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
                       ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
@@ -877,13 +880,6 @@ def bench_allreduce(args):
                 line["xgmi_probe"] = link_probe(dist, rank, world)
             except Exception as e:  # noqa: BLE001
                 line["xgmi_probe"] = {"error": str(e)}
-        # two / four transfer lanes: consecutive steps' groups in flight on split communicators. After
-        # the probe: the split communicators live on to the end of the job (on the socket rehearsal
-        # their existence slowed later RCCL calls), so nothing RCCL-moved is measured after them.
-        run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
-                      ("ring_l2", "ring", {"TIPS_LANES": "2"}),
-                      ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
-                                                  "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
         # Only in a job that spans every GPU of the node (the driver's last, N = 8, run) unless
         # TIPS_BENCH_PEER=1: if the first cross-GPU run of these kernels faulted and took the
         # GPUs down, no later bench run could be lost with it.
@@ -892,6 +888,10 @@ def bench_allreduce(args):
         elif workload == "bucket":
             compare_check["peer"] = ("skipped: the IPC peer schedules run only when the job spans all %d GPUs of "
                                      "the node (TIPS_BENCH_PEER=1 forces them)" % torch.cuda.device_count())
+        run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
+                      ("ring_l2", "ring", {"TIPS_LANES": "2"}),
+                      ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
+                                                  "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
     line["compare_check"] = compare_check
     line["compare_algbw_gib_s"] = compare
     ring_algbw = algbw if algo == _lib.ALGO_RING else (compare.get("ring") or 0) * GIB
