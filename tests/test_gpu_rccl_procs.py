@@ -127,3 +127,16 @@ def test_tuned_schedule_across_processes(gpu, p):
     picks = [tuple(c.get("tuned", ())) for c in results[0]["results"]]
     for res in results[1:]:
         assert [tuple(c.get("tuned", ())) for c in res["results"]] == picks, "ranks disagree on the tuned schedule"
+
+
+def test_tuner_scratch_failure_on_one_rank_fails_everywhere(gpu):
+    """One rank cannot set up the tuner's scratch copies (TIPS_TUNE_TEST_FAIL_RANK): every rank
+    learns it from one small allreduce before any candidate's transfers, and every rank's call
+    fails with TIPS_ERR_HIP instead of the others waiting forever in a group for it."""
+    env = rccl_env("tune")
+    env["TIPS_TUNE_TEST_FAIL_RANK"] = "1"
+    results = run_job(3, [{"dtype": F32, "n": 3 << 20, "seed": 1, "expect_error": -3}], **env)
+    check(results)
+    for res in results:
+        assert "some rank" in res["results"][0].get("error", ""), res
+

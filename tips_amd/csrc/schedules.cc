@@ -385,14 +385,30 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choi
   if (p <= tips::kMaxSrcs && env_i64("TIPS_TUNE_PEER", 0)) cand.push_back({TIPS_ALGO_PEER, 0, 1});
   HIP_TRY(hipStreamSynchronize(user));
   void *sin = nullptr, *sout = nullptr;
-  HIP_TRY(hipMalloc(&sin, (size_t)bytes));
   int rc = 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   std::vector<double> ms(cand.size(), 1e30);
   do {
-    if (hipMalloc(&sout, (size_t)bytes) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
-        hipEventCreate(&e1) != hipSuccess || hipMemcpyAsync(sin, in, (size_t)bytes, hipMemcpyDeviceToDevice, user) != hipSuccess) {
-      rc = fail(TIPS_ERR_HIP, "tune: scratch setup failed");
+    // scratch copies of the input: every rank learns whether every rank has them before any
+    // candidate's transfers start (one rank out of memory must fail the call everywhere, not
+    // leave the others waiting in a group for it)
+    int32_t ok = hipMalloc(&sin, (size_t)bytes) == hipSuccess && hipMalloc(&sout, (size_t)bytes) == hipSuccess &&
+                 hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+                 hipMemcpyAsync(sin, in, (size_t)bytes, hipMemcpyDeviceToDevice, user) == hipSuccess;
+    (void)hipGetLastError();
+    if (env_i64("TIPS_TUNE_TEST_FAIL_RANK", -1) == st.rank) ok = 0;  // (tests: one rank short of memory)
+    int32_t* dok = nullptr;
+    if ((rc = order_after_replays(st)) != 0) break;
+    if (hipMalloc(&dok, sizeof(int32_t)) != hipSuccess ||
+        hipMemcpyAsync(dok, &ok, sizeof ok, hipMemcpyHostToDevice, st.comm_stream) != hipSuccess ||
+        ncclAllReduce(dok, dok, 1, ncclInt32, ncclMin, st.comm, st.comm_stream) != ncclSuccess ||
+        hipMemcpyAsync(&ok, dok, sizeof ok, hipMemcpyDeviceToHost, st.comm_stream) != hipSuccess ||
+        hipStreamSynchronize(st.comm_stream) != hipSuccess)
+      rc = fail(TIPS_ERR_RCCL, "tune: agreeing on the scratch buffers failed");
+    if (dok) (void)hipFree(dok);
+    if (rc) break;
+    if (!ok) {
+      rc = fail(TIPS_ERR_HIP, "tune: scratch buffers (2 x %lld bytes) could not be set up on some rank", (long long)bytes);
       break;
     }
     for (size_t c = 0; c < cand.size() && rc == 0; c++) {
@@ -435,7 +451,7 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choi
   HIP_TRY(hipStreamSynchronize(user));
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
-  (void)hipFree(sin);
+  if (sin) (void)hipFree(sin);
   if (sout) (void)hipFree(sout);
   if (rc) return rc;
   size_t b = 0;
