@@ -140,3 +140,18 @@ def test_tuner_scratch_failure_on_one_rank_fails_everywhere(gpu):
     for res in results:
         assert "some rank" in res["results"][0].get("error", ""), res
 
+
+def test_staging_failure_on_one_rank_fails_everywhere(gpu):
+    """Staging grows at the same call on every rank (its size depends only on the plan's
+    arguments: tests/test_plans.py::test_staging_size_is_rank_independent), so the ranks agree on
+    the outcome: one rank that cannot allocate it (TIPS_STAGING_TEST_FAIL_RANK) fails that call on
+    every rank rather than leaving the others in a group waiting for it; a later call that needs no
+    growth runs normally, bit-exact."""
+    env = rccl_env("direct")
+    env["TIPS_STAGING_TEST_FAIL_RANK"] = "2"
+    results = run_job(3, [{"dtype": F32, "n": 3 << 20, "seed": 1, "expect_error": -3},
+                          {"dtype": F32, "n": 1 << 20, "seed": 2}], **env)
+    check(results)
+    for res in results:
+        assert "some rank" in res["results"][0].get("error", ""), res
+

@@ -32,6 +32,16 @@ def test_send_recv_pairing(algo, p):
                     raise AssertionError("algo %d p %d n %d K %d dtype %d: %s" % (algo, p, n, K, dtype, e))
 
 
+@pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
+def test_staging_size_is_rank_independent(algo):
+    """Every rank's plan asks for the same staging bytes, so staging grows at the same call on
+    every rank and the ranks can agree on the allocation (schedules.cc grow_staging)."""
+    for p in (2, 3, 5, 8, 16):
+        for n in (1, 7, 4099, 262147, (1 << 20) + 3):
+            for K in ((1, 2, 4) if algo != pu.ONESHOT else (1,)):
+                assert len({pu.dump(algo, p, r, n, F32, K)["staging"] for r in range(p)}) == 1, (p, n, K)
+
+
 def test_bucket_bytes_conserved():
     """Config 3's shape (p = 8, 1 GiB f32): each rank sends 2(p-1)/p of the bucket in the ring and
     in direct (the bandwidth-optimal volume), (p-1) buckets in one-shot; every chunk byte is summed once."""

@@ -315,11 +315,35 @@ int replay(State& st, hipGraphExec_t exec, hipStream_t user) {
   return 0;
 }
 
+// Staging grows at the same call on every rank (its size is a function of the plan, which every
+// rank builds from the same arguments), so the ranks can agree on the outcome: one rank unable to
+// allocate fails the call on every rank instead of leaving the others waiting in a group for it.
+int grow_staging(State& st, int64_t bytes) {
+  int32_t ok = st.staging.ensure((size_t)std::max<int64_t>(bytes, 1)) == 0;
+  if (env_i64("TIPS_STAGING_TEST_FAIL_RANK", -1) == st.rank) ok = 0;  // (tests: one rank short of memory)
+  const std::string why = ok ? std::string() : last_error();
+  TRY(order_after_replays(st));
+  int32_t* d = nullptr;
+  int rc = 0;
+  if (hipMalloc(&d, sizeof(int32_t)) != hipSuccess ||
+      hipMemcpyAsync(d, &ok, sizeof ok, hipMemcpyHostToDevice, st.comm_stream) != hipSuccess ||
+      ncclAllReduce(d, d, 1, ncclInt32, ncclMin, st.comm, st.comm_stream) != ncclSuccess ||
+      hipMemcpyAsync(&ok, d, sizeof ok, hipMemcpyDeviceToHost, st.comm_stream) != hipSuccess ||
+      hipStreamSynchronize(st.comm_stream) != hipSuccess)
+    rc = fail(TIPS_ERR_RCCL, "agreeing on the staging allocation failed");
+  if (d) (void)hipFree(d);
+  if (rc) return rc;
+  if (!ok)
+    return fail(TIPS_ERR_HIP, "staging of %lld bytes could not be allocated on some rank%s%s", (long long)bytes,
+                why.empty() ? "" : ": ", why.c_str());
+  return 0;
+}
+
 int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t user, int L = 1) {
   L = std::max(1, std::min(L, (int)pl.steps.size()));
   const size_t nsteps = pl.steps.size();
   void* const stg_before = st.staging.p;
-  TRY(st.staging.ensure((size_t)std::max<int64_t>(pl.staging_bytes, 1)));
+  if ((size_t)std::max<int64_t>(pl.staging_bytes, 1) > st.staging.bytes) TRY(grow_staging(st, pl.staging_bytes));
   if (st.staging.p != stg_before && st.graphs) {  // graphs of the old staging can never replay again
     for (auto& kv : st.graphs->m) destroy_exec(st, kv.second.exec);
     st.graphs->m.clear();
