@@ -404,12 +404,13 @@ def link_probe(dist, rank, world, mib=256, iters=5, backend="nccl", device="cuda
 def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, fixed_ms):
     """The same gradients through the training API instead of fixed views: every gradient its own
     allocation (a parameter's .grad), as a model hands them over.
-      optimizer:       DistributedOptimizer.synchronize() - the allreduce half of step(): .grad
-                       summed in place through the fusion buckets (tips_fused_allreduce)
-      allreduce_grads: allreduce_grads(grads) - new output tensors (tips_fused_allreduce_oop)
-    Both move 4 x the gradient bytes in HBM for pack + unpack (no clone). On one rank both are
-    the identity, as the reference's _allreduce_cond (__init__.py:94-103); there the call each
-    makes at N > 1 is timed instead (fused_allreduce_ / fused_allreduce on the same lists).
+      optimizer:       DistributedOptimizer.synchronize() - the allreduce half of step(): every
+                       .grad a view of one flat buffer (gradient bucket views), the flat buffer
+                       allreduced in place (no pack, no unpack; the first step copies .grad in)
+      allreduce_grads: allreduce_grads(grads) - new output tensors (tips_fused_allreduce_oop:
+                       4 x the gradient bytes in HBM for pack + unpack, no clone)
+    On one rank both are the identity, as the reference's _allreduce_cond (__init__.py:94-103);
+    there the call each makes at N > 1 is timed instead.
     Host-timed like the main line, over the same rotating sets; max over ranks."""
     rot = len(rot_sets)
     params = []
@@ -427,15 +428,14 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         from tips_amd.ops import FusedList
         fls = [FusedList([p_.numel() for p_ in ps]) for ps in params]
         flats = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads]  # the optimizer's bucket views
-        views = [list(torch.split(f, sizes)) for f in flats]
-        fvs = [FusedList(sizes) for _ in flats]
-        calls = {"optimizer": lambda i: fvs[i].allreduce_(views[i]),
+        from tips_amd.optim import _allreduce_flat_
+        calls = {"optimizer": lambda i: _allreduce_flat_(flats[i]),
                  "packed_separate_grads": lambda i: fls[i].allreduce_(grads[i]),
                  "allreduce_grads": lambda i: tips_amd.fused_allreduce(grads[i])}
         what = ("one rank: both API calls are the identity (reference _allreduce_cond); timed is what each runs at "
-                "N > 1: the optimizer's FusedList.allreduce_ over its gradient bucket views (one contiguous run, "
-                "reduced where it lies: no device work at all on one rank), the same over separately allocated "
-                "gradients (pack + unpack), and allreduce_grads' fused_allreduce(grads) out of place")
+                "N > 1: the optimizer's in-place allreduce of the flat buffer its gradient bucket views live in "
+                "(no device work at all on one rank), FusedList.allreduce_ over separately allocated gradients "
+                "(pack + unpack), and allreduce_grads' fused_allreduce(grads) out of place")
     out = {"calls": what, "bytes_per_rank": sum(sizes) * 4, "fixed_view_ms": round(fixed_ms, 4)}
     ref = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads] if world == 1 else None
     for name, fn in calls.items():
@@ -561,10 +561,10 @@ def bench_allreduce(args):
     # the schedule the (largest) reduced buffer gets: the bucket itself, or a <= 64 MiB fusion bucket
     algo = L.tips_resolve_algorithm(world, sizes[0] * 4 if workload == "bucket" else
                                     max(sizes) * 4 if workload == "negotiated1000" else 64 << 20)
-    # every tensor at a 256-B aligned offset of one flat buffer, 256 B apart at least (separate
-    # allocations of a caching allocator never touch): the fusion path packs them. (Back-to-back
-    # tensors - a flat gradient buffer's views - are reduced where they lie instead; that path is
-    # the gradient_api "optimizer" leg.)
+    # every tensor at a 256-B aligned offset of one flat buffer, 256 B apart at least, as separate
+    # allocations of a caching allocator lie: the fusion path packs them (its layout depends only on
+    # the counts). (A flat gradient buffer allreduced as one tensor is the gradient_api
+    # "optimizer" leg.)
     offs, total = [], 0
     gap = 64 if workload in ("fused1000", "resnet50") else 0  # (the bucket / named workloads: no gap)
     for k in sizes:

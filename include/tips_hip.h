@@ -188,9 +188,11 @@ TIPS_API int tips_host_unregister(void* ptr);
 /* Tensor fusion (no reference counterpart): allreduce n device
  * tensors in place, packed into buckets of at most the fusion threshold
  * (TIPS_FUSION_THRESHOLD bytes, default 64 MiB; tensors at or above it are
- * reduced on their own). One dtype for all. Stream-ordered on `stream`; calls
- * from different streams are safe (every bucket operation runs on the
- * library's fusion streams, joined with the caller's stream both ways). */
+ * reduced on their own). One dtype for all. The bucket layout depends only on
+ * counts, dtype and threshold, never on where the tensors lie, so every rank
+ * pairs the same elements. Stream-ordered on `stream`; calls from different
+ * streams are safe (every bucket operation runs on the library's fusion
+ * streams, joined with the caller's stream both ways). */
 TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
 /* The same, out of place: outs[i] = SUM over ranks of ins[i] (ins[i] == outs[i]
  * allowed); the inputs are left unchanged. What the reference's per-gradient

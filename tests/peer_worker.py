@@ -241,7 +241,9 @@ def workload_sizes(name):
 def fused_case(c, rank, size, L, _lib, sp):
     """BASELINE config 4 (1000 fp32 grads, 2^U(8,17) elements) or config 5 (the 214 ResNet-50
     gradients) through the fusion buckets, as the named API would run them every step:
-    mode "inplace" (tips_fused_allreduce), "oop" (tips_fused_allreduce_oop), "grads"
+    mode "inplace" (tips_fused_allreduce), "layouts" (the same list, views of one buffer on rank 0
+    and separate allocations elsewhere: the layout must not depend on addresses), "oop"
+    (tips_fused_allreduce_oop), "grads"
     (tips_amd.allreduce_grads, the reference's per-gradient loop fused, __init__.py:203-222) or
     "optimizer" (DistributedOptimizer.step over SGD(lr=1): p - sum of all ranks' gradients).
     Every tensor is checked bit-exact against the oracle's rank-order fold of all ranks' inputs
@@ -261,11 +263,14 @@ def fused_case(c, rank, size, L, _lib, sp):
     mine = inputs(rank)
     views = list(torch.split(mine, sizes))
     before = mine.clone()
-    if mode == "inplace":  # views of one flat buffer: one contiguous run, reduced where it lies
+    if mode == "inplace":  # views of one flat buffer (packed like any tensors: the layout ignores addresses)
         tips_amd.fused_allreduce_(views)
         got = views
     elif mode == "inplace_separate":  # separately allocated tensors: packed into the buckets
         got = [v.clone() for v in views]
+        tips_amd.fused_allreduce_(got)
+    elif mode == "layouts":  # rank 0: views of one flat buffer; the others: separate tensors
+        got = views if rank == 0 else [v.clone() for v in views]
         tips_amd.fused_allreduce_(got)
     elif mode == "oop":
         got = tips_amd.fused_allreduce(views)

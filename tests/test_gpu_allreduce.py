@@ -206,18 +206,19 @@ def test_fused_pack_unpack_round_trip(gpu, monkeypatch, threshold, measure_pack)
             assert torch.equal(o, b)
 
 
-def test_fused_contiguous_runs(gpu, monkeypatch):
-    """Tensors that follow each other in memory (a flat buffer's views) form one run, reduced where
-    it lies without packing (fusion.cc build_entry): in place it must leave the bytes around the run
-    alone; out of place into the views of another flat buffer it is one in -> out allreduce. Mixed
-    with separate tensors and a gap that splits two runs."""
+def test_fused_views_of_one_buffer(gpu, monkeypatch):
+    """Views of one flat buffer mixed with separate tensors (measure-pack mode: every byte through
+    pack -> bucket -> unpack at one rank): the layout ignores where tensors lie, so the views are
+    packed like any tensor; in place it must leave the bytes around them alone; out of place into
+    the views of another flat buffer."""
     import torch
-    monkeypatch.setenv("TIPS_FUSION_DIRECT_BYTES", str(1 << 16))
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", "1")
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(1 << 18))
     sizes = [1000, 3, 70000, 257, 20000]
     flat = torch.randn(sum(sizes) + 10, device="cuda")
     guard = flat[-10:].clone()
     run = list(torch.split(flat[:sum(sizes)], sizes))
-    other = [torch.randn(n, device="cuda") for n in (5, 9999)]
+    other = [torch.randn(n, device="cuda") for n in (5, 9999, 70000)]
     lst = run[:2] + other[:1] + run[2:] + other[1:]
     before = [t.clone() for t in lst]
     gpu.fused_allreduce_(lst)

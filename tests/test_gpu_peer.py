@@ -164,7 +164,7 @@ def test_fusion_workloads_8_processes(gpu, workload):
     place, allreduce_grads and DistributedOptimizer.step(); every tensor bit-exact against the
     oracle's rank-order fold of the 8 ranks' gradients (reference per-gradient loop:
     tips/tensorflow/__init__.py:203-222)."""
-    cases = [{"fused": workload, "seed": 3, "mode": m} for m in ("inplace", "inplace_separate", "oop", "grads", "optimizer")]
+    cases = [{"fused": workload, "seed": 3, "mode": m} for m in ("inplace", "inplace_separate", "layouts", "oop", "grads", "optimizer")]
     check(run_job(8, cases, timeout=600, TIPS_PEER_WS_MIB="64"))
 
 

@@ -75,8 +75,10 @@ def test_rccl_transport_is_real(gpu):
 def test_fusion_workloads_over_rccl(gpu, workload, p):
     """Configs 4 and 5 through the fusion buckets over real RCCL ranks with the default (AUTO)
     schedule: direct for every bucket at p > 2, one-shot for buckets of 256 KiB or less; in place,
-    out of place, allreduce_grads and DistributedOptimizer.step(), bit-exact against the fold."""
-    cases = [{"fused": workload, "seed": 4, "mode": m} for m in ("inplace", "inplace_separate", "oop", "grads", "optimizer")]
+    out of place, allreduce_grads and DistributedOptimizer.step(), and with rank 0's tensors views of
+    one buffer while the others' are separate allocations; bit-exact against the fold."""
+    cases = [{"fused": workload, "seed": 4, "mode": m}
+             for m in ("inplace", "inplace_separate", "layouts", "oop", "grads", "optimizer")]
     check(run_job(p, cases, timeout=600, **rccl_env("auto")))
 
 

@@ -52,7 +52,7 @@ struct Entry {
   std::vector<void*> outs;
   std::vector<int64_t> counts;
   std::vector<Bucket> buckets;
-  std::vector<BatchItem> direct;  // runs reduced where they lie, without packing (see build_entry)
+  std::vector<BatchItem> direct;  // tensors of at least the threshold, reduced where they lie (build_entry)
   CopyTile* dev = nullptr;   // descriptor table in HBM
   size_t ntiles = 0;
   uint64_t stamp = 0;        // last use (LRU)
@@ -104,15 +104,16 @@ void free_entry(State& st, Entry* e) {
 
 // Build a tensor list's buckets and descriptors; upload the table on fuse_stream.
 //
-// Tensors that follow each other in memory with no gap - in both their inputs and their
-// outputs - form one run and are handled as one segment (a flat gradient buffer's views are one
-// run). A run is reduced where it lies, with no pack and no unpack, when it is a single tensor of
-// at least the threshold or several tensors of at least TIPS_FUSION_DIRECT_BYTES (4 MiB) together:
-// only its own bytes are touched, so nothing outside the tensors changes. Every other run is
-// packed into the current bucket at a 256-B aligned offset.
+// The layout is a function of the element counts, the dtype and the threshold alone - never of
+// where the tensors lie - because every rank must issue the same allreduces over the same bucket
+// offsets: a tensor of at least the threshold is reduced where it lies (its own allreduce, only
+// its own bytes touched); every other tensor is packed into the current bucket at a 256-B aligned
+// offset. (An earlier version reduced tensors that happened to lie back to back in memory as one
+// run; an allocator that placed them so on one rank and not on another would have paired
+// different elements across ranks. A flat buffer is reduced without copies by allreducing the
+// buffer itself: DistributedOptimizer does that with its gradient bucket views.)
 int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, int n, int64_t threshold) {
   const int64_t es = tips::dtype_size(e->dtype), tile = e->tile;
-  const int64_t direct_min = std::min(threshold, std::max<int64_t>(kAlignBytes, env_i64("TIPS_FUSION_DIRECT_BYTES", 4 << 20)));
   std::vector<CopyTile> pack, unpack;
   std::vector<int64_t> sizes;  // per bucket
   std::vector<int64_t> first;  // per bucket: first tile index into pack / unpack
@@ -132,13 +133,13 @@ int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, in
     if (nb < 2 && packed >= (32 << 20) && env_i64("TIPS_FUSION_BALANCE", 1)) nb = 2;
     if (nb > 1 && env_i64("TIPS_FUSION_BALANCE", 1)) target = std::min(threshold, round_up((packed + nb - 1) / nb, kAlignBytes));
   }
-  auto place = [&](const char* in, char* out, int64_t bytes, int members) {
+  auto place = [&](const char* in, char* out, int64_t bytes) {
     if (e->identity) {  // one rank: in place nothing, out of place a copy
       for (int64_t t = 0; in != out && t < bytes; t += tile)
         pack.push_back(CopyTile{in + t, out + t, std::min(tile, bytes - t)});
       return;
     }
-    if (bytes >= threshold || (members > 1 && bytes >= direct_min)) {
+    if (bytes >= threshold) {
       e->direct.push_back(BatchItem{in, out, bytes / es});
       return;
     }
@@ -157,27 +158,10 @@ int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, in
     }
     sizes.back() = off + bytes;
   };
-  const char* run_in = nullptr;
-  char* run_out = nullptr;
-  int64_t run_bytes = 0;
-  int members = 0;
   for (int i = 0; i < n; i++) {
     const int64_t bytes = items[i].count * es;
-    if (bytes == 0) continue;
-    const char* in = (const char*)items[i].in;
-    char* out = (char*)items[i].out;
-    if (members > 0 && in == run_in + run_bytes && out == run_out + run_bytes) {
-      run_bytes += bytes;
-      members++;
-      continue;
-    }
-    if (members > 0) place(run_in, run_out, run_bytes, members);
-    run_in = in;
-    run_out = out;
-    run_bytes = bytes;
-    members = 1;
+    if (bytes > 0) place((const char*)items[i].in, (char*)items[i].out, bytes);
   }
-  if (members > 0) place(run_in, run_out, run_bytes, members);
   const int64_t npack = (int64_t)pack.size();
   for (size_t b = 0; b < sizes.size(); b++) {
     const int64_t end = b + 1 < sizes.size() ? first[b + 1] : npack;
@@ -316,7 +300,7 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
     TRY(join(user, st.fuse_stream, st.ev_done));
     return 0;
   } else {
-    // bucket stream: the direct runs first (nothing to pack: their exchange starts at once and
+    // bucket stream: the direct tensors first (nothing to pack: their exchange starts at once and
     //                overlaps pack(0)), then allreduce(b) after pack(b)
     // fuse stream:   pack(0) pack(1) | unpack(0) pack(2) | unpack(1) pack(3) | ... unpack(B-1);
     //                unpack(b) after allreduce(b); pack(b+2) reuses slot b % 2 after unpack(b)

@@ -22,6 +22,14 @@ import warnings
 Average = 'Average'
 
 
+def _allreduce_flat_(flat):
+    """In-place SUM of one contiguous device tensor over the ranks (tips_allreduce, in == out)."""
+    from . import _lib, basics, tensors
+    basics.init()
+    _lib.call("tips_allreduce", flat.data_ptr(), flat.data_ptr(), flat.numel(), tensors.dtype_code(flat), _lib.OP_SUM,
+              tensors.stream_of(flat))
+
+
 class _DistributedOptimizer(object):
     """Wraps a torch.optim.Optimizer; step() allreduces the gradients first (__init__.py:252-335)."""
 
@@ -66,10 +74,11 @@ class _DistributedOptimizer(object):
     def synchronize(self):
         """Allreduce every parameter's .grad (compute_gradients, __init__.py:296-310).
 
-        Dense contiguous device gradients without compression are summed IN PLACE through the
-        fusion buckets (tips_fused_allreduce: pack, one allreduce per bucket, unpack straight
-        back into .grad - 4 x the gradient bytes of HBM traffic, no copies). The others go
-        through allreduce_grads and are replaced by its outputs."""
+        Dense contiguous device gradients without compression are summed IN PLACE: with gradient
+        bucket views (default) as one allreduce of the flat buffer they are views of, no copies;
+        with TIPS_GRAD_BUCKET_VIEW=0 through the fusion buckets (tips_fused_allreduce: pack, one
+        allreduce per bucket, unpack straight back into .grad - 4 x the gradient bytes of HBM
+        traffic). The others go through allreduce_grads and are replaced by its outputs."""
         from . import Compression, _fusable, allreduce_grads, size
         from .ops import FusedList
         params = self._params_with_grad()
@@ -107,10 +116,11 @@ class _DistributedOptimizer(object):
             fl, flat, offs = ent
             if flat is not None:
                 # Gradient bucket views: every .grad becomes a view of one flat buffer, back to back,
-                # so the fused allreduce finds ONE contiguous run and reduces it where it lies - no
-                # pack, no unpack (fusion.cc build_entry). A .grad that is not (or no longer) its
-                # view - the first step, or after zero_grad(set_to_none=True) - is copied in once;
-                # with set_to_none=False autograd accumulates straight into the views.
+                # and the flat buffer is allreduced in place as one tensor - no pack, no unpack. Its
+                # size is the sum of the parameters' sizes, the same on every rank. A .grad that is
+                # not (or no longer) its view - the first step, or after
+                # zero_grad(set_to_none=True) - is copied in once; with set_to_none=False autograd
+                # accumulates straight into the views.
                 base, es = flat.data_ptr(), flat.element_size()
                 for p, o in zip(group, offs):
                     g = p.grad
@@ -118,7 +128,9 @@ class _DistributedOptimizer(object):
                         v = flat[o:o + g.numel()].view_as(g)
                         v.copy_(g)
                         p.grad = v
-            fl.allreduce_([p.grad for p in group])
+                _allreduce_flat_(flat)
+            else:
+                fl.allreduce_([p.grad for p in group])
         if rest:
             reduced = allreduce_grads([p.grad for p in rest], compression=self._compression, op=self._op,
                                       sparse_as_dense=self._sparse_as_dense)
