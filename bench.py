@@ -456,7 +456,7 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
                 leg["hbm_achieved_GBps"] = round(moved / t / 1e9, 1)
             got = fn(0)
             torch.cuda.synchronize()
-            got = {"optimizer": views[0], "packed_separate_grads": grads[0]}.get(name, got)
+            got = {"optimizer": [flats[0]], "packed_separate_grads": grads[0]}.get(name, got)
             leg["check"] = "identity, bit-exact" if torch.equal(torch.cat([g.reshape(-1) for g in got]), ref[0]) else "FAIL"
         out[name] = leg
     del params, grads, opts
