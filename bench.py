@@ -26,6 +26,7 @@ a reported baseline, not the target.
 import argparse
 import json
 import os
+import signal
 import subprocess
 import sys
 import time
@@ -54,6 +55,8 @@ def parse():
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
+    ap.add_argument("--no-env-variants", action="store_true",
+                    help="N>1: skip the child jobs that rerun direct under other RCCL settings")
     ap.add_argument("--no-extras", action="store_true",
                     help="N=1: time the headline kernel only (no same-buffer, PCIe or host-memory legs), as under rocprofv3")
     ap.add_argument("--workload", default="auto", choices=["auto", "sum", "bucket", "fused1000", "resnet50", "negotiated1000"],
@@ -463,6 +466,70 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
     return out
 
 
+# RCCL reads these once, at its first communicator: a setting can only be compared in a job of its
+# own. NCCL_NCHANNELS_PER_PEER is how many channels RCCL gives each peer of a point-to-point group
+# (the direct schedule's whole exchange); RCCL's own all-pairs allreduce for 8 GPUs
+# (share/rccl/msccl-algorithms/allreduce-allpairs-8n-*.xml) runs 8 thread blocks per peer.
+# (8 per peer is left out: over RCCL's socket transport a plain grouped ncclSend/ncclRecv then
+# delivers wrong bytes, no TIPS code involved - profiles/r02/rccl_nchannels_probe.txt.)
+ENV_VARIANTS = [("nchannels_per_peer_4", {"NCCL_NCHANNELS_PER_PEER": "4"})]
+
+
+def env_variant_jobs(args, dist, rank, world, timeout_s=240):
+    """Rank 0 reruns the bucket allreduce with the direct schedule as a child job of `world` ranks
+    (torch.distributed.run, the same GPUs) per RCCL setting in ENV_VARIANTS, while every rank of
+    this job waits at a gloo barrier, idle on the GPU. A child that fails or outlasts `timeout_s`
+    is killed (its own process group) and reported; the main line is never at stake."""
+    import socket
+    out = {}
+    for name, env in ENV_VARIANTS:
+        dist.barrier()
+        if rank == 0:
+            s_ = socket.socket()
+            s_.bind(("127.0.0.1", 0))
+            port = s_.getsockname()[1]
+            s_.close()
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                   "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+                   "--gpus", str(world), "--steps", "10", "--warmup", "2", "--algo", "direct", "--no-compare",
+                   "--no-env-variants"] + (["--bucket-mib", str(args.bucket_mib)] if args.bucket_mib else [])
+            cenv = {k: v for k, v in os.environ.items()
+                    if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                                 "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TIPS_BOOTSTRAP_PORT")}
+            cenv.update(env)
+            res = {"env": env}
+            # within this job's watchdog, with a margin for the line and teardown
+            budget = min(timeout_s, int(_RESULT.get("deadline", time.time() + timeout_s) - time.time()) - 40)
+            if budget < 60:
+                out[name] = dict(res, error="skipped: %d s left before the watchdog" % (budget + 40))
+                dist.barrier()
+                continue
+            cenv["TIPS_BENCH_WATCHDOG"] = str(budget - 15)
+            try:
+                p = subprocess.Popen(cmd, env=cenv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                     start_new_session=True)
+                _RESULT["child_pgid"] = p.pid
+                try:
+                    o, e = p.communicate(timeout=budget)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    o, e = p.communicate()
+                    res["error"] = "timed out after %d s" % budget
+                _RESULT["child_pgid"] = None
+                lines = [ln for ln in (o or "").splitlines() if ln.startswith("{")]
+                if lines:
+                    d = json.loads(lines[-1])
+                    res.update({k: d.get(k) for k in ("value", "ms_per_step", "check", "error")})
+                    res["algbw_gib_s"] = d.get("algbw_gib_s")
+                elif "error" not in res:
+                    res["error"] = "no result line (exit %s): %s" % (p.returncode, (e or "")[-400:])
+            except Exception as ex:  # noqa: BLE001 - a variant never costs the main line
+                res["error"] = "%s: %s" % (type(ex).__name__, ex)
+            out[name] = res
+        dist.barrier()
+    return out
+
+
 _RESULT = {}  # rank 0's finished result line, if the main measurement completed
 
 
@@ -491,6 +558,11 @@ def start_watchdog(seconds, rank):
 
     def fire():
         sys.stderr.write("bench.py rank %d: watchdog fired after %d s (hung collective?)\n" % (rank, seconds))
+        if _RESULT.get("child_pgid"):  # an RCCL-setting child job still running: it goes too
+            try:
+                os.killpg(_RESULT["child_pgid"], signal.SIGKILL)
+            except OSError:
+                pass
         line = _RESULT.get("line")
         if _RESULT.get("printed"):  # the one JSON line is out; only teardown hung
             os._exit(0)
@@ -502,6 +574,7 @@ def start_watchdog(seconds, rank):
             print(json.dumps(line), flush=True)
         os._exit(0 if _RESULT.get("done") else 3)
 
+    _RESULT["deadline"] = time.time() + seconds
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()
@@ -894,6 +967,10 @@ def bench_allreduce(args):
                                                   "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
     line["compare_check"] = compare_check
     line["compare_algbw_gib_s"] = compare
+    if world > 1 and workload == "bucket" and not args.no_compare and not args.no_env_variants \
+            and not os.environ.get("TIPS_NO_RCCL"):
+        note_progress("the RCCL-setting child jobs")
+        line["env_variants"] = env_variant_jobs(args, dist, rank, world)
     ring_algbw = algbw if algo == _lib.ALGO_RING else (compare.get("ring") or 0) * GIB
     if world > 1 and workload == "bucket" and ring_algbw:  # the north star's ring target: >= 70 % of one xGMI link
         rb = ring_algbw * 2 * (world - 1) / world

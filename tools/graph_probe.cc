@@ -70,7 +70,7 @@ int main(int argc, char** argv) {
   }
   ncclComm_t comm;
   NK(ncclCommInitRank(&comm, size, id, rank));
-  const size_t n = 1 << 20;
+  const size_t n = getenv("PROBE_N") ? (size_t)atoll(getenv("PROBE_N")) : (size_t)1 << 20;  // floats per buffer
   float *a, *b;
   CK(hipMalloc(&a, n * 4));
   CK(hipMalloc(&b, n * 4 * (size_t)size));
@@ -152,6 +152,13 @@ int main(int argc, char** argv) {
     return ok ? 0 : 1;
   };
   if (reset() || body() || check("eager")) return 1;
+  if (getenv("PROBE_EAGER_ONLY")) {
+    for (int it = 0; it < 3; it++)
+      if (reset() || body() || check("eager again")) return 1;
+    NK(ncclCommDestroy(comm));
+    printf("rank %d mode %d: PASS (eager only)\n", rank, mode);
+    return 0;
+  }
   if (nosync) {  // more eager calls still in flight when the capture starts (PROBE_NOSYNC=1)
     if (reset()) return 1;
     for (int it = 0; it < 2; it++)
