@@ -157,3 +157,25 @@ def test_staging_failure_on_one_rank_fails_everywhere(gpu):
     for res in results:
         assert "some rank" in res["results"][0].get("error", ""), res
 
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_control_plane_and_api_over_rccl(gpu, p):
+    """The rest of the surface over real RCCL ranks (so far only run over the peer transport):
+    named requests through the negotiation thread (300 tensors, 6 dtypes, a different enqueue
+    order on every rank), broadcast / allgatherv / the checked allreduce on RCCL collectives,
+    DistributedOptimizer, DistributedGradientTape, host buffers (bounce pair and pipelined
+    pieces) and the shape validation of named requests; bit-exact against the oracle's fold."""
+    import numpy as np
+    from gpu_util import F16, F64, I32
+    rng = np.random.default_rng(13)
+    dts = [F32, F32, F32, F64, I32, F16]
+    tensors = [[int(dts[int(rng.integers(len(dts)))]), int(rng.choice([0, 1, 7, 300, 4099, 65536, 300000]))]
+               for _ in range(300)]
+    cases = [{"named": tensors, "seed": 5}, {"collectives": True, "seed": 5 + p, "big": 1536 * 1024},
+             {"optimizer": True, "seed": 7}, {"tape": True, "seed": 11}, {"shapes": True}]
+    cases += [{"dtype": d, "n": n, "seed": 40 + d, "host": True, "inplace": inplace}
+              for d in (F32, I32, F16) for n, inplace in ((1000, False), (1310721, True))]
+    env = rccl_env("auto")
+    env.update(TIPS_FUSION_THRESHOLD=str(1 << 20), TIPS_HOST_PIECE_BYTES=str(1 << 20))
+    check(run_job(p, cases, timeout=600, **env))

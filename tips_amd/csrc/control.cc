@@ -31,7 +31,9 @@ int exchange_i64(State& st, const int64_t* mine, int words, std::vector<int64_t>
     TRY(peer_allgatherv(st, (const char*)(d + (size_t)words * st.size), (char*)d, b.data(), disp.data(), st.io_stream));
   } else {
     TRY(ensure_comm(st));
+    TRY(rccl_enter(st, st.io_stream));
     NCCL_TRY(ncclAllGather(d + (size_t)words * st.size, d, (size_t)words, ncclInt64, st.comm, st.io_stream));
+    TRY(rccl_leave(st, st.io_stream));
   }
   HIP_TRY(hipMemcpyAsync(all->data(), d, sizeof(int64_t) * words * st.size, hipMemcpyDeviceToHost, st.io_stream));
   HIP_TRY(hipStreamSynchronize(st.io_stream));
@@ -151,8 +153,18 @@ int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root
     if (peer_selected(st))
       return peer_broadcast(st, (const char*)i, (char*)o, (int64_t)bytes, root, s);
     TRY(ensure_comm(st));
+    // every rank must name the same root and size, or ncclBroadcast pairs nothing (the peer
+    // schedule checks the same at its call barrier): one small exchange, the same verdict everywhere
+    const int64_t mine[2] = {root, (int64_t)bytes};
+    std::vector<int64_t> all;
+    TRY(exchange_i64(st, mine, 2, &all));
+    for (int j = 0; j < st.size; j++)
+      if (all[2 * j] != root || all[2 * j + 1] != (int64_t)bytes)
+        return fail(TIPS_ERR_MISMATCH, "broadcast: rank %d broadcasts %lld B from root %lld, rank %d %lld B from root %d",
+                    j, (long long)all[2 * j + 1], (long long)all[2 * j], st.rank, (long long)bytes, root);
+    TRY(rccl_enter(st, s));
     NCCL_TRY(ncclBroadcast(i, o, bytes, ncclInt8, root, st.comm, s));
-    return 0;
+    return rccl_leave(st, s);
   });
 }
 
@@ -187,6 +199,7 @@ int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* cou
                         return peer_allgatherv(st, (const char*)i, ob, b.data(), d.data(), s);
                       }
                       TRY(ensure_comm(st));
+                      TRY(rccl_enter(st, s));
                       NCCL_TRY(ncclGroupStart());
                       for (int r = 0; r < st.size; r++) {
                         if (r == st.rank) continue;
@@ -195,7 +208,7 @@ int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* cou
                           NCCL_TRY(ncclRecv(ob + disp[r] * es, (size_t)(counts[r] * es), ncclInt8, r, st.comm, s));
                       }
                       NCCL_TRY(ncclGroupEnd());
-                      return 0;
+                      return rccl_leave(st, s);
                     });
 }
 

@@ -167,6 +167,7 @@ struct State {
   // graph and then replayed with one launch on graph_stream, which joins the caller both ways
   hipStream_t graph_stream = nullptr;
   hipEvent_t ev_graph[5] = {};  // replay joins: caller in, comm in, comp in, caller out, eager after replays
+  hipEvent_t ev_rccl[2] = {};   // rccl_enter / rccl_leave
   PlanGraphs* graphs = nullptr;
   bool graph_pending = false;  // a replay may still run on graph_stream: eager plan work waits for it
   bool eager_pending = false;  // eager plan work was queued on comm / comp since the last replay
@@ -195,6 +196,13 @@ void rccl_env_defaults();  // before any ncclCommInitRank of ours
 // schedules.cc: device-resident allreduce, caller holds st.mu
 int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream);
 void graphs_release(State& st);  // schedules.cc (shutdown, before the communicator goes)
+// schedules.cc: an RCCL operation on `comm` issued outside a plan (a control-plane collective, the
+// TIPS_ALGO_RCCL comparison) goes on stream `s` between these two calls: after everything queued
+// for the communicator (the comm stream, whose prologues also wait for the transfer lanes and the
+// replayed plans), and before everything queued for it later. Two RCCL kernels of one
+// communicator then never run at the same time, whatever streams the callers use.
+int rccl_enter(State& st, hipStream_t s);
+int rccl_leave(State& st, hipStream_t s);
 void lanes_release(State& st);   // schedules.cc (shutdown: the split communicators and their streams)
 // peer.cc: allreduce over IPC-mapped peer memory (1 < p <= kMaxSrcs, one node), caller holds st.mu
 int peer_allreduce(State& st, const char* in, char* out, int64_t n, int dtype, hipStream_t stream);

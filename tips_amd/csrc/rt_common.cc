@@ -61,6 +61,8 @@ int ensure_streams(State& st) {
   }
   for (hipEvent_t& e : st.ev_graph)
     if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (hipEvent_t& e : st.ev_rccl)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (!st.comp_stream) HIP_TRY(hipStreamCreateWithFlags(&st.comp_stream, hipStreamNonBlocking));
   if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
   if (!st.h2d_stream) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream, hipStreamNonBlocking));

@@ -127,7 +127,8 @@ void tips_shutdown(void) {
   st.recv_ev.release();
   st.sum_ev.release();
   for (hipEvent_t* e : {&st.ev_start, &st.ev_done, &st.ev_comp_done, &st.ev_comp_prev, &st.ev_graph[0],
-                        &st.ev_graph[1], &st.ev_graph[2], &st.ev_graph[3], &st.ev_graph[4]})
+                        &st.ev_graph[1], &st.ev_graph[2], &st.ev_graph[3], &st.ev_graph[4], &st.ev_rccl[0],
+                        &st.ev_rccl[1]})
     if (*e) {
       (void)hipEventDestroy(*e);
       *e = nullptr;

@@ -500,8 +500,9 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
   const int algo = resolve_algo(st.algo, st.size, n * es);
   if (algo == TIPS_ALGO_RCCL) {
     TRY(ensure_comm(st));
+    TRY(rccl_enter(st, stream));
     NCCL_TRY(ncclAllReduce(in, out, (size_t)n, nccl_type(dtype), ncclSum, st.comm, stream));
-    return 0;
+    return rccl_leave(st, stream);
   }
   if (st.size == 1) {  // MPI_Allreduce on one rank returns the input
     if (in != out) HIP_TRY(hipMemcpyAsync(out, in, (size_t)(n * es), hipMemcpyDeviceToDevice, stream));
@@ -537,6 +538,19 @@ void lanes_release(State& st) {
   st.lane_stream.clear();
   st.lane_ev.release();
   st.xfer_ev.release();
+}
+
+int rccl_enter(State& st, hipStream_t s) {
+  TRY(order_after_replays(st));
+  for (size_t l = 0; l < st.lane_stream.size(); l++) TRY(join(st.comm_stream, st.lane_stream[l], st.lane_ev.ev[l + 1]));
+  if (s != st.comm_stream) TRY(join(s, st.comm_stream, st.ev_rccl[0]));
+  return 0;
+}
+
+int rccl_leave(State& st, hipStream_t s) {
+  if (s != st.comm_stream) TRY(join(st.comm_stream, s, st.ev_rccl[1]));
+  st.eager_pending = true;  // a replay waits for the comm stream, which now waits for this
+  return 0;
 }
 
 void graphs_release(State& st) {
