@@ -150,3 +150,32 @@ def test_plan_argument_errors():
     assert L.tips_schedule_plan(2, 4, 0, 100, F32, 1, None, 0) == -1  # ncclAllReduce has no plan
     assert L.tips_schedule_plan(pu.RING, 4, 0, 100, 42, 1, None, 0) == -1
     assert L.tips_schedule_plan(pu.RING, 32, 5, 100, F32, 2, None, 0) > 0  # the ring takes any p
+
+
+# ------------------------------------------------------------------ randomized (hypothesis)
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as hs  # noqa: E402
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow], derandomize=True)
+@given(algo=hs.sampled_from([pu.RING, pu.DIRECT, pu.ONESHOT]), p=hs.integers(2, 12), n=hs.integers(0, 40000),
+       K=hs.integers(1, 8), dtype=hs.sampled_from([F32, F64, I32, I64, F16, BF16]), inplace=hs.booleans(),
+       lanes=hs.integers(1, 3))
+def test_plans_randomized(oracle, algo, p, n, K, dtype, inplace, lanes):
+    """Random schedule shapes: every property the parametrized tests check, at once - send /
+    receive pairing, rank-independent staging, bit-exact interpretation against the oracle's order,
+    and no unordered conflict in the executor's streams (with transfer lanes) for rank 0."""
+    if n == 0:
+        return  # (allreduce_device returns before any plan for an empty bucket)
+    plans = [pu.dump(algo, p, r, n, dtype, K) for r in range(p)]
+    pu.pairing(plans)
+    assert len({pl["staging"] for pl in plans}) == 1
+    rng = np.random.default_rng(n * 31 + p)
+    ins = [rand(dtype, n, rng) for _ in range(p)]
+    outs = pu.interpret(plans, ins, dtype, inplace=inplace)
+    exp = oracle.ring(ins, code=dtype)[0] if algo == pu.RING else oracle.fold(ins, code=dtype, wide_acc=True)
+    for o in outs:
+        assert np.array_equal(o.view(np.uint8), exp.view(np.uint8))
+    assert not pu.hazards(plans[0], ES[dtype], n * ES[dtype], inplace=inplace, lanes=lanes,
+                          modes=("eager", "eager", "replay", "eager") if lanes == 1 else ("eager", "eager"))
