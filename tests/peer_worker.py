@@ -420,7 +420,14 @@ def main():
     _lib.call("tips_set_algorithm", algo)
     sp = torch.cuda.current_stream().cuda_stream
     results = []
+    base_env = dict(os.environ)
     for c in cases:
+        # per-case settings the library reads per call (pipeline depth, transfer lanes, ...)
+        for k in list(os.environ):
+            if k.startswith("TIPS_") and k not in base_env:
+                del os.environ[k]
+        os.environ.update({k: base_env[k] for k in base_env if k.startswith("TIPS_")})
+        os.environ.update(c.get("env", {}))
         case_algo = ALGO_NAMES[c["algo"]] if c.get("algo") else algo
         JOB_ALGO = case_algo
         if os.environ.get("TIPS_WORKER_SET_ALGO", "1") == "1":

@@ -179,3 +179,21 @@ def test_control_plane_and_api_over_rccl(gpu, p):
     env = rccl_env("auto")
     env.update(TIPS_FUSION_THRESHOLD=str(1 << 20), TIPS_HOST_PIECE_BYTES=str(1 << 20))
     check(run_job(p, cases, timeout=600, **env))
+
+
+@pytest.mark.parametrize("p", [3, 4])
+def test_randomized_schedules_over_rccl(gpu, p):
+    """Seeded random cases over real RCCL ranks, each its own schedule, pipeline depth, transfer
+    lanes, dtype, size and in-place flag (settings the library reads per call); every result
+    bit-exact against that schedule's oracle."""
+    import numpy as np
+    rng = np.random.default_rng(2026 + p)
+    cases = []
+    for i in range(24):
+        algo = ["ring", "direct", "oneshot"][int(rng.integers(3))]
+        cases.append({"algo": algo, "dtype": int(rng.choice(ALL_DTYPES)), "n": int(rng.integers(1, 400000)),
+                      "seed": 100 + i, "inplace": bool(rng.integers(2)),
+                      "env": {"TIPS_PIPELINE_DEPTH": str(int(rng.integers(1, 7))), "TIPS_MIN_SUBCHUNK_BYTES": "4096",
+                              "TIPS_LANES": str(int(rng.integers(1, 3)))}})
+    check(run_job(p, cases, timeout=600, **rccl_env("direct")))
+
