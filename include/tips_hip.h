@@ -268,7 +268,8 @@ TIPS_API int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lane
  * (64 MiB) made again on the same buffers (same addresses and allocations) is captured once into a
  * HIP graph and replayed with one launch; streams, events and results are those of the eager
  * steps. Off by default; TIPS_GRAPHS=1 turns it on where the loaded HIP runtime and RCCL are
- * ROCm >= 7.2 (RCCL >= 2.27). Reports this process's captures, replays and cached graphs.
+ * ROCm >= 7.0 / RCCL >= 2.26 (torch's bundled runtime and /opt/rocm's 7.2 are both tested).
+ * Reports this process's captures, replays and cached graphs.
  * Returns 0 (graphs on), 1 (a failed capture turned them off for the job), 2 (off: not asked
  * for, or an older runtime), < 0 on error. */
 TIPS_API int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached);

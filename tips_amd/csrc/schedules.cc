@@ -118,7 +118,7 @@ bool xfers_conflict(const PStep& a, const PStep& b, char* const* base) {
 // latest earlier step on each other lane whose transfers touch its bytes (the ring's allgather
 // forwards what the previous step received). Every other order comes from wait_sum and the
 // compute stream, as with one lane (tests/plan_util.py hazards(lanes=...) checks both).
-int issue_steps(State& st, const Plan& pl, char* const* base, int L = 1) {
+int issue_steps(State& st, const Plan& pl, char* const* base, int L = 1, hipStream_t lane0 = nullptr) {
   const size_t nsteps = pl.steps.size();
   std::vector<std::vector<int>> deps(L > 1 ? nsteps : 0);
   std::vector<char> needed(L > 1 ? nsteps : 0, 0);
@@ -138,7 +138,7 @@ int issue_steps(State& st, const Plan& pl, char* const* base, int L = 1) {
   for (size_t i = 0; i < nsteps; i++) {
     const PStep& s = pl.steps[i];
     const int l = (int)(i % L);
-    hipStream_t cs = lane_stream(st, l);
+    hipStream_t cs = (l == 0 && lane0) ? lane0 : lane_stream(st, l);
     ncclComm_t cc = lane_comm(st, l);
     if (s.wait_sum >= 0 && !pl.steps[s.wait_sum].sums.empty())
       HIP_TRY(hipStreamWaitEvent(cs, st.sum_ev.ev[s.wait_sum], 0));
@@ -209,20 +209,18 @@ void destroy_exec(State& st, hipGraphExec_t e) {
   (void)hipGraphExecDestroy(e);
 }
 
-// TIPS_GRAPHS=1 turns replays on where captured RCCL point-to-point work is known to replay
-// correctly: the HIP runtime and RCCL of ROCm >= 7.2 (tools/graph_repro.cc, tests/test_gpu_graphs.py).
-// The ROCm 7.0.2 runtime and RCCL 2.26 that torch bundles (what a Python process of this library
-// runs on) crash in hipStreamEndCapture once a grouped ncclSend/ncclRecv was captured on a stream
-// forked from the capture's origin (tools/graph_probe.py mode 3; mode 5, the group on the origin
-// itself, replays wrong bytes), so there every plan stays eager. Off by default: replays cut the
-// host time of a call (64 -> 27 us one-shot p = 2, 72 -> 50 us direct p = 3) but over the socket
-// transport a call's completion got slower (profiles/r02/graph_host_cost.jsonl); xGMI is
-// unmeasured. TIPS_GRAPHS=2 forces replays on any runtime (probing only).
+// TIPS_GRAPHS=1 turns replays on where the capture pattern (capture_plan) was seen to replay
+// correctly: RCCL >= 2.26 on a HIP runtime >= 7.0, i.e. torch's bundled ROCm 7.0.2 (a Python
+// process) and /opt/rocm's 7.2 (a C / cgo / JNI host) - tests/test_gpu_graphs.py and
+// test_gpu_rccl_procs.py::test_replayed_plans_in_python_processes. Off by default: replays cut
+// the host time of a call (64 -> 27 us one-shot p = 2, 72 -> 50 us direct p = 3, C host) but over
+// the socket transport a call's completion got slower (profiles/r02/graph_host_cost.jsonl); xGMI
+// is unmeasured. TIPS_GRAPHS=2 forces replays on any runtime (probing only).
 bool graphs_supported() {
   static int ok = -1;
   if (ok < 0) {
     int rv = 0, hv = 0;
-    ok = ncclGetVersion(&rv) == ncclSuccess && hipRuntimeGetVersion(&hv) == hipSuccess && rv >= 22700 && hv >= 70200000;
+    ok = ncclGetVersion(&rv) == ncclSuccess && hipRuntimeGetVersion(&hv) == hipSuccess && rv >= 22600 && hv >= 70000000;
     (void)hipGetLastError();
   }
   return ok == 1;
@@ -241,20 +239,25 @@ bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
   return cs == hipStreamCaptureStatusNone;  // the caller's own capture takes the eager steps
 }
 
-// Captures the plan on graph_stream: comm and compute streams fork from it and join back, so the
-// graph holds exactly the eager executor's steps and edges. On failure every forked stream is
-// still joined back, so the capture ends and the streams leave capture mode.
+// Captures the plan on graph_stream, which issues the groups itself (the comm stream's part), with
+// the compute stream forked from it and joined back: the graph holds the eager executor's steps
+// and edges. The groups stay on the capture's origin stream because the ROCm 7.0.2 runtime and
+// RCCL 2.26 that torch bundles crash in hipStreamEndCapture when a grouped ncclSend/ncclRecv is
+// captured on a forked stream (tools/graph_probe.py mode 3, no library involved), while groups on
+// the origin with a forked stream beside them replay correctly there and on /opt/rocm's 7.2
+// (mode 5; tests/test_gpu_graphs.py). On failure the forked stream is still joined back, so the
+// capture ends and every stream leaves capture mode.
 int capture_plan(State& st, const Plan& pl, char* const* base, hipGraphExec_t* exec) {
   HIP_TRY(hipStreamBeginCapture(st.graph_stream, hipStreamCaptureModeRelaxed));
-  int rc = join(st.comm_stream, st.graph_stream, st.ev_start);
-  if (rc == 0 && hipStreamWaitEvent(st.comp_stream, st.ev_start, 0) != hipSuccess)
-    rc = fail(TIPS_ERR_HIP, "capture: compute stream fork failed");
-  if (rc == 0) rc = issue_steps(st, pl, base);
-  const int j1 = join(st.graph_stream, st.comm_stream, st.ev_done);
-  const int j2 = join(st.graph_stream, st.comp_stream, st.ev_comp_done);
+  int rc = hipEventRecord(st.ev_start, st.graph_stream) == hipSuccess &&
+                   hipStreamWaitEvent(st.comp_stream, st.ev_start, 0) == hipSuccess
+               ? 0
+               : fail(TIPS_ERR_HIP, "capture: compute stream fork failed");
+  if (rc == 0) rc = issue_steps(st, pl, base, 1, st.graph_stream);
+  const int jc = join(st.graph_stream, st.comp_stream, st.ev_comp_done);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(st.graph_stream, &g);
-  if (rc == 0) rc = j1 ? j1 : j2;
+  if (rc == 0) rc = jc;
   if (rc == 0 && (e != hipSuccess || !g)) rc = fail(TIPS_ERR_HIP, "hipStreamEndCapture failed: %s", hipGetErrorString(e));
   if (rc == 0) {
     const hipError_t ei = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);

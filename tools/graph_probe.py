@@ -30,7 +30,7 @@ def main():
     if rank == 0:
         assert nccl.ncclGetUniqueId(ctypes.byref(uid)) == 0
         with open(idf + ".tmp", "wb") as f:
-            f.write(bytes(uid.b) + b"\0" * (128 - len(bytes(uid.b))))
+            f.write(ctypes.string_at(ctypes.addressof(uid), 128))  # (uid.b would stop at the first NUL)
         os.rename(idf + ".tmp", idf)
     else:
         for _ in range(600):
