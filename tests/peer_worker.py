@@ -348,10 +348,24 @@ def graphs_case(c, rank, size, L, _lib, sp):
             if not same_bits(from_dev(y, dtype), expected(ins, dtype, JOB_ALGO), dtype):
                 bad.append("round %d buf %d (dtype %d, n %d) differs" % (rnd, i, dtype, n))
     torch.cuda.synchronize()
+    timing = {}
+    if c.get("time_calls"):  # host time inside tips_allreduce and wall time per call, buffer 0, back to back
+        import time
+        dtype, n, _, _ = specs[0]
+        x, y = bufs[0]
+        enq = 0.0
+        t0 = time.perf_counter()
+        for _ in range(c["time_calls"]):
+            a = time.perf_counter()
+            L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, sp)
+            enq += time.perf_counter() - a
+        torch.cuda.synchronize()
+        timing = {"enqueue_us": round(enq / c["time_calls"] * 1e6, 2),
+                  "call_us": round((time.perf_counter() - t0) / c["time_calls"] * 1e6, 2)}
     cap, rep, cached = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     off = L.tips_graph_stats(ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(cached))
-    return {"case": {"graphs": len(specs)}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5]),
-            "captured": cap.value, "replayed": rep.value, "cached": cached.value, "graphs_off": off}
+    return dict({"case": {"graphs": len(specs)}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5]),
+                 "captured": cap.value, "replayed": rep.value, "cached": cached.value, "graphs_off": off}, **timing)
 
 
 def golden_case(c, rank, size, L, _lib, sp):
