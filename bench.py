@@ -475,6 +475,42 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
 ENV_VARIANTS = [("nchannels_per_peer_4", {"NCCL_NCHANNELS_PER_PEER": "4"})]
 
 
+def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=50):
+    """Per-call time of small allreduces (AUTO: one-shot up to 256 KiB, then direct), eager and as
+    replayed HIP graphs (TIPS_GRAPHS=1): the wall time of `calls` back-to-back calls on the same
+    buffers, slowest rank; where host cost, not bytes, bounds a call (config 1 is a 1 MiB bucket)."""
+    out = {"calls": calls, "unit": "us per call, slowest rank"}
+    saved = os.environ.get("TIPS_GRAPHS")
+    _lib.call("tips_set_algorithm", _lib.ALGO_AUTO)
+    try:
+        for kib in (16, 256, 1024):
+            n = kib * 256
+            x = torch.full((n,), float(rank + 1), device="cuda")
+            y = torch.empty_like(x)
+            row = {}
+            for mode in ("eager", "graphs"):
+                os.environ["TIPS_GRAPHS"] = "1" if mode == "graphs" else "0"
+                for _ in range(3):  # (a plan is captured on its second call)
+                    L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, sp)
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(calls):
+                    L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, sp)
+                torch.cuda.synchronize()
+                row[mode] = round(max_over_ranks(dist, time.perf_counter() - t0) / calls * 1e6, 1)
+            world = dist.get_world_size()
+            ok = bool(torch.all(y == world * (world + 1) / 2).item())
+            row["check"] = "exact" if all_ranks_ok(dist, ok) else "FAIL on some rank"
+            out["%d_KiB" % kib] = row
+    finally:
+        if saved is None:
+            os.environ.pop("TIPS_GRAPHS", None)
+        else:
+            os.environ["TIPS_GRAPHS"] = saved
+    return out
+
+
 def env_variant_jobs(args, dist, rank, world, timeout_s=240):
     """Rank 0 reruns the bucket allreduce with the direct schedule as a child job of `world` ranks
     (torch.distributed.run, the same GPUs) per RCCL setting in ENV_VARIANTS, while every rank of
@@ -978,6 +1014,12 @@ def bench_allreduce(args):
         elif workload == "bucket":
             compare_check["peer"] = ("skipped: the IPC peer schedules run only when the job spans all %d GPUs of "
                                      "the node (TIPS_BENCH_PEER=1 forces them)" % torch.cuda.device_count())
+        if world > 1 and workload == "bucket":
+            note_progress("the small-bucket latency probe")
+            try:
+                line["small_bucket_latency"] = small_bucket_latency(torch, dist, _lib, L, rank, sp)
+            except Exception as e:  # noqa: BLE001
+                line["small_bucket_latency"] = {"error": str(e)}
         run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
                       ("ring_l2", "ring", {"TIPS_LANES": "2"}),
                       ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
