@@ -264,11 +264,12 @@ TIPS_API int tips_tuned_choice(int64_t bytes, int* algo, int* depth);
  * the job's, whose groups of consecutive plan steps are in flight together (1 = the comm stream
  * alone). TIPS_LANES sets it (the same on every rank) for an explicitly selected schedule. */
 TIPS_API int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lanes);
-/* Replayed plans (TIPS_GRAPHS): a ring / direct / one-shot call of at most TIPS_GRAPH_MAX_BYTES
- * (64 MiB) made again on the same buffers (same addresses and allocations) is captured once into a
- * HIP graph and replayed with one launch; streams, events and results are those of the eager
- * steps. Off by default; TIPS_GRAPHS=1 turns it on where the loaded HIP runtime and RCCL are
- * ROCm >= 7.0 / RCCL >= 2.26 (torch's bundled runtime and /opt/rocm's 7.2 are both tested).
+/* Replayed plans (TIPS_GRAPHS, default 1): a ring / direct / one-shot call of at most
+ * TIPS_GRAPH_MAX_BYTES (1 MiB: latency-bound buckets) made again on the same buffers (same
+ * addresses and allocations) is captured once into a HIP graph and replayed with one launch;
+ * streams, events and results are those of the eager steps. On where the loaded HIP runtime and
+ * RCCL are ROCm >= 7.0 / RCCL >= 2.26 (torch's bundled runtime and /opt/rocm's 7.2 are both
+ * tested); TIPS_GRAPHS=0 turns it off.
  * Reports this process's captures, replays and cached graphs.
  * Returns 0 (graphs on), 1 (a failed capture turned them off for the job), 2 (off: not asked
  * for, or an older runtime), < 0 on error. */

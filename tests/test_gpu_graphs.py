@@ -52,13 +52,13 @@ def run_repro(p, algo, **extra):
 
 @pytest.mark.parametrize("algo,p", [("oneshot", 2), ("ring", 2), ("ring", 3), ("direct", 3)])
 def test_replayed_plans_c_abi(gpu, algo, p):
-    for r in run_repro(p, algo, TIPS_GRAPHS="1"):
+    for r in run_repro(p, algo, TIPS_GRAPHS="1", TIPS_GRAPH_MAX_BYTES=str(2 << 20)):
         assert r["bad"] == 0 and r["graphs_off"] == 0, r
         # 3 buffers: eager on round 0, captured on round 1, replayed from then on; the reallocated
         # one is a new key at round 3 (eager), captured at 4
         assert r["captured"] >= 3 and r["replayed"] >= 11, r
 
 
-def test_graphs_off_by_default_c_abi(gpu):
-    for r in run_repro(2, "direct"):
+def test_graphs_off_c_abi(gpu):
+    for r in run_repro(2, "direct", TIPS_GRAPHS="0"):
         assert r["bad"] == 0 and r["captured"] == 0 and r["replayed"] == 0 and r["graphs_off"] == 2, r

@@ -209,13 +209,15 @@ void destroy_exec(State& st, hipGraphExec_t e) {
   (void)hipGraphExecDestroy(e);
 }
 
-// TIPS_GRAPHS=1 turns replays on where the capture pattern (capture_plan) was seen to replay
-// correctly: RCCL >= 2.26 on a HIP runtime >= 7.0, i.e. torch's bundled ROCm 7.0.2 (a Python
-// process) and /opt/rocm's 7.2 (a C / cgo / JNI host) - tests/test_gpu_graphs.py and
-// test_gpu_rccl_procs.py::test_replayed_plans_in_python_processes. Off by default: replays cut
-// the host time of a call (64 -> 27 us one-shot p = 2, 72 -> 50 us direct p = 3, C host) but over
-// the socket transport a call's completion got slower (profiles/r02/graph_host_cost.jsonl); xGMI
-// is unmeasured. TIPS_GRAPHS=2 forces replays on any runtime (probing only).
+// Replays are on (TIPS_GRAPHS=1, the default) where the capture pattern (capture_plan) was seen
+// to replay correctly: RCCL >= 2.26 on a HIP runtime >= 7.0, i.e. torch's bundled ROCm 7.0.2 (a
+// Python process) and /opt/rocm's 7.2 (a C / cgo / JNI host) - tests/test_gpu_graphs.py and
+// test_gpu_rccl_procs.py::test_replayed_plans_in_python_processes - and for buckets up to
+// TIPS_GRAPH_MAX_BYTES (1 MiB), where a call's host cost, not its bytes, bounds it: the host time
+// of a call drops 126 -> 22 us (one-shot p = 2, Python) and a call takes 15-25 % less below 1 MiB
+// on the socket rehearsal, the same at 1 MiB (profiles/r02/graph_host_cost*.jsonl,
+// rehearsal_n2_small_buckets.jsonl). TIPS_GRAPHS=0 turns them off; 2 forces them on any runtime
+// (probing only).
 bool graphs_supported() {
   static int ok = -1;
   if (ok < 0) {
@@ -228,9 +230,9 @@ bool graphs_supported() {
 
 bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
   if (st.graphs && st.graphs->off) return false;
-  const int64_t want = env_i64("TIPS_GRAPHS", 0);
+  const int64_t want = env_i64("TIPS_GRAPHS", 1);
   if (want <= 0 || (want == 1 && !graphs_supported())) return false;
-  if (pl.n * tips::dtype_size(pl.dtype) > env_i64("TIPS_GRAPH_MAX_BYTES", 64 << 20)) return false;
+  if (pl.n * tips::dtype_size(pl.dtype) > env_i64("TIPS_GRAPH_MAX_BYTES", 1 << 20)) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(user, &cs) != hipSuccess) {
     (void)hipGetLastError();
@@ -768,7 +770,7 @@ int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached) {
   if (st.graphs)
     for (const auto& kv : st.graphs->m) *cached += kv.second.exec != nullptr;
   if (st.graphs && st.graphs->off) return 1;
-  const int64_t want = env_i64("TIPS_GRAPHS", 0);
+  const int64_t want = env_i64("TIPS_GRAPHS", 1);
   return (want <= 0 || (want == 1 && !graphs_supported())) ? 2 : 0;
 }
 
