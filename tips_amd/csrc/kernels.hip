@@ -762,9 +762,11 @@ constexpr int kDefMode = 3, kDefUnroll = 1, kDefNT = 1, kDefThreads = 256;
 
 template <int DT, int NSRC>
 hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
-  // buffer loads, 1 vector per lane; non-temporal up to 4 sources, plain beyond
-  // (sweep: profiles/r01_sum_sweep_multi*.jsonl)
-  constexpr int LAUX = NSRC <= 4 ? 2 : 0;
+  // buffer loads, 1 vector per lane, non-temporal for every source count. Round 1 kept plain
+  // loads beyond 4 sources from a sweep that re-read one buffer set (plain 44.7 vs nt 47.3 us,
+  // 8 x 32 MiB, Infinity Cache assisted); with operands from HBM, as the direct schedule's fold
+  // mostly reads them, nt wins 48.6 vs 57.8 us (profiles/r02/multi_sum_variants.jsonl).
+  constexpr int LAUX = 2;
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
   int64_t grid = (nvec + (int64_t)kBlock - 1) / (int64_t)kBlock;
