@@ -769,11 +769,20 @@ hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
   constexpr int LAUX = 2;
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
-  int64_t grid = (nvec + (int64_t)kBlock - 1) / (int64_t)kBlock;
+  // 4 vectors per lane for many sources of 3-24 MiB each (8 x 4 MiB: 7.0 vs 8.3 us, 8 x 8 MiB:
+  // 12.6 vs 14.3 us; larger or smaller, or up to 4 sources, 1 vector wins or ties:
+  // profiles/r02/multi_sum_small.jsonl)
+  const bool u4 = NSRC > 4 && nvec * 16 >= (3 << 20) && nvec * 16 <= (24 << 20);
+  const int64_t per = (int64_t)kBlock * (u4 ? 4 : 1);
+  int64_t grid = (nvec + per - 1) / per;
   grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst,
-                     sl, nvec, nvec * ve, n);
+  if (u4)
+    hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 4, LAUX>), dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       (u32x4*)dst, sl, nvec, nvec * ve, n);
+  else
+    hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX>), dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       (u32x4*)dst, sl, nvec, nvec * ve, n);
   return hipGetLastError();
 }
 

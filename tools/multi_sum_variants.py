@@ -11,8 +11,10 @@ from tips_amd import _lib  # noqa: E402
 L = _lib.lib()
 torch.cuda.set_device(0)
 s = torch.cuda.current_stream()
-VARIANTS = list(range(8))
-for p, mib in ((8, 32), (8, 8), (4, 64)):
+import os
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4,5,6,7").split(",")]
+SHAPES = [tuple(int(x) for x in sh.split("x")) for sh in os.environ.get("SHAPES", "8x32,8x8,4x64").split(",")]
+for p, mib in SHAPES:
     n = mib * (1 << 18)
     sets = []
     for k in range(4):
