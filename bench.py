@@ -511,6 +511,56 @@ def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=50):
     return out
 
 
+def overlap_probe(torch, dist, tips_amd, _lib, algo_code, steps=10):
+    """A training step with DistributedOptimizer, its allreduces issued after backward vs during it
+    (TIPS_OVERLAP_BACKWARD: post-accumulate hooks issue each <= 25 MiB gradient bucket as it
+    completes, on a side stream). The model is 6 fp32 Linear(2048, 2048) layers, 25.2 M parameters
+    (ResNet-50 has 25.6 M), on a 2048-row synthetic batch; wall time per step, slowest rank.
+    `backward_only` is the same step without the optimizer (no allreduce): the floor overlap can
+    approach. The reference's per-gradient async ops overlap backward the same way
+    (__init__.py:212-222)."""
+    saved = os.environ.get("TIPS_OVERLAP_BACKWARD")
+    _lib.call("tips_set_algorithm", algo_code)
+    out = {"model": "6 x Linear(2048, 2048) + ReLU, fp32, 25.2 M parameters, batch 2048", "steps": steps,
+           "unit": "ms per step (forward + backward [+ allreduce + SGD]), slowest rank"}
+    g = torch.Generator(device="cuda").manual_seed(77)
+    x = torch.randn(2048, 2048, device="cuda", generator=g)
+    try:
+        for name, overlap, sync in (("backward_only", False, False), ("allreduce_after_backward", False, True),
+                                    ("allreduce_during_backward", True, True)):
+            os.environ["TIPS_OVERLAP_BACKWARD"] = "1" if overlap else "0"
+            torch.manual_seed(5)
+            layers = []
+            for _ in range(6):
+                layers += [torch.nn.Linear(2048, 2048), torch.nn.ReLU()]
+            m = torch.nn.Sequential(*layers).cuda()
+            opt = tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=1e-6))
+
+            def run(k):
+                for _ in range(k):
+                    opt.zero_grad(set_to_none=False)
+                    m(x).square().mean().backward()
+                    if sync:
+                        opt.step()
+
+            run(3)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            run(steps)
+            torch.cuda.synchronize()
+            out[name] = round(max_over_ranks(dist, time.perf_counter() - t0) / steps * 1e3, 3)
+            if overlap:
+                out["buckets"] = len(opt._buckets.buckets) if opt._buckets is not None else 0
+            del m, opt, layers
+    finally:
+        if saved is None:
+            os.environ.pop("TIPS_OVERLAP_BACKWARD", None)
+        else:
+            os.environ["TIPS_OVERLAP_BACKWARD"] = saved
+    return out
+
+
 def env_variant_jobs(args, dist, rank, world, timeout_s=240):
     """Rank 0 reruns the bucket allreduce with the direct schedule as a child job of `world` ranks
     (torch.distributed.run, the same GPUs) per RCCL setting in ENV_VARIANTS, while every rank of
@@ -1020,6 +1070,11 @@ def bench_allreduce(args):
                 line["small_bucket_latency"] = small_bucket_latency(torch, dist, _lib, L, rank, sp)
             except Exception as e:  # noqa: BLE001
                 line["small_bucket_latency"] = {"error": str(e)}
+            note_progress("the backward-overlap probe")
+            try:
+                line["backward_overlap"] = overlap_probe(torch, dist, tips_amd, _lib, algo_names[args.algo])
+            except Exception as e:  # noqa: BLE001
+                line["backward_overlap"] = {"error": str(e)}
         run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
                       ("ring_l2", "ring", {"TIPS_LANES": "2"}),
                       ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",

@@ -108,6 +108,67 @@ def optimizer_case(c, rank, size, L, _lib, sp):
     return {"case": {"optimizer": c["seed"]}, "rc": 0, "ok": bool(ok), "error": "" if ok else "parameters differ"}
 
 
+def overlap_case(c, rank, size, L, _lib, sp):
+    """DistributedOptimizer with backward-overlapped gradient buckets (optim._GradBuckets): the
+    hooks issue each bucket's in-place allreduce during backward, on a side stream, in bucket order.
+    `passes` backwards per step (backward_passes_per_step, average_aggregated_gradients), two
+    optimizer steps (the second after zero_grad(set_to_none=True): gradients copied into the views
+    again). Checks: every bucket was issued before step() (by the hooks), the summed gradients
+    equal the rank-order sum of all ranks' (averaged) local gradients bit for bit (AUTO at p > 2:
+    one-shot / direct, the rank-order fold), and the parameters equal p - lr * sum."""
+    import torch
+    import tips_amd
+    passes, avg = int(c.get("passes", 1)), bool(c.get("average", False))
+    os.environ["TIPS_GRAD_BUCKET_MIB"] = str(c.get("bucket_kib", 8) / 1024.0)
+
+    def model():
+        torch.manual_seed(c["seed"])
+        return torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.Tanh(), torch.nn.Linear(256, 256),
+                                   torch.nn.Tanh(), torch.nn.Linear(256, 128), torch.nn.Tanh(),
+                                   torch.nn.Linear(128, 10)).cuda()
+
+    def batch(r, it, k):
+        g = torch.Generator().manual_seed(c["seed"] * 1000 + r * 100 + it * 10 + k)
+        return torch.randn(16, 64, generator=g).cuda()
+
+    lr, bad = 0.01, []
+    ref = model()  # replays every rank's local passes on a copy of the parameters
+    m = model()
+    opt = tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=lr), backward_passes_per_step=passes,
+                                        average_aggregated_gradients=avg)
+    if opt._buckets is None or len(opt._buckets.buckets) < 3:
+        return {"case": {"overlap": c["seed"]}, "rc": 0, "ok": False, "error": "no overlapped buckets"}
+    for it in range(2):
+        sums = None
+        for r in range(size):
+            ref.zero_grad(set_to_none=True)
+            for k in range(passes):
+                ref(batch(r, it, k)).pow(2).sum().backward()
+            gs = [p.grad / passes if (avg and passes > 1) else p.grad.clone() for p in ref.parameters()]
+            sums = gs if sums is None else [s + g for s, g in zip(sums, gs)]
+        opt.zero_grad()
+        for k in range(passes):
+            m(batch(rank, it, k)).pow(2).sum().backward()
+            if k < passes - 1:
+                opt.step()  # counts the pass only
+        issued = list(opt._buckets.issue_log)
+        if issued != list(range(len(opt._buckets.buckets))):
+            bad.append("it %d: hooks issued %s of %d buckets" % (it, issued, len(opt._buckets.buckets)))
+        with torch.no_grad():
+            exp = [p - lr * s for p, s in zip(ref.parameters(), sums)]
+        opt.step()
+        torch.cuda.synchronize()
+        for i, (p, s) in enumerate(zip(m.parameters(), sums)):
+            if not torch.equal(p.grad, s):
+                bad.append("it %d: grad %d differs" % (it, i))
+        if not all(torch.allclose(p, e, rtol=0, atol=1e-6) for p, e in zip(m.parameters(), exp)):
+            bad.append("it %d: parameters differ" % it)
+        with torch.no_grad():  # keep the replica in step with the updated parameters
+            for pr, p in zip(ref.parameters(), m.parameters()):
+                pr.copy_(p)
+    return {"case": {"overlap": c["seed"], "passes": passes}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:4])}
+
+
 def tape_case(c, rank, size, L, _lib, sp):
     """tips_amd.DistributedGradientTape on the device: every rank differentiates its own seeded
     loss; gradient() returns the sum over ranks (fusion buckets -> peer schedule), which must equal
@@ -471,6 +532,9 @@ def main():
             continue
         if c.get("optimizer"):
             results.append(optimizer_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("overlap"):
+            results.append(overlap_case(c, rank, size, L, _lib, sp))
             continue
         dtype, n, seed = c["dtype"], c["n"], c["seed"]
         if c.get("count_per_rank"):  # deliberately inconsistent counts: every rank must fail, none hang

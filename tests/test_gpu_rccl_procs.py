@@ -184,6 +184,18 @@ def test_control_plane_and_api_over_rccl(gpu, p):
     check(run_job(p, cases, timeout=600, **env))
 
 
+@pytest.mark.parametrize("p", [2, 3])
+def test_overlapped_optimizer_over_rccl(gpu, p):
+    """DistributedOptimizer's backward-overlapped buckets over real RCCL ranks: the post-accumulate
+    hooks issue every bucket's in-place allreduce during backward (8 KiB and 64 KiB buckets, so a
+    small MLP makes many), in bucket order on every rank; one and two backward passes per step,
+    averaged; summed gradients bit-exact against the rank-order sum (p = 2 takes the one-shot for
+    these sizes, p = 3 the one-shot / direct fold), parameters p - lr * sum."""
+    cases = [{"overlap": True, "seed": 21, "bucket_kib": 8},
+             {"overlap": True, "seed": 22, "bucket_kib": 64, "passes": 2, "average": True}]
+    check(run_job(p, cases, timeout=600, **rccl_env("auto")))
+
+
 @pytest.mark.parametrize("p", [3, 4])
 def test_randomized_schedules_over_rccl(gpu, p):
     """Seeded random cases over real RCCL ranks, each its own schedule, pipeline depth, transfer

@@ -1,0 +1,178 @@
+"""CPU: backward-overlapped gradient buckets (tips_amd.optim._GradBuckets).
+
+The reference's per-gradient MPIAllreduce ops start as their gradients appear during backward
+(__init__.py:212-222, async op kernel ops.cc:86-115). Here post-accumulate grad hooks issue one
+in-place allreduce per bucket of the reversed parameter list. These tests run the hooks on CPU
+tensors with a stand-in allreduce (multiply by the number of ranks: every rank's gradient equal),
+so the layout, the issue order, the pass counting and the error paths are checked without a GPU.
+The same class over real RCCL ranks: tests/test_gpu_rccl_procs.py::test_overlapped_optimizer_over_rccl.
+"""
+import random
+
+import pytest
+import torch
+
+from tips_amd.optim import _GradBuckets
+
+RANKS = 3
+
+
+def make_model(seed=0, widths=(16, 32, 32, 24, 8)):
+    torch.manual_seed(seed)
+    layers = []
+    for a, b in zip(widths[:-1], widths[1:]):
+        layers += [torch.nn.Linear(a, b), torch.nn.Tanh()]
+    return torch.nn.Sequential(*layers[:-1])
+
+
+def loss_of(m, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return m(torch.randn(5, m[0].in_features, generator=g)).pow(2).sum()
+
+
+def local_grads(seed_model=0, seeds=(1,)):
+    m = make_model(seed_model)
+    for s in seeds:
+        loss_of(m, s).backward()
+    return [p.grad.clone() for p in m.parameters()]
+
+
+def buckets_for(m, bucket_bytes, passes=1, average=False):
+    calls = []
+
+    def issue(flat):
+        calls.append(flat.numel())
+        flat.mul_(RANKS)
+
+    gb = _GradBuckets(list(m.parameters()), bucket_bytes, passes, average, issue=issue)
+    return gb, calls
+
+
+def test_layout_reversed_contiguous_and_bounded():
+    m = make_model()
+    params = list(m.parameters())
+    gb, _ = buckets_for(m, bucket_bytes=2048)
+    # reverse order: the last parameter sits at offset 0 of the flat buffer
+    assert gb.where[id(params[-1])][2] == 0
+    prev_end = 0
+    for key, s, e, ps in gb.buckets:
+        assert s == prev_end and e > s
+        prev_end = e
+        assert sum(p.numel() for p in ps) == e - s
+        assert sum(p.numel() * 4 for p in ps) <= 2048 or len(ps) == 1  # one oversized parameter alone
+        for p in ps:
+            b, k, off = gb.where[id(p)]
+            assert s <= off and off + p.numel() <= e
+    assert prev_end == sum(p.numel() for p in params)
+    assert [p for b in gb.buckets for p in b[3]] == params[::-1]
+    gb.remove()
+
+
+def test_buckets_issue_in_index_order_whatever_the_hook_order():
+    m = make_model()
+    gb, _ = buckets_for(m, bucket_bytes=1024)
+    for p in m.parameters():
+        p.grad = torch.ones_like(p)
+    ps = list(m.parameters())
+    random.Random(7).shuffle(ps)
+    for p in ps:
+        gb._hook(p, final_pass=True, active=True)
+        issued = [t for t in gb.issue_log]
+        assert issued == list(range(len(issued)))  # always a prefix of 0, 1, 2, ...
+    assert gb.issue_log == list(range(len(gb.buckets)))
+    gb.synchronize()
+    assert gb.last_issue_log == list(range(len(gb.buckets)))
+    for p in m.parameters():
+        assert torch.equal(p.grad, torch.full_like(p, RANKS))
+    gb.remove()
+
+
+def test_real_backward_issues_during_backward_and_sums():
+    exp = [g * RANKS for g in local_grads()]
+    m = make_model()
+    gb, calls = buckets_for(m, bucket_bytes=1536)
+    loss_of(m).backward()
+    # every bucket was complete by the end of backward, so every one was issued by the hooks
+    assert gb.issue_log == list(range(len(gb.buckets))) and len(gb.buckets) > 2
+    gb.synchronize()
+    for p, e in zip(m.parameters(), exp):
+        assert torch.equal(p.grad, e)
+        assert p.grad.data_ptr() == gb.view(p).data_ptr()  # .grad is the bucket view
+    # a second iteration with set_to_none=False accumulates straight into the views
+    for p in m.parameters():
+        p.grad.zero_()
+    loss_of(m).backward()
+    gb.synchronize()
+    for p, e in zip(m.parameters(), exp):
+        assert torch.equal(p.grad, e)
+    assert sum(calls) == 2 * sum(p.numel() for p in m.parameters())
+    gb.remove()
+
+
+def test_accumulation_passes_and_average():
+    acc = local_grads(seeds=(1, 2))  # torch accumulates two backwards into .grad
+    m = make_model()
+    gb, _ = buckets_for(m, bucket_bytes=1536, passes=2, average=True)
+    state = {"pass": 0}
+    gb.final_pass = lambda: state["pass"] == 1
+    loss_of(m, 1).backward()
+    assert gb.issue_log == []  # the first pass only accumulates into the views
+    state["pass"] = 1
+    loss_of(m, 2).backward()
+    assert gb.issue_log == list(range(len(gb.buckets)))
+    gb.synchronize()
+    for p, a in zip(m.parameters(), acc):
+        assert torch.equal(p.grad, (a / 2) * RANKS)
+    gb.remove()
+
+
+def test_unused_parameter_contributes_zeros_and_stays_none():
+    m = make_model()
+    extra = torch.nn.Parameter(torch.randn(7))
+    gb = _GradBuckets(list(m.parameters()) + [extra], 1 << 20, 1, False, issue=lambda f: f.mul_(RANKS))
+    loss_of(m).backward()
+    # extra sits in bucket 0 (reversed order) and never gets a gradient: nothing issued by the hooks
+    assert gb.issue_log == []
+    gb.synchronize()
+    assert extra.grad is None
+    assert torch.equal(gb.view(extra), torch.zeros(7))
+    exp = [g * RANKS for g in local_grads()]
+    for p, e in zip(m.parameters(), exp):
+        assert torch.equal(p.grad, e)
+    gb.remove()
+
+
+def test_synchronize_without_backward_reduces_each_group_once():
+    m = make_model()
+    gb, calls = buckets_for(m, bucket_bytes=512)
+    for p in m.parameters():
+        p.grad = torch.full_like(p, 2.0)
+    gb.synchronize()
+    assert len(calls) == 1 and calls[0] == sum(p.numel() for p in m.parameters())
+    assert gb.last_issue_log == [("group", (torch.float32, torch.device("cpu")))]
+    for p in m.parameters():
+        assert torch.equal(p.grad, torch.full_like(p, 2.0 * RANKS))
+    gb.remove()
+
+
+def test_second_backward_after_issue_is_an_error():
+    m = make_model()
+    gb, _ = buckets_for(m, bucket_bytes=1536)
+    loss_of(m).backward()
+    loss_of(m).backward()
+    with pytest.raises(RuntimeError, match="accumulated again"):
+        gb.synchronize()
+    gb.remove()
+
+
+def test_mixed_dtypes_make_separate_groups():
+    m = make_model()
+    m[-1].double()
+    gb, calls = buckets_for(m, bucket_bytes=1 << 20)
+    keys = [b[0] for b in gb.buckets]
+    assert keys[0][0] == torch.float64 and all(k[0] == torch.float32 for k in keys[1:])
+    loss = m[-1](m[:-1](torch.randn(3, 16)).double()).pow(2).sum()
+    loss.backward()
+    gb.synchronize()
+    assert gb.last_issue_log == [0, 1]
+    gb.remove()

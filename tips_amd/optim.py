@@ -6,10 +6,12 @@ The reference wraps a TF optimizer: compute_gradients() allreduces every
 gradient (_make_allreduce_grads_fn, __init__.py:189-227) before the wrapped
 optimizer applies them, optionally after backward_passes_per_step local
 accumulations (LocalGradientAggregationHelper, gradient_aggregation.py). Here
-the wrapped object is a torch.optim.Optimizer and the hook point is step():
-the parameters' .grad tensors are summed over ranks through
-tips_amd.allreduce_grads (device tensors through the fusion buckets), written
-back in place, and then the wrapped optimizer steps.
+the wrapped object is a torch.optim.Optimizer: the parameters' .grad tensors
+are summed over ranks in place and then the wrapped optimizer steps. Dense
+device gradients are views of per-dtype flat buffers whose buckets are
+allreduced during backward as they complete (_GradBuckets, as the reference's
+async per-gradient ops overlap backward); the rest go through
+tips_amd.allreduce_grads in step().
 
 As in the reference, op / prescale / postscale never reach the reduction
 (__init__.py:82-87, 194-201): the gradients are SUMMED over ranks, op=Average
@@ -28,6 +30,178 @@ def _allreduce_flat_(flat):
     basics.init()
     _lib.call("tips_allreduce", flat.data_ptr(), flat.data_ptr(), flat.numel(), tensors.dtype_code(flat), _lib.OP_SUM,
               tensors.stream_of(flat))
+
+
+class _GradBuckets(object):
+    """Gradient buckets whose allreduces start during backward.
+
+    In the reference every gradient's MPIAllreduce is an async op of the TF graph
+    (__init__.py:212-222, ops.cc:86-115): it starts as soon as its gradient exists, while the
+    rest of backward still runs. The torch mirror gets the same overlap from post-accumulate
+    grad hooks. The parameters are laid out in REVERSE order (backward produces the last layer's
+    gradients first) in one flat buffer per (dtype, device), and cut into buckets of at most
+    `bucket_bytes`; every .grad becomes a view of its slice. When the last gradient of a bucket
+    has been accumulated, the bucket's slice is allreduced in place on a side stream that waited
+    for the backward stream, so the exchange runs beside the remaining backward kernels.
+
+    Ranks must issue the same allreduces in the same order. Buckets are therefore issued strictly
+    in index order (a bucket whose gradients are ready waits for every earlier bucket), and the
+    layout depends only on the parameter list. synchronize() issues whatever backward did not
+    (parameters without a gradient contribute zeros), then makes the caller's stream wait for the
+    side streams. A group none of whose buckets was issued during backward (synchronize() called
+    without a backward, as bench.py's optimizer leg does) is reduced as one allreduce of its
+    whole flat buffer. `issue(flat_slice)` is the in-place allreduce (a test may pass its own)."""
+
+    def __init__(self, params, bucket_bytes, passes, average, issue=None):
+        import threading
+        import torch
+        self._torch = torch
+        self._passes, self._average = int(passes), bool(average)
+        self._issue_fn = issue or _allreduce_flat_
+        self._lock = threading.Lock()
+        self.params = list(params)
+        self.groups = {}   # (dtype, device) -> {"n": elements, "flat": tensor}
+        self.buckets = []  # [group key, start, end (elements of the group's flat buffer), [params]]
+        self.where = {}    # id(param) -> (bucket index, group key, offset)
+        cur, cur_bytes = None, 0
+        for p in reversed(self.params):
+            key = (p.dtype, p.device)
+            g = self.groups.setdefault(key, {"n": 0, "flat": None})
+            nbytes = p.numel() * p.element_size()
+            if cur is None or cur[0] != key or (cur_bytes and cur_bytes + nbytes > bucket_bytes):
+                cur = [key, g["n"], g["n"], []]
+                self.buckets.append(cur)
+                cur_bytes = 0
+            self.where[id(p)] = (len(self.buckets) - 1, key, g["n"])
+            g["n"] += p.numel()
+            cur[2] = g["n"]
+            cur[3].append(p)
+            cur_bytes += nbytes
+        for (dt, dev), g in self.groups.items():
+            g["flat"] = torch.zeros(g["n"], dtype=dt, device=dev)
+        self._streams = {}
+        self.issue_log = []  # (bucket index, or ("group", key)) in issue order, this iteration
+        self._reset()
+        self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+
+    def remove(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    def _reset(self):
+        self.ready = [0] * len(self.buckets)
+        self.issued = [False] * len(self.buckets)
+        self.next = 0
+        self.seen = set()
+        self.sparse = set()  # ids of parameters whose gradient came sparse: reduced by allreduce_grads
+        self.error = None
+
+    def view(self, p):
+        _, key, off = self.where[id(p)]
+        return self.groups[key]["flat"][off:off + p.numel()].view(p.shape)
+
+    def _side(self, device):
+        if device.type != "cuda":
+            return None
+        s = self._streams.get(device)
+        if s is None:
+            s = self._streams[device] = self._torch.cuda.Stream(device=device)
+        return s
+
+    def _adopt(self, p):
+        """Make p.grad the view of its slice (copying a gradient autograd allocated elsewhere in);
+        a sparse gradient is left alone and its slice zeroed."""
+        g, v = p.grad, self.view(p)
+        if g is None or g.is_sparse or g.dtype != p.dtype:
+            if g is not None:
+                self.sparse.add(id(p))
+            v.zero_()
+            return
+        if g.data_ptr() != v.data_ptr():
+            v.copy_(g)
+            p.grad = v
+
+    def _hook(self, p, final_pass=None, active=None):
+        """Post-accumulate grad hook (autograd's device thread, on the backward stream)."""
+        if not (self.active() if active is None else active):
+            return
+        self._adopt(p)
+        if not (self.final_pass() if final_pass is None else final_pass):
+            return  # an earlier backward of backward_passes_per_step: accumulate into the views only
+        with self._lock:
+            if id(p) in self.seen:
+                self.error = ("a gradient was accumulated again after its bucket's allreduce was issued: "
+                              "run one backward per step() (backward_passes_per_step for more)")
+                return
+            self.seen.add(id(p))
+            b = self.where[id(p)][0]
+            self.ready[b] += 1
+            while self.next < len(self.buckets) and self.ready[self.next] == len(self.buckets[self.next][3]):
+                self._issue(self.next)
+                self.next += 1
+
+    # the optimizer sets these two
+    def active(self):
+        return True
+
+    def final_pass(self):
+        return True
+
+    def _issue_range(self, key, start, end, tag):
+        torch = self._torch
+        flat = self.groups[key]["flat"][start:end]
+        side = self._side(key[1])
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(key[1]))
+            ctx = torch.cuda.stream(side)
+        else:
+            import contextlib
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if self._average and self._passes > 1:
+                flat.div_(self._passes)
+            if end > start:
+                self._issue_fn(flat)
+        self.issue_log.append(tag)
+
+    def _issue(self, b):
+        key, s, e, _ = self.buckets[b]
+        self._issue_range(key, s, e, b)
+        self.issued[b] = True
+
+    def synchronize(self):
+        """Issue every bucket backward did not, in index order; the caller's streams then wait for
+        the side streams. Returns the parameters whose gradient came sparse (for allreduce_grads)."""
+        torch = self._torch
+        err = self.error
+        with self._lock:
+            for p in self.params:
+                if id(p) not in self.seen:
+                    self._adopt(p)  # no gradient: zeros; otherwise the view (copied in if needed)
+            touched = {self.buckets[b][0] for b in range(len(self.buckets)) if self.issued[b]}
+            whole = set()
+            for b in range(self.next, len(self.buckets)):
+                key = self.buckets[b][0]
+                if key not in touched:
+                    if key not in whole:  # nothing of this group issued yet: one allreduce of all of it
+                        whole.add(key)
+                        self._issue_range(key, 0, self.groups[key]["n"], ("group", key))
+                elif not self.issued[b]:
+                    self._issue(b)
+            for dev, s in self._streams.items():
+                torch.cuda.current_stream(dev).wait_stream(s)
+            for p in self.params:
+                if p.grad is not None and id(p) not in self.sparse:
+                    v = self.view(p)
+                    if p.grad.data_ptr() != v.data_ptr():
+                        p.grad = v
+            sparse = [p for p in self.params if id(p) in self.sparse]
+            self.last_issue_log, self.issue_log = self.issue_log, []
+            self._reset()
+        if err:
+            raise RuntimeError(err)
+        return sparse
 
 
 class _DistributedOptimizer(object):
@@ -49,6 +223,26 @@ class _DistributedOptimizer(object):
         self._bucket_view = os.environ.get("TIPS_GRAD_BUCKET_VIEW", "1") != "0"
         if self._passes < 1:
             raise ValueError("backward_passes_per_step must be >= 1")
+        self._buckets = None
+        from . import Compression
+        if (os.environ.get("TIPS_OVERLAP_BACKWARD", "1") != "0" and self._bucket_view
+                and self._compression is Compression.none and not sparse_as_dense):
+            import torch
+            ps = [p for g in optimizer.param_groups for p in g["params"]
+                  if p.requires_grad and p.is_cuda and p.layout == torch.strided]
+            ps = list({id(p): p for p in ps}.values())  # (a parameter listed twice is one gradient)
+            if ps:
+                mib = float(os.environ.get("TIPS_GRAD_BUCKET_MIB", "25"))
+                self._buckets = _GradBuckets(ps, max(1, int(mib * (1 << 20))), self._passes, self._average_aggregated)
+                self._buckets.active = self._overlap_active
+                self._buckets.final_pass = lambda: (self._calls + 1) % self._passes == 0
+
+    @staticmethod
+    def _overlap_active():
+        """Hooks issue allreduces only once TiPS runs with more than one rank (never initialise
+        TiPS from inside backward: synchronize() issues what the hooks did not)."""
+        from . import basics
+        return basics.is_initialized() and basics.size() > 1
 
     # the wrapped optimizer's surface
     @property
@@ -82,6 +276,11 @@ class _DistributedOptimizer(object):
         from . import Compression, _fusable, allreduce_grads, size
         from .ops import FusedList
         params = self._params_with_grad()
+        if self._buckets is not None and size() > 1:
+            # backward-overlapped buckets: the hooks issued what was ready; issue the rest in order
+            sparse = set(id(p) for p in self._buckets.synchronize())
+            managed = set(self._buckets.where)
+            params = [p for p in params if id(p) not in managed or id(p) in sparse]
         if self._passes > 1 and self._average_aggregated:
             for p in params:
                 p.grad = p.grad / self._passes
