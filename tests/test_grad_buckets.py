@@ -176,3 +176,25 @@ def test_mixed_dtypes_make_separate_groups():
     gb.synchronize()
     assert gb.last_issue_log == [0, 1]
     gb.remove()
+
+
+def test_newest_owner_reduces_and_dropped_owner_is_collected():
+    import gc
+    import weakref
+    m = make_model()
+    old, old_calls = buckets_for(m, bucket_bytes=1536)
+    new, new_calls = buckets_for(m, bucket_bytes=1536)  # wrapping the same parameters again
+    loss_of(m).backward()
+    assert old.issue_log == [] and new.issue_log == list(range(len(new.buckets)))
+    new.synchronize()
+    exp = [g * RANKS for g in local_grads()]
+    for p, e in zip(m.parameters(), exp):
+        assert torch.equal(p.grad, e)  # reduced once, not twice
+    ref = weakref.ref(new)
+    del new, old
+    gc.collect()
+    assert ref() is None  # the hooks do not keep the buckets alive
+    for p in m.parameters():
+        p.grad = None
+    loss_of(m).backward()  # hooks of a collected owner do nothing
+    assert torch.equal(list(m.parameters())[0].grad, local_grads()[0])

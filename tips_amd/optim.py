@@ -32,6 +32,11 @@ def _allreduce_flat_(flat):
               tensors.stream_of(flat))
 
 
+def _remove_hooks(handles):
+    for h in handles:
+        h.remove()
+
+
 class _GradBuckets(object):
     """Gradient buckets whose allreduces start during backward.
 
@@ -82,11 +87,24 @@ class _GradBuckets(object):
         self._streams = {}
         self.issue_log = []  # (bucket index, or ("group", key)) in issue order, this iteration
         self._reset()
-        self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+        # The hooks hold this object weakly (a dropped optimizer stops reducing and is collected),
+        # and a parameter belongs to the most recent _GradBuckets built over it: wrapping the same
+        # parameters again (a new DistributedOptimizer) must not reduce their gradients twice.
+        import weakref
+        ref = weakref.ref(self)
+
+        def hook(p, _ref=ref):
+            gb = _ref()
+            if gb is not None and getattr(p, "_tips_grad_buckets", None) is _ref:
+                gb._hook(p)
+
+        for p in self.params:
+            p._tips_grad_buckets = ref
+        self._handles = [p.register_post_accumulate_grad_hook(hook) for p in self.params]
+        weakref.finalize(self, _remove_hooks, list(self._handles))
 
     def remove(self):
-        for h in self._handles:
-            h.remove()
+        _remove_hooks(self._handles)
         self._handles = []
 
     def _reset(self):
