@@ -198,3 +198,63 @@ def test_newest_owner_reduces_and_dropped_owner_is_collected():
         p.grad = None
     loss_of(m).backward()  # hooks of a collected owner do nothing
     assert torch.equal(list(m.parameters())[0].grad, local_grads()[0])
+
+
+def _gloo_worker(rank, world, port, q):
+    import os
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tips_amd.optim import _GradBuckets
+    try:
+        m = make_model()
+        gb = _GradBuckets(list(m.parameters()), 1024, 1, False, issue=lambda f: dist.all_reduce(f))
+        # every rank's hooks fire in its own order: the allreduces must still pair bucket for bucket
+        for p in m.parameters():
+            p.grad = torch.full_like(p, float(rank + 1))
+        ps = list(m.parameters())
+        random.Random(100 + rank).shuffle(ps)
+        for p in ps:
+            gb._hook(p, final_pass=True, active=True)
+        gb.synchronize()
+        tot = world * (world + 1) / 2
+        ok1 = all(torch.equal(p.grad, torch.full_like(p, tot)) for p in m.parameters())
+        # a real backward with rank-specific batches: sums equal the sum of every rank's gradients
+        for p in m.parameters():
+            p.grad.zero_()
+        loss_of(m, seed=10 + rank).backward()
+        gb.synchronize()
+        exp = None
+        for r in range(world):
+            g = local_grads(seeds=(10 + r,))
+            exp = g if exp is None else [a + b for a, b in zip(exp, g)]
+        ok2 = all(torch.allclose(p.grad, e, rtol=1e-6, atol=1e-6) for p, e in zip(m.parameters(), exp))
+        q.put((rank, ok1, ok2, len(gb.buckets)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bucket_order_pairs_across_gloo_ranks(world):
+    """World-size 2 / 3 gloo groups, torch.distributed.all_reduce standing in for tips_allreduce:
+    hooks fired in a different order on every rank still issue the same allreduces in the same
+    order (a mismatch would pair buckets of different sizes: an error or a hang)."""
+    import socket
+    import torch.multiprocessing as tmp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, ok1, ok2, nb in res:
+        assert ok1 and ok2 and nb > 3, (rank, ok1, ok2, nb)
