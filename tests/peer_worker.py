@@ -169,6 +169,32 @@ def overlap_case(c, rank, size, L, _lib, sp):
     return {"case": {"overlap": c["seed"], "passes": passes}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:4])}
 
 
+def pattern_case(c, rank, size, L, _lib, sp):
+    """A bucket past 2^31 elements (the reference's count is an int, utils.h:62) without host-side
+    inputs: f16 x_r[i] = (i % 64) + r on the device, so every partial sum is a small integer (exact
+    in f16 in any order) and the expected out[i] = p * (i % 64) + p (p - 1) / 2 is built on the
+    device too. Past 2^31 f16 elements the byte offsets pass 2^32: any 32-bit offset arithmetic in
+    the plans, the executor or the kernels would land bytes in the wrong place."""
+    import torch
+    n = int(c["pattern_n"])
+    base = torch.arange(64, device="cuda", dtype=torch.float16)
+    x = base.repeat(n // 64 + 1)[:n] + rank
+    y = torch.empty_like(x)
+    rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, 4, _lib.OP_SUM, sp)  # 4 = f16
+    torch.cuda.synchronize()
+    res = {"case": {"pattern_n": n}, "rc": int(rc)}
+    if rc:
+        res.update(ok=False, error=_lib.last_error())
+        return res
+    del x
+    exp = (base * size + size * (size - 1) / 2).repeat(n // 64 + 1)[:n]
+    res["ok"] = bool(torch.equal(y, exp))
+    if not res["ok"]:
+        bad = (y != exp).nonzero()
+        res["error"] = "%d elements differ, first at %d" % (bad.numel(), int(bad[0]))
+    return res
+
+
 def tape_case(c, rank, size, L, _lib, sp):
     """tips_amd.DistributedGradientTape on the device: every rank differentiates its own seeded
     loss; gradient() returns the sum over ranks (fusion buckets -> peer schedule), which must equal
@@ -535,6 +561,9 @@ def main():
             continue
         if c.get("overlap"):
             results.append(overlap_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("pattern_n"):
+            results.append(pattern_case(c, rank, size, L, _lib, sp))
             continue
         dtype, n, seed = c["dtype"], c["n"], c["seed"]
         if c.get("count_per_rank"):  # deliberately inconsistent counts: every rank must fail, none hang

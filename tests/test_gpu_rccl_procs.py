@@ -184,6 +184,13 @@ def test_control_plane_and_api_over_rccl(gpu, p):
     check(run_job(p, cases, timeout=600, **env))
 
 
+@pytest.mark.parametrize("algo,p", [("ring", 2), ("direct", 3)])
+def test_counts_past_int32_over_rccl(gpu, algo, p):
+    """A 2^31 + 13 element f16 bucket (4 GiB: byte offsets past 2^32) over real RCCL ranks, ring and
+    direct; exact integer-valued sums checked on the device (peer_worker.pattern_case)."""
+    check(run_job(p, [{"pattern_n": (1 << 31) + 13}], timeout=600, **rccl_env(algo)))
+
+
 @pytest.mark.parametrize("p", [2, 3])
 def test_overlapped_optimizer_over_rccl(gpu, p):
     """DistributedOptimizer's backward-overlapped buckets over real RCCL ranks: the post-accumulate

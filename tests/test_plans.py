@@ -179,3 +179,35 @@ def test_plans_randomized(oracle, algo, p, n, K, dtype, inplace, lanes):
         assert np.array_equal(o.view(np.uint8), exp.view(np.uint8))
     assert not pu.hazards(plans[0], ES[dtype], n * ES[dtype], inplace=inplace, lanes=lanes,
                           modes=("eager", "eager", "replay", "eager") if lanes == 1 else ("eager", "eager"))
+
+
+@pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
+@pytest.mark.parametrize("p,n,dtype", [(2, (1 << 31) + 13, F16), (3, (1 << 31) + 13, F32), (8, (1 << 31) + 13, F32),
+                                       (8, (3 << 31) + 7, F64)])
+def test_counts_past_int32(algo, p, n, dtype):
+    """Buckets of more than 2^31 elements (the reference's count is an int, utils.h:62; the C-ABI
+    takes int64): every rank's plan pairs, stays inside in / out / staging, and its sums and
+    receives together write every byte of out."""
+    es = ES[dtype]
+    plans = [pu.dump(algo, p, r, n, dtype) for r in range(p)]
+    pu.pairing(plans)
+    for r, pl in enumerate(plans):
+        lim = {pu.IN: n * es, pu.OUT: n * es, pu.STG: pl["staging"]}
+        writes = []
+        for st in pl["steps"]:
+            for x in st["xfers"]:
+                assert 0 <= x["off"] and x["off"] + x["bytes"] <= lim[x["buf"]], (r, x)
+                if not x["send"] and x["buf"] == pu.OUT:
+                    writes.append((x["off"], x["off"] + x["bytes"]))
+            for u in st["sums"]:
+                nb = u["count"] * es
+                for b, off in u["srcs"] + [u["dst"]]:
+                    assert 0 <= off and off + nb <= lim[b], (r, u)
+                if u["dst"][0] == pu.OUT:
+                    writes.append((u["dst"][1], u["dst"][1] + nb))
+        covered, end = 0, 0
+        for s, e in sorted(writes):
+            if e > end:
+                covered += e - max(s, end)
+                end = e
+        assert covered == n * es and end == n * es, (r, covered, n * es)
