@@ -123,9 +123,10 @@ def overlap_case(c, rank, size, L, _lib, sp):
 
     def model():
         torch.manual_seed(c["seed"])
-        return torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.Tanh(), torch.nn.Linear(256, 256),
-                                   torch.nn.Tanh(), torch.nn.Linear(256, 128), torch.nn.Tanh(),
-                                   torch.nn.Linear(128, 10)).cuda()
+        # odd widths: parameters of ragged sizes, padded to 256-B aligned slices in the flat buffer
+        return torch.nn.Sequential(torch.nn.Linear(64, 250), torch.nn.Tanh(), torch.nn.Linear(250, 251),
+                                   torch.nn.Tanh(), torch.nn.Linear(251, 127), torch.nn.Tanh(),
+                                   torch.nn.Linear(127, 10)).cuda()
 
     def batch(r, it, k):
         g = torch.Generator().manual_seed(c["seed"] * 1000 + r * 100 + it * 10 + k)

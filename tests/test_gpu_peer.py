@@ -196,3 +196,11 @@ def test_stale_mapping_refused_on_every_rank(gpu):
     for res in results:
         assert "stale or foreign IPC mapping" in res["results"][0]["error"]
     check(run_job(3, [{"dtype": F32, "n": 1000, "seed": 1}], TIPS_PEER_WS_MIB="4"))
+
+
+@pytest.mark.parametrize("ag", ["pull", "push"])
+def test_peer_counts_past_int32(gpu, ag):
+    """A 2^31 + 13 element f16 bucket (4 GiB; byte offsets past 2^32) through the peer schedule at
+    p = 3 in 256 MiB workspace pieces, both allgather modes; exact integer-valued sums checked on
+    the device (peer_worker.pattern_case)."""
+    check(run_job(3, [{"pattern_n": (1 << 31) + 13}], timeout=600, TIPS_PEER_WS_MIB="256", TIPS_PEER_AG=ag))

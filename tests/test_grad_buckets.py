@@ -37,6 +37,12 @@ def local_grads(seed_model=0, seeds=(1,)):
     return [p.grad.clone() for p in m.parameters()]
 
 
+def padded(p):
+    """A parameter's extent in the flat buffer: its elements rounded up to 256 B."""
+    al = 256 // p.element_size()
+    return (p.numel() + al - 1) // al * al
+
+
 def buckets_for(m, bucket_bytes, passes=1, average=False):
     calls = []
 
@@ -58,12 +64,12 @@ def test_layout_reversed_contiguous_and_bounded():
     for key, s, e, ps in gb.buckets:
         assert s == prev_end and e > s
         prev_end = e
-        assert sum(p.numel() for p in ps) == e - s
+        assert sum(padded(p) for p in ps) == e - s
         assert sum(p.numel() * 4 for p in ps) <= 2048 or len(ps) == 1  # one oversized parameter alone
         for p in ps:
             b, k, off = gb.where[id(p)]
-            assert s <= off and off + p.numel() <= e
-    assert prev_end == sum(p.numel() for p in params)
+            assert s <= off and off + p.numel() <= e and off * 4 % 256 == 0  # 256-B aligned slices
+    assert prev_end == sum(padded(p) for p in params)
     assert [p for b in gb.buckets for p in b[3]] == params[::-1]
     gb.remove()
 
@@ -105,7 +111,7 @@ def test_real_backward_issues_during_backward_and_sums():
     gb.synchronize()
     for p, e in zip(m.parameters(), exp):
         assert torch.equal(p.grad, e)
-    assert sum(calls) == 2 * sum(p.numel() for p in m.parameters())
+    assert sum(calls) == 2 * sum(padded(p) for p in m.parameters())
     gb.remove()
 
 
@@ -148,7 +154,7 @@ def test_synchronize_without_backward_reduces_each_group_once():
     for p in m.parameters():
         p.grad = torch.full_like(p, 2.0)
     gb.synchronize()
-    assert len(calls) == 1 and calls[0] == sum(p.numel() for p in m.parameters())
+    assert len(calls) == 1 and calls[0] == sum(padded(p) for p in m.parameters())
     assert gb.last_issue_log == [("group", (torch.float32, torch.device("cpu")))]
     for p in m.parameters():
         assert torch.equal(p.grad, torch.full_like(p, 2.0 * RANKS))

@@ -78,7 +78,10 @@ class _GradBuckets(object):
                 self.buckets.append(cur)
                 cur_bytes = 0
             self.where[id(p)] = (len(self.buckets) - 1, key, g["n"])
-            g["n"] += p.numel()
+            # every parameter (so every bucket) starts 256-B aligned, as fusion buckets pack
+            # (fusion.cc): the kernels' 16-B vector path; the padding stays zero
+            al = max(1, 256 // p.element_size())
+            g["n"] += (p.numel() + al - 1) // al * al
             cur[2] = g["n"]
             cur[3].append(p)
             cur_bytes += nbytes
@@ -247,7 +250,8 @@ class _DistributedOptimizer(object):
                 and self._compression is Compression.none and not sparse_as_dense):
             import torch
             ps = [p for g in optimizer.param_groups for p in g["params"]
-                  if p.requires_grad and p.is_cuda and p.layout == torch.strided]
+                  if p.requires_grad and p.is_cuda and p.layout == torch.strided
+                  and p.dtype in (torch.float32, torch.float64, torch.float16, torch.bfloat16)]
             ps = list({id(p): p for p in ps}.values())  # (a parameter listed twice is one gradient)
             if ps:
                 mib = float(os.environ.get("TIPS_GRAD_BUCKET_MIB", "25"))
