@@ -155,8 +155,16 @@ def overlap_case(c, rank, size, L, _lib, sp):
         issued = list(opt._buckets.issue_log)
         if issued != list(range(len(opt._buckets.buckets))):
             bad.append("it %d: hooks issued %s of %d buckets" % (it, issued, len(opt._buckets.buckets)))
+        # right after backward, work on the caller's stream already sees the reduced gradients
+        # (the end-of-backward callback ordered it after the side stream), before any synchronize
+        snap = [p.grad.clone() for p in m.parameters()]
+        for i, (g, s) in enumerate(zip(snap, sums)):
+            if not torch.equal(g, s):
+                bad.append("it %d: grad %d read after backward differs" % (it, i))
         with torch.no_grad():
             exp = [p - lr * s for p, s in zip(ref.parameters(), sums)]
+        if it == 1:
+            opt.synchronize()  # as a caller that clips would: step() must not reduce again
         opt.step()
         torch.cuda.synchronize()
         for i, (p, s) in enumerate(zip(m.parameters(), sums)):

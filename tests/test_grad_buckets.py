@@ -264,3 +264,19 @@ def test_bucket_order_pairs_across_gloo_ranks(world):
         assert p.exitcode == 0
     for rank, ok1, ok2, nb in res:
         assert ok1 and ok2 and nb > 3, (rank, ok1, ok2, nb)
+
+
+def test_end_of_backward_callback_joins_once_per_backward():
+    """A backward that issued buckets queues one autograd final callback, which orders the
+    streams the buckets were issued from after the side streams (on CPU: counted only)."""
+    m = make_model()
+    gb, _ = buckets_for(m, bucket_bytes=1536)
+    loss_of(m).backward()
+    assert getattr(gb, "backward_joins", 0) == 1 and not gb._cb_queued
+    gb.synchronize()
+    for p in m.parameters():
+        p.grad.zero_()
+    loss_of(m).backward()
+    assert gb.backward_joins == 2
+    gb.synchronize()
+    gb.remove()

@@ -111,6 +111,8 @@ class _GradBuckets(object):
         self._handles = []
 
     def _reset(self):
+        self._cb_queued = False
+        self._origins = {}  # device -> {stream handle: stream} the buckets were issued from
         self.ready = [0] * len(self.buckets)
         self.issued = [False] * len(self.buckets)
         self.next = 0
@@ -161,6 +163,16 @@ class _GradBuckets(object):
             while self.next < len(self.buckets) and self.ready[self.next] == len(self.buckets[self.next][3]):
                 self._issue(self.next)
                 self.next += 1
+                if not self._cb_queued:
+                    # at the end of this backward the streams it ran on wait for the issued
+                    # allreduces: whatever the caller does with .grad next (clipping, a norm, step)
+                    # is ordered after them, as the reference's compute_gradients hands back reduced
+                    # gradients (__init__.py:296-310)
+                    try:
+                        self._torch.autograd.Variable._execution_engine.queue_callback(self._after_backward)
+                        self._cb_queued = True
+                    except RuntimeError:  # not inside a backward pass (a direct _hook call)
+                        pass
 
     # the optimizer sets these two
     def active(self):
@@ -169,12 +181,24 @@ class _GradBuckets(object):
     def final_pass(self):
         return True
 
+    def _after_backward(self):
+        """Autograd's final callback of a backward that issued buckets: its streams wait for the
+        side streams (stream order only; the host does not block)."""
+        with self._lock:
+            self._cb_queued = False
+            for dev, origins in self._origins.items():
+                for o in origins.values():
+                    o.wait_stream(self._streams[dev])
+            self.backward_joins = getattr(self, "backward_joins", 0) + 1
+
     def _issue_range(self, key, start, end, tag):
         torch = self._torch
         flat = self.groups[key]["flat"][start:end]
         side = self._side(key[1])
         if side is not None:
-            side.wait_stream(torch.cuda.current_stream(key[1]))
+            cur = torch.cuda.current_stream(key[1])
+            self._origins.setdefault(key[1], {})[cur.cuda_stream] = cur
+            side.wait_stream(cur)
             ctx = torch.cuda.stream(side)
         else:
             import contextlib
@@ -245,6 +269,7 @@ class _DistributedOptimizer(object):
         if self._passes < 1:
             raise ValueError("backward_passes_per_step must be >= 1")
         self._buckets = None
+        self._synchronized = False
         from . import Compression
         if (os.environ.get("TIPS_OVERLAP_BACKWARD", "1") != "0" and self._bucket_view
                 and self._compression is Compression.none and not sparse_as_dense):
@@ -294,9 +319,13 @@ class _DistributedOptimizer(object):
         bucket views (default) as one allreduce of the flat buffer they are views of, no copies;
         with TIPS_GRAD_BUCKET_VIEW=0 through the fusion buckets (tips_fused_allreduce: pack, one
         allreduce per bucket, unpack straight back into .grad - 4 x the gradient bytes of HBM
-        traffic). The others go through allreduce_grads and are replaced by its outputs."""
+        traffic). With backward-overlapped buckets (_GradBuckets, the default at N > 1) most of
+        that was issued during backward, and the end of backward already ordered the caller's
+        stream after it; this issues the rest and joins. step() does not reduce again in an
+        iteration where the caller already called synchronize() (to clip gradients, say)."""
         from . import Compression, _fusable, allreduce_grads, size
         from .ops import FusedList
+        self._synchronized = True
         params = self._params_with_grad()
         if self._buckets is not None and size() > 1:
             # backward-overlapped buckets: the hooks issued what was ready; issue the rest in order
@@ -367,7 +396,9 @@ class _DistributedOptimizer(object):
         self._calls += 1
         if self._calls % self._passes:
             return None
-        self.synchronize()
+        if not self._synchronized:  # (a caller that ran synchronize() itself, e.g. to clip, is not reduced twice)
+            self.synchronize()
+        self._synchronized = False
         return self._optimizer.step(closure) if closure is not None else self._optimizer.step()
 
 
