@@ -115,6 +115,30 @@ def cpu_baseline(bucket_elems):
     return out
 
 
+def cpu_ring_baseline(world, elems=16 << 20, iters=20):
+    """N > 1: the reference's allreduce at the same rank count on host cores - MPI_Allreduce
+    (MPI_FLOAT, MPI_SUM) under MPICH, mpirun -np N, one bounded 64 MiB bucket per rank (config 3's
+    1 GiB would take ~1 s per call at np = 8). Reported as `cpu_ring_baseline` in the
+    same units as `value` (N x bucket bytes per second). Rank 0 runs it before anything touches
+    the GPU; the other ranks wait for it in the bootstrap."""
+    harness = os.path.join(REPO, "oracle", "build", "mpi_allreduce_ref")
+    mpirun = "/opt/conda/bin/mpirun"
+    if not (os.path.exists(harness) and os.path.exists(mpirun)):
+        return {"error": "reference MPI baseline unavailable on box (no MPICH harness)"}
+    try:
+        r = subprocess.run([mpirun, "-np", str(world), harness, "bench", "0", str(elems), str(iters)],
+                           capture_output=True, text=True, timeout=150)
+        t = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["sec_per_call"]
+    except Exception as e:  # noqa: BLE001 - never fail the bench on the baseline leg
+        return {"error": "reference MPI baseline failed: %r" % (e,)}
+    return {"value": round(world * elems * 4 / t / GIB, 3), "unit": "GiB/s", "cores": world, "kind": "reference",
+            "ms_per_call": round(t * 1e3, 3),
+            "sample": "MPI_Allreduce(in,out,%d,MPI_FLOAT,MPI_SUM,MPI_COMM_WORLD) as in tips/core/collective/"
+                      "utils.h:60-65, MPICH 3.3.2, mpirun -np %d (1 core each), one %d MiB fp32 bucket per rank, "
+                      "%d timed calls after 1 warm-up; value = %d x bucket bytes / time, as the GPU line's"
+                      % (elems, world, elems * 4 >> 20, iters, world)}
+
+
 def pmc_traffic(kernel_substr):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json), or None."""
     import glob
@@ -681,6 +705,9 @@ def bench_allreduce(args):
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "420")), rank)
     topo = gpu_topology() if rank == 0 and world > 1 else None
+    cpu_ring = None
+    if rank == 0 and world > 1 and not args.no_cpu_baseline and args.workload in ("auto", "bucket"):
+        cpu_ring = cpu_ring_baseline(world)  # (child processes: before this process touches the GPU)
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))  # (several ranks per GPU only under TIPS_NO_RCCL)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import tips_amd
@@ -940,6 +967,8 @@ def bench_allreduce(args):
         line["gradient_api"] = gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, ms)
     if topo:
         line["gpu_topology"] = topo
+    if cpu_ring:
+        line["cpu_ring_baseline"] = cpu_ring
     if fallbacks:
         line["failed_schedules"] = fallbacks
     if workload == "negotiated1000":

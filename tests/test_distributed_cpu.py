@@ -174,3 +174,14 @@ def test_gpu_topology_parse(monkeypatch):
     topo = bench.gpu_topology()
     assert topo["hops"] == [["0", "1", "1"], ["1", "0", "1"], ["1", "1", "0"]]
     assert topo["link_type"][1] == ["XGMI", "0", "XGMI"]
+
+
+def test_cpu_ring_baseline_runs_the_reference_call():
+    """bench.cpu_ring_baseline: the reference's MPI_Allreduce under MPICH at np = N (the N > 1
+    lines' `cpu_ring_baseline`), here on a tiny bucket; reported in the GPU line's units."""
+    sys.path.insert(0, REPO)
+    import bench
+    out = bench.cpu_ring_baseline(2, elems=1 << 16, iters=3)
+    if "error" in out and "unavailable" in out["error"]:
+        pytest.skip(out["error"])
+    assert out["value"] > 0 and out["cores"] == 2 and out["kind"] == "reference", out
