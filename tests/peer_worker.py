@@ -237,8 +237,9 @@ def collectives_case(c, rank, size, L, _lib, sp):
     over the peer transport (tips_broadcast, tips_allgatherv and the record exchange routed to
     peer.cc when the peer schedule is selected). Broadcast: every dtype, device and host, and one
     bucket larger than the workspace (pieces); the result must equal the root's tensor bit for
-    bit. Allgather: ragged first dimensions, one rank contributing zero rows. A root that differs
-    between ranks must fail on every rank with TIPS_ERR_MISMATCH and leave the job usable."""
+    bit. Allgather: ragged first dimensions, one rank contributing zero rows, and the reference's
+    two allgather KATs (utils_test.cc:39-112). A root that differs between ranks must fail on every
+    rank with TIPS_ERR_MISMATCH and leave the job usable."""
     import numpy as np
     import torch
     import tips_amd
@@ -277,6 +278,21 @@ def collectives_case(c, rank, size, L, _lib, sp):
     gi = tips_amd.allgather_op(np.arange(rank + 1, dtype=np.int64) + 10 * rank)
     if not np.array_equal(gi, np.concatenate([np.arange(r + 1, dtype=np.int64) + 10 * r for r in range(size)])):
         bad.append("host allgather differs")
+    # the reference's allgather KATs, their inputs and checks (tol 1e-5; exact here):
+    # utils_test.cc:39-64 TestAllgatherOp - a [2, 3] float tensor of the rank's value, gathered into
+    # [2 * size, 3], slice i all i;
+    ka = tips_amd.allgather_op(torch.full((2, 3), float(rank), device="cuda"))
+    torch.cuda.synchronize()
+    if tuple(ka.shape) != (2 * size, 3) or not all(bool((ka[2 * i:2 * i + 2] == i).all()) for i in range(size)):
+        bad.append("utils_test TestAllgatherOp KAT differs")
+    # utils_test.cc:66-112 TestAllgathervOp - the first dimensions (int32 rank + 1) gathered first,
+    # then [rank + 1, 4] float tensors of value rank + 1 gathered into [sum, 4], rows in rank order
+    fr = tips_amd.allgather_op(np.array([rank + 1], dtype=np.int32))
+    kv = tips_amd.allgather_op(torch.full((rank + 1, 4), float(rank + 1), device="cuda"))
+    torch.cuda.synchronize()
+    want = torch.cat([torch.full((r + 1, 4), float(r + 1)) for r in range(size)])
+    if not np.array_equal(fr, np.arange(1, size + 1, dtype=np.int32)) or not torch.equal(kv.cpu(), want):
+        bad.append("utils_test TestAllgathervOp KAT differs")
     tips_amd.set_consistency_check(True)
     try:
         x = tensor(rank, torch.float32, 1000, 80).cuda()
