@@ -241,6 +241,28 @@ TIPS_API int tips_enqueue_allreduce_shaped_n(const char* const* names, const voi
                                              int64_t* handles);
 /* tips_wait on each of n handles (handles <= 0 are skipped): TIPS_OK or the first failure. */
 TIPS_API int tips_wait_n(const int64_t* handles, int n);
+/* Named broadcast through the same negotiation (the reference's MPIBroadcast op,
+ * ops.cc:214-286 -> EnqueueTensorCollective(RequestType_BROADCAST); PerformCollectiveOp's
+ * broadcast branch, coordinator.cc:275-295): rank 0 checks dtype and shape with
+ * ConstructResponseMessage's rules and text ("Mismatched broadcast tensor shapes: ..."), and
+ * that every rank names the same root. out = root's `in`, on `stream`, in rank 0's readiness
+ * order with the other requests. (The reference's branch always broadcasts from rank 0 -
+ * "root_rank should be passed in", coordinator.cc:280; here `root` is honoured.) */
+TIPS_API int64_t tips_enqueue_broadcast(const char* name, const void* in, void* out, const int64_t* shape, int ndim,
+                                        int dtype, int root, void* stream);
+/* Output allocator of a named allgather: returns device memory of `bytes` (or NULL). Called
+ * once, from the negotiation thread, when the output's size is known - as the reference's
+ * PerformCollectiveOp allocates the op's output only then (context->allocate_output,
+ * coordinator.cc:305-313). The caller owns what it returns. */
+typedef void* (*tips_alloc_fn)(void* ctx, int64_t bytes);
+/* Named allgather (MPIAllgather, ops.cc:156-212 -> RequestType_ALLGATHER): every rank's tensor
+ * concatenated along dimension 0, in rank order. Rank 0 checks ndim and every dimension but
+ * the first (GatherFirstRankSizes's rules and text, coordinator.cc:40-88) and sends every rank
+ * the first dimensions; each rank then allocates its output through alloc(ctx, bytes), stores
+ * the output's first dimension in *out_rows (valid once tips_wait / tips_poll report done) and
+ * gathers on `stream`. ndim >= 1. */
+TIPS_API int64_t tips_enqueue_allgather(const char* name, const void* in, const int64_t* shape, int ndim, int dtype,
+                                        void* stream, tips_alloc_fn alloc, void* ctx, int64_t* out_rows);
 /* The negotiation protocol with an executor that only logs (no GPU): each
  * rank enqueues the newline-separated "name dtype count" lines of `requests`
  * ("@sleep ms" pauses, "@wait" blocks until every earlier request is

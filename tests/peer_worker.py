@@ -178,6 +178,69 @@ def overlap_case(c, rank, size, L, _lib, sp):
     return {"case": {"overlap": c["seed"], "passes": passes}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:4])}
 
 
+def named_collectives_case(c, rank, size, L, _lib, sp):
+    """Named broadcast / allgather / allreduce requests through the negotiation (the reference's
+    three request types, coordinator.cc:243-353), enqueued in a different order on every rank:
+    broadcasts from several roots, allgathers with ragged first dimensions (one rank contributing
+    zero rows) and 3-d shapes, allreduces in between. Then a broadcast whose root differs between
+    ranks must fail on every rank (rank 0's root check) and a later request must still run."""
+    import numpy as np
+    import torch
+    import tips_amd
+    seed = c["seed"]
+
+    def t(r, salt, shape, dtype=torch.float32):
+        g = torch.Generator().manual_seed(seed * 1000 + 31 * salt + r)
+        return (torch.randn(*shape, generator=g) * 10).to(dtype)
+
+    jobs = []
+    for k in range(6):
+        jobs.append(("bc%d" % k, "bc", k % size, (7 + 3 * k, 5), torch.float32 if k % 2 else torch.int32))
+        jobs.append(("ag%d" % k, "ag", None, None, torch.float32 if k % 3 else torch.bfloat16))
+        jobs.append(("ar%d" % k, "ar", None, (100 + k,), torch.float32))
+    order = list(range(len(jobs)))
+    np.random.default_rng(seed * 7 + rank).shuffle(order)
+
+    def ag_rows(k, r):
+        return 0 if (r == 1 and k == 2) else (k + r) % 4 + 1
+
+    handles = {}
+    for i in order:
+        name, kind, root, shape, dt = jobs[i]
+        k = int(name[2:])
+        if kind == "bc":
+            handles[name] = tips_amd.broadcast_async(t(rank, i, shape, dt).cuda(), root, name)
+        elif kind == "ag":
+            handles[name] = tips_amd.allgather_async(t(rank, i, (ag_rows(k, rank), 3, 2), dt).cuda(), name)
+        else:
+            handles[name] = tips_amd.allreduce_async(t(rank, i, shape, dt).cuda(), name)
+    bad = []
+    for i, (name, kind, root, shape, dt) in enumerate(jobs):
+        k = int(name[2:])
+        got = tips_amd.synchronize(handles[name]).cpu()
+        if kind == "bc":
+            exp = t(root, i, shape, dt)
+        elif kind == "ag":
+            exp = torch.cat([t(r, i, (ag_rows(k, r), 3, 2), dt) for r in range(size)])
+        else:
+            exp = t(0, i, shape, dt)
+            for r in range(1, size):
+                exp = exp + t(r, i, shape, dt)
+        same = torch.equal(got, exp) if kind != "ar" else torch.allclose(got, exp, rtol=1e-6, atol=1e-5)
+        if got.shape != exp.shape or not same:
+            bad.append("%s (%s) differs: %s vs %s" % (name, kind, tuple(got.shape), tuple(exp.shape)))
+    try:
+        tips_amd.synchronize(tips_amd.broadcast_async(t(rank, 99, (16,)).cuda(), rank % 2, "bad_root"))
+        bad.append("a root differing between ranks was accepted")
+    except tips_amd.TipsError as e:
+        if "Mismatched broadcast root ranks" not in str(e):
+            bad.append("bad root: %s" % e)
+    got = tips_amd.synchronize(tips_amd.broadcast_async(t(rank, 98, (16,)).cuda(), 0, "after")).cpu()
+    if not torch.equal(got, t(0, 98, (16,))):
+        bad.append("broadcast after the refused one differs")
+    return {"case": {"named_collectives": seed}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5])}
+
+
 def pattern_case(c, rank, size, L, _lib, sp):
     """A bucket past 2^31 elements (the reference's count is an int, utils.h:62) without host-side
     inputs: f16 x_r[i] = (i % 64) + r on the device, so every partial sum is a small integer (exact
@@ -586,6 +649,9 @@ def main():
             continue
         if c.get("overlap"):
             results.append(overlap_case(c, rank, size, L, _lib, sp))
+            continue
+        if c.get("named_collectives"):
+            results.append(named_collectives_case(c, rank, size, L, _lib, sp))
             continue
         if c.get("pattern_n"):
             results.append(pattern_case(c, rank, size, L, _lib, sp))

@@ -204,3 +204,12 @@ def test_peer_counts_past_int32(gpu, ag):
     p = 3 in 256 MiB workspace pieces, both allgather modes; exact integer-valued sums checked on
     the device (peer_worker.pattern_case)."""
     check(run_job(3, [{"pattern_n": (1 << 31) + 13}], timeout=600, TIPS_PEER_WS_MIB="256", TIPS_PEER_AG=ag))
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_named_broadcast_allgather_over_peer(gpu, p):
+    """The negotiated broadcast / allgather / allreduce mix over the peer transport (TIPS_ALGO_PEER:
+    tips_broadcast / tips_allgatherv go through the IPC workspaces); see the RCCL twin."""
+    port = str(29500 + os.getpid() % 150 + 3 * p)
+    check(run_job(p, [{"named_collectives": True, "seed": 13 + p}], timeout=600, TIPS_PEER_WS_MIB="4",
+                  MASTER_ADDR="127.0.0.1", MASTER_PORT=port))

@@ -184,6 +184,15 @@ def test_control_plane_and_api_over_rccl(gpu, p):
     check(run_job(p, cases, timeout=600, **env))
 
 
+@pytest.mark.parametrize("p", [2, 3])
+def test_named_broadcast_allgather_over_rccl(gpu, p):
+    """tips_enqueue_broadcast / tips_enqueue_allgather (Python broadcast_async / allgather_async)
+    with named allreduces, a different enqueue order on every rank, over real RCCL ranks: rank 0's
+    order and checks, the allgather's output allocated once the sizes are known; bit-exact
+    broadcast and allgather, a root mismatch refused on every rank (peer_worker.named_collectives_case)."""
+    check(run_job(p, [{"named_collectives": True, "seed": 3 + p}], timeout=600, **rccl_env("auto")))
+
+
 @pytest.mark.parametrize("algo,p", [("ring", 2), ("direct", 3)])
 def test_counts_past_int32_over_rccl(gpu, algo, p):
     """A 2^31 + 13 element f16 bucket (4 GiB: byte offsets past 2^32) over real RCCL ranks, ring and

@@ -119,3 +119,35 @@ def test_shape_rank_and_scalar():
         assert got["a"] == "ERR Mismatched allreduce tensor shapes: [4] vs [4,1]"
         assert got["b"] == "OK"
         assert got["c"] == "ERR Mismatched allreduce tensor shapes: [4] vs [2,2]"
+
+
+def test_broadcast_and_allgather_requests():
+    """Named broadcast and allgather requests (the reference's RequestType_BROADCAST / _ALLGATHER,
+    coordinator.cc:129-186, 40-88) through the same negotiation, mixed with allreduces, enqueued in
+    different orders: rank 0 applies each type's rule and every rank logs the same verdicts in the
+    same order; an allgather's decision carries every rank's first dimension (tensor_sizes)."""
+    r0 = ("g 0 12 3,4 ag\n"            # allgather: rows 3 / 5 / 1, 4 columns everywhere -> sizes 3,5,1
+          "b 0 6 2,3 bc:1\n"           # broadcast from rank 1, same shape everywhere
+          "s 0 8 2,4 ag\n"             # allgather: second dimension differs on rank 2
+          "bs 0 8 2,4 bc:0\n"          # broadcast: shapes differ on rank 1
+          "br 1 4 - bc:0\n"            # broadcast: roots differ on rank 2
+          "ak 0 5 - ag\n"              # allgather of 1-d tensors of 5 / 2 / 0 rows
+          "op 0 4 - ar\n"              # allreduce on ranks 0, 1 and allgather on rank 2
+          "x 0 10")
+    r1 = ("x 0 10\nak 0 2 - ag\nop 0 4 - ar\nbr 1 4 - bc:0\nbs 0 8 4,2 bc:0\ns 0 8 2,4 ag\nb 0 6 2,3 bc:1\n"
+          "g 0 20 5,4 ag")
+    r2 = ("op 0 4 - ag\nb 0 6 2,3 bc:1\ng 0 4 1,4 ag\nbr 1 4 - bc:2\nak 0 0 - ag\ns 0 6 2,3 ag\nbs 0 8 2,4 bc:0\n"
+          "x 0 10")
+    res = run([r0, r1, r2])
+    logs = [lines(log) for _, _, log, _ in res]
+    for _, rc, _, err in res:
+        assert rc == 0, err
+    assert logs[0] == logs[1] == logs[2]
+    got = dict(l.split(" ", 1) for l in logs[0])
+    assert got["g"] == "OK sizes=3,5,1"
+    assert got["ak"] == "OK sizes=5,2,0"
+    assert got["b"] == "OK" and got["x"] == "OK"
+    assert got["s"] == "ERR Mismatched allgather tensor shapes: 1-th dimension 4 vs 3"
+    assert got["bs"] == "ERR Mismatched broadcast tensor shapes: [2,4] vs [4,2]"
+    assert got["br"] == "ERR Mismatched broadcast root ranks: 0 vs 2"
+    assert got["op"] == "ERR Mismatched operations found: 0 vs 1."

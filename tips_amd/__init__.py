@@ -8,7 +8,7 @@ libtips_hip.so (include/tips_hip.h); there is no CPU fallback.
 """
 from .basics import TipsBasics, init, is_initialized, rank, shutdown, size
 from .compression import Compression, Compressor, FP16Compressor, NoneCompressor
-from .ops import (Handle, allgather_op, allreduce_async, allreduce_async_many, synchronize_many, allreduce_op, broadcast_op, poll, synchronize, broadcast_variables, bucket_sum, fused_allreduce,
+from .ops import (Handle, allgather_async, allgather_op, allreduce_async, broadcast_async, allreduce_async_many, synchronize_many, allreduce_op, broadcast_op, poll, synchronize, broadcast_variables, bucket_sum, fused_allreduce,
                   fused_allreduce_, rank_op, registered_host_buffer, set_algorithm, set_consistency_check, size_op)
 from ._lib import TipsError, TipsLibraryError
 from . import tensors as _tensors
@@ -28,7 +28,7 @@ class IndexedSlices(object):
         self.dense_shape = dense_shape
 
 __all__ = [
-    "allreduce", "IndexedSlices", "allreduce_async", "allreduce_async_many", "synchronize_many", "poll", "synchronize", "Handle", "allreduce_grads", "allreduce_op", "allgather_op", "broadcast_op", "broadcast_variables",
+    "allreduce", "IndexedSlices", "allreduce_async", "broadcast_async", "allgather_async", "allreduce_async_many", "synchronize_many", "poll", "synchronize", "Handle", "allreduce_grads", "allreduce_op", "allgather_op", "broadcast_op", "broadcast_variables",
     "set_consistency_check", "registered_host_buffer", "bucket_sum", "fused_allreduce", "fused_allreduce_", "init",
     "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",

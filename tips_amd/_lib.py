@@ -51,6 +51,8 @@ _lib = None
 
 _c_void_pp = ctypes.POINTER(ctypes.c_void_p)
 _c_i64_p = ctypes.POINTER(ctypes.c_int64)
+# tips_alloc_fn (include/tips_hip.h): void* (*)(void* ctx, int64_t bytes)
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 # (name, restype, argtypes) — must match include/tips_hip.h
 _SIGNATURES = [
@@ -96,6 +98,12 @@ _SIGNATURES = [
       _c_i64_p]),
     ("tips_wait_n", ctypes.c_int, [_c_i64_p, ctypes.c_int]),
     ("tips_wait", ctypes.c_int, [ctypes.c_int64]),
+    ("tips_enqueue_broadcast", ctypes.c_int64,
+     [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+      ctypes.c_void_p]),
+    ("tips_enqueue_allgather", ctypes.c_int64,
+     [ctypes.c_char_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, _c_i64_p]),
     ("tips_negotiation_selftest", ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),

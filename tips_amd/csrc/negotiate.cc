@@ -51,6 +51,11 @@ struct Req {
   int64_t count = 0;
   std::vector<int64_t> shape;  // dims (the reference's TensorShape; [count] for unshaped requests)
   int dtype = 0;
+  int type = TIPS_REQ_ALLREDUCE;  // message::RequestType: allreduce, allgather, broadcast
+  int root = 0;                   // broadcast
+  tips_alloc_fn alloc = nullptr;  // allgather: output allocator, called once the sizes are known
+  void* actx = nullptr;
+  int64_t* out_rows = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   std::shared_ptr<GroupEv> gev;  // set when the request ran inside a fused batch (then ev is unused)
@@ -99,10 +104,14 @@ struct Reader {
   }
 };
 
-// announce (rank -> rank 0): u8 shutdown, u32 n, n x {i32 dtype, i64 count, u32 ndim, ndim x i64 dim, str name}
-//   (the fields of the reference's RequestMessage, collective_messages.fbs: dtype, name, shape)
-// response (rank 0 -> all):  u8 shutdown, u32 n, n x {u8 ok, str name, str error}
+// announce (rank -> rank 0): u8 shutdown, u32 n,
+//   n x {i32 type, i32 root, i32 dtype, i64 count, u32 ndim, ndim x i64 dim, str name}
+//   (the fields of the reference's RequestMessage, collective_messages.fbs: request type, dtype,
+//   name, shape; plus the broadcast root, which the reference never sends)
+// response (rank 0 -> all):  u8 shutdown, u32 n, n x {u8 ok, str name, str error, u32 m, m x i64 size}
+//   (sizes: an allgather's first dimension per rank, the ResponseMessage's tensor_sizes)
 struct Announce {
+  int type = TIPS_REQ_ALLREDUCE, root = 0;
   int dtype;
   int64_t count;
   std::vector<int64_t> shape;
@@ -112,6 +121,7 @@ struct Announce {
 struct Decision {
   bool ok;
   std::string name, err;
+  std::vector<int64_t> sizes;
 };
 
 // ---- rank 0's table (IncreTensorCount + ConstructResponseMessage) ---------------
@@ -121,6 +131,7 @@ struct Decision {
 struct Table {
   struct Row {
     std::vector<int64_t> rec;  // p records of TIPS_REQUEST_WORDS
+    std::vector<int> roots;    // broadcast root each rank named
     std::vector<char> seen;
     int nseen = 0;
     bool queued = false;
@@ -136,6 +147,7 @@ struct Table {
       Row r;
       r.rec.assign((size_t)p * TIPS_REQUEST_WORDS, 0);
       r.seen.assign(p, 0);
+      r.roots.assign(p, 0);
       it = rows.emplace(a.name, std::move(r)).first;
     }
     Row& r = it->second;
@@ -145,8 +157,9 @@ struct Table {
       r.seen[rank] = 1;
       r.nseen++;
       int64_t* rec = &r.rec[(size_t)rank * TIPS_REQUEST_WORDS];
-      rec[0] = TIPS_REQ_ALLREDUCE;
+      rec[0] = a.type;
       rec[1] = a.dtype;
+      r.roots[rank] = a.root;
       rec[2] = (int64_t)a.shape.size();  // (<= TIPS_MAX_DIMS: checked at enqueue and on decode)
       for (size_t d = 0; d < a.shape.size(); d++) rec[3 + d] = a.shape[d];
     }
@@ -166,8 +179,18 @@ struct Table {
       if (!r.dup.empty()) {
         out.push_back({false, name, r.dup});
       } else {
-        const int rc = check_records(r.rec.data(), p);
-        out.push_back({rc == 0, name, rc == 0 ? std::string() : last_error()});
+        const int W = TIPS_REQUEST_WORDS;
+        int rc = check_records(r.rec.data(), p);
+        Decision d{rc == 0, name, rc == 0 ? std::string() : last_error(), {}};
+        if (d.ok && r.rec[0] == TIPS_REQ_BROADCAST)
+          for (int i = 1; i < p && d.ok; i++)
+            if (r.roots[i] != r.roots[0]) {
+              d.ok = false;
+              d.err = "Mismatched broadcast root ranks: " + std::to_string(r.roots[0]) + " vs " + std::to_string(r.roots[i]);
+            }
+        if (d.ok && r.rec[0] == TIPS_REQ_ALLGATHER)  // GatherFirstRankSizes (coordinator.cc:40-88)
+          for (int i = 0; i < p; i++) d.sizes.push_back(r.rec[(size_t)i * W + 3]);
+        out.push_back(std::move(d));
       }
       rows.erase(it);
     }
@@ -231,10 +254,17 @@ class Negotiator {
   }
 
   int64_t enqueue(const std::string& name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
-                  hipStream_t s) {
+                  hipStream_t s, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
+                  void* actx = nullptr, int64_t* out_rows = nullptr) {
     if (ndim < 0 || ndim > TIPS_MAX_DIMS) return fail(TIPS_ERR_INVALID_ARG, "bad ndim %d", ndim);
+    if (type == TIPS_REQ_ALLGATHER && ndim < 1) return fail(TIPS_ERR_INVALID_ARG, "An empty tensor found");
     auto r = std::make_shared<Req>();
     r->name = name;
+    r->type = type;
+    r->root = root;
+    r->alloc = alloc;
+    r->actx = actx;
+    r->out_rows = out_rows;
     r->in = in;
     r->out = out;
     r->count = 1;
@@ -250,8 +280,8 @@ class Negotiator {
       // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
       // st.device is fixed from init on)
       TRY(set_device(S()));
-      if (r->count > 0 && !(is_device_ptr(in) && is_device_ptr(out)))
-        return fail(TIPS_ERR_INVALID_ARG, "named allreduce needs device pointers");
+      if (r->count > 0 && !(is_device_ptr(in) && (type == TIPS_REQ_ALLGATHER || is_device_ptr(out))))
+        return fail(TIPS_ERR_INVALID_ARG, "named requests need device pointers");
       {
         std::lock_guard<std::mutex> l(m_);
         if (!ev_pool_.empty()) {
@@ -371,6 +401,8 @@ class Negotiator {
       w.put<uint8_t>(stopping ? 1 : 0);
       w.put<uint32_t>((uint32_t)batch.size());
       for (auto& r : batch) {
+        w.put<int32_t>(r->type);
+        w.put<int32_t>(r->root);
         w.put<int32_t>(r->dtype);
         w.put<int64_t>(r->count);
         w.put<uint32_t>((uint32_t)r->shape.size());
@@ -388,6 +420,8 @@ class Negotiator {
         d.ok = rd.get<uint8_t>() != 0;
         d.name = rd.str();
         d.err = rd.str();
+        const uint32_t m = rd.get<uint32_t>();
+        for (uint32_t k = 0; k < m && rd.ok && k < (1u << 20); k++) d.sizes.push_back(rd.get<int64_t>());
         ds.push_back(std::move(d));
       }
       if (!rd.ok) {
@@ -447,6 +481,8 @@ class Negotiator {
       const uint32_t n = rd.get<uint32_t>();
       for (uint32_t i = 0; i < n && rd.ok; i++) {
         Announce a;
+        a.type = rd.get<int32_t>();
+        a.root = rd.get<int32_t>();
         a.dtype = rd.get<int32_t>();
         a.count = rd.get<int64_t>();
         const uint32_t ndim = rd.get<uint32_t>();
@@ -468,6 +504,8 @@ class Negotiator {
       w.put<uint8_t>(d.ok ? 1 : 0);
       w.str(d.name);
       w.str(d.err);
+      w.put<uint32_t>((uint32_t)d.sizes.size());
+      for (int64_t v : d.sizes) w.put<int64_t>(v);
     }
     *resp = w.b;
     return true;
@@ -488,7 +526,11 @@ class Negotiator {
         if (it == by_name_.end()) continue;  // (cannot happen: every rank announced it)
         reqs[i] = it->second;
         by_name_.erase(it);
-        if (dry_) log_.push_back(ds[i].name + (ds[i].ok ? " OK" : " ERR " + ds[i].err));
+        if (dry_) {
+          std::string sz;
+          for (size_t k = 0; k < ds[i].sizes.size(); k++) sz += (k ? "," : " sizes=") + std::to_string(ds[i].sizes[k]);
+          log_.push_back(ds[i].name + (ds[i].ok ? " OK" + sz : " ERR " + ds[i].err));
+        }
       }
     }
     std::vector<int> state(n, 0);
@@ -499,8 +541,6 @@ class Negotiator {
     }
     if (!dry_) {
       State& st = S();
-      std::lock_guard<std::mutex> lk(st.mu);
-      int rc0 = set_device(st);
       const bool fuse = env_i64("TIPS_NEGOTIATED_FUSION", 1) != 0;
       const int64_t threshold = fusion_threshold_bytes();
       for (size_t i = 0; i < n;) {
@@ -508,11 +548,22 @@ class Negotiator {
           i++;
           continue;
         }
+        if (reqs[i]->type != TIPS_REQ_ALLREDUCE) {  // broadcast / allgather: one at a time, in order
+          if (run_other(*reqs[i], ds[i].sizes) != 0) {
+            state[i] = -1;
+            msg[i] = last_error();
+          }
+          i++;
+          continue;
+        }
+        std::lock_guard<std::mutex> lk(st.mu);
+        const int rc0 = set_device(st);
         const int dtype = reqs[i]->dtype;
         const int64_t es = tips::dtype_size(dtype);
         size_t j = i;
         int64_t bytes = 0;
-        while (fuse && j < n && reqs[j] && state[j] == 2 && reqs[j]->dtype == dtype && reqs[j]->count * es < threshold &&
+        while (fuse && j < n && reqs[j] && state[j] == 2 && reqs[j]->type == TIPS_REQ_ALLREDUCE &&
+               reqs[j]->dtype == dtype && reqs[j]->count * es < threshold &&
                round_up(bytes, kAlignBytes) + reqs[j]->count * es <= threshold) {
           bytes = round_up(bytes, kAlignBytes) + reqs[j]->count * es;
           j++;
@@ -541,6 +592,36 @@ class Negotiator {
         reqs[i]->err = msg[i];
       }
     cv_.notify_all();
+  }
+
+  // PerformCollectiveOp's broadcast and allgather branches (coordinator.cc:275-336) for one
+  // decided request, through the synchronous collectives (they take st.mu themselves). The
+  // allgather's output is allocated only now, when rank 0 has sent every rank's first
+  // dimension, as the reference's allocate_output; its first dimension goes to *out_rows.
+  int run_other(Req& r, const std::vector<int64_t>& sizes) {
+    if (r.type == TIPS_REQ_BROADCAST) {
+      TRY(tips_broadcast(r.in, r.out, r.count, r.dtype, r.root, r.stream));
+    } else {
+      const int64_t es = tips::dtype_size(r.dtype);
+      int64_t row = 1, rows = 0;
+      for (size_t d = 1; d < r.shape.size(); d++) row *= r.shape[d];
+      std::vector<int64_t> counts;
+      for (int64_t v : sizes) {
+        counts.push_back(v * row);
+        rows += v;
+      }
+      if ((int)counts.size() != S().size) return fail(TIPS_ERR_MISMATCH, "allgather %s: sizes of %zu ranks", r.name.c_str(), counts.size());
+      const int64_t bytes = rows * row * es;
+      if (bytes > 0) {
+        if (!r.alloc) return fail(TIPS_ERR_INVALID_ARG, "allgather %s: no output allocator", r.name.c_str());
+        r.out = r.alloc(r.actx, bytes);
+        if (!r.out) return fail(TIPS_ERR_HIP, "allgather %s: the output allocator returned NULL for %lld B", r.name.c_str(), (long long)bytes);
+      }
+      if (r.out_rows) *r.out_rows = rows;
+      TRY(tips_allgatherv(r.in, r.count, r.out, counts.data(), r.dtype, r.stream));
+    }
+    HIP_TRY(hipEventRecord(r.ev, r.stream));
+    return 0;
   }
 
   // reqs[i, j): one fused allreduce on their stream (or, if they came on several, on a
@@ -649,16 +730,22 @@ Negotiator* negotiator() {  // started by the first named request (collective)
 }
 
 int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
-                      void* stream) {
+                      void* stream, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
+                      void* actx = nullptr, int64_t* out_rows = nullptr) {
   TRY(check_dtype(dtype));
   if (!name || !*name || ndim < 0 || ndim > TIPS_MAX_DIMS || (ndim > 0 && !shape))
-    return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
+    return fail(TIPS_ERR_INVALID_ARG, "bad named request");
   int64_t count = 1;
   for (int d = 0; d < ndim; d++) count *= shape[d] < 0 ? 0 : shape[d];
-  if (count > 0 && (!in || !out)) return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
+  if (count > 0 && (!in || (type != TIPS_REQ_ALLGATHER && !out))) return fail(TIPS_ERR_INVALID_ARG, "bad named request");
+  if (type == TIPS_REQ_ALLGATHER && !alloc) return fail(TIPS_ERR_INVALID_ARG, "named allgather needs an output allocator");
+  if (type == TIPS_REQ_BROADCAST) {
+    const int size = tips_size();
+    if (root < 0 || (size > 0 && root >= size)) return fail(TIPS_ERR_INVALID_ARG, "root rank %d out of range", root);
+  }
   Negotiator* n = negotiator();
   if (!n) return TIPS_ERR_NOT_INITIALIZED;
-  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream);
+  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, type, root, alloc, actx, out_rows);
 }
 
 }  // namespace
@@ -671,6 +758,16 @@ int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int6
 int64_t tips_enqueue_allreduce_shaped(const char* name, const void* in, void* out, const int64_t* shape, int ndim,
                                       int dtype, void* stream) {
   return enqueue_named(name, in, out, shape, ndim, dtype, stream);
+}
+
+int64_t tips_enqueue_broadcast(const char* name, const void* in, void* out, const int64_t* shape, int ndim,
+                               int dtype, int root, void* stream) {
+  return enqueue_named(name, in, out, shape, ndim, dtype, stream, TIPS_REQ_BROADCAST, root);
+}
+
+int64_t tips_enqueue_allgather(const char* name, const void* in, const int64_t* shape, int ndim, int dtype,
+                               void* stream, tips_alloc_fn alloc, void* ctx, int64_t* out_rows) {
+  return enqueue_named(name, in, nullptr, shape, ndim, dtype, stream, TIPS_REQ_ALLGATHER, 0, alloc, ctx, out_rows);
 }
 
 int tips_poll(int64_t handle) {
@@ -753,14 +850,14 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   std::vector<int64_t> handles;
   const char* p = requests;
   const auto t0 = std::chrono::steady_clock::now();
-  // lines: "name dtype count [d0,d1,...]" (shape: default [count]), "@sleep ms", "@wait" (all so far
-  // resolved), "@mark" (log "# mark us")
+  // lines: "name dtype count [d0,d1,...|-] [ar|ag|bc:ROOT]" (shape: default [count]; request type:
+  // default allreduce), "@sleep ms", "@wait" (all so far resolved), "@mark" (log "# mark us")
   while (*p) {
     const char* e = strchr(p, '\n');
     std::string line(p, e ? (size_t)(e - p) : strlen(p));
     p = e ? e + 1 : p + line.size();
     if (line.empty()) continue;
-    char nm[256], dims[256] = "";
+    char nm[256], dims[256] = "", kind[64] = "ar";
     long long dt = 0, cnt = 0;
     if (line.rfind("@sleep ", 0) == 0) {
       std::this_thread::sleep_for(std::chrono::milliseconds(atoi(line.c_str() + 7)));
@@ -770,15 +867,19 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
     } else if (line == "@mark") {
       const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
       neg.note("# mark " + std::to_string((long long)us.count()));
-    } else if (sscanf(line.c_str(), "%255s %lld %lld %255s", nm, &dt, &cnt, dims) >= 3) {
+    } else if (sscanf(line.c_str(), "%255s %lld %lld %255s %63s", nm, &dt, &cnt, dims, kind) >= 3) {
       std::vector<int64_t> shape;
+      if (strcmp(dims, "-") == 0) dims[0] = 0;
+      const int type = strncmp(kind, "ag", 2) == 0 ? TIPS_REQ_ALLGATHER : strncmp(kind, "bc", 2) == 0 ? TIPS_REQ_BROADCAST
+                                                                                                  : TIPS_REQ_ALLREDUCE;
+      const int root = (type == TIPS_REQ_BROADCAST && kind[2] == ':') ? atoi(kind + 3) : 0;
       for (const char* q = dims; *q;) {
         shape.push_back(strtoll(q, nullptr, 10));
         q = strchr(q, ',');
         q = q ? q + 1 : "";
       }
       if (shape.empty()) shape.push_back(cnt);
-      const int64_t h = neg.enqueue(nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr);
+      const int64_t h = neg.enqueue(nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr, type, root);
       if (h < 0) return (int)h;
       handles.push_back(h);
     }

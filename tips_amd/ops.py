@@ -229,13 +229,21 @@ def bucket_sum(a, b, out=None):
 
 
 class Handle(object):
-    """An in-flight named allreduce (tips_enqueue_allreduce); see allreduce_async."""
+    """An in-flight named request (tips_enqueue_allreduce / _broadcast / _allgather); see
+    allreduce_async, broadcast_async, allgather_async."""
 
     def __init__(self, handle, output, name):
         self.handle = handle
         self.output = output
         self.name = name
         self.done = False
+        self._finish = None  # allgather: builds the output once the request has run
+
+    def _complete(self):
+        self.done = True
+        if self._finish is not None:
+            self.output = self._finish()
+            self._finish = None
 
 
 def allreduce_async(tensor, name):
@@ -260,6 +268,71 @@ def allreduce_async(tensor, name):
         raise _lib.TipsError("tips_enqueue_allreduce", int(h), _lib.last_error())
     hd = Handle(int(h), out, name)
     hd._keep = src  # the input must stay alive until the reduction has run
+    return hd
+
+
+def broadcast_async(tensor, root_rank, name):
+    """Start a negotiated broadcast of a device tensor under `name` (MPIBroadcast, ops.cc:214-286 ->
+    EnqueueTensorCollective(RequestType_BROADCAST)); the Handle's output is root_rank's tensor.
+    Ranks may call it in any order; rank 0 checks dtype, shape and root on every rank."""
+    basics.init()
+    if not tensors.is_device(tensor):
+        raise ValueError("broadcast_async needs a device tensor")
+    code = tensors.dtype_code(tensor)
+    src = tensor.contiguous()
+    out = tensors.empty_like(src)
+    shape = _shape(src)
+    sp, _keep = _lib.i64_array(shape or [1])
+    h = _lib.lib().tips_enqueue_broadcast(name.encode(), src.data_ptr(), out.data_ptr(), sp, len(shape), code,
+                                          int(root_rank), tensors.stream_of(src))
+    if h < 0:
+        raise _lib.TipsError("tips_enqueue_broadcast", int(h), _lib.last_error())
+    hd = Handle(int(h), out, name)
+    hd._keep = src
+    return hd
+
+
+def allgather_async(tensor, name):
+    """Start a negotiated allgather of a device tensor under `name` (MPIAllgather, ops.cc:156-212
+    -> RequestType_ALLGATHER): every rank's tensor concatenated along dimension 0 in rank order.
+    Rank 0 checks all but the first dimension (GatherFirstRankSizes, coordinator.cc:40-88) and
+    sends every rank the first dimensions; the output is allocated then, on the negotiation
+    thread, through a callback (as the reference's allocate_output in PerformCollectiveOp)."""
+    import ctypes
+    import torch
+    basics.init()
+    if not tensors.is_device(tensor):
+        raise ValueError("allgather_async needs a device tensor")
+    code = tensors.dtype_code(tensor)
+    src = tensor.contiguous()
+    shape = _shape(src)
+    if not shape:
+        raise ValueError("An empty tensor found")
+    sp, _keep = _lib.i64_array(shape)
+    rows = ctypes.c_int64(-1)
+    hd = Handle(0, None, name)
+    box = {}
+
+    def alloc(_ctx, nbytes):
+        buf = torch.empty(int(nbytes), dtype=torch.uint8, device=src.device)
+        box["buf"] = buf
+        return buf.data_ptr()
+
+    cb = _lib.ALLOC_FN(alloc)
+
+    def finish():
+        out_shape = (int(rows.value),) + tuple(shape[1:])
+        if "buf" in box:
+            return box.pop("buf").view(src.dtype).view(out_shape)
+        return torch.empty(out_shape, dtype=src.dtype, device=src.device)
+
+    h = _lib.lib().tips_enqueue_allgather(name.encode(), src.data_ptr(), sp, len(shape), code, tensors.stream_of(src),
+                                          ctypes.cast(cb, ctypes.c_void_p), None, ctypes.byref(rows))
+    if h < 0:
+        raise _lib.TipsError("tips_enqueue_allgather", int(h), _lib.last_error())
+    hd.handle = int(h)
+    hd._keep = (src, sp, rows, cb)  # alive until the request has run (the callback, the out-param)
+    hd._finish = finish
     return hd
 
 
@@ -306,7 +379,7 @@ def synchronize_many(handles):
         arr = (ctypes.c_int64 * len(pend))(*[h.handle for h in pend])
         _lib.call("tips_wait_n", arr, len(pend))
         for h in pend:
-            h.done = True
+            h._complete()
     return [h.output for h in handles]
 
 
@@ -315,7 +388,8 @@ def poll(handle):
     if handle.done:
         return True
     rc = _lib.call("tips_poll", handle.handle)
-    handle.done = rc == 1
+    if rc == 1:
+        handle._complete()
     return handle.done
 
 
@@ -323,7 +397,7 @@ def synchronize(handle):
     """Wait for a Handle and return its output tensor (raises TipsError on a negotiation error)."""
     if not handle.done:
         _lib.call("tips_wait", handle.handle)
-        handle.done = True
+        handle._complete()
     return handle.output
 
 
