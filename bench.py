@@ -921,6 +921,14 @@ def bench_allreduce(args):
                        "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": kbytes,
                        "note": "one launch of the schedule's sub-chunk shape, timed alone on re-read buffers "
                                "(Infinity Cache assisted: in the schedule a freshly received slot may be on-die too)"}
+        if nsrc > 2:  # HBM bytes from the committed PMC passes over the fold (8 x 32 MiB, rotating sets)
+            try:
+                with open(os.path.join(REPO, "profiles", "r02", "pmc_multi_sum.json")) as f:
+                    k = next(iter(json.load(f)["kernels"].values()))
+                kernel_roof["traffic_over_algorithmic_pmc"] = round(k["traffic_over_algorithmic"], 5)
+                kernel_roof["traffic_source"] = "profiles/r02/pmc_multi_sum.json (8 x 32 MiB sources)"
+            except Exception:  # noqa: BLE001
+                pass
         del bufs, srcs, dst
 
     algbw = total_elems * 4 / (ms / 1e3)  # bytes/s per rank
