@@ -661,6 +661,16 @@ def crash_line():
     return lambda text: h.crash_line_set(text.encode() if text else None)
 
 
+_T0 = time.time()
+
+
+def progress(rank, what):
+    """Rank 0's phase log on stderr (the JSON line alone goes to stdout): a long N > 1 run, the
+    socket rehearsals above all, shows where it is."""
+    if rank == 0:
+        print("[bench %7.1f s] %s" % (time.time() - _T0, what), file=sys.stderr, flush=True)
+
+
 def start_watchdog(seconds, rank):
     """A hung collective must end the run with a message, never hang the box. If the main
     measurement already finished (only the optional comparison runs hung), its line is printed."""
@@ -713,6 +723,7 @@ def bench_allreduce(args):
     import tips_amd
     from tips_amd import _lib
     tips_amd.init()  # unique id through the gloo group, one RCCL communicator per GPU
+    progress(rank, "initialised: %d ranks" % world)
     L = _lib.lib()
     algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL,
                   "oneshot": _lib.ALGO_ONESHOT, "peer": _lib.ALGO_PEER, "tune": _lib.ALGO_TUNE}
@@ -846,6 +857,7 @@ def bench_allreduce(args):
             fallbacks.append({"algorithm": inv.get(algo, str(algo)), "error": str(e)})
             algo = nxt
             _lib.call("tips_set_algorithm", algo)
+    progress(rank, "warm-up done (schedule measured when tuning)")
     tuned = None
     if algo == _lib.ALGO_TUNE:  # the warm-up measured the schedules; report (and check) the one kept
         import ctypes
@@ -882,8 +894,10 @@ def bench_allreduce(args):
         del ref, tmp, got, exp
         return good, msg
 
+    progress(rank, "timed: %.3f ms per step" % ms)
     ok, check = parity(algo)
     all_ok = all_ranks_ok(dist, ok)
+    progress(rank, "parity: %s" % check)
 
     # the reduce kernel of this schedule, timed alone at its per-launch shape (HBM roofline)
     kernel_roof = None
@@ -1020,6 +1034,7 @@ def bench_allreduce(args):
 
     def note_progress(what):
         """What rank 0 prints if a fatal signal ends the process during `what`."""
+        progress(rank, what)
         if last_words:
             last_words(json.dumps(dict(line, compare_algbw_gib_s=compare, compare_check=compare_check,
                                        compare_error="process ended by a signal during %s" % what)))
