@@ -208,8 +208,10 @@ TIPS_API int tips_fused_allreduce_oop(const void* const* ins, void* const* outs,
  * MASTER_ADDR:TIPS_NEGOTIATION_PORT, default MASTER_PORT + 19) which names
  * every rank has enqueued, validates them with ConstructResponseMessage's
  * rules and error text, and every rank reduces them in rank 0's
- * readiness order (as ready_to_reduce), on the stream passed here. Device pointers only.
- * Returns a handle > 0, or a negative status. The first call starts the
+ * readiness order (as ready_to_reduce), on the stream passed here. Device pointers run
+ * stream-ordered; host pointers (both in and out host, as the reference's MPIAllreduce is a CPU
+ * op, ops.cc:118) run on the negotiation thread, staged through HBM like tips_allreduce's, and
+ * are done when tips_wait returns. Returns a handle > 0, or a negative status. The first call starts the
  * thread (collective); tips_shutdown stops it (collective).
  * While named requests are in flight, do not issue the synchronous
  * collectives (tips_allreduce, tips_broadcast, ...) from another thread:
@@ -260,7 +262,7 @@ typedef void* (*tips_alloc_fn)(void* ctx, int64_t bytes);
  * the first (GatherFirstRankSizes's rules and text, coordinator.cc:40-88) and sends every rank
  * the first dimensions; each rank then allocates its output through alloc(ctx, bytes), stores
  * the output's first dimension in *out_rows (valid once tips_wait / tips_poll report done) and
- * gathers on `stream`. ndim >= 1. */
+ * gathers on `stream`. ndim >= 1. A host `in` gets a host output: alloc must then return host memory. */
 TIPS_API int64_t tips_enqueue_allgather(const char* name, const void* in, const int64_t* shape, int ndim, int dtype,
                                         void* stream, tips_alloc_fn alloc, void* ctx, int64_t* out_rows);
 /* The negotiation protocol with an executor that only logs (no GPU): each

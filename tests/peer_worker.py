@@ -182,8 +182,9 @@ def named_collectives_case(c, rank, size, L, _lib, sp):
     """Named broadcast / allgather / allreduce requests through the negotiation (the reference's
     three request types, coordinator.cc:243-353), enqueued in a different order on every rank:
     broadcasts from several roots, allgathers with ragged first dimensions (one rank contributing
-    zero rows) and 3-d shapes, allreduces in between. Then a broadcast whose root differs between
-    ranks must fail on every rank (rank 0's root check) and a later request must still run."""
+    zero rows) and 3-d shapes, allreduces in between; then the same three types on host (numpy)
+    tensors, as the reference's CPU ops. Then a broadcast whose root differs between ranks must
+    fail on every rank (rank 0's root check) and a later request must still run."""
     import numpy as np
     import torch
     import tips_amd
@@ -229,6 +230,36 @@ def named_collectives_case(c, rank, size, L, _lib, sp):
         same = torch.equal(got, exp) if kind != "ar" else torch.allclose(got, exp, rtol=1e-6, atol=1e-5)
         if got.shape != exp.shape or not same:
             bad.append("%s (%s) differs: %s vs %s" % (name, kind, tuple(got.shape), tuple(exp.shape)))
+    # host tensors (numpy): the reference's ops are CPU ops; run on the negotiation thread, staged
+    hjobs = [("h_ar%d" % k, "ar") for k in range(3)] + [("h_bc%d" % k, "bc") for k in range(3)] + \
+        [("h_ag%d" % k, "ag") for k in range(3)]
+    horder = list(range(len(hjobs)))
+    np.random.default_rng(seed * 11 + rank).shuffle(horder)
+    hh = {}
+    for i in horder:
+        name, kind = hjobs[i]
+        k = int(name[-1])
+        if kind == "ar":
+            hh[name] = tips_amd.allreduce_async(t(rank, 200 + i, (4099,)).numpy(), name)
+        elif kind == "bc":
+            hh[name] = tips_amd.broadcast_async(t(rank, 200 + i, (33, 3), torch.int32).numpy(), k % size, name)
+        else:
+            hh[name] = tips_amd.allgather_async(t(rank, 200 + i, (k + rank, 5)).numpy(), name)
+    for i, (name, kind) in enumerate(hjobs):
+        k = int(name[-1])
+        got = tips_amd.synchronize(hh[name])
+        if kind == "ar":
+            exp = t(0, 200 + i, (4099,))
+            for r in range(1, size):
+                exp = exp + t(r, 200 + i, (4099,))
+            ok = isinstance(got, np.ndarray) and np.allclose(got, exp.numpy(), rtol=1e-6, atol=1e-5)
+        elif kind == "bc":
+            ok = isinstance(got, np.ndarray) and np.array_equal(got, t(k % size, 200 + i, (33, 3), torch.int32).numpy())
+        else:
+            exp = np.concatenate([t(r, 200 + i, (k + r, 5)).numpy() for r in range(size)])
+            ok = isinstance(got, np.ndarray) and got.shape == exp.shape and np.array_equal(got, exp)
+        if not ok:
+            bad.append("host %s (%s) differs" % (name, kind))
     try:
         tips_amd.synchronize(tips_amd.broadcast_async(t(rank, 99, (16,)).cuda(), rank % 2, "bad_root"))
         bad.append("a root differing between ranks was accepted")

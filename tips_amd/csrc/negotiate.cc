@@ -56,6 +56,7 @@ struct Req {
   tips_alloc_fn alloc = nullptr;  // allgather: output allocator, called once the sizes are known
   void* actx = nullptr;
   int64_t* out_rows = nullptr;
+  bool host = false;  // host memory (the reference's CPU op): run synchronously, staged through HBM
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   std::shared_ptr<GroupEv> gev;  // set when the request ran inside a fused batch (then ev is unused)
@@ -280,8 +281,14 @@ class Negotiator {
       // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
       // st.device is fixed from init on)
       TRY(set_device(S()));
-      if (r->count > 0 && !(is_device_ptr(in) && (type == TIPS_REQ_ALLGATHER || is_device_ptr(out))))
-        return fail(TIPS_ERR_INVALID_ARG, "named requests need device pointers");
+      // device tensors run stream-ordered on `s`; host tensors (the reference's MPIAllreduce is a
+      // CPU op, ops.cc:118) run synchronously on the executor thread, staged through HBM as
+      // tips_allreduce stages them. Both pointers of a request live on the same side.
+      if (r->count > 0) {
+        const bool din = is_device_ptr(in), dout = type == TIPS_REQ_ALLGATHER ? din : is_device_ptr(out);
+        if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "named request %s: one device and one host pointer", name.c_str());
+        r->host = !din;
+      }
       {
         std::lock_guard<std::mutex> l(m_);
         if (!ev_pool_.empty()) {
@@ -548,10 +555,12 @@ class Negotiator {
           i++;
           continue;
         }
-        if (reqs[i]->type != TIPS_REQ_ALLREDUCE) {  // broadcast / allgather: one at a time, in order
+        if (reqs[i]->type != TIPS_REQ_ALLREDUCE || reqs[i]->host) {  // broadcast / allgather / host: one at a time
           if (run_other(*reqs[i], ds[i].sizes) != 0) {
             state[i] = -1;
             msg[i] = last_error();
+          } else if (reqs[i]->host) {
+            state[i] = 3;  // finished: the host call returned with out written
           }
           i++;
           continue;
@@ -562,7 +571,7 @@ class Negotiator {
         const int64_t es = tips::dtype_size(dtype);
         size_t j = i;
         int64_t bytes = 0;
-        while (fuse && j < n && reqs[j] && state[j] == 2 && reqs[j]->type == TIPS_REQ_ALLREDUCE &&
+        while (fuse && j < n && reqs[j] && state[j] == 2 && reqs[j]->type == TIPS_REQ_ALLREDUCE && !reqs[j]->host &&
                reqs[j]->dtype == dtype && reqs[j]->count * es < threshold &&
                round_up(bytes, kAlignBytes) + reqs[j]->count * es <= threshold) {
           bytes = round_up(bytes, kAlignBytes) + reqs[j]->count * es;
@@ -599,7 +608,9 @@ class Negotiator {
   // allgather's output is allocated only now, when rank 0 has sent every rank's first
   // dimension, as the reference's allocate_output; its first dimension goes to *out_rows.
   int run_other(Req& r, const std::vector<int64_t>& sizes) {
-    if (r.type == TIPS_REQ_BROADCAST) {
+    if (r.type == TIPS_REQ_ALLREDUCE) {  // a host allreduce (device ones are fused above)
+      TRY(tips_allreduce(r.in, r.out, r.count, r.dtype, TIPS_OP_SUM, r.stream));
+    } else if (r.type == TIPS_REQ_BROADCAST) {
       TRY(tips_broadcast(r.in, r.out, r.count, r.dtype, r.root, r.stream));
     } else {
       const int64_t es = tips::dtype_size(r.dtype);
@@ -620,7 +631,7 @@ class Negotiator {
       if (r.out_rows) *r.out_rows = rows;
       TRY(tips_allgatherv(r.in, r.count, r.out, counts.data(), r.dtype, r.stream));
     }
-    HIP_TRY(hipEventRecord(r.ev, r.stream));
+    if (!r.host) HIP_TRY(hipEventRecord(r.ev, r.stream));
     return 0;
   }
 

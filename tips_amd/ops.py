@@ -253,17 +253,17 @@ def allreduce_async(tensor, name):
     negotiation, ops.cc:86-115, coordinator.cc:223-513): ranks may call this in
     any order; each named tensor is reduced once every rank has enqueued it, in
     rank 0's order, with the reference's dtype/shape validation. `name` must be
-    the same on every rank (the reference uses the TF node name)."""
+    the same on every rank (the reference uses the TF node name). Device tensors are reduced
+    stream-ordered; host tensors (numpy / CPU torch: the reference's op is a CPU op) on the
+    negotiation thread, done when synchronize() returns."""
     basics.init()
-    if not tensors.is_device(tensor):
-        raise ValueError("allreduce_async needs a device tensor")
     code = tensors.dtype_code(tensor)
-    src = tensor.contiguous()
+    src = tensors.contiguous(tensor)
     out = tensors.empty_like(src)
     shape = _shape(src)  # validated across ranks with ConstructResponseMessage's rule (coordinator.cc:129-146)
     sp, _keep = _lib.i64_array(shape or [1])
-    h = _lib.lib().tips_enqueue_allreduce_shaped(name.encode(), src.data_ptr(), out.data_ptr(), sp, len(shape), code,
-                                                 tensors.stream_of(src))
+    h = _lib.lib().tips_enqueue_allreduce_shaped(name.encode(), tensors.data_ptr(src), tensors.data_ptr(out), sp,
+                                                 len(shape), code, tensors.stream_of(src))
     if h < 0:
         raise _lib.TipsError("tips_enqueue_allreduce", int(h), _lib.last_error())
     hd = Handle(int(h), out, name)
@@ -274,17 +274,16 @@ def allreduce_async(tensor, name):
 def broadcast_async(tensor, root_rank, name):
     """Start a negotiated broadcast of a device tensor under `name` (MPIBroadcast, ops.cc:214-286 ->
     EnqueueTensorCollective(RequestType_BROADCAST)); the Handle's output is root_rank's tensor.
-    Ranks may call it in any order; rank 0 checks dtype, shape and root on every rank."""
+    Ranks may call it in any order; rank 0 checks dtype, shape and root on every rank. Device or
+    host tensors, as allreduce_async."""
     basics.init()
-    if not tensors.is_device(tensor):
-        raise ValueError("broadcast_async needs a device tensor")
     code = tensors.dtype_code(tensor)
-    src = tensor.contiguous()
+    src = tensors.contiguous(tensor)
     out = tensors.empty_like(src)
     shape = _shape(src)
     sp, _keep = _lib.i64_array(shape or [1])
-    h = _lib.lib().tips_enqueue_broadcast(name.encode(), src.data_ptr(), out.data_ptr(), sp, len(shape), code,
-                                          int(root_rank), tensors.stream_of(src))
+    h = _lib.lib().tips_enqueue_broadcast(name.encode(), tensors.data_ptr(src), tensors.data_ptr(out), sp, len(shape),
+                                          code, int(root_rank), tensors.stream_of(src))
     if h < 0:
         raise _lib.TipsError("tips_enqueue_broadcast", int(h), _lib.last_error())
     hd = Handle(int(h), out, name)
@@ -297,14 +296,13 @@ def allgather_async(tensor, name):
     -> RequestType_ALLGATHER): every rank's tensor concatenated along dimension 0 in rank order.
     Rank 0 checks all but the first dimension (GatherFirstRankSizes, coordinator.cc:40-88) and
     sends every rank the first dimensions; the output is allocated then, on the negotiation
-    thread, through a callback (as the reference's allocate_output in PerformCollectiveOp)."""
+    thread, through a callback (as the reference's allocate_output in PerformCollectiveOp). Device
+    or host tensors, as allreduce_async (a host tensor gets a host output)."""
     import ctypes
-    import torch
+    import numpy as np
     basics.init()
-    if not tensors.is_device(tensor):
-        raise ValueError("allgather_async needs a device tensor")
     code = tensors.dtype_code(tensor)
-    src = tensor.contiguous()
+    src = tensors.contiguous(tensor)
     shape = _shape(src)
     if not shape:
         raise ValueError("An empty tensor found")
@@ -313,21 +311,31 @@ def allgather_async(tensor, name):
     hd = Handle(0, None, name)
     box = {}
 
+    torch_src = tensors.is_torch(src)
+
     def alloc(_ctx, nbytes):
-        buf = torch.empty(int(nbytes), dtype=torch.uint8, device=src.device)
+        if torch_src:
+            import torch
+            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=src.device)
+        else:
+            buf = np.empty(int(nbytes), dtype=np.uint8)
         box["buf"] = buf
-        return buf.data_ptr()
+        return tensors.data_ptr(buf)
 
     cb = _lib.ALLOC_FN(alloc)
 
     def finish():
         out_shape = (int(rows.value),) + tuple(shape[1:])
         if "buf" in box:
-            return box.pop("buf").view(src.dtype).view(out_shape)
-        return torch.empty(out_shape, dtype=src.dtype, device=src.device)
+            return box.pop("buf").view(src.dtype).reshape(out_shape)
+        if torch_src:
+            import torch
+            return torch.empty(out_shape, dtype=src.dtype, device=src.device)
+        return np.empty(out_shape, dtype=src.dtype)
 
-    h = _lib.lib().tips_enqueue_allgather(name.encode(), src.data_ptr(), sp, len(shape), code, tensors.stream_of(src),
-                                          ctypes.cast(cb, ctypes.c_void_p), None, ctypes.byref(rows))
+    h = _lib.lib().tips_enqueue_allgather(name.encode(), tensors.data_ptr(src), sp, len(shape), code,
+                                          tensors.stream_of(src), ctypes.cast(cb, ctypes.c_void_p), None,
+                                          ctypes.byref(rows))
     if h < 0:
         raise _lib.TipsError("tips_enqueue_allgather", int(h), _lib.last_error())
     hd.handle = int(h)
