@@ -429,8 +429,14 @@ def test_named_async_allreduce_single_rank(gpu):
     while not gpu.poll(hp):
         pass
     assert torch.equal(hp.output, ts[2])
-    with pytest.raises(ValueError):
-        gpu.allreduce_async(torch.zeros(3), "host")
+    # host tensors go through the same negotiation (the reference's op is a CPU op); the handle
+    # dropped unwaited stays safe: the module keeps its buffers until the request has run
+    hh = gpu.allreduce_async(torch.full((3,), 2.0), "host")
+    assert torch.equal(gpu.synchronize(hh), torch.full((3,), 2.0))
+    gpu.allreduce_async(torch.zeros(5), "host_dropped")
+    import numpy as np
+    hn = gpu.allgather_async(np.arange(6, dtype=np.int64).reshape(3, 2), "host_ag")
+    assert np.array_equal(gpu.synchronize(hn), np.arange(6, dtype=np.int64).reshape(3, 2))
 
 
 def test_named_async_many_single_rank(gpu, monkeypatch):

@@ -228,9 +228,16 @@ def bucket_sum(a, b, out=None):
     return out
 
 
+_INFLIGHT = {}  # handle -> Handle: the buffers of every named request stay alive until it has run
+
+
 class Handle(object):
     """An in-flight named request (tips_enqueue_allreduce / _broadcast / _allgather); see
-    allreduce_async, broadcast_async, allgather_async."""
+    allreduce_async, broadcast_async, allgather_async. Until the request has run (synchronize /
+    poll reports it, or it failed) the module holds it, with its input and output: the library
+    reads and writes them when rank 0's order reaches the name, possibly after the caller dropped
+    its own references (a freed host buffer would be written into; a freed device block could
+    already belong to another tensor)."""
 
     def __init__(self, handle, output, name):
         self.handle = handle
@@ -239,7 +246,15 @@ class Handle(object):
         self.done = False
         self._finish = None  # allgather: builds the output once the request has run
 
+    def _track(self):
+        _INFLIGHT[self.handle] = self
+        return self
+
+    def _release(self):
+        _INFLIGHT.pop(self.handle, None)
+
     def _complete(self):
+        self._release()
         self.done = True
         if self._finish is not None:
             self.output = self._finish()
@@ -268,7 +283,7 @@ def allreduce_async(tensor, name):
         raise _lib.TipsError("tips_enqueue_allreduce", int(h), _lib.last_error())
     hd = Handle(int(h), out, name)
     hd._keep = src  # the input must stay alive until the reduction has run
-    return hd
+    return hd._track()
 
 
 def broadcast_async(tensor, root_rank, name):
@@ -288,7 +303,7 @@ def broadcast_async(tensor, root_rank, name):
         raise _lib.TipsError("tips_enqueue_broadcast", int(h), _lib.last_error())
     hd = Handle(int(h), out, name)
     hd._keep = src
-    return hd
+    return hd._track()
 
 
 def allgather_async(tensor, name):
@@ -341,7 +356,7 @@ def allgather_async(tensor, name):
     hd.handle = int(h)
     hd._keep = (src, sp, rows, cb)  # alive until the request has run (the callback, the out-param)
     hd._finish = finish
-    return hd
+    return hd._track()
 
 
 def allreduce_async_many(tensor_list, names):
@@ -375,7 +390,7 @@ def allreduce_async_many(tensor_list, names):
     for h, o, x, name in zip(hs, outs, srcs, names):
         hd = Handle(int(h), o, name)
         hd._keep = x
-        out.append(hd)
+        out.append(hd._track())
     return out
 
 
@@ -385,7 +400,12 @@ def synchronize_many(handles):
     pend = [h for h in handles if not h.done]
     if pend:
         arr = (ctypes.c_int64 * len(pend))(*[h.handle for h in pend])
-        _lib.call("tips_wait_n", arr, len(pend))
+        try:
+            _lib.call("tips_wait_n", arr, len(pend))
+        except _lib.TipsError:
+            for h in pend:  # every handle has been waited on (tips_wait_n waits for all of them)
+                h._release()
+            raise
         for h in pend:
             h._complete()
     return [h.output for h in handles]
@@ -395,7 +415,11 @@ def poll(handle):
     """True once the named allreduce has completed on the device."""
     if handle.done:
         return True
-    rc = _lib.call("tips_poll", handle.handle)
+    try:
+        rc = _lib.call("tips_poll", handle.handle)
+    except _lib.TipsError:
+        handle._release()
+        raise
     if rc == 1:
         handle._complete()
     return handle.done
@@ -404,7 +428,11 @@ def poll(handle):
 def synchronize(handle):
     """Wait for a Handle and return its output tensor (raises TipsError on a negotiation error)."""
     if not handle.done:
-        _lib.call("tips_wait", handle.handle)
+        try:
+            _lib.call("tips_wait", handle.handle)
+        except _lib.TipsError:
+            handle._release()
+            raise
         handle._complete()
     return handle.output
 
