@@ -437,6 +437,10 @@ def test_named_async_allreduce_single_rank(gpu):
     import numpy as np
     hn = gpu.allgather_async(np.arange(6, dtype=np.int64).reshape(3, 2), "host_ag")
     assert np.array_equal(gpu.synchronize(hn), np.arange(6, dtype=np.int64).reshape(3, 2))
+    # the op functions with a name go through the negotiation (the reference's ops always do)
+    assert torch.equal(gpu.allreduce_op(ts[3], name="layer/1:0"), ts[3])
+    assert torch.equal(gpu.broadcast_op(ts[4], 0, name="bcast w"), ts[4])
+    assert torch.equal(gpu.allgather_op(ts[5].view(-1, 1), name="ag"), ts[5].view(-1, 1))
 
 
 def test_named_async_many_single_rank(gpu, monkeypatch):

@@ -44,7 +44,11 @@ def _shape(t):
 
 
 def allreduce_op(tensor, name=None):
-    """Sum `tensor` over all ranks (ops.py:61-65 -> MPIAllreduce, ops.cc:86-115)."""
+    """Sum `tensor` over all ranks (ops.py:61-65 -> MPIAllreduce, ops.cc:86-115). With a `name`,
+    through the negotiation like the reference's op (rank 0 validates and orders it; the name
+    normalised as ops.py:33-35 does), and returns when it has run; without one, stream-ordered."""
+    if name is not None:
+        return synchronize(allreduce_async(tensor, _normalize_name(name)))
     basics.init()
     code = tensors.dtype_code(tensor)
     src = tensors.contiguous(tensor)
@@ -63,7 +67,10 @@ def allreduce_op(tensor, name=None):
 
 def allgather_op(tensor, name=None):
     """Concatenate `tensor` from all ranks along dimension 0 (ops.py:72-76 -> MPIAllgather,
-    ops.cc:156-212; sizes exchanged as GatherFirstRankSizes does, coordinator.cc:40-88)."""
+    ops.cc:156-212; sizes exchanged as GatherFirstRankSizes does, coordinator.cc:40-88). With a
+    `name`, through the negotiation (allgather_async), as allreduce_op."""
+    if name is not None:
+        return synchronize(allgather_async(tensor, _normalize_name(name)))
     basics.init()
     code = tensors.dtype_code(tensor)
     src = tensors.contiguous(tensor)
@@ -108,7 +115,10 @@ def _gather_records(rec):
 
 
 def broadcast_op(tensor, root_rank=0, name=None):
-    """`tensor` of rank `root_rank`, on every rank (ops.py:83-87 -> MPIBroadcast, ops.cc:214-286)."""
+    """`tensor` of rank `root_rank`, on every rank (ops.py:83-87 -> MPIBroadcast, ops.cc:214-286).
+    With a `name`, through the negotiation (broadcast_async), as allreduce_op."""
+    if name is not None:
+        return synchronize(broadcast_async(tensor, root_rank, _normalize_name(name)))
     basics.init()
     code = tensors.dtype_code(tensor)
     src = tensors.contiguous(tensor)
