@@ -614,6 +614,9 @@ def golden_case(c, rank, size, L, _lib, sp):
 def main():
     rank, size, uid, cases = int(sys.argv[1]), int(sys.argv[2]), bytes.fromhex(sys.argv[3]), json.loads(sys.argv[4])
     import ctypes
+    import faulthandler
+    import signal
+    faulthandler.register(signal.SIGUSR1, all_threads=True)  # run_job's timeout: where every thread stands
 
     import numpy as np
     import torch

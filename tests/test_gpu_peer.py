@@ -12,8 +12,10 @@ with TIPS_ERR_MISMATCH and leave the job usable for the next call.
 """
 import json
 import os
+import signal
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -28,6 +30,7 @@ ERR_MISMATCH = -7
 
 def run_job(p, cases, timeout=300, **extra_env):
     uid = os.urandom(128).hex()
+    timeout = min(timeout, int(os.environ.get("TIPS_TEST_JOB_TIMEOUT", timeout)))  # a shorter cap for probes
     env = dict(os.environ, TIPS_NO_RCCL="1", TIPS_PEER_TIMEOUT_S="60", TIPS_VERBOSE="1")
     env.update(extra_env)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "peer_worker.py"), str(r), str(p), uid,
@@ -38,6 +41,19 @@ def run_job(p, cases, timeout=300, **extra_env):
         for pr in procs:
             o, e = pr.communicate(timeout=timeout)
             outs.append((pr.returncode, o, e))
+    except subprocess.TimeoutExpired:
+        # a hang: every worker still running dumps its Python threads' stacks (faulthandler on
+        # SIGUSR1), so the failure names the case and the library call each rank stands in
+        for pr in procs:
+            if pr.poll() is None:
+                pr.send_signal(signal.SIGUSR1)
+        time.sleep(2)
+        tails = []
+        for r, pr in enumerate(procs):
+            pr.kill()
+            o, e = pr.communicate()
+            tails.append("rank %d (rc %s):\n%s\n--- stdout:\n%s" % (r, pr.returncode, e[-4000:], o[-2000:]))
+        raise AssertionError("job timed out after %d s\n%s" % (timeout, "\n".join(tails)))
     finally:
         for pr in procs:
             if pr.poll() is None:

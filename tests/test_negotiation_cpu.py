@@ -26,10 +26,10 @@ def _worker(rank, size, port, requests, q):
     q.put((rank, rc, out.value.decode(), L.tips_last_error().decode()))
 
 
-def run(per_rank):
+def run(per_rank, port=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _port()
+    port = port or _port()
     size = len(per_rank)
     procs = [ctx.Process(target=_worker, args=(r, size, port, per_rank[r], q)) for r in range(size)]
     for p in procs:
@@ -151,3 +151,20 @@ def test_broadcast_and_allgather_requests():
     assert got["bs"] == "ERR Mismatched broadcast tensor shapes: [2,4] vs [4,2]"
     assert got["br"] == "ERR Mismatched broadcast root ranks: 0 vs 2"
     assert got["op"] == "ERR Mismatched operations found: 0 vs 1."
+
+
+def test_foreign_listener_on_the_negotiation_port():
+    """Another program already listens on the negotiation port and accepts but never answers (as an
+    RCCL socket in the same ephemeral range can): rank 0 takes the next free port, the other ranks'
+    hello gets no answer there and they move on to rank 0's; every rank runs every request."""
+    foreign = socket.socket()
+    foreign.bind(("127.0.0.1", 0))
+    foreign.listen(8)
+    try:
+        res = run(["a 0 10\nb 0 20", "b 0 20\na 0 10", "a 0 10\nb 0 20"], port=foreign.getsockname()[1])
+    finally:
+        foreign.close()
+    logs = [lines(log) for _, rc, log, _ in res]
+    for rank, rc, log, err in res:
+        assert rc == 0, err
+    assert all(l == logs[0] for l in logs) and sorted(logs[0]) == ["a OK", "b OK"]

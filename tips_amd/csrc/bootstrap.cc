@@ -81,7 +81,7 @@ int bootstrap_exchange(int rank, int size, const char* host, int port, void* id,
       *err = std::string("bootstrap: socket: ") + strerror(errno);
       return -1;
     }
-    if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0) {
+    if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0 && !connected_to_self(fd)) {
       int32_t me = rank;
       bool ok = send_all(fd, &me, sizeof me) && recv_all(fd, id, (size_t)id_bytes, ms_left());
       ::close(fd);

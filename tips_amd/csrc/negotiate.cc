@@ -202,7 +202,23 @@ struct Table {
 
 class Negotiator {
  public:
-  int start(int rank, int size, const char* host, int port, bool dry_run, int timeout_s) {
+  // Rank 0 listens on the first free port of [port, port + kPortTries); every other rank connects
+  // and says hello {magic, job key, rank, size}; rank 0 answers {magic, job key}. A rank counts as
+  // joined only after that answer: a connect that reached another program's listener on one of
+  // these ports (RCCL's own sockets live in the same ephemeral range), or this socket itself
+  // (TCP simultaneous open), is closed and the next candidate tried, instead of leaving rank 0
+  // waiting for a rank that believes it has joined.
+  static constexpr int kPortTries = 16;
+  static constexpr uint64_t kMagic = 0x30474e4553504954ull;  // "TIPSNEG0"
+  struct Hello {
+    uint64_t magic, key;
+    int32_t rank, size;
+  };
+  struct Ack {
+    uint64_t magic, key;
+  };
+
+  int start(int rank, int size, const char* host, int port, bool dry_run, int timeout_s, uint64_t key = 0) {
     rank_ = rank;
     size_ = size;
     dry_ = dry_run;
@@ -211,40 +227,49 @@ class Negotiator {
     std::string err;
     if (size > 1) {
       if (rank == 0) {
-        lfd_ = listen_on(port, size, &err);
-        if (lfd_ < 0) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: %s", err.c_str());
+        for (int k = 0; k < kPortTries && lfd_ < 0; k++) lfd_ = listen_on(port + k, size, &err);
+        if (lfd_ < 0) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: ports %d-%d: %s", port, port + kPortTries - 1, err.c_str());
         peers_.assign(size, -1);
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
         for (int joined = 0; joined < size - 1;) {
+          const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
           pollfd pfd{lfd_, POLLIN, 0};
-          if (::poll(&pfd, 1, timeout_ms_) <= 0) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: ranks did not connect");
+          if (left <= 0 || ::poll(&pfd, 1, (int)left) <= 0)
+            return fail(TIPS_ERR_BOOTSTRAP, "negotiation: %d rank(s) did not connect", size - 1 - joined);
           int c = ::accept(lfd_, nullptr, nullptr);
           if (c < 0) continue;
-          int32_t peer = -1;
-          if (!recv_all(c, &peer, sizeof peer, timeout_ms_) || peer <= 0 || peer >= size || peers_[peer] >= 0) {
+          Hello h{};
+          const Ack a{kMagic, key};
+          if (!recv_all(c, &h, sizeof h, 2000) || h.magic != kMagic || h.key != key || h.size != size || h.rank <= 0 ||
+              h.rank >= size || peers_[h.rank] >= 0 || !send_all(c, &a, sizeof a)) {
             ::close(c);
             continue;
           }
           set_nodelay(c);
-          peers_[peer] = c;
+          peers_[h.rank] = c;
           joined++;
         }
       } else {
-        sockaddr_in sa;
-        if (!resolve(host, port, &sa)) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: cannot resolve %s", host);
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
-        while (true) {
-          int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-          if (fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0) {
-            int32_t me = rank;
-            if (send_all(fd, &me, sizeof me)) {
+        const Hello h{kMagic, key, rank, size};
+        while (up_ < 0) {
+          for (int k = 0; k < kPortTries && up_ < 0; k++) {
+            sockaddr_in sa;
+            if (!resolve(host, port + k, &sa)) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: cannot resolve %s", host);
+            int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+            Ack a{};
+            if (fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0 && !connected_to_self(fd) &&
+                send_all(fd, &h, sizeof h) && recv_all(fd, &a, sizeof a, 2000) && a.magic == kMagic && a.key == key) {
               set_nodelay(fd);
               up_ = fd;
-              break;
+            } else if (fd >= 0) {
+              ::close(fd);
             }
           }
-          if (fd >= 0) ::close(fd);
+          if (up_ >= 0) break;
           if (std::chrono::steady_clock::now() > deadline)
-            return fail(TIPS_ERR_BOOTSTRAP, "negotiation: rank %d could not reach rank 0 at %s:%d", rank, host, port);
+            return fail(TIPS_ERR_BOOTSTRAP, "negotiation: rank %d could not reach rank 0 at %s:%d-%d", rank, host, port,
+                        port + kPortTries - 1);
           std::this_thread::sleep_for(std::chrono::milliseconds(20));
         }
       }
@@ -723,6 +748,7 @@ Negotiator* negotiator() {  // started by the first named request (collective)
   if (!g_neg) {
     State& st = S();
     int rank, size;
+    uint64_t key;
     {
       std::lock_guard<std::mutex> lk(st.mu);
       if (!st.initialized) {
@@ -731,9 +757,10 @@ Negotiator* negotiator() {  // started by the first named request (collective)
       }
       rank = st.rank;
       size = st.size;
+      key = st.peer_key;  // the job's unique-id hash: a hello from another job is refused
     }
     auto neg = std::make_unique<Negotiator>();
-    if (neg->start(rank, size, master_addr(), negotiation_port(), false, (int)env_i64("TIPS_NEGOTIATION_TIMEOUT", 600)))
+    if (neg->start(rank, size, master_addr(), negotiation_port(), false, (int)env_i64("TIPS_NEGOTIATION_TIMEOUT", 600), key))
       return nullptr;
     g_neg = std::move(neg);
   }

@@ -95,6 +95,19 @@ inline bool recv_msg(int fd, std::string* m, int timeout_ms) {
   return n == 0 || recv_all(fd, &(*m)[0], n, timeout_ms);
 }
 
+// A connect() to a loopback port in the ephemeral range with no listener can succeed by TCP
+// simultaneous open with ITSELF (source port == destination port). A retry loop that connects
+// before the listener is up is exposed to it: the "connection" then carries our own hello back
+// to us and the listener never hears from this rank. Such a socket must be closed and retried.
+inline bool connected_to_self(int fd) {
+  sockaddr_in a{}, b{};
+  socklen_t la = sizeof a, lb = sizeof b;
+  if (getsockname(fd, reinterpret_cast<sockaddr*>(&a), &la) != 0 ||
+      getpeername(fd, reinterpret_cast<sockaddr*>(&b), &lb) != 0)
+    return false;
+  return a.sin_port == b.sin_port && a.sin_addr.s_addr == b.sin_addr.s_addr;
+}
+
 inline void set_nodelay(int fd) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);

@@ -19,8 +19,12 @@ run() {  # name seconds cmd...
   return $rc
 }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
+# a heartbeat under gpurun_out: a multi-process test that runs for minutes prints nothing meanwhile
+# (each step keeps its own time limit, so a real hang still ends)
+( while sleep 45; do date +%T >> "$OUT/heartbeat.txt"; done ) &
+trap 'kill $! 2>/dev/null' EXIT
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -u -m pytest tests -q -m gpu --timeout 600 --timeout-method thread ${PYTEST_ARGS:-}
+  run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -u -m pytest tests -v -m gpu --timeout 600 --timeout-method thread ${PYTEST_ARGS:-}
   rc=$?; fatal $rc && exit $rc
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
   rc=$?; fatal $rc && exit $rc
