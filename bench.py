@@ -428,6 +428,122 @@ def link_probe(dist, rank, world, mib=256, iters=5, backend="nccl", device="cuda
     return out
 
 
+def fusion_layout(sizes, es=4, threshold=64 << 20, align=256):
+    """The buckets fusion.cc build_entry forms from these element counts (balanced buckets, 256-B
+    aligned offsets; every tensor here is under the threshold): [[(tensor index, offset), ...], ...]."""
+    def up(v):
+        return (v + align - 1) // align * align
+    packed = sum(up(k * es) for k in sizes if k * es < threshold)
+    nb = (packed + threshold - 1) // threshold
+    if nb < 2 and packed >= (32 << 20):
+        nb = 2
+    target = min(threshold, up((packed + nb - 1) // nb)) if nb > 1 else threshold
+    buckets, fill = [], 0
+    for i, k in enumerate(sizes):
+        nbytes = k * es
+        if nbytes == 0:
+            continue
+        off = up(fill) if buckets else 0
+        if not buckets or off + nbytes > threshold or off >= target:
+            buckets.append([])
+            off = 0
+        buckets[-1].append((i, off))
+        fill = off + nbytes
+    return buckets
+
+
+def fusion_one_rank_kernels(torch, L, _lib, sizes, offs, rot_sets, cp, stream, moved, tile=8192,
+                            threshold=64 << 20):
+    """One rank, configs 4/5: (1) the fusion's pack kernel (tips_copy_tiles_variant 1 = the shipped
+    copy_tiles_g_kernel, the launch fusion.cc issues per bucket) on this layout's per-bucket tile
+    tables, rotating gradient sets, HIP events on the launch stream: the dominant kernel's
+    roofline (unpack is the same kernel over the mirrored tiles); (2) the whole fused step
+    captured into one HIP graph per gradient set (torch.cuda.graph around tips_fused_allreduce)
+    and replayed: the step without its host cost."""
+    import numpy as np
+    buckets = fusion_layout(sizes, threshold=threshold)
+    slots = torch.empty(2 * threshold // 4, dtype=torch.float32, device="cuda")
+    tabs = []  # [set][bucket] -> (device table, ntiles, payload bytes)
+    for xs, pp, _k in rot_sets:
+        ptrs = [int(v) for v in _k]  # the set's data pointers (the keep-alive uint64 array)
+        per = []
+        for b, members in enumerate(buckets):
+            rec, payload = [], 0
+            for i, off in members:
+                nb = sizes[i] * 4
+                dst = slots.data_ptr() + (b % 2) * threshold + off
+                rec += [(ptrs[i] + t, dst + t, min(tile, nb - t)) for t in range(0, nb, tile)]
+                payload += nb
+            t = torch.from_numpy(np.array(rec, dtype=np.int64)).cuda()
+            per.append((t, len(rec), payload))
+        tabs.append(per)
+    sp = stream.cuda_stream
+
+    def launch(r, b):
+        t, n, _ = tabs[r][b]
+        rc = L.tips_copy_tiles_variant(t.data_ptr(), n, 1, tile, sp)
+        if rc:
+            raise _lib.TipsError("tips_copy_tiles_variant", rc, _lib.last_error())
+
+    for r in range(len(tabs)):
+        for b in range(len(buckets)):
+            launch(r, b)
+    torch.cuda.synchronize()
+    # the packed bucket 0 of set 0 holds exactly its tensors' bytes
+    launch(0, 0)
+    torch.cuda.synchronize()
+    s8 = slots.view(torch.uint8)
+    x0 = rot_sets[0][0]
+    ok = all(torch.equal(s8[off:off + sizes[i] * 4], x0[offs[i]:offs[i] + sizes[i]].view(torch.uint8))
+             for i, off in buckets[0])
+    reps = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for k in range(reps):
+        for b in range(len(buckets)):
+            launch(k % len(tabs), b)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * len(buckets))
+    per_launch = 2 * sum(p for _, _, p in tabs[0]) / len(buckets)  # read + write of one bucket's tensors
+    roof = {"bound": "hbm", "achieved": round(per_launch / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(per_launch / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": "copy_tiles_g_kernel (fusion pack; unpack is the same kernel on the mirrored tiles)",
+            "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": int(per_launch),
+            "launches_per_step": 2 * len(buckets), "buckets": len(buckets), "tile_bytes": tile,
+            "check": "bit-exact bucket bytes" if ok else "FAIL: packed bytes differ",
+            "note": "per-bucket pack launches of fusion.cc's layout, gradient set i %% %d (HBM-only), HIP events "
+                    "on the launch stream; algorithmic bytes = read + write of the bucket's tensors" % len(tabs)}
+    del slots, tabs
+    # the whole step, captured once per gradient set and replayed
+    side = torch.cuda.Stream()
+    side.wait_stream(stream)
+    graphs = []
+    with torch.cuda.stream(side):
+        for xs, pp, _k in rot_sets:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                rc = L.tips_fused_allreduce(pp, cp, len(sizes), _lib.FLOAT32, side.cuda_stream)
+            if rc:
+                raise _lib.TipsError("tips_fused_allreduce (capture)", rc, _lib.last_error())
+            graphs.append(g)
+        for i in range(2 * len(graphs)):
+            graphs[i % len(graphs)].replay()
+        torch.cuda.synchronize()
+        e0.record(side)
+        for i in range(40):
+            graphs[i % len(graphs)].replay()
+        e1.record(side)
+        torch.cuda.synchronize()
+    gus = e0.elapsed_time(e1) * 1e3 / 40
+    del graphs
+    graph = {"us_per_step": round(gus, 2), "achieved": round(moved / (gus * 1e-6) / 1e9, 1),
+             "frac": round(moved / (gus * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+             "note": "the fused step (pack, identity, unpack per bucket, stream joins) captured with "
+                     "torch.cuda.graph around tips_fused_allreduce, one graph per gradient set, 40 replays"}
+    return roof, graph
+
+
 def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, fixed_ms):
     """The same gradients through the training API instead of fixed views: every gradient its own
     allocation (a parameter's .grad), as a model hands them over.
@@ -985,6 +1101,12 @@ def bench_allreduce(args):
                                 "reduces gradient set i %% %d, so no step finds its gradients in the 256 MiB "
                                 "Infinity Cache" % rot)}
         del line["xgmi"]
+        if measure_pack:  # the dominant kernel (fusion pack / unpack) timed per launch; the step's rate beside it
+            line["step_roofline"] = line["roofline"]
+            line["step_roofline"]["note"] = "whole step (host-bound: launches and stream joins)" + \
+                line["step_roofline"]["note"][len("one rank"):]
+            line["roofline"], line["graph_replayed_step"] = fusion_one_rank_kernels(
+                torch, L, _lib, sizes, offs, rot_sets, cp, stream, moved)
     if workload in ("fused1000", "resnet50"):
         line["gradient_api"] = gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, ms)
     if topo:
