@@ -185,3 +185,22 @@ def test_cpu_ring_baseline_runs_the_reference_call():
     if "error" in out and "unavailable" in out["error"]:
         pytest.skip(out["error"])
     assert out["value"] > 0 and out["cores"] == 2 and out["kind"] == "reference", out
+
+
+def test_fusion_layout_mirror():
+    """bench.fusion_layout (what the one-rank pack-kernel leg times) follows fusion.cc build_entry:
+    every tensor once, in order, at 256-B aligned offsets, no bucket past the threshold, and the
+    balanced split - at least 2 buckets once 32 MiB are packed, no bucket far above its share."""
+    sys.path.insert(0, REPO)
+    import bench
+    for sizes in (bench.fused1000_sizes(), bench.resnet50_grad_sizes(), [1000, 3, 70000, 257]):
+        b = bench.fusion_layout(sizes)
+        order = [i for m in b for i, _ in m]
+        assert order == [i for i, k in enumerate(sizes) if k]
+        fills = [max(off + sizes[i] * 4 for i, off in m) for m in b]
+        assert all(off % 256 == 0 for m in b for _, off in m) and max(fills) <= 64 << 20
+        packed = sum((k * 4 + 255) // 256 * 256 for k in sizes)
+        assert len(b) == max(1, (packed + (64 << 20) - 1) // (64 << 20)) or (len(b) == 2 and packed >= 32 << 20)
+        if len(b) > 1:
+            share = packed / len(b)
+            assert all(f <= share + max(sizes) * 4 + 256 for f in fills)
