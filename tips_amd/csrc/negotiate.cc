@@ -241,11 +241,15 @@ class Negotiator {
           Hello h{};
           const Ack a{kMagic, key};
           if (!recv_all(c, &h, sizeof h, 2000) || h.magic != kMagic || h.key != key || h.size != size || h.rank <= 0 ||
-              h.rank >= size || peers_[h.rank] >= 0 || !send_all(c, &a, sizeof a)) {
+              h.rank >= size || !send_all(c, &a, sizeof a)) {
             ::close(c);
             continue;
           }
           set_nodelay(c);
+          if (peers_[h.rank] >= 0) {  // that rank gave up on an earlier connection (no answer in time): its latest wins
+            ::close(peers_[h.rank]);
+            joined--;
+          }
           peers_[h.rank] = c;
           joined++;
         }
@@ -259,7 +263,7 @@ class Negotiator {
             int fd = ::socket(AF_INET, SOCK_STREAM, 0);
             Ack a{};
             if (fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0 && !connected_to_self(fd) &&
-                send_all(fd, &h, sizeof h) && recv_all(fd, &a, sizeof a, 2000) && a.magic == kMagic && a.key == key) {
+                send_all(fd, &h, sizeof h) && recv_all(fd, &a, sizeof a, 5000) && a.magic == kMagic && a.key == key) {
               set_nodelay(fd);
               up_ = fd;
             } else if (fd >= 0) {
