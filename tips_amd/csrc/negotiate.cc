@@ -306,7 +306,7 @@ class Negotiator {
     if (ndim == 0) r->shape.push_back(1);  // a scalar travels as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
     r->dtype = dtype;
     r->stream = s;
-    if (!dry_) {  // device-resident tensors only: the negotiated path runs on the caller's stream
+    if (!dry_) {  // the real executor (the dry run of tips_negotiation_selftest touches no memory)
       // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
       // st.device is fixed from init on)
       TRY(set_device(S()));
