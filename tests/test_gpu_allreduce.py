@@ -206,6 +206,36 @@ def test_fused_pack_unpack_round_trip(gpu, monkeypatch, threshold, measure_pack)
             assert torch.equal(o, b)
 
 
+def test_fused_call_captures_into_a_graph(gpu, monkeypatch):
+    """tips_fused_allreduce_oop captured with torch.cuda.graph (what bench.py's graph_replayed_step
+    replays): one rank in measure-pack mode, so every byte goes pack -> bucket -> unpack. Each
+    replay must rewrite the outputs from the inputs' current values."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", "1")
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(1 << 20))
+    rng = np.random.default_rng(77)
+    sizes = [int(round(2 ** rng.uniform(0, 17))) for _ in range(60)]
+    ins = [torch.randn(n, device="cuda") for n in sizes]
+    outs = [torch.empty_like(t) for t in ins]
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        gpu.fused_allreduce(ins, out_list=outs)  # builds the plan outside the capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            gpu.fused_allreduce(ins, out_list=outs)
+        for k in range(3):
+            for t in ins:
+                t.add_(1.0)
+            for o in outs:
+                o.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            for t, o in zip(ins, outs):
+                assert torch.equal(o, t)
+
+
 def test_fused_views_of_one_buffer(gpu, monkeypatch):
     """Views of one flat buffer mixed with separate tensors (measure-pack mode: every byte through
     pack -> bucket -> unpack at one rank): the layout ignores where tensors lie, so the views are
