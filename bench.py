@@ -139,10 +139,10 @@ def cpu_ring_baseline(world, elems=16 << 20, iters=20):
                       % (elems, world, elems * 4 >> 20, iters, world)}
 
 
-def pmc_traffic(kernel_substr):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json), or None."""
+def pmc_traffic(kernel_substr, file_pattern="*pmc*.json"):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/<file_pattern>), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", file_pattern)), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -1107,6 +1107,10 @@ def bench_allreduce(args):
                 line["step_roofline"]["note"][len("one rank"):]
             line["roofline"], line["graph_replayed_step"] = fusion_one_rank_kernels(
                 torch, L, _lib, sizes, offs, rot_sets, cp, stream, moved)
+            tr = pmc_traffic("copy_tiles_g_kernel", "*pmc_%s.json" % workload)  # this workload's PMC passes
+            if tr:
+                line["roofline"]["traffic"] = round(tr["bytes"])
+                line["roofline"]["traffic_source"] = tr["source"]
     if workload in ("fused1000", "resnet50"):
         line["gradient_api"] = gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, ms)
     if topo:
