@@ -136,6 +136,41 @@ def test_bootstrap_broadcast_multiprocess(size):
         assert raw == bytes(range(128))
 
 
+def test_bootstrap_survives_a_silent_listener():
+    """Rank 1 first reaches another program's socket on the port, which accepts and never answers;
+    its wait for the id is bounded (5 s), so it retries and gets the id from rank 0 once rank 0
+    listens there, well inside its 60 s timeout."""
+    import socket
+    import threading
+    import time
+    port = _free_port()
+    foreign = socket.socket()
+    foreign.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    foreign.bind(("127.0.0.1", port))
+    foreign.listen(4)
+    held = []
+    t = threading.Thread(target=lambda: held.append(foreign.accept()[0]))
+    t.start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    r1 = ctx.Process(target=_bootstrap_worker, args=(1, 2, port, q))
+    r1.start()
+    t.join(60)
+    foreign.close()  # the accepted connection stays open and silent
+    time.sleep(0.5)
+    t0 = time.time()
+    r0 = ctx.Process(target=_bootstrap_worker, args=(0, 2, port, q))
+    r0.start()
+    res = sorted(q.get(timeout=60) for _ in range(2))
+    for p_ in (r0, r1):
+        p_.join(30)
+    for c in held:
+        c.close()
+    assert [rc for _, rc, _ in res] == [0, 0]
+    assert all(raw == bytes(range(128)) for _, _, raw in res)
+    assert time.time() - t0 < 30
+
+
 def test_bootstrap_timeout():
     from tips_amd import _lib
     L = _lib.lib()

@@ -8,6 +8,7 @@
 // deadline), says who it is, and receives the id.
 #include "net.h"
 
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -58,13 +59,15 @@ int bootstrap_exchange(int rank, int size, const char* host, int port, void* id,
       int c = ::accept(fd, nullptr, nullptr);
       if (c < 0) continue;
       int32_t peer = -1;
-      if (!recv_all(c, &peer, sizeof peer, ms_left()) || peer <= 0 || peer >= size || seen[peer] ||
+      if (!recv_all(c, &peer, sizeof peer, std::min(ms_left(), 5000)) || peer <= 0 || peer >= size ||
           !send_all(c, id, (size_t)id_bytes)) {
         ::close(c);
         continue;
       }
-      seen[peer] = true;
-      joined++;
+      if (!seen[peer]) {  // a rank that asks again (its earlier answer timed out) just gets the id again
+        seen[peer] = true;
+        joined++;
+      }
       ::close(c);
     }
     ::close(fd);
@@ -83,7 +86,9 @@ int bootstrap_exchange(int rank, int size, const char* host, int port, void* id,
     }
     if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0 && !connected_to_self(fd)) {
       int32_t me = rank;
-      bool ok = send_all(fd, &me, sizeof me) && recv_all(fd, id, (size_t)id_bytes, ms_left());
+      // a bounded wait: a listener that never answers (another program's socket on this port) costs
+      // one attempt, not the whole timeout
+      bool ok = send_all(fd, &me, sizeof me) && recv_all(fd, id, (size_t)id_bytes, std::min(ms_left(), 5000));
       ::close(fd);
       if (ok) return 0;
     } else {
