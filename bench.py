@@ -454,67 +454,63 @@ def fusion_layout(sizes, es=4, threshold=64 << 20, align=256):
 
 def fusion_one_rank_kernels(torch, L, _lib, sizes, offs, rot_sets, cp, stream, moved, tile=8192,
                             threshold=64 << 20):
-    """One rank, configs 4/5: (1) the fusion's pack kernel (tips_copy_tiles_variant 1 = the shipped
-    copy_tiles_g_kernel, the launch fusion.cc issues per bucket) on this layout's per-bucket tile
-    tables, rotating gradient sets, HIP events on the launch stream: the dominant kernel's
-    roofline (unpack is the same kernel over the mirrored tiles); (2) the whole fused step
-    captured into one HIP graph per gradient set (torch.cuda.graph around tips_fused_allreduce)
-    and replayed: the step without its host cost."""
-    import numpy as np
-    buckets = fusion_layout(sizes, threshold=threshold)
-    slots = torch.empty(2 * threshold // 4, dtype=torch.float32, device="cuda")
-    tabs = []  # [set][bucket] -> (device table, ntiles, payload bytes)
-    for xs, pp, _k in rot_sets:
-        ptrs = [int(v) for v in _k]  # the set's data pointers (the keep-alive uint64 array)
-        per = []
-        for b, members in enumerate(buckets):
-            rec, payload = [], 0
-            for i, off in members:
-                nb = sizes[i] * 4
-                dst = slots.data_ptr() + (b % 2) * threshold + off
-                rec += [(ptrs[i] + t, dst + t, min(tile, nb - t)) for t in range(0, nb, tile)]
-                payload += nb
-            t = torch.from_numpy(np.array(rec, dtype=np.int64)).cuda()
-            per.append((t, len(rec), payload))
-        tabs.append(per)
+    """One rank, configs 4/5: (1) the fusion's pack kernel - the launch fusion.cc issues per bucket
+    (copy_segs_kernel over the bucket's tiles of the layout), through tips_fused_pack_bucket - over
+    rotating gradient sets, HIP events on the launch stream: the dominant kernel's roofline (unpack
+    is the same kernel with source and destination swapped); (2) the whole fused step captured
+    into one HIP graph per gradient set (torch.cuda.graph around tips_fused_allreduce) and
+    replayed: the step without its host cost."""
+    nb = int(_lib.check("tips_fused_pack_bucket", L.tips_fused_pack_bucket(rot_sets[0][1], cp, len(sizes),
+                                                                          _lib.FLOAT32, -1, None, None)))
+    dst = torch.empty(threshold // 4, dtype=torch.float32, device="cuda")
     sp = stream.cuda_stream
+    payload = [0] * nb
 
     def launch(r, b):
-        t, n, _ = tabs[r][b]
-        rc = L.tips_copy_tiles_variant(t.data_ptr(), n, 1, tile, sp)
-        if rc:
-            raise _lib.TipsError("tips_copy_tiles_variant", rc, _lib.last_error())
+        rc = L.tips_fused_pack_bucket(rot_sets[r][1], cp, len(sizes), _lib.FLOAT32, b, dst.data_ptr(), sp)
+        if rc < 0:
+            raise _lib.TipsError("tips_fused_pack_bucket", int(rc), _lib.last_error())
+        payload[b] = int(rc)
 
-    for r in range(len(tabs)):
-        for b in range(len(buckets)):
+    for r in range(len(rot_sets)):  # (builds and uploads every set's tables once)
+        for b in range(nb):
             launch(r, b)
     torch.cuda.synchronize()
-    # the packed bucket 0 of set 0 holds exactly its tensors' bytes
+    # the packed bucket 0 of set 0 holds exactly its tensors' bytes, at the layout's offsets
     launch(0, 0)
     torch.cuda.synchronize()
-    s8 = slots.view(torch.uint8)
-    x0 = rot_sets[0][0]
-    ok = all(torch.equal(s8[off:off + sizes[i] * 4], x0[offs[i]:offs[i] + sizes[i]].view(torch.uint8))
-             for i, off in buckets[0])
+    import ctypes
+    lo = (ctypes.c_int64 * len(sizes))()
+    L.tips_fused_layout(cp, len(sizes), _lib.FLOAT32, lo)
+    b0 = fusion_layout(sizes, threshold=threshold)[0]
+    d8, x0 = dst.view(torch.uint8), rot_sets[0][0]
+    ok = all(torch.equal(d8[int(lo[i]):int(lo[i]) + sizes[i] * 4], x0[offs[i]:offs[i] + sizes[i]].view(torch.uint8))
+             for i, _ in b0)
     reps = 20
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # a gate: the stream first spins ~5 ms, so every launch below is queued before the first runs
+    # and the events time the kernels back to back, not the host issuing them (each
+    # tips_fused_pack_bucket call resolves its layout and pointer table on the host)
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(12_000_000)
     e0.record(stream)
     for k in range(reps):
-        for b in range(len(buckets)):
-            launch(k % len(tabs), b)
+        for b in range(nb):
+            launch(k % len(rot_sets), b)
     e1.record(stream)
     torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / (reps * len(buckets))
-    per_launch = 2 * sum(p for _, _, p in tabs[0]) / len(buckets)  # read + write of one bucket's tensors
+    us = e0.elapsed_time(e1) * 1e3 / (reps * nb)
+    per_launch = 2 * sum(payload) / nb  # read + write of one bucket's tensors
     roof = {"bound": "hbm", "achieved": round(per_launch / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(per_launch / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-            "kernel": "copy_tiles_g_kernel (fusion pack; unpack is the same kernel on the mirrored tiles)",
+            "kernel": "copy_segs_kernel (fusion pack; unpack is the same kernel, source and destination swapped)",
             "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": int(per_launch),
-            "launches_per_step": 2 * len(buckets), "buckets": len(buckets), "tile_bytes": tile,
+            "launches_per_step": 2 * nb, "buckets": nb, "tile_bytes": tile,
             "check": "bit-exact bucket bytes" if ok else "FAIL: packed bytes differ",
-            "note": "per-bucket pack launches of fusion.cc's layout, gradient set i %% %d (HBM-only), HIP events "
-                    "on the launch stream; algorithmic bytes = read + write of the bucket's tensors" % len(tabs)}
-    del slots, tabs
+            "note": "per-bucket pack launches of fusion.cc's layout (tips_fused_pack_bucket), gradient set i %% %d "
+                    "(HBM-only), HIP events on the launch stream; algorithmic bytes = read + write of the bucket's "
+                    "tensors" % len(rot_sets)}
+    del dst
     # the whole step, captured once per gradient set and replayed
     side = torch.cuda.Stream()
     side.wait_stream(stream)
@@ -550,8 +546,10 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
       optimizer:       DistributedOptimizer.synchronize() - the allreduce half of step(): every
                        .grad a view of one flat buffer (gradient bucket views), the flat buffer
                        allreduced in place (no pack, no unpack; the first step copies .grad in)
-      allreduce_grads: allreduce_grads(grads) - new output tensors (tips_fused_allreduce_oop:
-                       4 x the gradient bytes in HBM for pack + unpack, no clone)
+      allreduce_grads: allreduce_grads(grads) - new output tensors, views of one flat buffer
+                       (tips_fused_allreduce_flat: each bucket packed into it and allreduced in
+                       place, 2 x the gradient bytes in HBM; the flat buffer and its views are
+                       reused once the previous call's outputs are released)
     On one rank both are the identity, as the reference's _allreduce_cond (__init__.py:94-103);
     there the call each makes at N > 1 is timed instead.
     Host-timed like the main line, over the same rotating sets; max over ranks."""
@@ -574,11 +572,12 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         from tips_amd.optim import _allreduce_flat_
         calls = {"optimizer": lambda i: _allreduce_flat_(flats[i]),
                  "packed_separate_grads": lambda i: fls[i].allreduce_(grads[i]),
-                 "allreduce_grads": lambda i: tips_amd.fused_allreduce(grads[i])}
+                 "allreduce_grads": lambda i: tips_amd._reduce_grads(grads[i])}
         what = ("one rank: both API calls are the identity (reference _allreduce_cond); timed is what each runs at "
                 "N > 1: the optimizer's in-place allreduce of the flat buffer its gradient bucket views live in "
                 "(no device work at all on one rank), FusedList.allreduce_ over separately allocated gradients "
-                "(pack + unpack), and allreduce_grads' fused_allreduce(grads) out of place")
+                "(pack + unpack), and allreduce_grads' N > 1 body (_reduce_grads: pack into one flat output, "
+                "per bucket)")
     out = {"calls": what, "bytes_per_rank": sum(sizes) * 4, "fixed_view_ms": round(fixed_ms, 4)}
     ref = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads] if world == 1 else None
     for name, fn in calls.items():
@@ -593,7 +592,8 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         t = max_over_ranks(dist, time.perf_counter() - t0) / steps
         leg = {"ms_per_step": round(t * 1e3, 4), "vs_fixed_view": round(t * 1e3 / fixed_ms, 3)}
         if world == 1:
-            moved = 0 if name == "optimizer" else 4 * sum(sizes) * 4  # bucket views: nothing to pack
+            # bucket views: nothing to pack; flat outputs: pack only; separate outputs: pack + unpack
+            moved = {"optimizer": 0, "allreduce_grads": 2 * sum(sizes) * 4}.get(name, 4 * sum(sizes) * 4)
             leg["algorithmic_hbm_bytes"] = moved
             if moved:
                 leg["hbm_achieved_GBps"] = round(moved / t / 1e9, 1)
@@ -1107,7 +1107,7 @@ def bench_allreduce(args):
                 line["step_roofline"]["note"][len("one rank"):]
             line["roofline"], line["graph_replayed_step"] = fusion_one_rank_kernels(
                 torch, L, _lib, sizes, offs, rot_sets, cp, stream, moved)
-            tr = pmc_traffic("copy_tiles_g_kernel", "*pmc_%s.json" % workload)  # this workload's PMC passes
+            tr = pmc_traffic("copy_segs_kernel", "*pmc_%s.json" % workload)  # this workload's PMC passes
             if tr:
                 line["roofline"]["traffic"] = round(tr["bytes"])
                 line["roofline"]["traffic_source"] = tr["source"]
@@ -1153,6 +1153,25 @@ def bench_allreduce(args):
             "us_per_tensor": round(th * 1e6 / len(sizes), 2), "steps": hsteps,
             "check": "identity at one rank" if world == 1 and h_ok else ("FAIL" if not h_ok else "not checked"),
             "note": "214 numpy gradients, one tips_amd.allreduce each (host staged), the reference's per-op structure"}
+        # The same 214 numpy gradients through allreduce_grads' N > 1 body: one fused host call
+        # (tips_fused_allreduce_host: host threads pack page-locked pieces, H2D -> allreduce -> D2H
+        # pipelined per piece, unpack into new numpy arrays).
+        for _ in range(2):
+            outs = tips_amd._reduce_grads(hg)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(hsteps):
+            outs = tips_amd._reduce_grads(hg)
+        tf = max_over_ranks(dist, time.perf_counter() - t0) / hsteps
+        f_ok = world > 1 or all(np.array_equal(o, gr) for o, gr in zip(outs, hg))
+        line["host_to_host_fused"] = {
+            "ms_per_step": round(tf * 1e3, 3), "algbw_gib_s": round(total_elems * 4 / tf / GIB, 2),
+            "steps": hsteps, "threads": int(os.environ.get("TIPS_HOST_THREADS", "8")),
+            "piece_bytes": int(os.environ.get("TIPS_HOST_FUSED_PIECE_BYTES", str(8 << 20))),
+            "vs_per_tensor": round(th / tf, 2),
+            "check": "identity at one rank, bit-exact" if world == 1 and f_ok else ("FAIL" if not f_ok else "not checked"),
+            "note": "the same 214 numpy gradients through allreduce_grads' N > 1 body (tips_fused_allreduce_host): "
+                    "one call, new numpy outputs, pageable inputs; at one rank the round trip through HBM is kept"}
         del hg, outs
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True

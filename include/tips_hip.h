@@ -199,6 +199,36 @@ TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int 
  * allreduce loop returns (tips/tensorflow/__init__.py:203-222), fused. */
 TIPS_API int tips_fused_allreduce_oop(const void* const* ins, void* const* outs, const int64_t* counts, int n,
                                       int dtype, void* stream);
+/* The byte offset of each tensor of a fused list in ONE flat buffer laid out as the fusion buckets
+ * (offsets[i], 256-B aligned; may be NULL); returns the flat buffer's size in bytes (< 0 = error).
+ * A pure host function of counts, dtype and TIPS_FUSION_THRESHOLD - the same on every rank. */
+TIPS_API int64_t tips_fused_layout(const int64_t* counts, int n, int dtype, int64_t* offsets);
+/* flat = SUM over ranks of ins, tensor i at offsets[i] of tips_fused_layout (device memory of its
+ * size): each bucket is packed straight into its region of `flat` and allreduced there in place -
+ * no fusion slot, no unpack (2 x the gradient bytes of HBM traffic instead of 4 x). What
+ * allreduce_grads returns views of (the reference's per-gradient loop, __init__.py:203-222). Inputs
+ * unchanged; padding bytes of `flat` unspecified. One rank: one copy launch. Stream-ordered. */
+TIPS_API int tips_fused_allreduce_flat(const void* const* ins, const int64_t* counts, int n, int dtype, void* flat,
+                                       void* stream);
+/* Measurement entry (bench.py, tools/copy_sweep_balanced.py): the pack launch the fusion issues for
+ * bucket `bucket` of this list's layout (copy_segs_kernel over the bucket's tiles), into `dst` (device
+ * memory of the bucket's padded size), on `stream`. Returns the bytes of the tensors the bucket holds
+ * (the launch reads and writes each once), or with bucket < 0 the number of buckets; < 0 = error. */
+TIPS_API int64_t tips_fused_pack_bucket(const void* const* ins, const int64_t* counts, int n, int dtype, int bucket,
+                                        void* dst, void* stream);
+/* Fusion caches of this process: layouts built / found (a layout is a function of the counts only,
+ * so fresh gradient tensors every step still hit), and per-call pointer tables built (uploaded) /
+ * found. Any pointer may be NULL. */
+TIPS_API int tips_fusion_stats(int64_t* layouts_built, int64_t* layout_hits, int64_t* tables_built,
+                               int64_t* table_hits);
+/* Host tensors (numpy / CPU framework tensors, pageable or page-locked): outs[i] = SUM over ranks of
+ * ins[i]. The list is packed by the library's host threads (TIPS_HOST_THREADS, 8) into page-locked
+ * pieces of one byte stream (TIPS_HOST_FUSED_PIECE_BYTES, 8 MiB); each piece runs H2D -> allreduce in
+ * HBM -> D2H pipelined on separate streams while the threads pack the next and unpack the previous.
+ * The layout depends on the counts only. Blocks until every out is written (the reference's op is a
+ * CPU op, ops.cc:118; its per-gradient loop, __init__.py:212-222, fused). */
+TIPS_API int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const int64_t* counts, int n,
+                                       int dtype);
 
 /* ---- named, asynchronous allreduce with cross-rank negotiation ---- */
 

@@ -482,6 +482,41 @@ def fused_case(c, rank, size, L, _lib, sp):
         got = tips_amd.fused_allreduce(views)
     elif mode == "grads":
         got = tips_amd.allreduce_grads(views)
+    elif mode == "grads_fresh":
+        # a training loop's pattern: FRESH gradient tensors every step (new allocations, new values);
+        # allreduce_grads' outputs are views of one flat buffer (tips_fused_allreduce_flat), and the
+        # layout - a function of the counts alone - is built once and then found every step
+        s0 = tips_amd.fusion_stats()
+        steps = 4
+        for step in range(steps):
+            g.manual_seed(c["seed"] * 100 + rank + 7919 * (step + 1))
+            fresh = [torch.empty(k, device="cuda").uniform_(-1.0, 1.0, generator=g) for k in sizes]
+            out = tips_amd.allreduce_grads(fresh)
+            torch.cuda.synchronize()
+            allin = []
+            for r in range(size):
+                g.manual_seed(c["seed"] * 100 + r + 7919 * (step + 1))
+                allin.append(torch.cat([torch.empty(k, device="cuda").uniform_(-1.0, 1.0, generator=g)
+                                        for k in sizes]).cpu().numpy())
+            exp = oracle_bind.fold(allin, code=0, wide_acc=True)
+            gotf = torch.cat([t.reshape(-1) for t in out]).cpu().numpy()
+            if not np.array_equal(gotf.view(np.uint32), exp.view(np.uint32)):
+                return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": False,
+                        "error": "step %d: %d elements differ" % (step, int((gotf != exp).sum()))}
+            del out
+        s1 = tips_amd.fusion_stats()
+        d = {k: s1[k] - s0[k] for k in s0}
+        ok = d["layouts_built"] <= 1 and d["layout_hits"] >= steps - 1
+        return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": ok, "stats": d,
+                "error": "" if ok else "fusion caches: %r" % d}
+    elif mode == "host_grads":
+        # the reference's op is a CPU op (ops.cc:118): host gradients (numpy), fused into page-locked
+        # pieces (tips_fused_allreduce_host) by allreduce_grads
+        host = [v.cpu().numpy() for v in views]
+        out = tips_amd.allreduce_grads(host)
+        got = [torch.from_numpy(o).cuda() for o in out]
+        if not all(np.array_equal(h, v.cpu().numpy()) for h, v in zip(host, views)):
+            return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": False, "error": "inputs modified"}
     else:
         params = [torch.nn.Parameter(torch.zeros(k, device="cuda")) for k in sizes]
         for p, v in zip(params, views):

@@ -261,6 +261,108 @@ def test_fused_views_of_one_buffer(gpu, monkeypatch):
     assert torch.equal(flat[-10:], guard)
 
 
+@pytest.mark.parametrize("measure_pack", ["1", "0"])
+@pytest.mark.parametrize("threshold", [8192, 1 << 20, 64 << 20])
+def test_fused_flat_outputs(gpu, monkeypatch, threshold, measure_pack):
+    """tips_fused_allreduce_flat at one rank (the identity): every tensor lands at its
+    tips_fused_layout offset of one flat buffer - through the per-bucket packs (measure-pack mode,
+    as at N > 1) or one copy launch - for every dtype, odd element counts (ragged 16-B ends, 2-B
+    tails for 16-bit types), inputs that are only element-aligned (views at offset 1), empty tensors
+    and tensors above the threshold (reduced out of place into their own region)."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(threshold))
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", measure_pack)
+    tdt = {F32: torch.float32, F64: torch.float64, I32: torch.int32, I64: torch.int64, F16: torch.float16,
+           BF16: torch.bfloat16}
+    rng = np.random.default_rng(threshold % 1000 + int(measure_pack))
+    for dtype in ALL_DTYPES:
+        sizes = [int(round(2 ** rng.uniform(0, 15))) for _ in range(120)] + [0, 3, 1, 40000, 7]
+        base = torch.randint(-1000, 1000, (sum(sizes) + len(sizes) + 2,), device="cuda").to(tdt[dtype])
+        ins, off = [], 1  # offset 1: element-aligned only
+        for s in sizes:
+            ins.append(base[off:off + s])
+            off += s + 1
+        for _ in range(2):
+            outs = gpu.fused_allreduce_flat(ins)
+            torch.cuda.synchronize()
+            for o, t in zip(outs, ins):
+                assert o.shape == t.shape and o.dtype == t.dtype and torch.equal(o, t)
+            del outs
+
+
+def test_fused_flat_output_reuse(gpu, monkeypatch):
+    """allreduce_grads' flat outputs are reused only once the caller has released every output:
+    held outputs (or a tensor derived from one) keep their buffer; a later call gets another."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", "1")
+    ins = [torch.randn(n, device="cuda") for n in (1000, 3, 70000, 257)]
+    a = gpu.fused_allreduce_flat(ins)
+    pa = a[0].data_ptr()
+    b = gpu.fused_allreduce_flat(ins)  # a still held: a new set
+    assert b[0].data_ptr() != pa
+    keep = b[2][5:9]  # a derived view keeps b's storage
+    del a
+    c = gpu.fused_allreduce_flat(ins)  # a released: its set is handed out again
+    assert c[0].data_ptr() == pa
+    pb = b[0].data_ptr()
+    del b, c
+    d = gpu.fused_allreduce_flat(ins)
+    assert d[0].data_ptr() != pb  # (b's storage is still referenced through `keep`)
+    torch.cuda.synchronize()
+    for o, t in zip(d, ins):
+        assert torch.equal(o, t)
+    assert torch.equal(keep, ins[2][5:9])
+
+
+def test_fusion_caches_with_fresh_tensors(gpu, monkeypatch):
+    """The fusion layout depends on the counts only: fresh tensors of the same sizes every call find
+    it (tips_fusion_stats), in place, out of place and flat; the same pointers find their table too."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", "1")
+    sizes = [4099, 17, 100000, 3]
+    s0 = gpu.fusion_stats()
+    for step in range(4):
+        ts = [torch.full((n,), float(step), device="cuda") for n in sizes]
+        outs = gpu.fused_allreduce_flat(ts)
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, t) for o, t in zip(outs, ts))
+    s1 = gpu.fusion_stats()
+    assert s1["layouts_built"] - s0["layouts_built"] == 1 and s1["layout_hits"] - s0["layout_hits"] >= 3
+    fixed = [torch.randn(n, device="cuda") for n in sizes]
+    gpu.fused_allreduce_(fixed)
+    s2 = gpu.fusion_stats()
+    gpu.fused_allreduce_(fixed)
+    s3 = gpu.fusion_stats()
+    assert s3["tables_built"] == s2["tables_built"] and s3["table_hits"] > s2["table_hits"]
+
+
+@pytest.mark.parametrize("piece", [256, 4096, 8 << 20])
+def test_fused_host_identity(gpu, monkeypatch, piece):
+    """tips_fused_allreduce_host at one rank (the identity after H2D -> HBM -> D2H): many host tensors
+    of every dtype, pageable numpy and CPU torch, empty ones, pieces from 256 B (tensors span many
+    pieces; the copy threads split every piece) to 8 MiB; bit-exact, inputs unchanged."""
+    import torch
+    monkeypatch.setenv("TIPS_HOST_FUSED_PIECE_BYTES", str(piece))
+    rng = np.random.default_rng(piece % 977)
+    for dtype in ALL_DTYPES:
+        sizes = [int(round(2 ** rng.uniform(0, 14))) for _ in range(60)] + [0, 1, 3]
+        ins = [rand(dtype, s, rng) for s in sizes]
+        if dtype == BF16:  # (numpy has no bfloat16: CPU torch tensors)
+            ins = [torch.from_numpy(x.view(np.int16)).view(torch.bfloat16) for x in ins]
+        before = [x.copy() if dtype != BF16 else x.clone() for x in ins]
+        outs = gpu.fused_allreduce_host(ins)
+        for o, x, b in zip(outs, ins, before):
+            if dtype == BF16:
+                assert torch.equal(o.view(torch.int16), b.view(torch.int16)) and torch.equal(x.view(torch.int16), b.view(torch.int16))
+            else:
+                assert same_bits(o, b, dtype) and same_bits(x, b, dtype)
+    ts = [torch.randn(n) for n in (5, 100003, 64)]
+    outs = gpu.fused_allreduce_host(ts)
+    assert all(torch.equal(o, t) for o, t in zip(outs, ts))
+    with pytest.raises(TypeError):
+        gpu.fused_allreduce_host([np.zeros(4, np.float32), np.zeros(4, np.float64)])
+
+
 def test_allreduce_grads_identity_single_rank(gpu):
     import torch
     grads = [torch.randn(10, device="cuda"), None, torch.randn(3, 3, device="cuda")]

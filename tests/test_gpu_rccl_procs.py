@@ -82,6 +82,22 @@ def test_fusion_workloads_over_rccl(gpu, workload, p):
     check(run_job(p, cases, timeout=600, **rccl_env("auto")))
 
 
+@pytest.mark.parametrize("workload", ["config4", "config5"])
+def test_allreduce_grads_fresh_tensors_over_rccl(gpu, workload):
+    """allreduce_grads over 3 real RCCL ranks with FRESH gradient tensors every step (a training
+    loop with zero_grad(set_to_none=True)): the outputs are views of one flat buffer per dtype
+    (tips_fused_allreduce_flat), each step bit-exact against the oracle's fold, and the fusion layout
+    (a function of the counts alone) is built once and found on every later step
+    (tips_fusion_stats). Then the same gradients as host (numpy) tensors through the fused host
+    path (tips_fused_allreduce_host), bit-exact."""
+    cases = [{"fused": workload, "seed": 9, "mode": m} for m in ("grads_fresh", "host_grads")]
+    results = run_job(3, cases, timeout=600, **rccl_env("auto"))
+    check(results)
+    for res in results:
+        st = res["results"][0]["stats"]
+        assert st["layouts_built"] <= 1 and st["layout_hits"] >= 3, st
+
+
 @pytest.mark.parametrize("algo,p,lanes", [("ring", 2, 2), ("ring", 3, 3), ("direct", 3, 2), ("direct", 4, 2)])
 def test_transfer_lanes_across_processes(gpu, algo, p, lanes):
     """TIPS_LANES: step i's group on lane i % L, each lane a communicator split from the job's

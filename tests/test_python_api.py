@@ -98,6 +98,10 @@ def _fake_two_ranks(monkeypatch):
 
     monkeypatch.setattr(tips_amd, "allgather_op", gather)
     monkeypatch.setattr(tips_amd, "size", lambda: 2)
+    # dense host gradients go through the fused host path at N > 1: here each through the (faked)
+    # tips_amd.allreduce, so the tests below see one reduction per gradient
+    monkeypatch.setattr(tips_amd._ops, "fused_allreduce_host",
+                        lambda ts, out_list=None: [tips_amd.allreduce(t) for t in ts])
 
 
 def test_indexed_slices_take_the_allgather_branch(monkeypatch):

@@ -10,7 +10,9 @@ from .basics import TipsBasics, init, is_initialized, rank, shutdown, size
 from .compression import Compression, Compressor, FP16Compressor, NoneCompressor
 from .ops import (Handle, allgather_async, allgather_op, allreduce_async, broadcast_async, allreduce_async_many, synchronize_many, allreduce_op, broadcast_op, poll, synchronize, broadcast_variables, bucket_sum, fused_allreduce,
                   fused_allreduce_, rank_op, registered_host_buffer, set_algorithm, set_consistency_check, size_op)
+from .ops import fused_allreduce_flat, fused_allreduce_host, fusion_stats
 from ._lib import TipsError, TipsLibraryError
+from . import ops as _ops
 from . import tensors as _tensors
 
 Average = 'Average'
@@ -33,7 +35,7 @@ __all__ = [
     "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
-    "DistributedOptimizer", "DistributedGradientTape",
+    "DistributedOptimizer", "DistributedGradientTape", "fused_allreduce_flat", "fused_allreduce_host", "fusion_stats",
 ]
 
 
@@ -122,22 +124,142 @@ def allreduce_grads(grads, compression=Compression.none, op=None, fused=True, sp
         grads = [_to_dense(g) if g is not None else g for g in grads]
     if size() <= 1:
         return list(grads)
+    return _reduce_grads(grads, compression, op, fused)
+
+
+def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
+    """What allreduce_grads runs at N > 1 (bench.py times it on one rank, where allreduce_grads
+    itself is the identity). With fused=True:
+      - dense device gradients, per dtype: fused_allreduce_flat - the outputs are views of one flat
+        buffer laid out as the fusion buckets, each bucket packed into it and allreduced in place
+        (a layout depends on the counts only, so fresh gradient tensors every step hit the caches);
+      - dense host gradients (numpy / CPU torch: the reference's op is a CPU op, ops.cc:118), per
+        dtype: fused_allreduce_host - packed into page-locked pieces by host threads, pipelined
+        H2D -> allreduce -> D2H, unpacked into new host tensors;
+      - the rest (sparse) one by one, through the reference's allgather branch."""
+    none = compression is Compression.none
+    global _DATA_PTR
+    if _DATA_PTR is None:
+        import torch
+        _DATA_PTR = torch.Tensor.data_ptr
+    if fused and none:
+        plan = _find_plan(grads)
+        if plan is not None:  # the same tensor objects as a recent call: no per-tensor inspection
+            return plan.run(grads)
     out = list(grads)
-    if fused:
-        groups = {}
-        for i, g in enumerate(grads):
-            if _fusable(g):
-                c, ctx = compression.compress(g)
-                groups.setdefault(c.dtype, []).append((i, c.contiguous(), ctx))
-        for members in groups.values():
-            # out of place: pack reads each gradient, unpack writes a new tensor (no clone)
-            sums = fused_allreduce([c for _, c, _ in members])
-            for (i, _, ctx), s in zip(members, sums):
-                out[i] = compression.decompress(s, ctx)
+    dev, host = {}, {}
+    simple = fused and none  # only dense, contiguous device tensors: the split can be remembered
     for i, g in enumerate(grads):
-        if g is not None and (not fused or not _fusable(g)):
+        if g is None:
+            continue
+        if not fused:
             out[i] = allreduce(g, compression=compression, op=op)
+            continue
+        kind = _kind(g)
+        if kind is None:
+            out[i] = allreduce(g, compression=compression, op=op)
+            simple = False
+            continue
+        c, ctx = (g, None) if none else compression.compress(g)
+        if kind == "dev":
+            if not c.is_contiguous():
+                c = c.contiguous()
+                simple = False
+            dev.setdefault((c.dtype, c.device), []).append((i, c, ctx))
+        else:
+            c = _tensors.contiguous(c)
+            host.setdefault(str(c.dtype), []).append((i, c, ctx))
+    plan_groups = []
+    for members in dev.values():
+        ts = [c for _, c, _ in members]
+        fo = _ops._flat_outputs(ts, _tensors.dtype_code(ts[0]))
+        sums = _ops._flat_run(fo, ts, list(map(_DATA_PTR, ts)))
+        for (i, _, ctx), s in zip(members, sums):
+            out[i] = s if none else compression.decompress(s, ctx)
+        plan_groups.append(([i for i, _, _ in members], fo))
+    for members in host.values():
+        sums = _ops.fused_allreduce_host([c for _, c, _ in members])
+        for (i, _, ctx), s in zip(members, sums):
+            out[i] = s if none else compression.decompress(s, ctx)
+    if simple and not host:
+        _remember_plan(grads, plan_groups)
     return out
+
+
+_DATA_PTR = None  # torch.Tensor.data_ptr, bound on first use
+_PLANS = []       # recent _GradPlans, most recent first
+
+
+class _GradPlan(object):
+    """How _reduce_grads split one list of dense device gradients, kept for a later call with the
+    SAME tensor objects (a training loop whose .grad tensors persist, or a set of gradient buffers
+    used in turn): such a call is recognised through weak references - a tensor that died or was
+    replaced never matches - and skips the per-tensor inspection (kind, dtype, contiguity, shape),
+    which costs more host time for 1000 gradients than the fused allreduce's device work. Only the
+    data pointers are read again (a tensor's storage can be swapped in place)."""
+
+    def __init__(self, grads, groups):
+        import weakref
+        self.refs = [weakref.ref(g) if g is not None else _DEAD_REF for g in grads]
+        self.n = len(grads)
+        self.groups = groups  # [(positions, _FlatOutputs)]
+        self.whole = len(groups) == 1 and groups[0][0] == list(range(self.n))
+
+    def matches(self, grads):
+        import operator
+        import weakref
+        return len(grads) == self.n and all(map(operator.is_, map(weakref.ref.__call__, self.refs), grads))
+
+    def run(self, grads):
+        out = list(grads)
+        for pos, fo in self.groups:
+            ts = grads if self.whole else [grads[i] for i in pos]
+            sums = _ops._flat_run(fo, ts, list(map(_DATA_PTR, ts)))
+            if self.whole:
+                return sums
+            for i, s in zip(pos, sums):
+                out[i] = s
+        return out
+
+
+class _Gone(object):
+    pass
+
+
+def _dead():
+    import weakref
+    return weakref.ref(_Gone())  # (the object is gone at once: the reference reads None, as a None gradient)
+
+
+_DEAD_REF = _dead()
+
+
+def _find_plan(grads):
+    for k, p in enumerate(_PLANS):
+        if p.matches(grads):
+            if k:
+                _PLANS.insert(0, _PLANS.pop(k))
+            return p
+    return None
+
+
+def _remember_plan(grads, groups):
+    if not groups:
+        return
+    _PLANS.insert(0, _GradPlan(grads, groups))
+    del _PLANS[8:]
+
+
+def _kind(g):
+    """'dev' for a dense device tensor, 'host' for a dense host tensor (numpy, CPU torch), None for
+    anything reduced on its own (sparse)."""
+    if _tensors.is_torch(g):
+        if g.is_sparse:
+            return None
+        return "dev" if g.is_cuda else "host"
+    if isinstance(g, IndexedSlices):
+        return None
+    return "host"
 
 
 def _fusable(g):

@@ -85,6 +85,13 @@ _SIGNATURES = [
     ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_fused_allreduce_oop", ctypes.c_int,
      [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_fused_layout", ctypes.c_int64, [_c_i64_p, ctypes.c_int, ctypes.c_int, _c_i64_p]),
+    ("tips_fused_allreduce_flat", ctypes.c_int,
+     [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tips_fusion_stats", ctypes.c_int, [_c_i64_p, _c_i64_p, _c_i64_p, _c_i64_p]),
+    ("tips_fused_pack_bucket", ctypes.c_int64,
+     [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tips_fused_allreduce_host", ctypes.c_int, [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int]),
     ("tips_enqueue_allreduce", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_enqueue_allreduce_shaped", ctypes.c_int64,

@@ -2,20 +2,30 @@
 //
 // The reference issues one MPIAllreduce per gradient, each negotiated through
 // rank 0 (tips/tensorflow/__init__.py:212-222, coordinator.cc:355-513). Here a
-// list of device tensors is packed into buckets of at most the fusion
-// threshold (TIPS_FUSION_THRESHOLD, 64 MiB) by copy_tiles_kernel, each bucket
-// is allreduced once, and the sums are unpacked into the outputs (in place or
-// not). One path serves tips_fused_allreduce (in place), tips_fused_allreduce_oop
-// and the negotiated path's readiness batches (negotiate.cc).
+// list of tensors is laid out in buckets of at most the fusion threshold
+// (TIPS_FUSION_THRESHOLD, 64 MiB), each bucket is allreduced once, and the sums
+// land in the outputs. Three forms share one layout:
+//   - tips_fused_allreduce (in place) / _oop: pack -> bucket slot -> allreduce -> unpack;
+//   - tips_fused_allreduce_flat: pack straight into one flat output buffer laid out as the
+//     buckets, allreduce each bucket there in place (no slot, no unpack: 2 x the bytes of HBM
+//     traffic instead of 4 x) - what allreduce_grads returns views of;
+//   - the negotiated path's readiness batches (negotiate.cc) use the first form.
 //
-// Streams: every device operation of a call runs on the two fusion streams
-// (pack / unpack on fuse_stream, bucket allreduces on bucket_stream), joined with
-// the caller's stream at entry and exit. Calls from different caller streams are
-// therefore ordered through fuse_stream and can never write a shared bucket slot
-// concurrently. Descriptor tables ({src, dst, bytes} per 8 KiB tile) are built on
-// the host once per distinct tensor list and cached in HBM; a new list uploads
-// its table on fuse_stream, and an evicted table is freed stream-ordered behind
-// its last use. Nothing here synchronises the device.
+// Layouts are a function of (dtype, counts, threshold, tile) alone, never of where the tensors
+// lie: every rank must issue the same allreduces over the same bucket offsets, and a training
+// loop hands over fresh gradient tensors every step. A layout is built once (bucket cut, a
+// 256-B aligned byte offset per tensor in one "flat" byte space, the segments each tile of that
+// space meets). Per call only the pointers change: they are resolved on the host into one
+// {src, dst, begin, end} record per tensor and two per tile (the tile's one or two segments, or
+// where its segments start: copy_segs_kernel reads them with one scalar load before its first
+// data load) and uploaded
+// through a page-locked ring - unless this layout saw the same pointer set recently
+// (LRU of 16 per layout), in which case nothing is uploaded. tips_fusion_stats counts both caches.
+//
+// Streams: every device operation of a call runs on the two fusion streams (pack / unpack on
+// fuse_stream, bucket allreduces on bucket_stream), joined with the caller's stream at entry and
+// exit, so calls from different caller streams never write a shared bucket slot concurrently.
+// Nothing here synchronises the device.
 #include <string.h>
 
 #include <algorithm>
@@ -27,184 +37,327 @@ namespace rt {
 
 namespace {
 
-constexpr int64_t kDefaultCopyTile = 8 * 1024;  // tools/fusion_tile_sweep.sh: 8 KiB beat 16-64 KiB
-constexpr size_t kMaxEntries = 32;             // cached tensor lists
-constexpr int kUploadSlots = 4;                // page-locked staging of descriptor uploads
+constexpr int64_t kDefaultCopyTile = 8 * 1024;  // tools/copy_sweep_balanced.py: 8 KiB beat 4 / 16 KiB
+constexpr size_t kMaxLayouts = 32;
+constexpr size_t kMaxTables = 16;  // pointer sets per layout
+constexpr int kUploadSlots = 4;    // page-locked staging of table uploads
 
 int64_t copy_tile_bytes() {
-  return std::min<int64_t>(tips::kCopyTileBytes,
-                           round_up(std::max<int64_t>(4096, env_i64("TIPS_COPY_TILE_BYTES", kDefaultCopyTile)), 4096));
+  const int64_t t = env_i64("TIPS_COPY_TILE_BYTES", kDefaultCopyTile);
+  return t <= 4096 ? 4096 : t <= 8192 ? 8192 : 16384;
 }
+
+// store cache policy of the segment copy: 2 = sc1 (default: the line leaves the XCD's L2, as the
+// sum kernels' stores), 1 = nt, 0 = plain (TIPS_COPY_STORE_POLICY, the tuning sweep's knob)
+int copy_store_policy() { return (int)std::min<int64_t>(2, std::max<int64_t>(0, env_i64("TIPS_COPY_STORE_POLICY", 2))); }
+
+enum Mode { kSlot = 0, kCopy = 1, kFlat = 2 };
 
 struct Bucket {
-  int64_t bytes;       // padded size reduced
-  char* buf;           // its fusion slot (bucket b uses slot b % 2)
-  int64_t pack0, npack;  // tiles [pack0, pack0 + npack) pack, the same count after unpack0 unpack
-  int64_t unpack0;
+  int64_t off;    // byte offset in the flat space (tile-aligned, so no tile straddles two buckets)
+  int64_t bytes;  // padded size reduced (a multiple of 256)
+  int tile0, ntiles;
 };
 
-struct Entry {
-  uint64_t key = 0;
-  bool identity = false;  // one rank: only the out-of-place copies (dev[0..ntiles)), no buckets
-  int dtype = 0;
-  int64_t tile = 0;
+struct Table {  // resolved segment records of one pointer set
+  uint64_t hash = 0;
+  int mode = 0;
   std::vector<const void*> ins;
   std::vector<void*> outs;
-  std::vector<int64_t> counts;
-  std::vector<Bucket> buckets;
-  std::vector<BatchItem> direct;  // tensors of at least the threshold, reduced where they lie (build_entry)
-  CopyTile* dev = nullptr;   // descriptor table in HBM
-  size_t ntiles = 0;
-  uint64_t stamp = 0;        // last use (LRU)
+  const void* base = nullptr;  // the flat output (kFlat) or the slot base (kSlot)
+  CopySeg* dev = nullptr;      // kSlot: [pack | unpack], else one table; nseg records each
+  uint64_t stamp = 0;
 };
-
-uint64_t key_of(const BatchItem* items, int n, int dtype, int64_t tile) {
-  uint64_t h = 1469598103934665603ull ^ (uint64_t)dtype;
-  auto mix = [&](uint64_t v) {
-    h ^= v;
-    h *= 1099511628211ull;
-  };
-  mix((uint64_t)n);
-  mix((uint64_t)tile);
-  for (int i = 0; i < n; i++) {
-    mix((uint64_t)(uintptr_t)items[i].in);
-    mix((uint64_t)(uintptr_t)items[i].out);
-    mix((uint64_t)items[i].count);
-  }
-  return h;
-}
-
-bool same_list(const Entry& e, const BatchItem* items, int n, int dtype, int64_t tile) {
-  if (e.dtype != dtype || e.tile != tile || (int)e.counts.size() != n) return false;
-  for (int i = 0; i < n; i++)
-    if (e.ins[i] != items[i].in || e.outs[i] != items[i].out || e.counts[i] != items[i].count) return false;
-  return true;
-}
 
 }  // namespace
 
+struct Layout {
+  uint64_t key = 0;
+  int dtype = 0;
+  int64_t tile = 0, threshold = 0;
+  bool balance = true;
+  std::vector<int64_t> counts;
+  std::vector<int64_t> off;     // per tensor: byte offset in the flat space (-1: empty tensor)
+  std::vector<int> bucket;      // per tensor: its bucket, -1 = reduced where it lies (>= threshold) or empty
+  std::vector<Bucket> buckets;
+  std::vector<int> direct;      // tensors of at least the threshold, list order
+  std::vector<int> seg_tensor;  // segment k -> tensor (segments in flat order; empty tensors have none)
+  std::vector<int> tiles;       // per tile of the flat space: {first segment meeting it, how many}
+  int64_t flat_bytes = 0;
+  int ntiles = 0;
+  std::vector<Table*> tables;
+  uint64_t stamp = 0;
+};
+
+// Bucket cut and offsets: a pure function of (dtype, counts, threshold, tile, balance).
+// Balanced buckets: B = the fewest buckets of at most `threshold` that hold the packed bytes, at
+// least 2 once there are 32 MiB (so pack(1) overlaps the exchange of bucket 0), filled up to
+// total / B each instead of greedily to the threshold (a greedy split of config 4 leaves a 15 MiB
+// tail bucket, a launch that small ramps up and drains at 4.3 TB/s). A tensor of at least the
+// threshold gets a region of its own after the buckets and is reduced where it lies.
+void build_layout(Layout* L, const int64_t* counts, int n) {
+  const int64_t es = tips::dtype_size(L->dtype), threshold = L->threshold, tile = L->tile;
+  L->counts.assign(counts, counts + n);
+  L->off.assign(n, -1);
+  L->bucket.assign(n, -1);
+  int64_t packed = 0;
+  for (int i = 0; i < n; i++) {
+    const int64_t b = counts[i] * es;
+    if (b > 0 && b < threshold) packed += round_up(b, kAlignBytes);
+  }
+  int64_t target = threshold;
+  int64_t nb = (packed + threshold - 1) / threshold;
+  if (nb < 2 && packed >= (32 << 20) && L->balance) nb = 2;
+  if (nb > 1 && L->balance) target = std::min(threshold, round_up((packed + nb - 1) / nb, kAlignBytes));
+  int64_t cur = 0;  // bytes placed in the current bucket
+  for (int i = 0; i < n; i++) {
+    const int64_t bytes = counts[i] * es;
+    if (bytes <= 0) continue;
+    if (bytes >= threshold) {
+      L->direct.push_back(i);
+      continue;
+    }
+    int64_t o = round_up(cur, kAlignBytes);
+    if (L->buckets.empty() || o + bytes > threshold || o >= target) {  // a new bucket
+      L->buckets.push_back(Bucket{0, 0, 0, 0});
+      o = 0;
+    }
+    L->bucket[i] = (int)L->buckets.size() - 1;
+    L->off[i] = o;  // bucket-relative for now
+    cur = o + bytes;
+    L->buckets.back().bytes = round_up(cur, kAlignBytes);
+  }
+  int64_t f = 0;
+  for (Bucket& b : L->buckets) {
+    b.off = f;
+    b.tile0 = (int)(f / tile);
+    b.ntiles = (int)((b.bytes + tile - 1) / tile);
+    f = round_up(f + b.bytes, tile);
+  }
+  for (int i = 0; i < n; i++)
+    if (L->bucket[i] >= 0) L->off[i] += L->buckets[L->bucket[i]].off;
+  for (int i : L->direct) {
+    L->off[i] = f;
+    f = round_up(f + counts[i] * es, kAlignBytes);
+  }
+  L->flat_bytes = f;
+  L->ntiles = (int)((f + tile - 1) / tile);
+  // segments in flat order: the buckets' tensors (list order within each bucket, buckets in order
+  // = list order), then the direct tensors
+  for (int i = 0; i < n; i++)
+    if (L->bucket[i] >= 0) L->seg_tensor.push_back(i);
+  for (int i : L->direct) L->seg_tensor.push_back(i);
+  // tile t meets segments [first, first + count): first = the first ending past the tile's start,
+  // and every one after it that begins before the tile's end (at most tile / 256 + 1: segments
+  // begin 256-B aligned)
+  const int nseg = (int)L->seg_tensor.size();
+  L->tiles.assign(2 * (size_t)L->ntiles, 0);
+  int k = 0, e = 0;
+  for (int t = 0; t < L->ntiles; t++) {
+    const int64_t start = (int64_t)t * tile, stop = start + tile;
+    while (k < nseg && L->off[L->seg_tensor[k]] + counts[L->seg_tensor[k]] * es <= start) k++;
+    e = std::max(e, k);
+    while (e < nseg && L->off[L->seg_tensor[e]] < stop) e++;
+    L->tiles[2 * t] = k;
+    L->tiles[2 * t + 1] = e - k;
+  }
+}
+
 struct FusionCache {
-  std::vector<Entry*> entries;
+  std::vector<Layout*> layouts;
   uint64_t clock = 0;
   struct Upload {
-    CopyTile* host = nullptr;  // hipHostMalloc
-    size_t cap = 0;            // tiles
+    void* host = nullptr;  // hipHostMalloc
+    size_t cap = 0;        // bytes
     hipEvent_t done = nullptr;  // after the copy that last read it
     bool used = false;
   } up[kUploadSlots];
   int next_up = 0;
+  int64_t layouts_built = 0, layout_hits = 0, tables_built = 0, table_hits = 0;
 };
 
 namespace {
 
-void free_entry(State& st, Entry* e) {
-  if (e->dev) (void)hipFreeAsync(e->dev, st.fuse_stream);  // behind its last use on fuse_stream
-  delete e;
+void free_table(State& st, Table* t) {
+  if (t->dev) (void)hipFreeAsync(t->dev, st.fuse_stream);  // behind its last use on fuse_stream
+  delete t;
 }
 
-// Build a tensor list's buckets and descriptors; upload the table on fuse_stream.
-//
-// The layout is a function of the element counts, the dtype and the threshold alone - never of
-// where the tensors lie - because every rank must issue the same allreduces over the same bucket
-// offsets: a tensor of at least the threshold is reduced where it lies (its own allreduce, only
-// its own bytes touched); every other tensor is packed into the current bucket at a 256-B aligned
-// offset. (An earlier version reduced tensors that happened to lie back to back in memory as one
-// run; an allocator that placed them so on one rank and not on another would have paired
-// different elements across ranks. A flat buffer is reduced without copies by allreducing the
-// buffer itself: DistributedOptimizer does that with its gradient bucket views.)
-int build_entry(State& st, FusionCache& fc, Entry* e, const BatchItem* items, int n, int64_t threshold) {
-  const int64_t es = tips::dtype_size(e->dtype), tile = e->tile;
-  std::vector<CopyTile> pack, unpack;
-  std::vector<int64_t> sizes;  // per bucket
-  std::vector<int64_t> first;  // per bucket: first tile index into pack / unpack
-  // Balanced buckets: B = the fewest buckets of at most `threshold` that hold the packed bytes,
-  // at least 2 once there are 32 MiB (so pack(1) overlaps the exchange of bucket 0), filled up to
-  // total / B each instead of greedily to the threshold. A greedy split of config 4 leaves a
-  // 15 MiB tail bucket (a launch that small ramps up and drains at 4.3 TB/s) and exposes a
-  // full 64 MiB pack before the first exchange.
-  int64_t target = threshold;
-  if (!e->identity) {
-    int64_t packed = 0;  // upper bound of the packed bytes: every tensor below the threshold
-    for (int i = 0; i < n; i++) {
-      const int64_t b = items[i].count * es;
-      if (b < threshold) packed += round_up(b, kAlignBytes);
-    }
-    int64_t nb = (packed + threshold - 1) / threshold;
-    if (nb < 2 && packed >= (32 << 20) && env_i64("TIPS_FUSION_BALANCE", 1)) nb = 2;
-    if (nb > 1 && env_i64("TIPS_FUSION_BALANCE", 1)) target = std::min(threshold, round_up((packed + nb - 1) / nb, kAlignBytes));
-  }
-  auto place = [&](const char* in, char* out, int64_t bytes) {
-    if (e->identity) {  // one rank: in place nothing, out of place a copy
-      for (int64_t t = 0; in != out && t < bytes; t += tile)
-        pack.push_back(CopyTile{in + t, out + t, std::min(tile, bytes - t)});
-      return;
-    }
-    if (bytes >= threshold) {
-      e->direct.push_back(BatchItem{in, out, bytes / es});
-      return;
-    }
-    int64_t off = sizes.empty() ? 0 : round_up(sizes.back(), kAlignBytes);
-    // a new bucket when this one would pass the threshold, or has reached its balanced share
-    if (sizes.empty() || off + bytes > threshold || off >= target) {
-      sizes.push_back(0);
-      first.push_back((int64_t)pack.size());
-      off = 0;
-    }
-    char* slot = (char*)st.fusion.p + (int64_t)((sizes.size() - 1) % 2) * threshold;
-    for (int64_t t = 0; t < bytes; t += tile) {
-      const int64_t tb = std::min(tile, bytes - t);
-      pack.push_back(CopyTile{in + t, slot + off + t, tb});
-      unpack.push_back(CopyTile{slot + off + t, out + t, tb});
-    }
-    sizes.back() = off + bytes;
-  };
-  for (int i = 0; i < n; i++) {
-    const int64_t bytes = items[i].count * es;
-    if (bytes > 0) place((const char*)items[i].in, (char*)items[i].out, bytes);
-  }
-  const int64_t npack = (int64_t)pack.size();
-  for (size_t b = 0; b < sizes.size(); b++) {
-    const int64_t end = b + 1 < sizes.size() ? first[b + 1] : npack;
-    e->buckets.push_back(Bucket{round_up(sizes[b], kAlignBytes), (char*)st.fusion.p + (int64_t)(b % 2) * threshold,
-                                first[b], end - first[b], npack + first[b]});
-  }
-  e->ntiles = pack.size() + unpack.size();
-  if (e->ntiles == 0) return 0;
-  const size_t bytes = e->ntiles * sizeof(CopyTile);
-  HIP_TRY(hipMallocAsync((void**)&e->dev, bytes, st.fuse_stream));
+void free_layout(State& st, Layout* L) {
+  for (Table* t : L->tables) free_table(st, t);
+  delete L;
+}
+
+// Host -> device on fuse_stream through a page-locked slot (the pageable path would block).
+// A slot is reused once the copy that last read it has run; with 4 slots that wait is rare.
+int upload(State& st, FusionCache& fc, void* dev, const void* src, size_t bytes) {
   FusionCache::Upload& u = fc.up[fc.next_up];
   fc.next_up = (fc.next_up + 1) % kUploadSlots;
-  if (u.used) HIP_TRY(hipEventSynchronize(u.done));  // the copy that last read this slot has run
-  if (u.cap < e->ntiles) {
+  if (u.used) HIP_TRY(hipEventSynchronize(u.done));
+  if (u.cap < bytes) {
     if (u.host) HIP_TRY(hipHostFree(u.host));
     u.host = nullptr;
     u.cap = 0;
-    const size_t cap = std::max<size_t>(e->ntiles, 16384);
-    HIP_TRY(hipHostMalloc((void**)&u.host, cap * sizeof(CopyTile), hipHostMallocDefault));
+    const size_t cap = std::max<size_t>(bytes, 256 << 10);
+    HIP_TRY(hipHostMalloc(&u.host, cap, hipHostMallocDefault));
     u.cap = cap;
   }
   if (!u.done) HIP_TRY(hipEventCreateWithFlags(&u.done, hipEventDisableTiming));
-  memcpy(u.host, pack.data(), pack.size() * sizeof(CopyTile));
-  memcpy(u.host + pack.size(), unpack.data(), unpack.size() * sizeof(CopyTile));
-  HIP_TRY(hipMemcpyAsync(e->dev, u.host, bytes, hipMemcpyHostToDevice, st.fuse_stream));
+  memcpy(u.host, src, bytes);
+  HIP_TRY(hipMemcpyAsync(dev, u.host, bytes, hipMemcpyHostToDevice, st.fuse_stream));
   HIP_TRY(hipEventRecord(u.done, st.fuse_stream));
   u.used = true;
   return 0;
 }
 
-// The fusion slots: two buckets of `threshold` bytes, zeroed once (padding between packed
-// tensors is reduced too, never unpacked). A new threshold drops every cached table (they
-// hold addresses in the old slots), after the fusion streams have finished with them.
+uint64_t fnv(uint64_t h, uint64_t v) { return (h ^ v) * 1099511628211ull; }
+
+Layout* find_layout(State& st, FusionCache& fc, const int64_t* counts, int n, int dtype, int64_t threshold,
+                    int64_t tile, bool balance) {
+  uint64_t h = fnv(fnv(fnv(fnv(1469598103934665603ull, (uint64_t)dtype), (uint64_t)threshold), (uint64_t)tile),
+                   (uint64_t)balance);
+  h = fnv(h, (uint64_t)n);
+  for (int i = 0; i < n; i++) h = fnv(h, (uint64_t)counts[i]);
+  for (Layout* L : fc.layouts)
+    if (L->key == h && L->dtype == dtype && L->threshold == threshold && L->tile == tile && L->balance == balance &&
+        (int)L->counts.size() == n && std::equal(L->counts.begin(), L->counts.end(), counts)) {
+      L->stamp = ++fc.clock;
+      fc.layout_hits++;
+      return L;
+    }
+  if (fc.layouts.size() >= kMaxLayouts) {  // evict the least recently used layout
+    auto lru = std::min_element(fc.layouts.begin(), fc.layouts.end(),
+                                [](const Layout* a, const Layout* b) { return a->stamp < b->stamp; });
+    free_layout(st, *lru);
+    fc.layouts.erase(lru);
+  }
+  Layout* L = new Layout();
+  L->key = h;
+  L->dtype = dtype;
+  L->threshold = threshold;
+  L->tile = tile;
+  L->balance = balance;
+  build_layout(L, counts, n);
+  L->stamp = ++fc.clock;
+  fc.layouts.push_back(L);
+  fc.layouts_built++;
+  return L;
+}
+
+// The resolved segment table(s) of this call's pointers: a cached one when this layout saw the
+// same pointers (and mode and base) recently, else built on the host and uploaded.
+Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchItem* items, int n,
+                  const void* base) {
+  uint64_t h = fnv(fnv(1469598103934665603ull, (uint64_t)mode), (uint64_t)(uintptr_t)base);
+  for (int i = 0; i < n; i++) h = fnv(fnv(h, (uint64_t)(uintptr_t)items[i].in), (uint64_t)(uintptr_t)items[i].out);
+  for (Table* t : L.tables) {
+    if (t->hash != h || t->mode != mode || t->base != base) continue;
+    bool same = true;
+    for (int i = 0; i < n && same; i++) same = t->ins[i] == items[i].in && t->outs[i] == items[i].out;
+    if (same) {
+      t->stamp = ++fc.clock;
+      fc.table_hits++;
+      return t;
+    }
+  }
+  Table* t = nullptr;
+  if (L.tables.size() >= kMaxTables) {  // reuse the least recently used table's device buffer (stream order
+    auto lru = std::min_element(L.tables.begin(), L.tables.end(),   // keeps its earlier readers first)
+                                [](const Table* a, const Table* b) { return a->stamp < b->stamp; });
+    if ((*lru)->mode == mode) {
+      t = *lru;
+    } else {
+      free_table(st, *lru);
+      L.tables.erase(lru);
+    }
+  }
+  const int nseg = (int)L.seg_tensor.size();
+  const int ntab = mode == kSlot ? 2 : 1;
+  const size_t per = 2 * (size_t)L.ntiles + nseg;  // one table: [2 records per tile | segment records]
+  if (!t) {
+    t = new Table();
+    if (hipMallocAsync((void**)&t->dev, ntab * per * sizeof(CopySeg), st.fuse_stream) != hipSuccess) {
+      delete t;
+      fail(TIPS_ERR_HIP, "fusion: hipMallocAsync of a segment table failed");
+      return nullptr;
+    }
+    L.tables.push_back(t);
+  }
+  t->hash = h;
+  t->mode = mode;
+  t->base = base;
+  t->ins.resize(n);
+  t->outs.resize(n);
+  for (int i = 0; i < n; i++) {
+    t->ins[i] = items[i].in;
+    t->outs[i] = items[i].out;
+  }
+  const int64_t es = tips::dtype_size(L.dtype);
+  std::vector<CopySeg> rec(ntab * per);
+  for (int k = 0; k < nseg; k++) {
+    const int i = L.seg_tensor[k];
+    const int64_t b = L.off[i], e = b + L.counts[i] * es;
+    const int64_t in = (int64_t)(uintptr_t)items[i].in - b, out = (int64_t)(uintptr_t)items[i].out - b;
+    CopySeg* r = rec.data() + 2 * L.ntiles + k;
+    if (mode == kSlot) {
+      const int bk = L.bucket[i];
+      // bucket bk lives in slot bk % 2: virtual byte v of it at slot + (v - bucket offset)
+      const int64_t slot = bk < 0 ? 0 : (int64_t)(uintptr_t)base + (int64_t)(bk % 2) * L.threshold - L.buckets[bk].off;
+      r[0] = CopySeg{in, slot, b, e};    // pack
+      r[per] = CopySeg{slot, out, b, e};  // unpack
+    } else if (mode == kCopy) {
+      r[0] = CopySeg{in, out, b, e};
+    } else {  // kFlat: straight into the flat output
+      r[0] = CopySeg{in, (int64_t)(uintptr_t)base, b, e};
+    }
+  }
+  // tile records (two per tile): the segment itself when the tile meets one, both when it meets
+  // two (a tensor's end and the next one's start), else where its segments start
+  for (int tb = 0; tb < ntab; tb++) {
+    CopySeg* T = rec.data() + tb * per;
+    const CopySeg* S = T + 2 * L.ntiles;
+    for (int j = 0; j < L.ntiles; j++) {
+      const int first = L.tiles[2 * j], cnt = L.tiles[2 * j + 1];
+      T[2 * j] = cnt <= 2 ? S[first] : CopySeg{first, cnt, 0, -1};
+      T[2 * j + 1] = cnt == 2 ? S[first + 1] : CopySeg{0, 0, 0, 0};
+    }
+  }
+  t->stamp = ++fc.clock;
+  fc.tables_built++;
+  if (upload(st, fc, t->dev, rec.data(), rec.size() * sizeof(CopySeg)) != 0) {
+    t->hash = 0;  // (a failed upload must never be matched)
+    t->ins.clear();
+    return nullptr;
+  }
+  return t;
+}
+
+// The fusion slots: two buckets of `threshold` bytes (padding between packed tensors is reduced
+// too, never unpacked). A new threshold drops every cached table (they hold slot addresses),
+// after the fusion streams have finished with them.
 int ensure_slots(State& st, FusionCache& fc, int64_t threshold) {
   if (threshold == st.fusion_threshold && st.fusion.p) return 0;
   HIP_TRY(hipStreamSynchronize(st.fuse_stream));
   HIP_TRY(hipStreamSynchronize(st.bucket_stream));
-  for (Entry* e : fc.entries) free_entry(st, e);
-  fc.entries.clear();
+  for (Layout* L : fc.layouts) {
+    for (Table* t : L->tables) free_table(st, t);
+    L->tables.clear();
+  }
   HIP_TRY(hipStreamSynchronize(st.fuse_stream));
   st.fusion.release();
   TRY(st.fusion.ensure((size_t)(2 * threshold), /*zero=*/true));
   st.fusion_threshold = threshold;
+  return 0;
+}
+
+FusionCache& cache(State& st) {
+  if (!st.fusion_cache) st.fusion_cache = new FusionCache();
+  return *st.fusion_cache;
+}
+
+int copy_tiles(const Layout& L, const Table& t, int table, int tile0, int ntiles, hipStream_t s) {
+  const CopySeg* base = t.dev + (size_t)table * (2 * (size_t)L.ntiles + L.seg_tensor.size());
+  HIP_TRY(tips::launch_copy_segs(base, base + 2 * L.ntiles, tile0, ntiles, L.tile, copy_store_policy(), s));
   return 0;
 }
 
@@ -217,7 +370,7 @@ int64_t fusion_threshold_bytes() {
 void fusion_release(State& st) {
   FusionCache* fc = st.fusion_cache;
   if (!fc) return;
-  for (Entry* e : fc->entries) free_entry(st, e);
+  for (Layout* L : fc->layouts) free_layout(st, L);
   if (st.fuse_stream) (void)hipStreamSynchronize(st.fuse_stream);
   for (auto& u : fc->up) {
     if (u.done) (void)hipEventSynchronize(u.done), (void)hipEventDestroy(u.done);
@@ -227,105 +380,137 @@ void fusion_release(State& st) {
   st.fusion_cache = nullptr;
 }
 
+int fusion_stats(State& st, int64_t* v) {
+  FusionCache& fc = cache(st);
+  v[0] = fc.layouts_built;
+  v[1] = fc.layout_hits;
+  v[2] = fc.tables_built;
+  v[3] = fc.table_hits;
+  return 0;
+}
+
+// The layout's byte offsets, for callers that allocate the flat output (tips_fused_layout).
+int64_t fused_layout(const int64_t* counts, int n, int dtype, int64_t* offsets) {
+  Layout L;
+  L.dtype = dtype;
+  L.threshold = fusion_threshold_bytes();
+  L.tile = copy_tile_bytes();
+  L.balance = env_i64("TIPS_FUSION_BALANCE", 1) != 0;
+  build_layout(&L, counts, n);
+  if (offsets)
+    for (int i = 0; i < n; i++) offsets[i] = L.off[i] < 0 ? 0 : L.off[i];
+  return L.flat_bytes;
+}
+
 int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStream_t user) {
   if (n <= 0) return 0;
-  if (!st.fusion_cache) st.fusion_cache = new FusionCache();
-  FusionCache& fc = *st.fusion_cache;
-  const int64_t threshold = fusion_threshold_bytes(), tile = copy_tile_bytes();
-  const int64_t es = tips::dtype_size(dtype);
+  FusionCache& fc = cache(st);
+  const int64_t threshold = fusion_threshold_bytes();
   TRY(ensure_slots(st, fc, threshold));
-  // One rank: the allreduce of anything is the identity (as allreduce_device's), so a tensor
-  // reduced in place needs no work and one out of place a copy - no bucket. TIPS_FUSION_MEASURE_PACK=1
+  // One rank: the allreduce of anything is the identity (as allreduce_device's), so a list reduced
+  // in place needs no work and one out of place one copy launch - no bucket. TIPS_FUSION_MEASURE_PACK=1
   // keeps the buckets anyway, to measure on one GPU what packing costs a step at N > 1.
   const bool identity = st.size == 1 && !env_i64("TIPS_FUSION_MEASURE_PACK", 0);
-  const uint64_t key = key_of(items, n, dtype, tile) ^ (identity ? 0x9e3779b97f4a7c15ull : 0);
-  Entry* e = nullptr;
-  for (Entry* c : fc.entries)
-    if (c->key == key && c->identity == identity && same_list(*c, items, n, dtype, tile)) {
-      e = c;
-      break;
-    }
-  if (e && identity && e->ntiles == 0) {  // every tensor in place: nothing to do
-    e->stamp = ++fc.clock;
-    return 0;
-  }
+  bool in_place = true;
+  for (int i = 0; i < n && in_place; i++) in_place = items[i].in == items[i].out || items[i].count == 0;
+  if (identity && in_place) return 0;
+  std::vector<int64_t> counts((size_t)n);
+  for (int i = 0; i < n; i++) counts[i] = items[i].count;
   TRY(join(st.fuse_stream, user, st.ev_start));  // inputs ready (the bucket stream waits for it too)
   if (st.size > 1) HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
-  if (!e) {
-    if (fc.entries.size() >= kMaxEntries) {  // evict the least recently used list
-      auto lru = std::min_element(fc.entries.begin(), fc.entries.end(),
-                                  [](const Entry* a, const Entry* b) { return a->stamp < b->stamp; });
-      free_entry(st, *lru);
-      fc.entries.erase(lru);
-    }
-    e = new Entry();
-    e->key = key;
-    e->identity = identity;
-    e->dtype = dtype;
-    e->tile = tile;
-    for (int i = 0; i < n; i++) {
-      e->ins.push_back(items[i].in);
-      e->outs.push_back(items[i].out);
-      e->counts.push_back(items[i].count);
-    }
-    const int rc = build_entry(st, fc, e, items, n, threshold);
-    if (rc) {
-      free_entry(st, e);
-      return rc;
-    }
-    fc.entries.push_back(e);
+  Layout* L = find_layout(st, fc, counts.data(), n, dtype, threshold, copy_tile_bytes(),
+                          env_i64("TIPS_FUSION_BALANCE", 1) != 0);
+  if (!L) return TIPS_ERR_HIP;
+  if (L->seg_tensor.empty()) return join(user, st.fuse_stream, st.ev_done);
+  const int64_t es = tips::dtype_size(dtype);
+  if (identity) {  // one rank, out of place: every tensor copied in -> out, one launch over the whole space
+    Table* t = find_table(st, fc, *L, kCopy, items, n, nullptr);
+    if (!t) return TIPS_ERR_HIP;
+    TRY(copy_tiles(*L, *t, 0, 0, L->ntiles, st.fuse_stream));
+    return join(user, st.fuse_stream, st.ev_done);
   }
-  e->stamp = ++fc.clock;
-
-  const int B = (int)e->buckets.size();
-  auto pack = [&](int b) -> int {
-    HIP_TRY(tips::launch_pack_tiles(e->dev + e->buckets[b].pack0, (int)e->buckets[b].npack, e->tile, st.fuse_stream));
-    return 0;
-  };
-  auto unpack = [&](int b) -> int {
-    HIP_TRY(tips::launch_pack_tiles(e->dev + e->buckets[b].unpack0, (int)e->buckets[b].npack, e->tile, st.fuse_stream));
-    return 0;
-  };
-  if (identity) {  // one rank: the out-of-place tensors' copies, one launch
-    if (e->ntiles) HIP_TRY(tips::launch_pack_tiles(e->dev, (int)e->ntiles, e->tile, st.fuse_stream));
-    TRY(join(user, st.fuse_stream, st.ev_done));
-    return 0;
-  }
+  const int B = (int)L->buckets.size();
+  Table* t = B ? find_table(st, fc, *L, kSlot, items, n, st.fusion.p) : nullptr;
+  if (B && !t) return TIPS_ERR_HIP;
+  auto pack = [&](int b) { return copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, st.fuse_stream); };
+  auto unpack = [&](int b) { return copy_tiles(*L, *t, 1, L->buckets[b].tile0, L->buckets[b].ntiles, st.fuse_stream); };
+  auto slot = [&](int b) { return (char*)st.fusion.p + (int64_t)(b % 2) * threshold; };
   if (st.size == 1) {  // TIPS_FUSION_MEASURE_PACK: pack, (identity), unpack, in stream order
     for (int b = 0; b < B; b++) {
       TRY(pack(b));
       TRY(unpack(b));
     }
-    for (const BatchItem& d : e->direct) TRY(allreduce_device(st, d.in, d.out, d.count, dtype, st.fuse_stream));
-    TRY(join(user, st.fuse_stream, st.ev_done));
-    return 0;
-  } else {
-    // bucket stream: the direct tensors first (nothing to pack: their exchange starts at once and
-    //                overlaps pack(0)), then allreduce(b) after pack(b)
-    // fuse stream:   pack(0) pack(1) | unpack(0) pack(2) | unpack(1) pack(3) | ... unpack(B-1);
-    //                unpack(b) after allreduce(b); pack(b+2) reuses slot b % 2 after unpack(b)
-    for (const BatchItem& d : e->direct) TRY(allreduce_device(st, d.in, d.out, d.count, dtype, st.bucket_stream));
-    TRY(st.fuse_ev.ensure(2 * (size_t)B));
-    hipEvent_t* packed = st.fuse_ev.ev.data();
-    hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
-    for (int b = 0; b < std::min(B, 2); b++) {
-      TRY(pack(b));
-      HIP_TRY(hipEventRecord(packed[b], st.fuse_stream));
-    }
-    for (int b = 0; b < B; b++) {
-      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[b], 0));
-      TRY(allreduce_device(st, e->buckets[b].buf, e->buckets[b].buf, e->buckets[b].bytes / es, dtype, st.bucket_stream));
-      HIP_TRY(hipEventRecord(reduced[b], st.bucket_stream));
-      HIP_TRY(hipStreamWaitEvent(st.fuse_stream, reduced[b], 0));
-      TRY(unpack(b));
-      if (b + 2 < B) {
-        TRY(pack(b + 2));
-        HIP_TRY(hipEventRecord(packed[b + 2], st.fuse_stream));
-      }
+    for (int i : L->direct)
+      TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, st.fuse_stream));
+    return join(user, st.fuse_stream, st.ev_done);
+  }
+  // bucket stream: the direct tensors first (nothing to pack: their exchange starts at once and
+  //                overlaps pack(0)), then allreduce(b) after pack(b)
+  // fuse stream:   pack(0) pack(1) | unpack(0) pack(2) | unpack(1) pack(3) | ... unpack(B-1);
+  //                unpack(b) after allreduce(b); pack(b+2) reuses slot b % 2 after unpack(b)
+  for (int i : L->direct) TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, st.bucket_stream));
+  TRY(st.fuse_ev.ensure(2 * (size_t)B));
+  hipEvent_t* packed = st.fuse_ev.ev.data();
+  hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
+  for (int b = 0; b < std::min(B, 2); b++) {
+    TRY(pack(b));
+    HIP_TRY(hipEventRecord(packed[b], st.fuse_stream));
+  }
+  for (int b = 0; b < B; b++) {
+    HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[b], 0));
+    TRY(allreduce_device(st, slot(b), slot(b), L->buckets[b].bytes / es, dtype, st.bucket_stream));
+    HIP_TRY(hipEventRecord(reduced[b], st.bucket_stream));
+    HIP_TRY(hipStreamWaitEvent(st.fuse_stream, reduced[b], 0));
+    TRY(unpack(b));
+    if (b + 2 < B) {
+      TRY(pack(b + 2));
+      HIP_TRY(hipEventRecord(packed[b + 2], st.fuse_stream));
     }
   }
   TRY(join(user, st.fuse_stream, st.ev_done));
   TRY(join(user, st.bucket_stream, st.ev_comp_done));
+  return 0;
+}
+
+// flat = SUM over ranks of the inputs, tensor i at its layout offset: pack(b) straight into the
+// flat buffer's bucket b, allreduce it there in place. Every bucket has its own region, so all
+// packs go ahead on fuse_stream and allreduce(b) only waits for pack(b).
+int fused_allreduce_flat(State& st, const BatchItem* items, int n, int dtype, void* flat, hipStream_t user) {
+  if (n <= 0) return 0;
+  FusionCache& fc = cache(st);
+  const int64_t threshold = fusion_threshold_bytes();
+  std::vector<int64_t> counts((size_t)n);
+  for (int i = 0; i < n; i++) counts[i] = items[i].count;
+  TRY(join(st.fuse_stream, user, st.ev_start));
+  if (st.size > 1) HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
+  Layout* L = find_layout(st, fc, counts.data(), n, dtype, threshold, copy_tile_bytes(),
+                          env_i64("TIPS_FUSION_BALANCE", 1) != 0);
+  if (!L) return TIPS_ERR_HIP;
+  if (L->seg_tensor.empty()) return join(user, st.fuse_stream, st.ev_done);
+  Table* t = find_table(st, fc, *L, kFlat, items, n, flat);
+  if (!t) return TIPS_ERR_HIP;
+  const int64_t es = tips::dtype_size(dtype);
+  const bool measure = st.size == 1 && env_i64("TIPS_FUSION_MEASURE_PACK", 0);
+  if (st.size == 1 && !measure) {  // one rank: the identity - every tensor copied into place, one launch
+    TRY(copy_tiles(*L, *t, 0, 0, L->ntiles, st.fuse_stream));
+    return join(user, st.fuse_stream, st.ev_done);
+  }
+  const int B = (int)L->buckets.size();
+  hipStream_t red = st.size > 1 ? st.bucket_stream : st.fuse_stream;
+  for (int i : L->direct)
+    TRY(allreduce_device(st, items[i].in, (char*)flat + L->off[i], items[i].count, dtype, red));
+  TRY(st.fuse_ev.ensure((size_t)B));
+  for (int b = 0; b < B; b++) {
+    TRY(copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, st.fuse_stream));
+    if (st.size > 1) {
+      HIP_TRY(hipEventRecord(st.fuse_ev.ev[b], st.fuse_stream));
+      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.fuse_ev.ev[b], 0));
+      char* p = (char*)flat + L->buckets[b].off;
+      TRY(allreduce_device(st, p, p, L->buckets[b].bytes / es, dtype, st.bucket_stream));
+    }
+  }
+  TRY(join(user, st.fuse_stream, st.ev_done));
+  if (st.size > 1) TRY(join(user, st.bucket_stream, st.ev_comp_done));
   return 0;
 }
 
@@ -336,19 +521,28 @@ using namespace tips::rt;
 
 namespace {
 
-int fused_entry(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype, void* stream) {
+int check_list(const void* const* ins, const int64_t* counts, int n, int dtype, std::vector<BatchItem>* items,
+               void* const* outs) {
   TRY(check_dtype(dtype));
-  if (n < 0 || (n > 0 && (!ins || !outs || !counts))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
+  if (n < 0 || (n > 0 && (!ins || !counts))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
+  items->resize((size_t)n);
+  for (int i = 0; i < n; i++) {
+    void* o = outs ? outs[i] : const_cast<void*>(ins[i]);
+    if (counts[i] < 0 || (counts[i] > 0 && (!ins[i] || !o))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor %d", i);
+    (*items)[i] = BatchItem{ins[i], o, counts[i]};
+  }
+  return 0;
+}
+
+int fused_entry(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype, void* stream) {
+  if (!outs && n > 0) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
+  std::vector<BatchItem> items;
+  TRY(check_list(ins, counts, n, dtype, &items, outs));
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
   if (n == 0) return 0;
   TRY(set_device(st));
-  std::vector<BatchItem> items((size_t)n);
-  for (int i = 0; i < n; i++) {
-    if (counts[i] < 0 || (counts[i] > 0 && (!ins[i] || !outs[i]))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor %d", i);
-    items[i] = BatchItem{ins[i], outs[i], counts[i]};
-  }
   return fused_allreduce(st, items.data(), n, dtype, (hipStream_t)stream);
 }
 
@@ -363,6 +557,70 @@ int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dt
 int tips_fused_allreduce_oop(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype,
                              void* stream) {
   return fused_entry(ins, outs, counts, n, dtype, stream);
+}
+
+int64_t tips_fused_layout(const int64_t* counts, int n, int dtype, int64_t* offsets) {
+  TRY(check_dtype(dtype));
+  if (n < 0 || (n > 0 && !counts)) return fail(TIPS_ERR_INVALID_ARG, "bad count list");
+  for (int i = 0; i < n; i++)
+    if (counts[i] < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count %d", i);
+  return fused_layout(counts, n, dtype, offsets);
+}
+
+int tips_fused_allreduce_flat(const void* const* ins, const int64_t* counts, int n, int dtype, void* flat,
+                              void* stream) {
+  std::vector<BatchItem> items;
+  TRY(check_list(ins, counts, n, dtype, &items, nullptr));
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+  if (n == 0) return 0;
+  if (!flat) return fail(TIPS_ERR_INVALID_ARG, "null flat output");
+  TRY(set_device(st));
+  if (!is_device_ptr(flat)) return fail(TIPS_ERR_INVALID_ARG, "tips_fused_allreduce_flat needs device memory");
+  for (auto& it : items) it.out = it.count ? flat : nullptr;
+  return fused_allreduce_flat(st, items.data(), n, dtype, flat, (hipStream_t)stream);
+}
+
+int64_t tips_fused_pack_bucket(const void* const* ins, const int64_t* counts, int n, int dtype, int bucket, void* dst,
+                               void* stream) {
+  std::vector<BatchItem> items;
+  TRY(check_list(ins, counts, n, dtype, &items, nullptr));
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+  if (n == 0) return 0;
+  TRY(set_device(st));
+  FusionCache& fc = cache(st);
+  Layout* L = find_layout(st, fc, counts, n, dtype, fusion_threshold_bytes(), copy_tile_bytes(),
+                          env_i64("TIPS_FUSION_BALANCE", 1) != 0);
+  if (!L) return TIPS_ERR_HIP;
+  const int B = (int)L->buckets.size();
+  if (bucket < 0) return B;
+  if (bucket >= B || !dst) return fail(TIPS_ERR_INVALID_ARG, "bucket %d of %d", bucket, B);
+  const Bucket& bk = L->buckets[bucket];
+  for (auto& it : items) it.out = (char*)dst - bk.off;
+  const int64_t built = fc.tables_built;
+  Table* t = find_table(st, fc, *L, kFlat, items.data(), n, (char*)dst - bk.off);
+  if (!t) return TIPS_ERR_HIP;
+  if (fc.tables_built != built) TRY(join((hipStream_t)stream, st.fuse_stream, st.ev_done));  // the upload first
+  TRY(copy_tiles(*L, *t, 0, bk.tile0, bk.ntiles, (hipStream_t)stream));
+  int64_t payload = 0;
+  for (int i = 0; i < n; i++)
+    if (L->bucket[i] == bucket) payload += counts[i] * tips::dtype_size(dtype);
+  return payload;
+}
+
+int tips_fusion_stats(int64_t* layouts_built, int64_t* layout_hits, int64_t* tables_built, int64_t* table_hits) {
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  int64_t v[4];
+  fusion_stats(st, v);
+  if (layouts_built) *layouts_built = v[0];
+  if (layout_hits) *layout_hits = v[1];
+  if (tables_built) *tables_built = v[2];
+  if (table_hits) *table_hits = v[3];
+  return 0;
 }
 
 }  // extern "C"

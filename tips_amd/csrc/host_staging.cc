@@ -105,12 +105,196 @@ int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, in
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Many host tensors, fused (round 3). The reference's op is a CPU op (ops.cc:118): a model's
+// gradients arrive as many host tensors. One staged allreduce per tensor pays the host link's
+// latency per tensor (config 5: 214 tensors, 8.6 GiB/s); here the list is packed by host threads
+// into page-locked pieces of a flat byte stream (the layout a function of the counts alone, 64-B
+// aligned offsets), and each piece runs H2D -> allreduce in place in HBM -> D2H on three streams
+// while the threads pack the next piece and unpack the previous one.
+
+HostPool::HostPool(int nthreads) {
+  for (int i = 1; i < nthreads; i++) th_.emplace_back([this] { worker(); });
+}
+
+HostPool::~HostPool() {
+  {
+    std::lock_guard<std::mutex> l(m_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : th_) t.join();
+}
+
+void HostPool::grab() {  // take jobs until none is left (caller holds no lock)
+  for (int j; (j = next_.fetch_add(1)) < njobs_;) {
+    (*fn_)(j);
+    if (pending_.fetch_sub(1) == 1) {
+      std::lock_guard<std::mutex> l(m_);
+      done_cv_.notify_all();
+    }
+  }
+}
+
+void HostPool::worker() {
+  uint64_t seen = 0;
+  while (true) {
+    {
+      std::unique_lock<std::mutex> l(m_);
+      cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+    }
+    grab();
+  }
+}
+
+void HostPool::run(int njobs, const std::function<void(int)>& fn) {
+  if (njobs <= 0) return;
+  {
+    std::lock_guard<std::mutex> l(m_);
+    fn_ = &fn;
+    njobs_ = njobs;
+    next_.store(0);
+    pending_.store(njobs);
+    gen_++;
+  }
+  if (njobs > 1) cv_.notify_all();
+  grab();
+  std::unique_lock<std::mutex> l(m_);
+  done_cv_.wait(l, [&] { return pending_.load() == 0; });
+}
+
+namespace {
+
+struct HostSeg {
+  int64_t off, bytes;  // in the flat byte stream
+  const char* in;
+  char* out;
+};
+
+// Copy flat bytes [a, b) between the stream's segments and `buf` (which holds stream bytes from
+// base on): pack = tensors -> buf, else buf -> tensors. The padding between segments is skipped.
+void copy_range(const std::vector<HostSeg>& segs, int64_t a, int64_t b, char* buf, int64_t base, bool pack) {
+  auto it = std::upper_bound(segs.begin(), segs.end(), a,
+                             [](int64_t v, const HostSeg& s) { return v < s.off + s.bytes; });  // first with end > a
+  for (; it != segs.end() && it->off < b; ++it) {
+    const int64_t s = std::max(a, it->off), e = std::min(b, it->off + it->bytes);
+    if (e <= s) continue;
+    if (pack) memcpy(buf + (s - base), it->in + (s - it->off), (size_t)(e - s));
+    else memcpy(it->out + (s - it->off), buf + (s - base), (size_t)(e - s));
+  }
+}
+
+}  // namespace
+
+int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype) {
+  const int64_t es = tips::dtype_size(dtype);
+  std::vector<HostSeg> segs;
+  segs.reserve((size_t)n);
+  int64_t total = 0;
+  for (int i = 0; i < n; i++) {
+    const int64_t bytes = items[i].count * es;
+    if (bytes <= 0) continue;
+    total = round_up(total, 64);
+    segs.push_back(HostSeg{total, bytes, (const char*)items[i].in, (char*)items[i].out});
+    total += bytes;
+  }
+  if (segs.empty()) return 0;
+  total = round_up(total, kAlignBytes);  // (a whole number of elements, 256-B aligned pieces)
+  const int64_t piece = std::min<int64_t>(
+      total, round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_FUSED_PIECE_BYTES", 8 << 20)), kAlignBytes));
+  const int np = (int)((total + piece - 1) / piece);
+  const int R = 3;  // page-locked slots per direction; piece i uses slot i % R
+  const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(64, env_i64("TIPS_HOST_THREADS", 8)));
+  if (!st.host_pool || st.host_pool->size() != nthreads) {
+    delete st.host_pool;
+    st.host_pool = new HostPool(nthreads);
+  }
+  if (st.hpin_bytes < (size_t)(R * piece)) {
+    for (void*& p : st.hpin)
+      if (p) (void)hipHostFree(p), p = nullptr;
+    st.hpin_bytes = 0;
+    for (void*& p : st.hpin) HIP_TRY(hipHostMalloc(&p, (size_t)(R * piece), hipHostMallocDefault));
+    st.hpin_bytes = (size_t)(R * piece);
+  }
+  TRY(st.host_in.ensure((size_t)total));
+  TRY(st.pipe_ev.ensure(3 * (size_t)np));
+  char* dev = (char*)st.host_in.p;
+  char* pin_in = (char*)st.hpin[0];
+  char* pin_out = (char*)st.hpin[1];
+  hipEvent_t* ev = st.pipe_ev.ev.data();  // [3i] H2D done, [3i+1] reduced, [3i+2] D2H done
+  const int parts = nthreads;
+  auto host_copy = [&](int i, bool pack) {
+    const int64_t p0 = (int64_t)i * piece, p1 = std::min(total, p0 + piece);
+    char* buf = (pack ? pin_in : pin_out) + (int64_t)(i % R) * piece;
+    const int64_t per = round_up((p1 - p0 + parts - 1) / parts, 64);
+    st.host_pool->run(parts, [&](int j) {
+      const int64_t a = p0 + j * per, b = std::min(p1, a + per);
+      if (a < b) copy_range(segs, a, b, buf, p0, pack);
+    });
+  };
+  const int lag = 1;  // piece i - lag is unpacked while piece i is on the link
+  for (int i = 0; i < np; i++) {
+    const int64_t off = (int64_t)i * piece, len = std::min(piece, total - off);
+    if (i >= R) HIP_TRY(hipEventSynchronize(ev[3 * (i - R)]));  // slot i % R: its last H2D has read it
+    host_copy(i, true);
+    HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice,
+                           st.h2d_stream));
+    HIP_TRY(hipEventRecord(ev[3 * i], st.h2d_stream));
+    HIP_TRY(hipStreamWaitEvent(st.io_stream, ev[3 * i], 0));
+    TRY(allreduce_device(st, dev + off, dev + off, len / es, dtype, st.io_stream));
+    HIP_TRY(hipEventRecord(ev[3 * i + 1], st.io_stream));
+    HIP_TRY(hipStreamWaitEvent(st.d2h_stream, ev[3 * i + 1], 0));
+    // (slot i % R of pin_out was unpacked at iteration i - R + lag < i)
+    HIP_TRY(hipMemcpyAsync(pin_out + (int64_t)(i % R) * piece, dev + off, (size_t)len, hipMemcpyDeviceToHost,
+                           st.d2h_stream));
+    HIP_TRY(hipEventRecord(ev[3 * i + 2], st.d2h_stream));
+    if (i >= lag) {
+      HIP_TRY(hipEventSynchronize(ev[3 * (i - lag) + 2]));
+      host_copy(i - lag, false);
+    }
+  }
+  for (int j = std::max(0, np - lag); j < np; j++) {
+    HIP_TRY(hipEventSynchronize(ev[3 * j + 2]));
+    host_copy(j, false);
+  }
+  return 0;
+}
+
+void host_release(State& st) {
+  delete st.host_pool;
+  st.host_pool = nullptr;
+  for (void*& p : st.hpin)
+    if (p) (void)hipHostFree(p), p = nullptr;
+  st.hpin_bytes = 0;
+}
+
 }  // namespace rt
 }  // namespace tips
 
 using namespace tips::rt;
 
 extern "C" {
+
+int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype) {
+  TRY(check_dtype(dtype));
+  if (n < 0 || (n > 0 && (!ins || !outs || !counts))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
+  std::vector<BatchItem> items((size_t)n);
+  for (int i = 0; i < n; i++) {
+    if (counts[i] < 0 || (counts[i] > 0 && (!ins[i] || !outs[i]))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor %d", i);
+    items[i] = BatchItem{ins[i], outs[i], counts[i]};
+  }
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+  if (n == 0) return 0;
+  TRY(set_device(st));
+  for (int i = 0; i < n; i++)
+    if (items[i].count > 0 && (is_device_ptr(items[i].in) || is_device_ptr(items[i].out)))
+      return fail(TIPS_ERR_INVALID_ARG, "tips_fused_allreduce_host: tensor %d is in device memory", i);
+  return fused_allreduce_host(st, items.data(), n, dtype);
+}
 
 int tips_host_register(void* ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return fail(TIPS_ERR_INVALID_ARG, "bad host range");

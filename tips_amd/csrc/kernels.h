@@ -34,6 +34,21 @@ hipError_t launch_pack_tiles(const CopyTile* tiles_dev, int ntiles, int64_t max_
 hipError_t launch_copy_tiles_variant(const CopyTile* tiles_dev, int ntiles, int variant, int64_t max_tile_bytes,
                                      hipStream_t s);
 
+// Segment copy over a virtual byte space (fusion pack / unpack / identity copy, fusion.cc): tensor
+// k occupies virtual bytes [begin, end) and byte v of it lives at src + v on the source side and
+// dst + v on the destination side. Tiles of tile_bytes (4, 8 or 16 KiB) are cut from the virtual
+// space; tiles[2t], tiles[2t + 1] (two per tile of the whole space) are the records of the one or
+// two segments tile t meets (the second {0,0,0,0} when one), or {first segment, number of segments,
+// -, -1} when it meets more (then read from segs[]).
+// Segments begin 256-B aligned and in order. One launch copies tiles [tile0, tile0 + ntiles).
+// pol = store cache policy: 0 plain, 1 nt, 2 sc1.
+struct CopySeg {
+  int64_t src, dst;  // addresses of virtual byte 0 (as integers: src + v = the byte's address)
+  int64_t begin, end;
+};
+hipError_t launch_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int64_t tile_bytes,
+                            int pol, hipStream_t s);
+
 // Peer transfers of the xGMI peer schedule (peer.cc): up to kMaxXferSegs byte
 // segments {src, dst, bytes} copied by one launch, segments interleaved over
 // the workgroups so every xGMI link carries traffic at once. src/dst may be

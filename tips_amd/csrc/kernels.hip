@@ -552,6 +552,157 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __
 }
 
 // ---------------------------------------------------------------------------
+// Segment copy (fusion pack / unpack / identity copy since round 3; fusion.cc)
+//
+// Tiles are cut from a virtual byte space (a fusion bucket, or the flat layout of a whole tensor
+// list), not per tensor: every workgroup moves T = 4 KiB x U bytes of the space, whatever tensors
+// it meets; only the padding between tensors (< 256 B each) is skipped. The round-2 kernel cut
+// tiles per tensor, so ~75 % of config 4's 1000 tensors ended in a partly empty workgroup, and
+// moved a tile's last < 16 bytes one byte per lane. Tensors begin 256-B aligned in the space, so a
+// tile meets at most T / 256 + 1 segments: the workgroup stages them in LDS (one load per lane,
+// one barrier), each lane finds the segment of each of its 16-B vectors by binary search, issues
+// all its nt loads, then its stores. A vector at a tensor's ragged end, or of a tensor that is not
+// 16-B aligned, moves as dwords (shorts for 2-B element types) - one lane per tensor end.
+// (The addresses are built from integers, so they are cast to the global address space: a generic
+// pointer makes the compiler emit flat_load / flat_store, which also count against lgkmcnt.)
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) unsigned g_u32;
+typedef __attribute__((address_space(1))) unsigned short g_u16;
+typedef __attribute__((address_space(1))) char g_u8;
+
+template <int POL>
+__device__ __forceinline__ void store16_pol(int64_t d, u32x4 x) {
+  if constexpr (POL == 0) {
+    *reinterpret_cast<g_u32x4*>(d) = x;
+  } else if constexpr (POL == 1) {
+    __builtin_nontemporal_store(x, reinterpret_cast<g_u32x4*>(d));
+  } else {  // sc1: the line leaves the XCD's L2 (a vector store; the asm ends with the store's 2 wait states)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(reinterpret_cast<g_u32x4*>(d)), "v"(x)
+                 : "memory");
+  }
+}
+
+// The < 16 bytes of a vector at a tensor's ragged end, or a whole vector of a tensor that is not
+// 16-B aligned: loaded as dwords (shorts when the tensor's offset or length is only 2-B aligned,
+// 16-bit types) - phase 1 issues the loads, phase 2 the stores, so a lane waits for memory once.
+struct Small {
+  unsigned w[4];
+  unsigned short h[8];
+};
+
+__device__ __forceinline__ void small_load(int64_t s, int64_t d, int len, Small& m) {
+  if (((s | d | (int64_t)len) & 3) == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (4 * k < len) m.w[k] = *reinterpret_cast<const g_u32*>(s + 4 * k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (2 * k < len) m.h[k] = *reinterpret_cast<const g_u16*>(s + 2 * k);
+  }
+}
+
+__device__ __forceinline__ void small_store(int64_t s, int64_t d, int len, const Small& m) {
+  if (((s | d | (int64_t)len) & 3) == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (4 * k < len) *reinterpret_cast<g_u32*>(d + 4 * k) = m.w[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (2 * k < len) *reinterpret_cast<g_u16*>(d + 2 * k) = m.h[k];
+  }
+}
+
+// tiles[2t], tiles[2t + 1]: the tile's segment and {0, 0, 0, 0}; or its two segments (the tensor
+// ending in it, the tensor starting in it); or {first segment, count, -, -1} and - when it meets
+// more than two (then staged from segs[] in LDS).
+template <int U, int POL>
+__global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __restrict__ tiles,
+                                                          const CopySeg* __restrict__ segs, int tile0, int ntiles) {
+  constexpr int64_t kTileBytes = (int64_t)kBlock * 16 * U;
+  constexpr int kMaxSeg = (int)(kTileBytes / 256) + 1;
+  __shared__ CopySeg L[kMaxSeg];
+  const int64_t tt = xcd_tile(blockIdx.x, gridDim.x);
+  if (tt >= ntiles) return;  // (whole workgroup: before any barrier)
+  const int t = tile0 + (int)tt;
+  // One (scalar) load of both records before the first data load. (A tile -> segment index
+  // followed by the segment's record puts two dependent loads there: 17.5 against 14.1 us per
+  // config-4 bucket, measured.)
+  // (field by field: a record selected as a whole per lane becomes a private-memory copy)
+  const int64_t* tr = reinterpret_cast<const int64_t*>(tiles + 2 * (int64_t)t);
+  const int64_t a_src = tr[0], a_dst = tr[1], a_beg = tr[2], a_end = tr[3];
+  const int64_t b_src = tr[4], b_dst = tr[5], b_beg = tr[6], b_end = tr[7];
+  const int tid = threadIdx.x;
+  const bool multi = a_end < 0, two = b_end > 0;
+  const int64_t tb = (int64_t)t * kTileBytes;
+  if (!multi && !two && a_beg <= tb && a_end >= tb + kTileBytes && ((a_src | a_dst) & 15) == 0) {
+    // the tile lies inside one 16-B aligned tensor (most tiles): both sides are wave-uniform
+    // contiguous ranges, moved as the round-2 kernel moved a whole tile - buffer loads nt, buffer
+    // stores with the policy's cache bits, each store behind its own load
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a_src + tb), (short)0, (int)kTileBytes,
+                                                                  0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(a_dst + tb), (short)0, (int)kTileBytes,
+                                                                  0x00020000);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, 2);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (u * kBlock + tid) * 16, 0, POL == 0 ? 0 : POL == 1 ? 2 : 16);
+    return;
+  }
+  int cnt = 1;
+  if (multi) {  // workgroup-uniform branch
+    const int s0 = (int)a_src;
+    cnt = min((int)a_dst, kMaxSeg);
+    if (cnt <= 0) return;  // (uniform: no segment meets this tile)
+    if (tid < cnt) L[tid] = segs[s0 + tid];
+    __syncthreads();
+  }
+  int64_t sp[U], dp[U];
+  int len[U];
+  bool full[U];
+  u32x4 x[U];
+  Small m[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int64_t v = tb + (int64_t)u * (kBlock * 16) + (int64_t)tid * 16;
+    int64_t g_src, g_dst, g_beg, g_end;
+    if (multi) {
+      int lo = 0, hi = cnt - 1;  // the last segment beginning at or before v
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (L[mid].begin <= v) lo = mid;
+        else hi = mid - 1;
+      }
+      g_src = L[lo].src;
+      g_dst = L[lo].dst;
+      g_beg = L[lo].begin;
+      g_end = L[lo].end;
+    } else {
+      const bool b = two && v >= b_beg;
+      g_src = b ? b_src : a_src;
+      g_dst = b ? b_dst : a_dst;
+      g_beg = b ? b_beg : a_beg;
+      g_end = b ? b_end : a_end;
+    }
+    const int64_t left = g_end - v;
+    len[u] = (v >= g_beg && left > 0) ? (int)(left < 16 ? left : 16) : 0;
+    sp[u] = g_src + v;
+    dp[u] = g_dst + v;
+    full[u] = len[u] == 16 && ((sp[u] | dp[u]) & 15) == 0;
+    if (full[u]) x[u] = __builtin_nontemporal_load(reinterpret_cast<const g_u32x4*>(sp[u]));
+    else if (len[u] > 0) small_load(sp[u], dp[u], len[u], m[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (full[u]) store16_pol<POL>(dp[u], x[u]);
+    else if (len[u] > 0) small_store(sp[u], dp[u], len[u], m[u]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Peer transfer (xGMI peer schedule, peer.cc)
 
 struct XferList {
@@ -974,6 +1125,33 @@ hipError_t launch_copy_tiles_variant(const CopyTile* tiles_dev, int ntiles, int 
 hipError_t launch_pack_tiles(const CopyTile* tiles_dev, int ntiles, int64_t max_tile_bytes, hipStream_t s) {
   if (max_tile_bytes > 16384) return launch_copy_tiles(tiles_dev, ntiles, s);
   return launch_copy_tiles_variant(tiles_dev, ntiles, 1, max_tile_bytes, s);
+}
+
+namespace {
+
+template <int U>
+hipError_t run_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int pol, hipStream_t s) {
+  const unsigned grid = (unsigned)std::max<int64_t>(8, ((int64_t)ntiles + 7) / 8 * 8);
+  switch (pol) {
+    case 0: hipLaunchKernelGGL((copy_segs_kernel<U, 0>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles); break;
+    case 1: hipLaunchKernelGGL((copy_segs_kernel<U, 1>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles); break;
+    case 2: hipLaunchKernelGGL((copy_segs_kernel<U, 2>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int64_t tile_bytes,
+                            int pol, hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  switch (tile_bytes) {
+    case 4096: return run_copy_segs<1>(tiles, segs, tile0, ntiles, pol, s);
+    case 8192: return run_copy_segs<2>(tiles, segs, tile0, ntiles, pol, s);
+    case 16384: return run_copy_segs<4>(tiles, segs, tile0, ntiles, pol, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_xfer(const XferSeg* segs, int nseg, hipStream_t s) {

@@ -8,8 +8,12 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -131,8 +135,30 @@ struct Choice {
 };
 
 struct PeerState;   // peer.cc
-struct FusionCache;  // fusion.cc: pack/unpack descriptor tables of recent tensor lists
+struct FusionCache;  // fusion.cc: layouts and resolved segment tables of recent tensor lists
 struct PlanGraphs;   // schedules.cc: instantiated HIP graphs of recently replayed plans
+
+// host_staging.cc: a fork-join pool of host threads for packing / unpacking host tensors
+// (run(n, fn) calls fn(0..n-1) on the pool and the calling thread, returns when all are done).
+class HostPool {
+ public:
+  explicit HostPool(int nthreads);
+  ~HostPool();
+  void run(int njobs, const std::function<void(int)>& fn);
+  int size() const { return (int)th_.size() + 1; }
+
+ private:
+  void worker();
+  void grab();
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int njobs_ = 0;
+  std::atomic<int> next_{0}, pending_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
 
 struct State {
   std::mutex mu;
@@ -150,6 +176,9 @@ struct State {
   DevBuf staging, host_in, host_out, fusion, small;
   void* bounce_in = nullptr;  // page-locked kBounceBytes each (hipHostMalloc), for small pageable host tensors
   void* bounce_out = nullptr;
+  HostPool* host_pool = nullptr;  // fused host tensors: pack / unpack threads
+  void* hpin[2] = {};             // fused host tensors: page-locked piece slots, in and out
+  size_t hpin_bytes = 0;
   int algo = TIPS_ALGO_AUTO;
   int sim_transport = 0;  // simulators: 0 = device copies, 1 = RCCL send/recv to self
   uint64_t peer_key = 0;      // names the node-local control block of the peer schedule (hash of the unique id)
@@ -212,6 +241,10 @@ int peer_broadcast(State& st, const char* in, char* out, int64_t bytes, int root
 int peer_allgatherv(State& st, const char* in, char* out, const int64_t* bytes, const int64_t* displ, hipStream_t stream);
 // host_staging.cc: host-resident allreduce over pipelined pieces, caller holds st.mu
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
+// host_staging.cc: many host tensors in one flat stream of page-locked pieces (pack by host threads,
+// H2D -> allreduce -> D2H per piece, unpack); returns when every out is written. Caller holds st.mu.
+int fused_allreduce_host(State& st, const struct BatchItem* items, int n, int dtype);
+void host_release(State& st);  // (shutdown: the pool and the page-locked pieces)
 // fusion.cc: allreduce n same-dtype device tensors, in[i] -> out[i] (in == out allowed), packed
 // into buckets of at most the fusion threshold: pack -> one allreduce per bucket -> unpack.
 // Stream-ordered after `stream` and before its later work; all device work runs on the fusion
@@ -222,6 +255,11 @@ struct BatchItem {
   int64_t count;
 };
 int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStream_t stream);
+// The same into one flat output laid out as the buckets (fused_layout's offsets): pack(b) straight
+// into the flat buffer, allreduce there in place; no slot, no unpack. Caller holds st.mu.
+int fused_allreduce_flat(State& st, const BatchItem* items, int n, int dtype, void* flat, hipStream_t stream);
+int64_t fused_layout(const int64_t* counts, int n, int dtype, int64_t* offsets);  // flat bytes; pure host
+int fusion_stats(State& st, int64_t* v);  // layouts built, layout hits, tables built, table hits
 int64_t fusion_threshold_bytes();
 void fusion_release(State& st);  // (shutdown)
 // control.cc: ConstructResponseMessage's rules over p request records (TIPS_REQUEST_WORDS each)

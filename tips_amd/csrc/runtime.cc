@@ -113,6 +113,8 @@ void tips_shutdown(void) {
     st.comm = nullptr;
   }
   fusion_release(st);
+  if (st.d2h_stream) (void)hipStreamSynchronize(st.d2h_stream);
+  host_release(st);
   st.staging.release();
   st.host_in.release();
   st.host_out.release();

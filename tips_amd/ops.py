@@ -179,6 +179,140 @@ def fused_allreduce(tensor_list, out_list=None):
     return outs
 
 
+class _FlatOutputs(object):
+    """Output sets of fused_allreduce_flat for one list signature (dtype, device, shapes): the
+    layout's byte offsets (tips_fused_layout: a function of the counts alone) and a few sets of
+    {one flat buffer, one view of it per tensor}. A set is handed out again once every tensor of
+    it has been released by the caller: no Python reference to any of its views, and no other
+    tensor sharing its storage (derived views included). Allocating the buffer and 1000 views per
+    call costs milliseconds of host time - more than the device work of the whole allreduce."""
+
+    MAX_SETS = 4
+
+    def __init__(self, shapes, numels, code, dtype, device):
+        import torch
+        self.numels = numels
+        import ctypes
+        cp, _keep = _lib.i64_array(numels)
+        offs = (ctypes.c_int64 * len(numels))()
+        self.total = _lib.check("tips_fused_layout", _lib.lib().tips_fused_layout(cp, len(numels), code, offs))
+        self.es = torch.empty((), dtype=dtype).element_size()
+        self.offs = [int(o) // self.es for o in offs]
+        self.shapes, self.dtype, self.device = shapes, dtype, device
+        self.sets = []
+
+    def _free(self, s):
+        flat, views, use0, rc0 = s
+        import sys
+        import torch
+        if torch._C._storage_Use_Count(flat.untyped_storage()._cdata) != use0:
+            return False
+        return max(map(sys.getrefcount, views), default=rc0) <= rc0
+
+    def take(self):
+        """(flat buffer, views) for this call: a released set, or a new one."""
+        import sys
+        import torch
+        for s in self.sets:
+            if self._free(s):
+                return s[0], s[1]
+        flat = torch.empty(max(1, self.total // self.es), dtype=self.dtype, device=self.device)
+        views = [flat[o:o + n].view(shp) for o, n, shp in zip(self.offs, self.numels, self.shapes)]
+        if len(self.sets) < self.MAX_SETS:
+            use0 = torch._C._storage_Use_Count(flat.untyped_storage()._cdata)
+            rc0 = max(map(sys.getrefcount, views), default=0)
+            self.sets.append((flat, views, use0, rc0))
+        return flat, views
+
+
+_FLAT_OUTPUTS = {}  # (dtype, device, shapes) -> _FlatOutputs (small LRU)
+
+
+def fused_allreduce_flat(tensor_list):
+    """Out-of-place SUM of a list of same-dtype device tensors (tips_fused_allreduce_flat): the
+    outputs are views of ONE flat buffer laid out as the fusion buckets - each bucket packed straight
+    into it and allreduced there in place, no slot and no unpack (2 x the bytes of HBM traffic). The
+    flat buffer and views are reused for a later call of the same list signature once the caller has
+    released every output (_FlatOutputs). Inputs unchanged."""
+    basics.init()
+    if not tensor_list:
+        return []
+    code = _check_fusable(tensor_list, "fused_allreduce_flat")
+    return _flat_call(tensor_list, code, [t.data_ptr() for t in tensor_list])
+
+
+def _flat_outputs(tensor_list, code):
+    """The _FlatOutputs of this list's signature (dtype, device, shapes)."""
+    t0 = tensor_list[0]
+    shapes = tuple(t.shape for t in tensor_list)
+    key = (t0.dtype, t0.device, shapes)
+    fo = _FLAT_OUTPUTS.get(key)
+    if fo is None:
+        if len(_FLAT_OUTPUTS) >= 16:
+            _FLAT_OUTPUTS.pop(next(iter(_FLAT_OUTPUTS)))
+        fo = _FLAT_OUTPUTS[key] = _FlatOutputs(shapes, [t.numel() for t in tensor_list], code, t0.dtype, t0.device)
+        fo.cp = _lib.i64_array(fo.numels)
+        fo.code = code
+        fo.last = (None, None)  # (pointer list, its ptr_array) of the previous call
+    return fo
+
+
+def _flat_run(fo, tensor_list, ptrs):
+    """tips_fused_allreduce_flat of `tensor_list` (whose data pointers are `ptrs`) into an output set
+    of `fo`; returns the outputs."""
+    if ptrs == fo.last[0]:
+        pp = fo.last[1]
+    else:
+        pp = _lib.ptr_array(ptrs)
+        fo.last = (ptrs, pp)
+    flat, views = fo.take()
+    t0 = tensor_list[0]
+    _lib.call("tips_fused_allreduce_flat", pp[0], fo.cp[0], len(ptrs), fo.code, flat.data_ptr(),
+              _torch_mod().cuda.current_stream(t0.device).cuda_stream)
+    return list(views)
+
+
+def _torch_mod():
+    import torch
+    return torch
+
+
+def _flat_call(tensor_list, code, ptrs):
+    return _flat_run(_flat_outputs(tensor_list, code), tensor_list, ptrs)
+
+
+def fused_allreduce_host(tensor_list, out_list=None):
+    """Out-of-place SUM of a list of same-dtype HOST tensors (numpy / CPU torch) through
+    tips_fused_allreduce_host: packed by the library's host threads into page-locked pieces,
+    each piece H2D -> allreduce -> D2H pipelined, unpacked into the outputs. Returns when done."""
+    basics.init()
+    if not tensor_list:
+        return []
+    code = tensors.dtype_code(tensor_list[0])
+    srcs = []
+    for t in tensor_list:
+        if tensors.is_device(t):
+            raise ValueError("fused_allreduce_host needs host tensors")
+        if tensors.dtype_code(t) != code:
+            raise TypeError("fused_allreduce_host needs one dtype per call")
+        srcs.append(tensors.contiguous(t))
+    outs = [tensors.empty_like(s) for s in srcs] if out_list is None else list(out_list)
+    pi, _k1 = _lib.ptr_array([tensors.data_ptr(s) for s in srcs])
+    po, _k2 = _lib.ptr_array([tensors.data_ptr(o) for o in outs])
+    cp, _k3 = _lib.i64_array([tensors.numel(s) for s in srcs])
+    _lib.call("tips_fused_allreduce_host", pi, po, cp, len(srcs), code)
+    return outs
+
+
+def fusion_stats():
+    """{layouts_built, layout_hits, tables_built, table_hits} of this process's fusion caches
+    (tips_fusion_stats): layouts depend on the counts only, tables on the pointers."""
+    import ctypes
+    v = [ctypes.c_int64() for _ in range(4)]
+    _lib.call("tips_fusion_stats", *[ctypes.byref(x) for x in v])
+    return dict(zip(("layouts_built", "layout_hits", "tables_built", "table_hits"), [x.value for x in v]))
+
+
 class FusedList(object):
     """A list of device tensors reduced in place together, step after step (a model's gradients).
 
