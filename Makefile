@@ -10,7 +10,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals
 
 CRASH    := tools/lib/libcrashline.so
 
-REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe
+REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe tools/_bin/op_body
 
 all: $(LIB) $(CRASH) $(REPRO) oracle
 
@@ -34,6 +34,17 @@ $(LIB): $(OBJS)
 tools/_bin/graph_repro: tools/graph_repro.cc $(LIB) include/tips_hip.h
 	@mkdir -p tools/_bin
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Iinclude -o $@ $< -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib'
+
+# the op-body pattern through the C-ABI in a plain-C host (tests/test_gpu_op_body.py): checked
+# against the oracle's fold, so it links oracle/build/liboracle.so (test infrastructure only)
+tools/_bin/op_body: tests/c/op_body.c $(LIB) include/tips_hip.h oracle/build/liboracle.so
+	@mkdir -p tools/_bin
+	gcc -O2 -std=gnu11 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -Ioracle -o $@ $< \
+	  -Ltips_amd/lib -ltips_hip -Loracle/build -loracle -L/opt/rocm/lib -lamdhip64 -lpthread \
+	  -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -Wl,-rpath,/opt/rocm/lib
+
+oracle/build/liboracle.so: oracle/oracle.c oracle/oracle.h
+	$(MAKE) -C oracle build/liboracle.so
 
 tools/_bin/graph_probe: tools/graph_probe.cc
 	@mkdir -p tools/_bin

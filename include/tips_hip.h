@@ -112,6 +112,10 @@ TIPS_API int tips_init_rank(int rank, int size, int device, const void* unique_i
  * delivered into every other rank's buf. Rank 0 listens on port; others
  * connect to host:port, retrying for up to timeout_s seconds. */
 TIPS_API int tips_bootstrap_broadcast(int rank, int size, const char* host, int port, void* buf, int64_t bytes, int timeout_s);
+/* Join counters of this process (both TCP joins: the bootstrap and the negotiation channel):
+ * connections a joining rank dropped because they reached itself (TCP simultaneous open), and
+ * connections rank 0 dropped because the joiner never confirmed them (it gave up waiting). */
+TIPS_API int tips_net_stats(int64_t* self_connects_refused, int64_t* unconfirmed_joins_refused);
 /* Message of the calling thread's last failed call ("" if none). */
 TIPS_API const char* tips_last_error(void);
 /* Library version string. */
@@ -229,6 +233,12 @@ TIPS_API int tips_fusion_stats(int64_t* layouts_built, int64_t* layout_hits, int
  * CPU op, ops.cc:118; its per-gradient loop, __init__.py:212-222, fused). */
 TIPS_API int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const int64_t* counts, int n,
                                        int dtype);
+/* The same into ONE host buffer laid out as tips_fused_layout (the device flat layout): tensor i's sum at
+ * offsets[i] of `flat`. When `flat` is page-locked (tips_host_register) each piece's D2H lands in it
+ * directly - no unpack at all; otherwise through a page-locked slot and one contiguous copy per piece.
+ * What allreduce_grads returns views of for host gradients. Blocks until `flat` is written. */
+TIPS_API int tips_fused_allreduce_host_flat(const void* const* ins, const int64_t* counts, int n, int dtype,
+                                            void* flat);
 
 /* ---- named, asynchronous allreduce with cross-rank negotiation ---- */
 
@@ -242,11 +252,17 @@ TIPS_API int tips_fused_allreduce_host(const void* const* ins, void* const* outs
  * stream-ordered; host pointers (both in and out host, as the reference's MPIAllreduce is a CPU
  * op, ops.cc:118) run on the negotiation thread, staged through HBM like tips_allreduce's, and
  * are done when tips_wait returns. Returns a handle > 0, or a negative status. The first call starts the
- * thread (collective); tips_shutdown stops it (collective).
- * While named requests are in flight, do not issue the synchronous
- * collectives (tips_allreduce, tips_broadcast, ...) from another thread:
- * RCCL needs the same call order on every rank, and only the negotiated
- * requests are ordered by rank 0. */
+ * thread (collective: every rank's first named request must come after the same synchronous
+ * collectives - their number is compared at the join, and a difference fails every rank's start
+ * with both numbers instead of pairing RCCL calls wrongly). tips_shutdown stops it (collective).
+ * From then on every synchronous collective of this library (tips_allreduce, tips_allreduce_checked,
+ * tips_broadcast, tips_allgatherv, tips_allgather_i64, the tips_fused_* calls), from any thread, is
+ * routed through the same negotiation: announced as request "~sync.<k>" (k-th such call of the rank)
+ * with its type, dtype and shape, checked by rank 0 like any request, and run on the negotiation
+ * thread in rank 0's order - so a rank's RCCL calls are issued from one thread in one order, the same
+ * on every rank, as the reference's coordinator issues every collective. A routed call returns when
+ * its device work is queued on the caller's stream (host memory: when it is done), as a direct call.
+ * Synchronous calls from several threads at once must still come in the same order on every rank. */
 TIPS_API int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype,
                                         void* stream);
 /* The same with the tensor's shape (ndim <= TIPS_MAX_DIMS; ndim 0 = a scalar, announced as
@@ -273,6 +289,17 @@ TIPS_API int tips_enqueue_allreduce_shaped_n(const char* const* names, const voi
                                              int64_t* handles);
 /* tips_wait on each of n handles (handles <= 0 are skipped): TIPS_OK or the first failure. */
 TIPS_API int tips_wait_n(const int64_t* handles, int n);
+/* Completion callback of a named request (the reference's OpRecord::callback, ops.cc:107-110,
+ * which sets the op's status and calls TF's done()): status TIPS_OK or a negative status, message
+ * the failure's text ("" on success; valid during the call only). */
+typedef void (*tips_done_fn)(void* ctx, int status, const char* message);
+/* Register fn for the request `handle` (any of the three types): the library calls fn(ctx, status,
+ * message) exactly once, from its completion thread, when the request has finished - for device
+ * memory when its work on the device has completed - and releases the handle (tips_wait / tips_poll
+ * on it then fail). A request that has already finished is called back at once (from that thread).
+ * What an AsyncOpKernel body needs: enqueue, register, return; done() from the callback
+ * (INTEGRATION.md §2). */
+TIPS_API int tips_on_done(int64_t handle, tips_done_fn fn, void* ctx);
 /* Named broadcast through the same negotiation (the reference's MPIBroadcast op,
  * ops.cc:214-286 -> EnqueueTensorCollective(RequestType_BROADCAST); PerformCollectiveOp's
  * broadcast branch, coordinator.cc:275-295): rank 0 checks dtype and shape with

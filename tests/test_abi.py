@@ -171,6 +171,52 @@ def test_bootstrap_survives_a_silent_listener():
     assert time.time() - t0 < 30
 
 
+def _bootstrap_worker_env(rank, size, port, q, env, delay):
+    import os
+    import time
+    os.environ.update(env)
+    time.sleep(delay)
+    from tips_amd import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(128)
+    if rank == 0:
+        ctypes.memmove(buf, bytes(range(128)), 128)
+    rc = L.tips_bootstrap_broadcast(rank, size, b"127.0.0.1", port, buf, 128, 60)
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    L.tips_net_stats(ctypes.byref(a), ctypes.byref(b))
+    q.put((rank, rc, buf.raw, a.value, b.value))
+
+
+@pytest.mark.parametrize("knob,who", [("TIPS_TEST_SELF_CONNECT", 3), ("TIPS_TEST_DROP_FIRST_HELLO", 4)])
+def test_bootstrap_join_edge_cases(knob, who):
+    """The unique-id bootstrap's two join hazards, made deterministic:
+    - TIPS_TEST_SELF_CONNECT: rank 1 starts 1 s before rank 0 and its first attempts are bound to
+      the port they connect to, so they complete as a TCP simultaneous open with itself; each must
+      be dropped (tips_net_stats counts them) - read as an answer it would have been 'the id';
+    - TIPS_TEST_DROP_FIRST_HELLO: rank 1 gives up on its first connection right after asking (as
+      a rank whose answer timed out): rank 0 counts a rank only when it confirms receipt, so it
+      keeps listening and serves the retry instead of closing the listener on a rank that left."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env = {knob: "3" if knob == "TIPS_TEST_SELF_CONNECT" else "1"}
+    procs = [ctx.Process(target=_bootstrap_worker_env, args=(r, 3, port, q, env if r == 1 else {},
+                                                           1.0 if (r == 0 and knob == "TIPS_TEST_SELF_CONNECT") else 0.0))
+             for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=90) for _ in procs)
+    for p in procs:
+        p.join(30)
+    for rank, rc, raw, selfc, unconf in res:
+        assert rc == 0, rank
+        assert raw == bytes(range(128))
+    if knob == "TIPS_TEST_SELF_CONNECT":
+        assert res[1][3] >= 1, res
+    else:
+        assert res[0][4] >= 1, res
+
+
 def test_bootstrap_timeout():
     from tips_amd import _lib
     L = _lib.lib()

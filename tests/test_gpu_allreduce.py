@@ -363,6 +363,39 @@ def test_fused_host_identity(gpu, monkeypatch, piece):
         gpu.fused_allreduce_host([np.zeros(4, np.float32), np.zeros(4, np.float64)])
 
 
+@pytest.mark.parametrize("threads,piece", [(1, 4096), (8, 1 << 20), (16, 8 << 20)])
+def test_fused_host_flat_identity(gpu, monkeypatch, threads, piece):
+    """tips_fused_allreduce_host_flat at one rank: the outputs are views of one page-locked host
+    buffer (the device writes the sums straight into it), bit-exact for numpy of every dtype with
+    odd sizes and empty tensors and for CPU torch bf16; a released set is reused, a held one is
+    not, and a later call does not disturb the outputs a caller still holds."""
+    import torch
+    monkeypatch.setenv("TIPS_HOST_THREADS", str(threads))
+    monkeypatch.setenv("TIPS_HOST_FUSED_PIECE_BYTES", str(piece))
+    rng = np.random.default_rng(threads * 7 + piece % 1000)
+    for dtype in [F32, F64, I32, I64, F16]:
+        sizes = [int(round(2 ** rng.uniform(0, 16))) for _ in range(40)] + [0, 1, 3]
+        ins = [rand(dtype, s, rng).reshape(-1) for s in sizes]
+        outs = gpu.fused_allreduce_host_flat(ins)
+        for o, x in zip(outs, ins):
+            assert o.shape == x.shape and same_bits(o, x, dtype)
+        base = outs[0].base.ctypes.data  # (the address: a reference to the buffer would hold it)
+        held = outs
+        ins2 = [x[::-1].copy() for x in ins]
+        outs2 = gpu.fused_allreduce_host_flat(ins2)
+        assert outs2[0].base.ctypes.data != base  # held: a new set
+        for o, x, o2, x2 in zip(held, ins, outs2, ins2):
+            assert same_bits(o, x, dtype) and same_bits(o2, x2, dtype)
+        del held, outs
+        outs3 = gpu.fused_allreduce_host_flat(ins)
+        assert outs3[0].base.ctypes.data == base  # released: reused
+        for o, x in zip(outs3, ins):
+            assert same_bits(o, x, dtype)
+    tb = [torch.randn(n).to(torch.bfloat16) for n in (5, 100003, 64, 0)]
+    outs = gpu.fused_allreduce_host_flat(tb)
+    assert all(torch.equal(o.view(torch.int16), t.view(torch.int16)) for o, t in zip(outs, tb))
+
+
 def test_allreduce_grads_identity_single_rank(gpu):
     import torch
     grads = [torch.randn(10, device="cuda"), None, torch.randn(3, 3, device="cuda")]

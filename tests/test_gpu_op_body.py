@@ -1,0 +1,57 @@
+"""-m gpu: the TF op-body pattern through the C-ABI alone, in a plain-C host.
+
+tools/_bin/op_body (tests/c/op_body.c) runs as one process per rank, each a real RCCL rank on the
+box's one GPU (as tests/test_gpu_rccl_procs.py's workers: NCCL_HOSTID per process, socket
+transport). On every rank four threads issue named requests - device f32 / i32 and host f32
+allreduces and a broadcast - each thread in its own order and each rank in a different shuffle,
+every request completing through a tips_on_done callback, while a fifth thread issues synchronous
+tips_allreduce calls that the library routes through the same negotiation. Every output is checked
+bit-exact against the oracle's rank-order fold (oracle_fold) of all ranks' regenerated inputs
+(AUTO at p = 3: one-shot and direct schedules and fused batches - all rank-order folds). The
+reference pins the same path with callbacks in coordinator_test.cc:10-45."""
+import json
+import os
+import socket
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("p,tensors", [(3, 96), (2, 40)])
+def test_op_body_over_rccl(gpu, p, tensors):
+    exe = os.path.join(REPO, "tools", "_bin", "op_body")
+    assert os.path.exists(exe), "build it first: make tools/_bin/op_body (part of __graft_entry__.build())"
+    port = _port()
+    procs = []
+    for r in range(p):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(p), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), TIPS_BOOTSTRAP_PORT=str(port), NCCL_HOSTID="tips-op-body-%d" % r,
+                   NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", OP_BODY_TENSORS=str(tensors))
+        procs.append(subprocess.Popen([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            out, err = pr.communicate(timeout=260)
+            outs.append((pr.returncode, out, err))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    for rc, out, err in outs:
+        line = [l for l in out.splitlines() if l.startswith("{")]
+        assert line, (rc, out[-2000:], err[-2000:])
+        res = json.loads(line[-1])
+        assert rc == 0 and res["ok"], (res, err[-2000:])
+        assert res["callbacks"] == tensors

@@ -17,21 +17,30 @@ def _port():
     return p
 
 
-def _worker(rank, size, port, requests, q):
+def _worker(rank, size, port, requests, q, env=None, delay=0.0, stats=None):
     import ctypes
+    import os
+    import time
+    os.environ.update(env or {})  # (the join's test knobs are read once, at the first join)
+    time.sleep(delay)
     from tips_amd import _lib
     L = _lib.lib()
     out = ctypes.create_string_buffer(1 << 16)
     rc = L.tips_negotiation_selftest(rank, size, b"127.0.0.1", port, requests.encode(), out, len(out))
-    q.put((rank, rc, out.value.decode(), L.tips_last_error().decode()))
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    L.tips_net_stats(ctypes.byref(a), ctypes.byref(b))
+    res = (rank, rc, out.value.decode(), L.tips_last_error().decode())
+    q.put(res + ((a.value, b.value),) if stats else res)
 
 
-def run(per_rank, port=None):
+def run(per_rank, port=None, env=None, delay=None, stats=False):
+    """Each rank's selftest in its own process; env / delay: per-rank environment and start delay."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = port or _port()
     size = len(per_rank)
-    procs = [ctx.Process(target=_worker, args=(r, size, port, per_rank[r], q)) for r in range(size)]
+    procs = [ctx.Process(target=_worker, args=(r, size, port, per_rank[r], q, (env or {}).get(r),
+                                               (delay or {}).get(r, 0.0), stats)) for r in range(size)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=180) for _ in procs)
@@ -168,3 +177,79 @@ def test_foreign_listener_on_the_negotiation_port():
     for rank, rc, log, err in res:
         assert rc == 0, err
     assert all(l == logs[0] for l in logs) and sorted(logs[0]) == ["a OK", "b OK"]
+
+
+def test_op_body_threads_with_callbacks():
+    """The op-body pattern of INTEGRATION.md §2 without a GPU: on every rank four threads (a
+    framework's executor threads) issue named requests, each thread in its own order and each rank
+    in a different shuffle, and every request completes through a tips_on_done callback (the
+    reference's OpRecord callback, ops.cc:107-110, coordinator_test.cc:10-45). Every rank executes
+    the same names in the same order, and every callback fires exactly once."""
+    import random
+    names = ["layer%d/grad" % i for i in range(48)]
+    reqs = []
+    for r in range(3):
+        rnd = random.Random(100 + r)
+        order = names[:]
+        rnd.shuffle(order)
+        body = []
+        for k, n in enumerate(order):
+            t = k % 4
+            body.append("t%d: %s 0 %d" % (t, n, 64 + names.index(n)))
+            if rnd.random() < 0.1:
+                body.append("t%d: @sleep %d" % (t, rnd.randint(1, 5)))
+        body.append("t2: @wait")
+        reqs.append("\n".join(body))
+    res = run(reqs)
+    logs = [lines(log) for _, _, log, _ in res]
+    for rank, rc, log, err in res:
+        assert rc == 0, err
+        assert log.strip().endswith("callbacks %d" % len(names)), log[-200:]
+    assert logs[0] == logs[1] == logs[2]
+    assert sorted(l for l in logs[0] if not l.startswith("callbacks")) == sorted(n + " OK" for n in names)
+
+
+def test_op_body_callbacks_carry_errors():
+    """A callback reports a request's failure: a shape mismatch fails on every rank through its
+    callback, the other requests of the same threads still complete."""
+    r0 = "t1: a 0 8 2,4\nt2: b 0 4\nt1: c 0 4"
+    r1 = "t2: c 0 4\nt1: a 0 8 4,2\nt1: b 0 4"
+    res = run([r0, r1])
+    for _, rc, log, err in res:
+        assert rc == 0, err
+        got = dict(l.split(" ", 1) for l in lines(log))
+        assert got["a"] == "ERR Mismatched allreduce tensor shapes: [2,4] vs [4,2]"
+        assert got["b"] == "OK" and got["c"] == "OK" and got["callbacks"] == "3"
+
+
+def test_start_refused_when_sync_counts_differ():
+    """Every synchronous collective issued before the negotiation starts must have its partner on
+    every rank: rank 1 claims one more than rank 0, so the join's verdict fails every rank's start
+    with both numbers (instead of pairing rank 1's later RCCL calls with the wrong ones)."""
+    res = run(["@synccount 2\na 0 4", "@synccount 3\na 0 4"])
+    for rank, rc, log, err in res:
+        assert rc == -7, (rank, rc, err)
+        assert "rank 1 issued 3 synchronous collectives before the negotiation started, rank 0 issued 2" in err
+
+
+def test_join_survives_connecting_to_itself():
+    """Rank 1 starts first and its first attempts are bound to the port they connect to
+    (TIPS_TEST_SELF_CONNECT: TCP simultaneous open with itself, deterministic), before rank 0
+    listens: each such socket must be dropped (tips_net_stats counts them) and the join must still
+    complete. Without the check the socket would read its own hello back as rank 0's answer."""
+    res = run(["a 0 4\nb 0 8", "b 0 8\na 0 4"], env={1: {"TIPS_TEST_SELF_CONNECT": "3"}}, delay={0: 1.0}, stats=True)
+    for rank, rc, log, err, st in res:
+        assert rc == 0, err
+        assert sorted(lines(log)) == ["a OK", "b OK"]
+    assert res[1][4][0] >= 1, res[1][4]  # rank 1 refused at least one connection to itself
+
+
+def test_join_counts_a_rank_only_once_it_confirms():
+    """Rank 1 abandons its first connection right after its hello (TIPS_TEST_DROP_FIRST_HELLO, as a
+    rank whose answer did not come in time): rank 0 must not count that connection as joined (it
+    waits for the rank's confirmation) and must take the rank's next connection."""
+    res = run(["a 0 4", "a 0 4", "a 0 4"], env={1: {"TIPS_TEST_DROP_FIRST_HELLO": "1"}}, stats=True)
+    for rank, rc, log, err, st in res:
+        assert rc == 0, err
+        assert lines(log) == ["a OK"]
+    assert res[0][4][1] >= 1, res[0][4]  # rank 0 dropped at least one unconfirmed connection

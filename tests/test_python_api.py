@@ -100,8 +100,7 @@ def _fake_two_ranks(monkeypatch):
     monkeypatch.setattr(tips_amd, "size", lambda: 2)
     # dense host gradients go through the fused host path at N > 1: here each through the (faked)
     # tips_amd.allreduce, so the tests below see one reduction per gradient
-    monkeypatch.setattr(tips_amd._ops, "fused_allreduce_host",
-                        lambda ts, out_list=None: [tips_amd.allreduce(t) for t in ts])
+    monkeypatch.setattr(tips_amd._ops, "fused_allreduce_host_flat", lambda ts: [tips_amd.allreduce(t) for t in ts])
 
 
 def test_indexed_slices_take_the_allgather_branch(monkeypatch):

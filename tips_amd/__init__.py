@@ -10,7 +10,7 @@ from .basics import TipsBasics, init, is_initialized, rank, shutdown, size
 from .compression import Compression, Compressor, FP16Compressor, NoneCompressor
 from .ops import (Handle, allgather_async, allgather_op, allreduce_async, broadcast_async, allreduce_async_many, synchronize_many, allreduce_op, broadcast_op, poll, synchronize, broadcast_variables, bucket_sum, fused_allreduce,
                   fused_allreduce_, rank_op, registered_host_buffer, set_algorithm, set_consistency_check, size_op)
-from .ops import fused_allreduce_flat, fused_allreduce_host, fusion_stats
+from .ops import fused_allreduce_flat, fused_allreduce_host, fused_allreduce_host_flat, fusion_stats
 from ._lib import TipsError, TipsLibraryError
 from . import ops as _ops
 from . import tensors as _tensors
@@ -35,7 +35,7 @@ __all__ = [
     "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
-    "DistributedOptimizer", "DistributedGradientTape", "fused_allreduce_flat", "fused_allreduce_host", "fusion_stats",
+    "DistributedOptimizer", "DistributedGradientTape", "fused_allreduce_flat", "fused_allreduce_host", "fused_allreduce_host_flat", "fusion_stats",
 ]
 
 
@@ -178,7 +178,7 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
             out[i] = s if none else compression.decompress(s, ctx)
         plan_groups.append(([i for i, _, _ in members], fo))
     for members in host.values():
-        sums = _ops.fused_allreduce_host([c for _, c, _ in members])
+        sums = _ops.fused_allreduce_host_flat([c for _, c, _ in members])
         for (i, _, ctx), s in zip(members, sums):
             out[i] = s if none else compression.decompress(s, ctx)
     if simple and not host:

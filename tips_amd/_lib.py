@@ -53,6 +53,8 @@ _c_void_pp = ctypes.POINTER(ctypes.c_void_p)
 _c_i64_p = ctypes.POINTER(ctypes.c_int64)
 # tips_alloc_fn (include/tips_hip.h): void* (*)(void* ctx, int64_t bytes)
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+# tips_done_fn: void (*)(void* ctx, int status, const char* message)
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p)
 
 # (name, restype, argtypes) — must match include/tips_hip.h
 _SIGNATURES = [
@@ -92,6 +94,7 @@ _SIGNATURES = [
     ("tips_fused_pack_bucket", ctypes.c_int64,
      [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     ("tips_fused_allreduce_host", ctypes.c_int, [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int]),
+    ("tips_fused_allreduce_host_flat", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_enqueue_allreduce", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_enqueue_allreduce_shaped", ctypes.c_int64,
@@ -104,6 +107,8 @@ _SIGNATURES = [
      [ctypes.POINTER(ctypes.c_char_p), _c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
       _c_i64_p]),
     ("tips_wait_n", ctypes.c_int, [_c_i64_p, ctypes.c_int]),
+    ("tips_on_done", ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tips_net_stats", ctypes.c_int, [_c_i64_p, _c_i64_p]),
     ("tips_wait", ctypes.c_int, [ctypes.c_int64]),
     ("tips_enqueue_broadcast", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -18,6 +18,8 @@ namespace tips {
 
 using namespace net;
 
+constexpr uint8_t kIdAck = 0xA5;  // a joining rank's confirmation that it has the id
+
 
 // Returns 0 on success; on failure fills *err and returns -1.
 int bootstrap_exchange(int rank, int size, const char* host, int port, void* id, int id_bytes, int timeout_s,
@@ -59,12 +61,21 @@ int bootstrap_exchange(int rank, int size, const char* host, int port, void* id,
       int c = ::accept(fd, nullptr, nullptr);
       if (c < 0) continue;
       int32_t peer = -1;
+      uint8_t ack = 0;
       if (!recv_all(c, &peer, sizeof peer, std::min(ms_left(), 5000)) || peer <= 0 || peer >= size ||
           !send_all(c, id, (size_t)id_bytes)) {
         ::close(c);
         continue;
       }
-      if (!seen[peer]) {  // a rank that asks again (its earlier answer timed out) just gets the id again
+      // a rank counts as joined only once it confirms it has the id: a send can succeed into the
+      // socket of a rank that has already given up on this attempt (it then asks again, and this
+      // loop must still be listening for it)
+      if (!recv_all(c, &ack, 1, std::min(ms_left(), 5000)) || ack != kIdAck) {
+        unconfirmed_joins()++;
+        ::close(c);
+        continue;
+      }
+      if (!seen[peer]) {  // a rank that asks again just gets the id again
         seen[peer] = true;
         joined++;
       }
@@ -78,21 +89,27 @@ int bootstrap_exchange(int rank, int size, const char* host, int port, void* id,
     *err = std::string("bootstrap: cannot resolve ") + host;
     return -1;
   }
+  static std::atomic<int> drop_first{-1};  // TIPS_TEST_DROP_FIRST_HELLO=1 (tests only): give up on the first
+  if (drop_first.load() < 0) {             // connection right after asking, as a rank whose answer timed out
+    const char* v = getenv("TIPS_TEST_DROP_FIRST_HELLO");
+    int expect = -1;
+    drop_first.compare_exchange_strong(expect, v ? atoi(v) : 0);
+  }
   while (true) {
-    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (fd < 0) {
-      *err = std::string("bootstrap: socket: ") + strerror(errno);
-      return -1;
-    }
-    if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0 && !connected_to_self(fd)) {
-      int32_t me = rank;
+    const int fd = connect_peer(sa);  // (-1: refused, or it reached itself)
+    if (fd >= 0) {
+      const int32_t me = rank;
+      const uint8_t ack = kIdAck;
+      if (send_all(fd, &me, sizeof me) && drop_first.load() > 0) {
+        drop_first--;
+        ::close(fd);
+        continue;
+      }
       // a bounded wait: a listener that never answers (another program's socket on this port) costs
       // one attempt, not the whole timeout
-      bool ok = send_all(fd, &me, sizeof me) && recv_all(fd, id, (size_t)id_bytes, std::min(ms_left(), 5000));
+      const bool ok = recv_all(fd, id, (size_t)id_bytes, std::min(ms_left(), 5000)) && send_all(fd, &ack, 1);
       ::close(fd);
       if (ok) return 0;
-    } else {
-      ::close(fd);
     }
     if (ms_left() == 0) {
       *err = "bootstrap: rank " + std::to_string(rank) + " could not reach rank 0 at " + host + ":" +

@@ -110,6 +110,10 @@ int tips_allreduce_checked(const void* in, void* out, const int64_t* shape, int 
     rec[3 + d] = shape[d];
     count *= shape[d];
   }
+  int routed_rc;  // (through the negotiation, when it runs: rank 0 then checks the shape itself)
+  if (route_collective(TIPS_REQ_ALLREDUCE, dtype, shape, ndim, 0,
+                       [&] { return tips_allreduce_checked(in, out, shape, ndim, dtype, op, stream); }, &routed_rc))
+    return routed_rc;
   {
     State& st = S();
     std::lock_guard<std::mutex> lk(st.mu);
@@ -124,6 +128,11 @@ int tips_allreduce_checked(const void* in, void* out, const int64_t* shape, int 
 
 int tips_allgather_i64(const int64_t* values, int words, int64_t* out) {
   if (!out || !values || words < 1 || words > 4096) return fail(TIPS_ERR_INVALID_ARG, "bad allgather_i64 args");
+  int routed_rc;
+  const int64_t shape[2] = {1, words};
+  if (route_collective(TIPS_REQ_ALLGATHER, TIPS_INT64, shape, 2, 0, [&] { return tips_allgather_i64(values, words, out); },
+                       &routed_rc))
+    return routed_rc;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
@@ -137,6 +146,11 @@ int tips_allgather_i64(const int64_t* values, int words, int64_t* out) {
 int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root, void* stream) {
   TRY(check_dtype(dtype));
   if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count");
+  int routed_rc;
+  const int64_t shape[1] = {count};
+  if (route_collective(TIPS_REQ_BROADCAST, dtype, shape, 1, root,
+                       [&] { return tips_broadcast(in, out, count, dtype, root, stream); }, &routed_rc))
+    return routed_rc;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
@@ -170,6 +184,11 @@ int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root
 
 int tips_allgatherv(const void* in, int64_t count, void* out, const int64_t* counts, int dtype, void* stream) {
   TRY(check_dtype(dtype));
+  int routed_rc;
+  const int64_t shape[1] = {count < 0 ? 0 : count};
+  if (route_collective(TIPS_REQ_ALLGATHER, dtype, shape, 1, 0,
+                       [&] { return tips_allgatherv(in, count, out, counts, dtype, stream); }, &routed_rc))
+    return routed_rc;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");

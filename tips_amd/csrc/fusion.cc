@@ -534,10 +534,23 @@ int check_list(const void* const* ins, const int64_t* counts, int n, int dtype, 
   return 0;
 }
 
+// the shape a fused list is announced with when it is routed through the negotiation: [n, elements]
+void list_shape(const int64_t* counts, int n, int64_t* shape) {
+  shape[0] = n;
+  shape[1] = 0;
+  for (int i = 0; i < n; i++) shape[1] += counts[i];
+}
+
 int fused_entry(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype, void* stream) {
   if (!outs && n > 0) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
   std::vector<BatchItem> items;
   TRY(check_list(ins, counts, n, dtype, &items, outs));
+  int routed_rc;
+  int64_t shape[2];
+  list_shape(counts, n, shape);
+  if (route_collective(TIPS_REQ_ALLREDUCE, dtype, shape, 2, 0,
+                       [&] { return fused_entry(ins, outs, counts, n, dtype, stream); }, &routed_rc))
+    return routed_rc;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
@@ -571,6 +584,12 @@ int tips_fused_allreduce_flat(const void* const* ins, const int64_t* counts, int
                               void* stream) {
   std::vector<BatchItem> items;
   TRY(check_list(ins, counts, n, dtype, &items, nullptr));
+  int routed_rc;
+  int64_t shape[2];
+  list_shape(counts, n, shape);
+  if (route_collective(TIPS_REQ_ALLREDUCE, dtype, shape, 2, 0,
+                       [&] { return tips_fused_allreduce_flat(ins, counts, n, dtype, flat, stream); }, &routed_rc))
+    return routed_rc;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");

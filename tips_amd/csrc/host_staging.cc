@@ -188,20 +188,24 @@ void copy_range(const std::vector<HostSeg>& segs, int64_t a, int64_t b, char* bu
 
 }  // namespace
 
-int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype) {
+// The byte stream is the fusion layout of the list (fused_layout: 256-B aligned offsets, a function
+// of the counts alone, the same as tips_fused_allreduce_flat's), so every rank cuts the same pieces
+// and a flat host output has the device flat output's layout. With `flat` (host memory laid out so),
+// the sums land there: straight from the device when it is page-locked (no unpack at all), else
+// through a page-locked slot and one contiguous copy per piece. Without it, they are unpacked into
+// every items[i].out.
+int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, char* flat) {
   const int64_t es = tips::dtype_size(dtype);
+  std::vector<int64_t> counts((size_t)n), offs((size_t)n);
+  for (int i = 0; i < n; i++) counts[i] = items[i].count;
+  int64_t total = fused_layout(counts.data(), n, dtype, offs.data());
   std::vector<HostSeg> segs;
   segs.reserve((size_t)n);
-  int64_t total = 0;
-  for (int i = 0; i < n; i++) {
-    const int64_t bytes = items[i].count * es;
-    if (bytes <= 0) continue;
-    total = round_up(total, 64);
-    segs.push_back(HostSeg{total, bytes, (const char*)items[i].in, (char*)items[i].out});
-    total += bytes;
-  }
+  for (int i = 0; i < n; i++)
+    if (counts[i] > 0) segs.push_back(HostSeg{offs[i], counts[i] * es, (const char*)items[i].in, (char*)items[i].out});
   if (segs.empty()) return 0;
-  total = round_up(total, kAlignBytes);  // (a whole number of elements, 256-B aligned pieces)
+  std::sort(segs.begin(), segs.end(), [](const HostSeg& x, const HostSeg& y) { return x.off < y.off; });
+  total = round_up(total, kAlignBytes);
   const int64_t piece = std::min<int64_t>(
       total, round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_FUSED_PIECE_BYTES", 8 << 20)), kAlignBytes));
   const int np = (int)((total + piece - 1) / piece);
@@ -223,6 +227,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype) {
   char* dev = (char*)st.host_in.p;
   char* pin_in = (char*)st.hpin[0];
   char* pin_out = (char*)st.hpin[1];
+  const bool direct_out = flat && is_pinned_host(flat, total);  // D2H straight into the output
   hipEvent_t* ev = st.pipe_ev.ev.data();  // [3i] H2D done, [3i+1] reduced, [3i+2] D2H done
   const int parts = nthreads;
   auto host_copy = [&](int i, bool pack) {
@@ -231,10 +236,12 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype) {
     const int64_t per = round_up((p1 - p0 + parts - 1) / parts, 64);
     st.host_pool->run(parts, [&](int j) {
       const int64_t a = p0 + j * per, b = std::min(p1, a + per);
-      if (a < b) copy_range(segs, a, b, buf, p0, pack);
+      if (a >= b) return;
+      if (!pack && flat) memcpy(flat + a, buf + (a - p0), (size_t)(b - a));  // (padding included: contiguous)
+      else copy_range(segs, a, b, buf, p0, pack);
     });
   };
-  const int lag = 1;  // piece i - lag is unpacked while piece i is on the link
+  const int lag = direct_out ? np : 1;  // piece i - lag is unpacked while piece i is on the link
   for (int i = 0; i < np; i++) {
     const int64_t off = (int64_t)i * piece, len = std::min(piece, total - off);
     if (i >= R) HIP_TRY(hipEventSynchronize(ev[3 * (i - R)]));  // slot i % R: its last H2D has read it
@@ -247,13 +254,17 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype) {
     HIP_TRY(hipEventRecord(ev[3 * i + 1], st.io_stream));
     HIP_TRY(hipStreamWaitEvent(st.d2h_stream, ev[3 * i + 1], 0));
     // (slot i % R of pin_out was unpacked at iteration i - R + lag < i)
-    HIP_TRY(hipMemcpyAsync(pin_out + (int64_t)(i % R) * piece, dev + off, (size_t)len, hipMemcpyDeviceToHost,
-                           st.d2h_stream));
+    char* d2h = direct_out ? flat + off : pin_out + (int64_t)(i % R) * piece;
+    HIP_TRY(hipMemcpyAsync(d2h, dev + off, (size_t)len, hipMemcpyDeviceToHost, st.d2h_stream));
     HIP_TRY(hipEventRecord(ev[3 * i + 2], st.d2h_stream));
     if (i >= lag) {
       HIP_TRY(hipEventSynchronize(ev[3 * (i - lag) + 2]));
       host_copy(i - lag, false);
     }
+  }
+  if (direct_out) {
+    HIP_TRY(hipStreamSynchronize(st.d2h_stream));
+    return 0;
   }
   for (int j = std::max(0, np - lag); j < np; j++) {
     HIP_TRY(hipEventSynchronize(ev[3 * j + 2]));
@@ -285,6 +296,12 @@ int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const i
     if (counts[i] < 0 || (counts[i] > 0 && (!ins[i] || !outs[i]))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor %d", i);
     items[i] = BatchItem{ins[i], outs[i], counts[i]};
   }
+  int routed_rc;
+  int64_t shape[2] = {n, 0};
+  for (int i = 0; i < n; i++) shape[1] += counts[i];
+  if (route_collective(TIPS_REQ_ALLREDUCE, dtype, shape, 2, 0,
+                       [&] { return tips_fused_allreduce_host(ins, outs, counts, n, dtype); }, &routed_rc))
+    return routed_rc;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
@@ -293,7 +310,33 @@ int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const i
   for (int i = 0; i < n; i++)
     if (items[i].count > 0 && (is_device_ptr(items[i].in) || is_device_ptr(items[i].out)))
       return fail(TIPS_ERR_INVALID_ARG, "tips_fused_allreduce_host: tensor %d is in device memory", i);
-  return fused_allreduce_host(st, items.data(), n, dtype);
+  return fused_allreduce_host(st, items.data(), n, dtype, nullptr);
+}
+
+int tips_fused_allreduce_host_flat(const void* const* ins, const int64_t* counts, int n, int dtype, void* flat) {
+  TRY(check_dtype(dtype));
+  if (n < 0 || (n > 0 && (!ins || !counts || !flat))) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
+  std::vector<BatchItem> items((size_t)n);
+  for (int i = 0; i < n; i++) {
+    if (counts[i] < 0 || (counts[i] > 0 && !ins[i])) return fail(TIPS_ERR_INVALID_ARG, "bad tensor %d", i);
+    items[i] = BatchItem{ins[i], flat, counts[i]};
+  }
+  int routed_rc;
+  int64_t shape[2] = {n, 0};
+  for (int i = 0; i < n; i++) shape[1] += counts[i];
+  if (route_collective(TIPS_REQ_ALLREDUCE, dtype, shape, 2, 0,
+                       [&] { return tips_fused_allreduce_host_flat(ins, counts, n, dtype, flat); }, &routed_rc))
+    return routed_rc;
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+  if (n == 0) return 0;
+  TRY(set_device(st));
+  if (is_device_ptr(flat)) return fail(TIPS_ERR_INVALID_ARG, "tips_fused_allreduce_host_flat: flat is device memory");
+  for (int i = 0; i < n; i++)
+    if (items[i].count > 0 && is_device_ptr(items[i].in))
+      return fail(TIPS_ERR_INVALID_ARG, "tips_fused_allreduce_host_flat: tensor %d is in device memory", i);
+  return fused_allreduce_host(st, items.data(), n, dtype, (char*)flat);
 }
 
 int tips_host_register(void* ptr, int64_t bytes) {

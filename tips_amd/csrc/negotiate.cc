@@ -60,9 +60,24 @@ struct Req {
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   std::shared_ptr<GroupEv> gev;  // set when the request ran inside a fused batch (then ev is unused)
-  int state = 0;  // 0 queued, 1 announced, 2 launched (ev recorded), 3 done (dry run), -1 error
+  int state = 0;  // 0 queued, 1 announced, 2 launched (ev recorded), 3 done (host / dry run / routed), -1 error
+  int code = TIPS_ERR_MISMATCH;  // the failure's status (a routed collective's own; a negotiation error's)
   std::string err;
+  // A synchronous collective routed through the negotiation (route_collective): its body runs on
+  // the negotiation thread when rank 0's order reaches it, like any named request.
+  std::function<int()> body;
+  // tips_on_done: called once from the completion thread when the request has finished
+  tips_done_fn cb = nullptr;
+  void* cb_ctx = nullptr;
+  bool cb_queued = false;
 };
+
+// The negotiation thread itself: a collective entry point called there runs directly (it is the
+// body of a routed request, or the executor's own call), never routed again.
+thread_local bool tl_negotiation_thread = false;
+// Synchronous collectives this process issued directly (no negotiation running) while size > 1:
+// every rank must have issued the same number when the negotiation starts (checked at the join).
+std::atomic<int64_t> g_sync_direct{0};
 
 // ---- wire format: flat little-endian records ----------------------------------
 struct Writer {
@@ -210,15 +225,24 @@ class Negotiator {
   // waiting for a rank that believes it has joined.
   static constexpr int kPortTries = 16;
   static constexpr uint64_t kMagic = 0x30474e4553504954ull;  // "TIPSNEG0"
+  static constexpr uint64_t kConfirm = 0x31474e4553504954ull;  // "TIPSNEG1"
   struct Hello {
     uint64_t magic, key;
     int32_t rank, size;
+    int64_t sync_direct;  // synchronous collectives this rank issued before the negotiation started
   };
   struct Ack {
     uint64_t magic, key;
   };
 
-  int start(int rank, int size, const char* host, int port, bool dry_run, int timeout_s, uint64_t key = 0) {
+  // The join, a collective with one verdict for every rank:
+  //   joiner -> rank 0: Hello; rank 0 -> joiner: Ack; joiner -> rank 0: Confirm (it has the Ack and is
+  //   committed). Rank 0 counts a rank as joined only at its Confirm: a joiner that gave up before
+  //   the Ack arrived (it closed the socket) is not counted and its retry is accepted later.
+  //   Once every rank is in, rank 0 sends each the verdict: every rank must have issued the same
+  //   number of synchronous collectives before this point (their RCCL calls pair up only then).
+  int start(int rank, int size, const char* host, int port, bool dry_run, int timeout_s, uint64_t key = 0,
+            int64_t sync_direct = 0) {
     rank_ = rank;
     size_ = size;
     dry_ = dry_run;
@@ -226,69 +250,131 @@ class Negotiator {
     table_.p = size;
     std::string err;
     if (size > 1) {
+      const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
+      auto ms_left = [&] {
+        const auto l = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
+        return l > 0 ? (int)l : 0;
+      };
       if (rank == 0) {
         for (int k = 0; k < kPortTries && lfd_ < 0; k++) lfd_ = listen_on(port + k, size, &err);
         if (lfd_ < 0) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: ports %d-%d: %s", port, port + kPortTries - 1, err.c_str());
         peers_.assign(size, -1);
-        const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
+        std::vector<int64_t> counts(size, sync_direct);
         for (int joined = 0; joined < size - 1;) {
-          const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
           pollfd pfd{lfd_, POLLIN, 0};
-          if (left <= 0 || ::poll(&pfd, 1, (int)left) <= 0)
+          if (ms_left() <= 0 || ::poll(&pfd, 1, ms_left()) <= 0)
             return fail(TIPS_ERR_BOOTSTRAP, "negotiation: %d rank(s) did not connect", size - 1 - joined);
           int c = ::accept(lfd_, nullptr, nullptr);
           if (c < 0) continue;
           Hello h{};
           const Ack a{kMagic, key};
+          uint64_t confirm = 0;
           if (!recv_all(c, &h, sizeof h, 2000) || h.magic != kMagic || h.key != key || h.size != size || h.rank <= 0 ||
               h.rank >= size || !send_all(c, &a, sizeof a)) {
             ::close(c);
             continue;
           }
+          if (!recv_all(c, &confirm, sizeof confirm, 2000) || confirm != kConfirm) {
+            unconfirmed_joins()++;  // the joiner gave up on this connection; it will try again
+            ::close(c);
+            continue;
+          }
           set_nodelay(c);
-          if (peers_[h.rank] >= 0) {  // that rank gave up on an earlier connection (no answer in time): its latest wins
+          if (peers_[h.rank] >= 0) {  // (a rank whose earlier connection was confirmed and then lost: its latest wins)
             ::close(peers_[h.rank]);
             joined--;
           }
           peers_[h.rank] = c;
+          counts[h.rank] = h.sync_direct;
           joined++;
         }
+        std::string verdict;
+        for (int r = 1; r < size && verdict.empty(); r++)
+          if (counts[r] != counts[0])
+            verdict = "rank " + std::to_string(r) + " issued " + std::to_string(counts[r]) +
+                      " synchronous collectives before the negotiation started, rank 0 issued " +
+                      std::to_string(counts[0]) + ": the first named request must come at the same point of "
+                      "the collective order on every rank";
+        Writer w;
+        w.put<uint8_t>(verdict.empty() ? 1 : 0);
+        w.str(verdict);
+        for (int r = 1; r < size; r++) (void)send_msg(peers_[r], w.b);
+        if (!verdict.empty()) {
+          close_all();
+          return fail(TIPS_ERR_MISMATCH, "negotiation: %s", verdict.c_str());
+        }
       } else {
-        const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
-        const Hello h{kMagic, key, rank, size};
+        const Hello h{kMagic, key, rank, size, sync_direct};
+        static std::atomic<int> drop_first{-1};  // TIPS_TEST_DROP_FIRST_HELLO=1 (tests only): abandon the
+        if (drop_first.load() < 0) {             // first connection right after its hello, as a joiner
+          const char* v = getenv("TIPS_TEST_DROP_FIRST_HELLO");  // whose answer timed out would
+          int expect = -1;
+          drop_first.compare_exchange_strong(expect, v ? atoi(v) : 0);
+        }
         while (up_ < 0) {
           for (int k = 0; k < kPortTries && up_ < 0; k++) {
             sockaddr_in sa;
             if (!resolve(host, port + k, &sa)) return fail(TIPS_ERR_BOOTSTRAP, "negotiation: cannot resolve %s", host);
-            int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+            const int fd = connect_peer(sa);
+            if (fd < 0) continue;
             Ack a{};
-            if (fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0 && !connected_to_self(fd) &&
-                send_all(fd, &h, sizeof h) && recv_all(fd, &a, sizeof a, 5000) && a.magic == kMagic && a.key == key) {
+            const uint64_t confirm = kConfirm;
+            if (send_all(fd, &h, sizeof h) && drop_first.load() > 0) {
+              drop_first--;
+              ::close(fd);
+              continue;
+            }
+            if (recv_all(fd, &a, sizeof a, 5000) && a.magic == kMagic && a.key == key &&
+                send_all(fd, &confirm, sizeof confirm)) {
               set_nodelay(fd);
               up_ = fd;
-            } else if (fd >= 0) {
+            } else {
               ::close(fd);
             }
           }
           if (up_ >= 0) break;
-          if (std::chrono::steady_clock::now() > deadline)
+          if (ms_left() <= 0)
             return fail(TIPS_ERR_BOOTSTRAP, "negotiation: rank %d could not reach rank 0 at %s:%d-%d", rank, host, port,
                         port + kPortTries - 1);
           std::this_thread::sleep_for(std::chrono::milliseconds(20));
         }
+        std::string v;
+        if (!recv_msg(up_, &v, std::max(ms_left(), 1000))) {
+          close_all();
+          return fail(TIPS_ERR_BOOTSTRAP, "negotiation: rank %d got no verdict from rank 0", rank);
+        }
+        Reader rd(v);
+        const bool ok = rd.get<uint8_t>() != 0;
+        const std::string msg = rd.str();
+        if (!ok || !rd.ok) {
+          close_all();
+          return fail(TIPS_ERR_MISMATCH, "negotiation: %s", rd.ok ? msg.c_str() : "malformed verdict");
+        }
       }
     }
     running_ = true;
-    thread_ = std::thread([this] { loop(); });
+    thread_ = std::thread([this] {
+      tl_negotiation_thread = true;
+      loop();
+    });
     return 0;
+  }
+
+  void close_all() {
+    for (int& fd : peers_)
+      if (fd >= 0) ::close(fd), fd = -1;
+    if (up_ >= 0) ::close(up_);
+    if (lfd_ >= 0) ::close(lfd_);
+    up_ = lfd_ = -1;
   }
 
   int64_t enqueue(const std::string& name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
                   hipStream_t s, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
-                  void* actx = nullptr, int64_t* out_rows = nullptr) {
+                  void* actx = nullptr, int64_t* out_rows = nullptr, std::function<int()> body = nullptr) {
     if (ndim < 0 || ndim > TIPS_MAX_DIMS) return fail(TIPS_ERR_INVALID_ARG, "bad ndim %d", ndim);
     if (type == TIPS_REQ_ALLGATHER && ndim < 1) return fail(TIPS_ERR_INVALID_ARG, "An empty tensor found");
     auto r = std::make_shared<Req>();
+    r->body = std::move(body);
     r->name = name;
     r->type = type;
     r->root = root;
@@ -306,7 +392,7 @@ class Negotiator {
     if (ndim == 0) r->shape.push_back(1);  // a scalar travels as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
     r->dtype = dtype;
     r->stream = s;
-    if (!dry_) {  // the real executor (the dry run of tips_negotiation_selftest touches no memory)
+    if (!dry_ && !r->body) {  // the real executor (the dry run touches no memory; a routed body checks its own)
       // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
       // st.device is fixed from init on)
       TRY(set_device(S()));
@@ -343,50 +429,81 @@ class Negotiator {
     return r->handle;
   }
 
-  // 1 = done, 0 = pending, < 0 = error; a finished handle is released by the call that reports it
-  int poll(int64_t h, bool block) {
+  // 1 = done, 0 = pending, < 0 = error; a finished handle is released by the call that reports it.
+  // routed = the caller of a routed collective: waits until its body has run (state 3), never for
+  // device completion (the body queued that on the caller's stream, as a direct call would).
+  int poll(int64_t h, bool block, bool routed = false) {
     std::shared_ptr<Req> r;
     {
       std::unique_lock<std::mutex> l(m_);
       auto it = by_handle_.find(h);
       if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
       r = it->second;
+      if (r->cb) return fail(TIPS_ERR_INVALID_ARG, "request %s completes through its callback (tips_on_done)", r->name.c_str());
       if (block) cv_.wait(l, [&] { return r->state >= 2 || r->state < 0; });
       if (r->state == 0 || r->state == 1) return 0;
     }
     int rc = 1;
     if (r->state < 0) {
-      rc = fail(TIPS_ERR_MISMATCH, "%s", r->err.c_str());
-    } else if (r->state == 2) {
+      rc = fail(r->code, "%s", r->err.c_str());
+    } else if (r->state == 2 && !routed) {
       hipEvent_t ev = r->gev ? r->gev->ev : r->ev;
       hipError_t e = block ? hipEventSynchronize(ev) : hipEventQuery(ev);
       if (e == hipErrorNotReady) return 0;
       if (e != hipSuccess) rc = fail(TIPS_ERR_HIP, "request %s: %s", r->name.c_str(), hipGetErrorString(e));
     }
+    release(h, r);
+    return rc;
+  }
+
+  void release(int64_t h, const std::shared_ptr<Req>& r) {
     std::lock_guard<std::mutex> l(m_);
     if (r->ev) ev_pool_.push_back(r->ev);  // reused by the next request
     r->ev = nullptr;
     r->gev.reset();
     by_handle_.erase(h);
-    return rc;
+  }
+
+  // tips_on_done: fn(ctx, status, message) is called once, from the completion thread, when the
+  // request has finished (a device request: when its work on the device is done); the handle is
+  // released then. A request that has already finished is queued at once.
+  int on_done(int64_t h, tips_done_fn fn, void* ctx) {
+    std::lock_guard<std::mutex> l(m_);
+    auto it = by_handle_.find(h);
+    if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
+    auto& r = it->second;
+    if (r->cb) return fail(TIPS_ERR_INVALID_ARG, "request %s already has a completion callback", r->name.c_str());
+    r->cb = fn;
+    r->cb_ctx = ctx;
+    if (!waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
+    if (r->state >= 2 || r->state < 0) queue_done(r);
+    return 0;
   }
 
   // collective: every rank's loop learns from rank 0 that all ranks asked to stop
   int stop() {
     {
       std::lock_guard<std::mutex> l(m_);
-      if (!running_ && !thread_.joinable()) return 0;
+      if (!running_ && !thread_.joinable() && !waiter_.joinable()) return 0;
       want_stop_ = true;
       cv_.notify_all();
     }
     if (thread_.joinable()) thread_.join();
-    for (int fd : peers_)
-      if (fd >= 0) ::close(fd);
+    {  // the completion thread drains what is queued (the loop failed every unmatched request), then ends
+      std::lock_guard<std::mutex> l(m_);
+      waiter_stop_ = true;
+      done_cv_.notify_all();
+    }
+    if (waiter_.joinable()) waiter_.join();
+    close_all();
     peers_.clear();
-    if (up_ >= 0) ::close(up_);
-    if (lfd_ >= 0) ::close(lfd_);
-    up_ = lfd_ = -1;
     return loop_err_.empty() ? 0 : fail(TIPS_ERR_BOOTSTRAP, "%s", loop_err_.c_str());
+  }
+
+  // number of completion callbacks called so far (the selftest's log)
+  int64_t callbacks_called() {
+    std::lock_guard<std::mutex> l(m_);
+    return cb_called_;
   }
 
   ~Negotiator() {
@@ -475,11 +592,53 @@ class Negotiator {
     for (auto& name : unmatched) {  // never matched on every rank before the stop
       auto& r = by_name_[name];
       r->state = -1;
+      r->code = TIPS_ERR_MISMATCH;
       r->err = "request " + name + " was not enqueued on every rank before shutdown";
       if (dry_) log_.push_back(name + " ERR " + r->err);
+      if (r->cb) queue_done(r);
     }
     by_name_.clear();
     cv_.notify_all();
+  }
+
+  // (m_ held) hand a finished request with a callback to the completion thread
+  void queue_done(const std::shared_ptr<Req>& r) {
+    if (r->cb_queued) return;
+    r->cb_queued = true;
+    done_q_.push_back(r);
+    done_cv_.notify_all();
+  }
+
+  // The completion thread: in the order requests finished, wait for a device request's work, call
+  // its callback (without the lock: a callback may enqueue more requests) and release its handle.
+  void waiter_loop() {
+    while (true) {
+      std::shared_ptr<Req> r;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        done_cv_.wait(l, [&] { return !done_q_.empty() || waiter_stop_; });
+        if (done_q_.empty()) return;
+        r = done_q_.front();
+        done_q_.pop_front();
+      }
+      int status = 0;
+      std::string msg;
+      if (r->state < 0) {
+        status = r->code;
+        msg = r->err;
+      } else if (r->state == 2) {
+        hipEvent_t ev = r->gev ? r->gev->ev : r->ev;
+        const hipError_t e = hipEventSynchronize(ev);
+        if (e != hipSuccess) {
+          status = TIPS_ERR_HIP;
+          msg = std::string("request ") + r->name + ": " + hipGetErrorString(e);
+        }
+      }
+      r->cb(r->cb_ctx, status, msg.c_str());
+      release(r->handle, r);
+      std::lock_guard<std::mutex> l(m_);
+      cb_called_++;
+    }
   }
 
   // One lockstep cycle: my announce goes up, rank 0's decision comes back.
@@ -569,12 +728,17 @@ class Negotiator {
         }
       }
     }
-    std::vector<int> state(n, 0);
+    std::vector<int> state(n, 0), code(n, TIPS_ERR_MISMATCH);
     std::vector<std::string> msg(n);
     for (size_t i = 0; i < n; i++) {
       state[i] = ds[i].ok ? (dry_ ? 3 : 2) : -1;
       msg[i] = ds[i].err;
     }
+    auto failed = [&](size_t k, int rc) {
+      state[k] = -1;
+      code[k] = rc;
+      msg[k] = last_error();
+    };
     if (!dry_) {
       State& st = S();
       const bool fuse = env_i64("TIPS_NEGOTIATED_FUSION", 1) != 0;
@@ -584,24 +748,52 @@ class Negotiator {
           i++;
           continue;
         }
-        if (reqs[i]->type != TIPS_REQ_ALLREDUCE || reqs[i]->host) {  // broadcast / allgather / host: one at a time
-          if (run_other(*reqs[i], ds[i].sizes) != 0) {
-            state[i] = -1;
-            msg[i] = last_error();
-          } else if (reqs[i]->host) {
-            state[i] = 3;  // finished: the host call returned with out written
+        if (reqs[i]->body) {  // a routed synchronous collective: its own call, here, in rank 0's order
+          const int rc = reqs[i]->body();
+          if (rc != 0) failed(i, rc);
+          else state[i] = 3;
+          i++;
+          continue;
+        }
+        const int dtype = reqs[i]->dtype;
+        if (reqs[i]->type == TIPS_REQ_ALLREDUCE && reqs[i]->host && fuse) {
+          // a run of host allreduces of one dtype: one fused host call (page-locked pieces, H2D ->
+          // allreduce -> D2H pipelined, unpacked into each output), not one staged call per tensor
+          size_t j = i;
+          while (j < n && reqs[j] && state[j] == 2 && !reqs[j]->body && reqs[j]->type == TIPS_REQ_ALLREDUCE &&
+                 reqs[j]->host && reqs[j]->dtype == dtype)
+            j++;
+          if (j - i >= 2) {
+            std::vector<BatchItem> items;
+            for (size_t k = i; k < j; k++) items.push_back(BatchItem{reqs[k]->in, reqs[k]->out, reqs[k]->count});
+            int rc;
+            {
+              std::lock_guard<std::mutex> lk(st.mu);
+              rc = set_device(st);
+              if (rc == 0) rc = fused_allreduce_host(st, items.data(), (int)items.size(), dtype, nullptr);
+            }
+            for (size_t k = i; k < j; k++) {
+              if (rc != 0) failed(k, rc);
+              else state[k] = 3;
+            }
+            i = j;
+            continue;
           }
+        }
+        if (reqs[i]->type != TIPS_REQ_ALLREDUCE || reqs[i]->host) {  // broadcast / allgather / host: one at a time
+          const int rc = run_other(*reqs[i], ds[i].sizes);
+          if (rc != 0) failed(i, rc);
+          else if (reqs[i]->host) state[i] = 3;  // finished: the host call returned with out written
           i++;
           continue;
         }
         std::lock_guard<std::mutex> lk(st.mu);
         const int rc0 = set_device(st);
-        const int dtype = reqs[i]->dtype;
         const int64_t es = tips::dtype_size(dtype);
         size_t j = i;
         int64_t bytes = 0;
-        while (fuse && j < n && reqs[j] && state[j] == 2 && reqs[j]->type == TIPS_REQ_ALLREDUCE && !reqs[j]->host &&
-               reqs[j]->dtype == dtype && reqs[j]->count * es < threshold &&
+        while (fuse && j < n && reqs[j] && state[j] == 2 && !reqs[j]->body && reqs[j]->type == TIPS_REQ_ALLREDUCE &&
+               !reqs[j]->host && reqs[j]->dtype == dtype && reqs[j]->count * es < threshold &&
                round_up(bytes, kAlignBytes) + reqs[j]->count * es <= threshold) {
           bytes = round_up(bytes, kAlignBytes) + reqs[j]->count * es;
           j++;
@@ -616,10 +808,7 @@ class Negotiator {
           if (rc == 0 && hipEventRecord(r->ev, r->stream) != hipSuccess) rc = fail(TIPS_ERR_HIP, "hipEventRecord failed");
         }
         if (rc != 0)
-          for (size_t k = i; k < j; k++) {
-            state[k] = -1;
-            msg[k] = last_error();
-          }
+          for (size_t k = i; k < j; k++) failed(k, rc);
         i = j;
       }
     }
@@ -627,7 +816,9 @@ class Negotiator {
     for (size_t i = 0; i < n; i++)
       if (reqs[i]) {
         reqs[i]->state = state[i];
+        reqs[i]->code = code[i];
         reqs[i]->err = msg[i];
+        if (reqs[i]->cb) queue_done(reqs[i]);
       }
     cv_.notify_all();
   }
@@ -652,11 +843,19 @@ class Negotiator {
       }
       if ((int)counts.size() != S().size) return fail(TIPS_ERR_MISMATCH, "allgather %s: sizes of %zu ranks", r.name.c_str(), counts.size());
       const int64_t bytes = rows * row * es;
+      std::string why;
       if (bytes > 0) {
-        if (!r.alloc) return fail(TIPS_ERR_INVALID_ARG, "allgather %s: no output allocator", r.name.c_str());
-        r.out = r.alloc(r.actx, bytes);
-        if (!r.out) return fail(TIPS_ERR_HIP, "allgather %s: the output allocator returned NULL for %lld B", r.name.c_str(), (long long)bytes);
+        if (!r.alloc) why = "no output allocator";
+        else if (!(r.out = r.alloc(r.actx, bytes))) why = "the output allocator returned NULL for " + std::to_string(bytes) + " B";
       }
+      // every rank learns whether every rank has its output before any transfer: a rank that
+      // failed alone would otherwise leave the others waiting in the gather (one small exchange)
+      const int64_t mine = why.empty() ? 1 : 0;
+      std::vector<int64_t> all((size_t)S().size, 1);
+      TRY(tips_allgather_i64(&mine, 1, all.data()));
+      if (!why.empty()) return fail(TIPS_ERR_HIP, "allgather %s: %s", r.name.c_str(), why.c_str());
+      for (int q = 0; q < S().size; q++)
+        if (!all[q]) return fail(TIPS_ERR_HIP, "allgather %s: rank %d could not allocate its output", r.name.c_str(), q);
       if (r.out_rows) *r.out_rows = rows;
       TRY(tips_allgatherv(r.in, r.count, r.out, counts.data(), r.dtype, r.stream));
     }
@@ -712,11 +911,21 @@ class Negotiator {
   std::vector<hipEvent_t> ev_pool_;
   std::string loop_err_;
   hipStream_t neg_stream_ = nullptr;  // fused batches whose requests came on several streams
+  std::thread waiter_;                // completion callbacks (started by the first tips_on_done)
+  std::deque<std::shared_ptr<Req>> done_q_;
+  std::condition_variable done_cv_;
+  bool waiter_stop_ = false;
+  int64_t cb_called_ = 0;
+
   EventPool join_ev_;
+
+ public:
+  std::atomic<int64_t> sync_seq{0};  // routed synchronous collectives so far: their names
 };
 
 std::mutex g_neg_mu;
-std::unique_ptr<Negotiator> g_neg;
+std::shared_ptr<Negotiator> g_neg;  // (shared: a caller waiting on a request keeps it alive through a shutdown)
+std::string g_neg_failed;           // a failed start's verdict: later named requests fail with it at once
 
 int negotiation_port() {
   return (int)env_i64("TIPS_NEGOTIATION_PORT", env_i64("MASTER_PORT", 29500) + 19);
@@ -730,12 +939,49 @@ const char* master_addr() {
 }  // namespace
 
 int negotiation_stop() {
-  std::unique_ptr<Negotiator> n;
+  std::shared_ptr<Negotiator> n;
   {
     std::lock_guard<std::mutex> l(g_neg_mu);
     n.swap(g_neg);
+    g_neg_failed.clear();
   }
+  g_sync_direct = 0;
   return n ? n->stop() : 0;
+}
+
+// A synchronous collective entry point (tips_allreduce, tips_broadcast, tips_allgatherv, the fused
+// calls, ...) while this rank's negotiation runs - named requests may be in flight, and TF-like
+// callers issue them from other threads - is routed through it: it becomes request "~sync.<k>" (k
+// counts this rank's routed calls; announced with its type, dtype and shape, so rank 0 checks it
+// like any request), and its body runs on the negotiation thread when rank 0's order reaches it.
+// So every RCCL call of a rank is issued from one thread in one order, the same on every rank, as
+// the reference's coordinator issues every collective (coordinator.cc:355-513). Returns false when
+// the call is to run directly (no negotiation, one rank, or already on the negotiation thread);
+// else true, with *rc = the body's status (its error message in tips_last_error). A device call
+// returns once its work is queued on the caller's stream, a host call once it is done.
+bool route_collective(int type, int dtype, const int64_t* shape, int ndim, int root, const std::function<int()>& body,
+                      int* rc) {
+  if (tl_negotiation_thread) return false;
+  std::shared_ptr<Negotiator> n;
+  {
+    std::lock_guard<std::mutex> l(g_neg_mu);
+    n = g_neg;
+  }
+  if (!n || !n->running()) {
+    State& st = S();
+    if (st.initialized && st.size > 1) g_sync_direct++;
+    return false;
+  }
+  const std::string name = "~sync." + std::to_string((long long)n->sync_seq++);
+  const int64_t h = n->enqueue(name, nullptr, nullptr, shape, ndim, dtype, nullptr, type, root, nullptr, nullptr,
+                               nullptr, body);
+  if (h < 0) {
+    *rc = (int)h;
+    return true;
+  }
+  const int w = n->poll(h, true, /*routed=*/true);
+  *rc = w == 1 ? 0 : w;
+  return true;
 }
 
 }  // namespace rt
@@ -743,32 +989,40 @@ int negotiation_stop() {
 
 using namespace tips::rt;
 
-extern "C" {
 
 namespace {
 
-Negotiator* negotiator() {  // started by the first named request (collective)
+std::shared_ptr<Negotiator> negotiator(int* code) {  // started by the first named request (collective)
   std::lock_guard<std::mutex> l(g_neg_mu);
   if (!g_neg) {
+    if (!g_neg_failed.empty()) {
+      *code = fail(TIPS_ERR_MISMATCH, "%s", g_neg_failed.c_str());
+      return nullptr;
+    }
     State& st = S();
     int rank, size;
     uint64_t key;
     {
       std::lock_guard<std::mutex> lk(st.mu);
       if (!st.initialized) {
-        fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+        *code = fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
         return nullptr;
       }
       rank = st.rank;
       size = st.size;
       key = st.peer_key;  // the job's unique-id hash: a hello from another job is refused
     }
-    auto neg = std::make_unique<Negotiator>();
-    if (neg->start(rank, size, master_addr(), negotiation_port(), false, (int)env_i64("TIPS_NEGOTIATION_TIMEOUT", 600), key))
+    auto neg = std::make_shared<Negotiator>();
+    const int rc = neg->start(rank, size, master_addr(), negotiation_port(), false,
+                              (int)env_i64("TIPS_NEGOTIATION_TIMEOUT", 600), key, g_sync_direct.load());
+    if (rc) {
+      *code = rc;
+      if (rc == TIPS_ERR_MISMATCH) g_neg_failed = last_error();
       return nullptr;
+    }
     g_neg = std::move(neg);
   }
-  return g_neg.get();
+  return g_neg;
 }
 
 int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
@@ -785,12 +1039,20 @@ int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t
     const int size = tips_size();
     if (root < 0 || (size > 0 && root >= size)) return fail(TIPS_ERR_INVALID_ARG, "root rank %d out of range", root);
   }
-  Negotiator* n = negotiator();
-  if (!n) return TIPS_ERR_NOT_INITIALIZED;
+  int code = TIPS_ERR_NOT_INITIALIZED;
+  std::shared_ptr<Negotiator> n = negotiator(&code);
+  if (!n) return code;
   return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, type, root, alloc, actx, out_rows);
 }
 
+std::shared_ptr<Negotiator> current() {
+  std::lock_guard<std::mutex> l(g_neg_mu);
+  return g_neg;
+}
+
 }  // namespace
+
+extern "C" {
 
 int64_t tips_enqueue_allreduce(const char* name, const void* in, void* out, int64_t count, int dtype, void* stream) {
   if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request");
@@ -812,21 +1074,31 @@ int64_t tips_enqueue_allgather(const char* name, const void* in, const int64_t* 
   return enqueue_named(name, in, nullptr, shape, ndim, dtype, stream, TIPS_REQ_ALLGATHER, 0, alloc, ctx, out_rows);
 }
 
+
 int tips_poll(int64_t handle) {
-  std::lock_guard<std::mutex> l(g_neg_mu);
-  if (!g_neg) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
-  return g_neg->poll(handle, false);
+  auto n = current();
+  if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
+  return n->poll(handle, false);
 }
 
 int tips_wait(int64_t handle) {
-  Negotiator* n;
-  {
-    std::lock_guard<std::mutex> l(g_neg_mu);
-    if (!g_neg) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
-    n = g_neg.get();
-  }
+  auto n = current();
+  if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
   const int rc = n->poll(handle, true);
   return rc == 1 ? 0 : rc;
+}
+
+int tips_on_done(int64_t handle, tips_done_fn fn, void* ctx) {
+  if (!fn) return fail(TIPS_ERR_INVALID_ARG, "null completion callback");
+  auto n = current();
+  if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
+  return n->on_done(handle, fn, ctx);
+}
+
+int tips_net_stats(int64_t* self_connects_refused, int64_t* unconfirmed_joins_refused) {
+  if (self_connects_refused) *self_connects_refused = tips::net::self_connects().load();
+  if (unconfirmed_joins_refused) *unconfirmed_joins_refused = tips::net::unconfirmed_joins().load();
+  return 0;
 }
 
 int tips_enqueue_allreduce_n(const char* const* names, const void* const* ins, void* const* outs, const int64_t* counts,
@@ -883,53 +1155,120 @@ int tips_wait_n(const int64_t* handles, int n) {
   return rc ? fail(rc, "%s", first_err.c_str()) : 0;
 }
 
+namespace {
+
+struct SelftestCount {
+  std::atomic<int64_t> done{0};
+};
+
+void selftest_done(void* ctx, int status, const char* message) {
+  (void)status;
+  (void)message;
+  static_cast<SelftestCount*>(ctx)->done++;
+}
+
+}  // namespace
+
 int tips_negotiation_selftest(int rank, int size, const char* host, int port, const char* requests, char* out,
                               int64_t cap) {
   if (size < 1 || rank < 0 || rank >= size || !requests || !out || cap < 1)
     return fail(TIPS_ERR_INVALID_ARG, "bad selftest args");
-  Negotiator neg;
-  TRY(neg.start(rank, size, (host && *host) ? host : "127.0.0.1", port, true, 120));
-  std::vector<int64_t> handles;
-  const char* p = requests;
-  const auto t0 = std::chrono::steady_clock::now();
   // lines: "name dtype count [d0,d1,...|-] [ar|ag|bc:ROOT]" (shape: default [count]; request type:
-  // default allreduce), "@sleep ms", "@wait" (all so far resolved), "@mark" (log "# mark us")
-  while (*p) {
+  // default allreduce), "@sleep ms", "@wait" (all so far resolved), "@mark" (log "# mark us"),
+  // "@synccount N" (this rank claims N synchronous collectives before the join). A line "tK: ..."
+  // belongs to thread K: threads 1.. issue their lines concurrently with the main thread's (thread
+  // 0), as a framework's executor threads issue ops, and every request then completes through a
+  // tips_on_done callback (its "@wait" waits for its own callbacks); the log ends "callbacks N".
+  std::vector<std::vector<std::string>> per(1);
+  int64_t synccount = 0;
+  for (const char* p = requests; *p;) {
     const char* e = strchr(p, '\n');
     std::string line(p, e ? (size_t)(e - p) : strlen(p));
     p = e ? e + 1 : p + line.size();
     if (line.empty()) continue;
-    char nm[256], dims[256] = "", kind[64] = "ar";
-    long long dt = 0, cnt = 0;
-    if (line.rfind("@sleep ", 0) == 0) {
-      std::this_thread::sleep_for(std::chrono::milliseconds(atoi(line.c_str() + 7)));
-    } else if (line == "@wait") {
-      for (int64_t h : handles) (void)neg.poll(h, true);
-      handles.clear();
-    } else if (line == "@mark") {
-      const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
-      neg.note("# mark " + std::to_string((long long)us.count()));
-    } else if (sscanf(line.c_str(), "%255s %lld %lld %255s %63s", nm, &dt, &cnt, dims, kind) >= 3) {
-      std::vector<int64_t> shape;
-      if (strcmp(dims, "-") == 0) dims[0] = 0;
-      const int type = strncmp(kind, "ag", 2) == 0 ? TIPS_REQ_ALLGATHER : strncmp(kind, "bc", 2) == 0 ? TIPS_REQ_BROADCAST
-                                                                                                  : TIPS_REQ_ALLREDUCE;
-      const int root = (type == TIPS_REQ_BROADCAST && kind[2] == ':') ? atoi(kind + 3) : 0;
-      for (const char* q = dims; *q;) {
-        shape.push_back(strtoll(q, nullptr, 10));
-        q = strchr(q, ',');
-        q = q ? q + 1 : "";
-      }
-      if (shape.empty()) shape.push_back(cnt);
-      const int64_t h = neg.enqueue(nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr, type, root);
-      if (h < 0) return (int)h;
-      handles.push_back(h);
+    if (line.rfind("@synccount ", 0) == 0) {
+      synccount = atoll(line.c_str() + 11);
+      continue;
     }
+    size_t k = 0;
+    if (line[0] == 't' && line.find(':') != std::string::npos && isdigit((unsigned char)line[1])) {
+      k = (size_t)atoi(line.c_str() + 1);
+      line = line.substr(line.find(':') + 1);
+      while (!line.empty() && line[0] == ' ') line.erase(0, 1);
+      if (k > 64) return fail(TIPS_ERR_INVALID_ARG, "selftest: thread %zu", k);
+    }
+    if (per.size() <= k) per.resize(k + 1);
+    per[k].push_back(line);
   }
-  const int rc = neg.stop();  // collective: requests every rank announced are decided before it returns
-  for (int64_t h : handles) (void)neg.poll(h, false);
+  const bool cbs = per.size() > 1;
+  Negotiator neg;
+  TRY(neg.start(rank, size, (host && *host) ? host : "127.0.0.1", port, true, 120, 0, synccount));
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<SelftestCount> counts(per.size());
+  std::vector<int> issued(per.size(), 0), rcs(per.size(), 0);
+  auto run = [&](size_t k) {
+    std::vector<int64_t> handles;
+    for (const std::string& line : per[k]) {
+      char nm[256], dims[256] = "", kind[64] = "ar";
+      long long dt = 0, cnt = 0;
+      if (line.rfind("@sleep ", 0) == 0) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(atoi(line.c_str() + 7)));
+      } else if (line == "@wait") {
+        if (cbs) {
+          while (counts[k].done.load() < issued[k]) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        } else {
+          for (int64_t h : handles) (void)neg.poll(h, true);
+          handles.clear();
+        }
+      } else if (line == "@mark") {
+        const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
+        neg.note("# mark " + std::to_string((long long)us.count()));
+      } else if (sscanf(line.c_str(), "%255s %lld %lld %255s %63s", nm, &dt, &cnt, dims, kind) >= 3) {
+        std::vector<int64_t> shape;
+        if (strcmp(dims, "-") == 0) dims[0] = 0;
+        const int type = strncmp(kind, "ag", 2) == 0 ? TIPS_REQ_ALLGATHER : strncmp(kind, "bc", 2) == 0 ? TIPS_REQ_BROADCAST
+                                                                                                    : TIPS_REQ_ALLREDUCE;
+        const int root = (type == TIPS_REQ_BROADCAST && kind[2] == ':') ? atoi(kind + 3) : 0;
+        for (const char* q = dims; *q;) {
+          shape.push_back(strtoll(q, nullptr, 10));
+          q = strchr(q, ',');
+          q = q ? q + 1 : "";
+        }
+        if (shape.empty()) shape.push_back(cnt);
+        const int64_t h = neg.enqueue(nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr, type, root);
+        if (h < 0) {
+          rcs[k] = (int)h;
+          return;
+        }
+        if (cbs) {
+          issued[k]++;
+          if (neg.on_done(h, selftest_done, &counts[k]) != 0) {
+            rcs[k] = TIPS_ERR_INVALID_ARG;
+            return;
+          }
+        } else {
+          handles.push_back(h);
+        }
+      }
+    }
+    if (!cbs)
+      for (int64_t h : handles) (void)neg.poll(h, false);
+  };
+  std::vector<std::thread> threads;
+  for (size_t k = 1; k < per.size(); k++) threads.emplace_back(run, k);
+  run(0);
+  for (auto& t : threads) t.join();
+  const int rc = neg.stop();  // collective: requests every rank announced are decided before it returns;
+                              // the completion thread has called every callback when it returns
+  for (int r : rcs)
+    if (r) return r;
   std::string log;
-  for (auto& s : neg.log()) log += s + "\n";
+  for (auto& l : neg.log()) log += l + "\n";
+  if (cbs) {
+    int64_t n = 0;
+    for (auto& c : counts) n += c.done.load();
+    log += "callbacks " + std::to_string((long long)n) + "\n";
+  }
   snprintf(out, (size_t)cap, "%s", log.c_str());
   return rc;
 }

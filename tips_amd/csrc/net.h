@@ -13,6 +13,9 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <stdlib.h>
+
+#include <atomic>
 #include <string>
 
 namespace tips {
@@ -111,6 +114,51 @@ inline bool connected_to_self(int fd) {
 inline void set_nodelay(int fd) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+}
+
+// Join counters (tips_net_stats): connections a joining rank dropped because they reached itself,
+// and connections rank 0 dropped because the joiner never confirmed them.
+inline std::atomic<int64_t>& self_connects() {
+  static std::atomic<int64_t> n{0};
+  return n;
+}
+inline std::atomic<int64_t>& unconfirmed_joins() {
+  static std::atomic<int64_t> n{0};
+  return n;
+}
+
+// A joining rank's connect to sa, for both joins (bootstrap, negotiation). Returns a connected
+// socket that did not reach itself, or -1. TIPS_TEST_SELF_CONNECT=n (tests only): the first n
+// attempts of the process bind their source port to the destination port first, so that with no
+// listener there yet the connect completes as a TCP simultaneous open with itself - the case the
+// check below exists for, made deterministic.
+inline int connect_peer(const sockaddr_in& sa) {
+  static std::atomic<int> forced{-1};
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  if (fd < 0) return -1;
+  if (forced.load() < 0) {
+    const char* v = getenv("TIPS_TEST_SELF_CONNECT");
+    int expect = -1;
+    forced.compare_exchange_strong(expect, v ? atoi(v) : 0);
+  }
+  if (forced.load() > 0) {
+    forced--;
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in me = sa;
+    me.sin_addr.s_addr = sa.sin_addr.s_addr;
+    (void)::bind(fd, reinterpret_cast<const sockaddr*>(&me), sizeof me);  // (fails once a listener holds the port)
+  }
+  if (::connect(fd, reinterpret_cast<const sockaddr*>(&sa), sizeof sa) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  if (connected_to_self(fd)) {
+    self_connects()++;
+    ::close(fd);
+    return -1;
+  }
+  return fd;
 }
 
 }  // namespace net

@@ -242,8 +242,9 @@ int peer_allgatherv(State& st, const char* in, char* out, const int64_t* bytes, 
 // host_staging.cc: host-resident allreduce over pipelined pieces, caller holds st.mu
 int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, int dtype);
 // host_staging.cc: many host tensors in one flat stream of page-locked pieces (pack by host threads,
-// H2D -> allreduce -> D2H per piece, unpack); returns when every out is written. Caller holds st.mu.
-int fused_allreduce_host(State& st, const struct BatchItem* items, int n, int dtype);
+// H2D -> allreduce -> D2H per piece, unpack into every out - or, with `flat`, the sums into one host
+// buffer of fused_layout's layout); returns when they are written. Caller holds st.mu.
+int fused_allreduce_host(State& st, const struct BatchItem* items, int n, int dtype, char* flat);
 void host_release(State& st);  // (shutdown: the pool and the page-locked pieces)
 // fusion.cc: allreduce n same-dtype device tensors, in[i] -> out[i] (in == out allowed), packed
 // into buckets of at most the fusion threshold: pack -> one allreduce per bucket -> unpack.
@@ -266,6 +267,13 @@ void fusion_release(State& st);  // (shutdown)
 int check_records(const int64_t* t, int p);
 // negotiate.cc: stop the negotiation thread (collective; call without holding st.mu)
 int negotiation_stop();
+// negotiate.cc: a synchronous collective entry point calls this first (without holding st.mu).
+// While this rank's negotiation runs, the call is routed through it - announced as a request of
+// `type` with the given dtype / shape / root, its `body` (the entry point itself) run on the
+// negotiation thread in rank 0's order - and true is returned with *rc = the body's status. False:
+// run directly (no negotiation, or already on the negotiation thread).
+bool route_collective(int type, int dtype, const int64_t* shape, int ndim, int root, const std::function<int()>& body,
+                      int* rc);
 
 // ---------------------------------------------------------------------------
 // host staging: the reference's ops work on host (TF CPU) tensors (ops.cc:88-90)

@@ -242,6 +242,11 @@ int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, 
   TRY(check_dtype(dtype));
   if (op != TIPS_OP_SUM) return fail(TIPS_ERR_UNSUPPORTED, "only SUM is implemented (op %d)", op);
   if (count < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count");
+  int routed_rc;
+  const int64_t shape[1] = {count};
+  if (route_collective(TIPS_REQ_ALLREDUCE, dtype, shape, 1, 0,
+                       [&] { return tips_allreduce(in, out, count, dtype, op, stream); }, &routed_rc))
+    return routed_rc;
   State& st = S();
   std::lock_guard<std::mutex> lk(st.mu);
   if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");

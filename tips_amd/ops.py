@@ -304,6 +304,108 @@ def fused_allreduce_host(tensor_list, out_list=None):
     return outs
 
 
+class _HostFlatOutputs(object):
+    """Output sets of fused_allreduce_host_flat for one host list signature (numpy, or CPU torch):
+    one flat host buffer laid out as tips_fused_layout, page-locked once (tips_host_register) so
+    the device writes the sums straight into it, and one view of it per tensor. A set is handed out
+    again once every output of it has been released (as _FlatOutputs: no reference to a view, no
+    other array or tensor on its memory)."""
+
+    MAX_SETS = 4
+
+    def __init__(self, shapes, numels, code, dtype, is_torch):
+        import ctypes
+        cp, _keep = _lib.i64_array(numels)
+        offs = (ctypes.c_int64 * len(numels))()
+        self.total = max(256, _lib.check("tips_fused_layout", _lib.lib().tips_fused_layout(cp, len(numels), code, offs)))
+        self.cp = _lib.i64_array(numels)
+        self.code, self.numels, self.shapes, self.dtype, self.is_torch = code, numels, shapes, dtype, is_torch
+        self.es = _itemsize(dtype, is_torch)
+        self.offs = [int(o) for o in offs]
+        self.sets = []
+
+    def _free(self, s):
+        import sys
+        flat, views, c0, rc0 = s
+        if self.is_torch:
+            import torch
+            if torch._C._storage_Use_Count(flat.untyped_storage()._cdata) != c0:
+                return False
+        elif sys.getrefcount(flat) != c0:
+            return False
+        return max(map(sys.getrefcount, views), default=rc0) <= rc0
+
+    def take(self):
+        import sys
+        for s in self.sets:
+            if self._free(s):
+                return s[0], s[1]
+        if self.is_torch:
+            import torch
+            flat = torch.empty(self.total, dtype=torch.uint8)
+            views = [flat[o:o + n * self.es].view(self.dtype).view(shp)
+                     for o, n, shp in zip(self.offs, self.numels, self.shapes)]
+        else:
+            import numpy as np
+            flat = np.empty(self.total, dtype=np.uint8)
+            views = [flat[o:o + n * self.es].view(self.dtype).reshape(shp)
+                     for o, n, shp in zip(self.offs, self.numels, self.shapes)]
+        if len(self.sets) < self.MAX_SETS:
+            # a kept set is page-locked for the life of the process (the device's D2H lands in it
+            # directly); one past MAX_SETS is not (it is freed with its last output)
+            _lib.call("tips_host_register", tensors.data_ptr(flat), self.total)
+            if self.is_torch:
+                import torch
+                c0 = torch._C._storage_Use_Count(flat.untyped_storage()._cdata)
+            else:
+                c0 = sys.getrefcount(flat)
+            self.sets.append((flat, views, c0, max(map(sys.getrefcount, views), default=0)))
+            return self.sets[-1][0:2]
+        return flat, views
+
+
+def _itemsize(dtype, is_torch):
+    if is_torch:
+        import torch
+        return torch.empty((), dtype=dtype).element_size()
+    import numpy as np
+    return np.dtype(dtype).itemsize
+
+
+_HOST_FLAT = {}  # (dtype, torch?, shapes) -> _HostFlatOutputs
+
+
+def fused_allreduce_host_flat(tensor_list):
+    """Out-of-place SUM of a list of same-dtype HOST tensors (numpy / CPU torch), the outputs views
+    of one page-locked flat host buffer (tips_fused_allreduce_host_flat): host threads pack the
+    inputs into page-locked pieces, each piece H2D -> allreduce -> D2H straight into the output
+    buffer - no unpack. The buffer and its views are reused by a later call of the same list
+    signature once the caller has released every output. Returns when the outputs are written."""
+    basics.init()
+    if not tensor_list:
+        return []
+    code = tensors.dtype_code(tensor_list[0])
+    srcs = []
+    for t in tensor_list:
+        if tensors.is_device(t):
+            raise ValueError("fused_allreduce_host_flat needs host tensors")
+        if tensors.dtype_code(t) != code:
+            raise TypeError("fused_allreduce_host_flat needs one dtype per call")
+        srcs.append(tensors.contiguous(t))
+    is_torch = tensors.is_torch(srcs[0])
+    shapes = tuple(tuple(s.shape) for s in srcs)
+    key = (str(srcs[0].dtype), is_torch, shapes)
+    fo = _HOST_FLAT.get(key)
+    if fo is None:
+        if len(_HOST_FLAT) >= 16:
+            _HOST_FLAT.pop(next(iter(_HOST_FLAT)))
+        fo = _HOST_FLAT[key] = _HostFlatOutputs(shapes, [tensors.numel(s) for s in srcs], code, srcs[0].dtype, is_torch)
+    flat, views = fo.take()
+    pi, _k1 = _lib.ptr_array([tensors.data_ptr(s) for s in srcs])
+    _lib.call("tips_fused_allreduce_host_flat", pi, fo.cp[0], len(srcs), code, tensors.data_ptr(flat))
+    return list(views)
+
+
 def fusion_stats():
     """{layouts_built, layout_hits, tables_built, table_hits} of this process's fusion caches
     (tips_fusion_stats): layouts depend on the counts only, tables on the pointers."""
