@@ -563,7 +563,7 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
     grads = [[p_.grad for p_ in ps] for ps in params]
     opts = [tips_amd.DistributedOptimizer(torch.optim.SGD(ps, lr=0.0)) for ps in params]
     if world > 1:
-        calls = {"optimizer": lambda i: opts[i].synchronize(), "allreduce_grads": lambda i: tips_amd.allreduce_grads(grads[i])}
+        calls = {"optimizer": lambda i: opts[i].synchronize(whole_groups=True), "allreduce_grads": lambda i: tips_amd.allreduce_grads(grads[i])}
         what = "DistributedOptimizer.synchronize() / tips_amd.allreduce_grads"
     else:
         from tips_amd.ops import FusedList
@@ -578,6 +578,8 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
                 "(no device work at all on one rank), FusedList.allreduce_ over separately allocated gradients "
                 "(pack + unpack), and allreduce_grads' N > 1 body (_reduce_grads: pack into one flat output, "
                 "per bucket)")
+    import warnings  # (the optimizer leg calls synchronize() repeatedly with no backward: it warns)
+    warnings.filterwarnings("ignore", message="DistributedOptimizer.synchronize")
     out = {"calls": what, "bytes_per_rank": sum(sizes) * 4, "fixed_view_ms": round(fixed_ms, 4)}
     ref = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads] if world == 1 else None
     for name, fn in calls.items():

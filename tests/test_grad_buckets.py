@@ -148,16 +148,26 @@ def test_unused_parameter_contributes_zeros_and_stays_none():
     gb.remove()
 
 
-def test_synchronize_without_backward_reduces_each_group_once():
+def test_synchronize_without_backward_issues_bucket_by_bucket_unless_told():
+    """How far the hooks got is rank-local, so synchronize() always issues the rest bucket by
+    bucket; one allreduce per group only on the caller's word that no backward ran anywhere."""
     m = make_model()
     gb, calls = buckets_for(m, bucket_bytes=512)
     for p in m.parameters():
         p.grad = torch.full_like(p, 2.0)
     gb.synchronize()
+    assert gb.last_issue_log == list(range(len(gb.buckets))) and len(calls) == len(gb.buckets) > 1
+    for p in m.parameters():
+        assert torch.equal(p.grad, torch.full_like(p, 2.0 * RANKS))
+    calls.clear()
+    gb.synchronize(whole_groups=True)
     assert len(calls) == 1 and calls[0] == sum(padded(p) for p in m.parameters())
     assert gb.last_issue_log == [("group", (torch.float32, torch.device("cpu")))]
     for p in m.parameters():
-        assert torch.equal(p.grad, torch.full_like(p, 2.0 * RANKS))
+        assert torch.equal(p.grad, torch.full_like(p, 2.0 * RANKS ** 2))
+    loss_of(m).backward()  # the hooks issue buckets: whole_groups would not pair across ranks
+    with pytest.raises(RuntimeError, match="would not pair"):
+        gb.synchronize(whole_groups=True)
     gb.remove()
 
 
@@ -212,7 +222,8 @@ def _gloo_worker(rank, world, port, q):
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     from tips_amd.optim import _GradBuckets
     try:
         m = make_model()
@@ -237,7 +248,24 @@ def _gloo_worker(rank, world, port, q):
             g = local_grads(seeds=(10 + r,))
             exp = g if exp is None else [a + b for a, b in zip(exp, g)]
         ok2 = all(torch.allclose(p.grad, e, rtol=1e-6, atol=1e-6) for p, e in zip(m.parameters(), exp))
-        q.put((rank, ok1, ok2, len(gb.buckets)))
+        # a parameter that gets a gradient on some ranks only, in the FIRST bucket (the last
+        # parameter): on rank 0 the hooks issue nothing during backward, elsewhere every bucket.
+        # The allreduces still pair (a whole-group allreduce on rank 0 would not: gloo raises on
+        # the size mismatch, or the ranks hang until the timeout).
+        m3 = make_model()
+        extra = torch.nn.Parameter(torch.full((7,), 1.0))
+        ps3 = list(m3.parameters()) + [extra]
+        gb3 = _GradBuckets(ps3, 1024, 1, False, issue=lambda f: dist.all_reduce(f))
+        out = m3(torch.randn(5, 16, generator=torch.Generator().manual_seed(30 + rank))).pow(2).sum()
+        if rank != 0:
+            out = out + (extra * float(rank)).sum()
+        out.backward()
+        hooks_issued = list(gb3.issue_log)
+        gb3.synchronize()
+        ok3 = torch.equal(gb3.view(extra), torch.full((7,), float(sum(range(world)))))
+        ok3 = ok3 and (extra.grad is None) == (rank == 0)
+        ok3 = ok3 and (hooks_issued == []) == (rank == 0) and gb3.last_issue_log == list(range(len(gb3.buckets)))
+        q.put((rank, ok1, ok2 and ok3, len(gb.buckets)))
     finally:
         dist.destroy_process_group()
 

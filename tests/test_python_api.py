@@ -218,6 +218,51 @@ def test_distributed_optimizer_backward_passes_and_validation(monkeypatch):
         tips_amd.DistributedOptimizer(object())
 
 
+def test_distributed_optimizer_synchronize_then_step(monkeypatch):
+    """step() skips its own reduction only after a synchronize() of this very pass with no backward
+    after it (the clip-gradients pattern). A synchronize() followed by another backward without a
+    step (evaluation), or one in an earlier accumulation pass, does not excuse step(): it reduces
+    again, with a warning; a second synchronize() without a backward in between warns too."""
+    import warnings
+    import torch
+    import tips_amd
+    _fake_two_ranks(monkeypatch)
+    calls = []
+    monkeypatch.setattr(tips_amd, "allreduce", lambda t, **kw: calls.append(1) or t)
+    m = _toy_model()
+    x = torch.randn(5, 4)
+    n = len(list(m.parameters()))
+    opt = tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.0))
+    m(x).sum().backward()
+    opt.synchronize()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        opt.step()  # the clip pattern: reduced once, in synchronize()
+    assert len(calls) == n
+    opt.zero_grad()
+    m(x).sum().backward()
+    opt.synchronize()  # e.g. an evaluation that never steps
+    opt.zero_grad()
+    m(x).sum().backward()
+    with pytest.warns(UserWarning, match="before a later backward"):
+        opt.step()
+    assert len(calls) == 3 * n
+    opt.synchronize()
+    with pytest.warns(UserWarning, match="called again with no backward"):
+        opt.synchronize()
+    assert len(calls) == 5 * n
+    calls.clear()
+    acc = tips_amd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.0), backward_passes_per_step=2)
+    opt.zero_grad()
+    m(x).sum().backward()
+    acc.synchronize()  # in the first (accumulation) pass
+    acc.step()
+    m(x).sum().backward()
+    with pytest.warns(UserWarning, match="earlier accumulation pass"):
+        acc.step()
+    assert len(calls) == 2 * n
+
+
 def test_distributed_gradient_tape(monkeypatch):
     """DistributedGradientTape (reference __init__.py:460-569): gradient() differentiates, then sums
     the gradients over the ranks (a SUM for op=Average too); an unused source stays None; a single

@@ -3,6 +3,8 @@
 // host memory and must return there: this file moves them through HBM with
 // both PCIe directions and the device allreduce overlapped.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <thread>
 
@@ -242,10 +244,28 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     });
   };
   const int lag = direct_out ? np : 1;  // piece i - lag is unpacked while piece i is on the link
+  // TIPS_HOST_TRACE=1: where one call's time goes (stderr), for tuning the piece and thread counts
+  static const bool trace = env_i64("TIPS_HOST_TRACE", 0) != 0;
+  double t_pack = 0, t_wait = 0, t_unpack = 0, t_issue = 0;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto since = [](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count();
+  };
+  auto report = [&] {
+    if (trace)
+      fprintf(stderr, "[tips host] bytes %lld pieces %d threads %d direct_out %d: pack %.0f us, wait %.0f us, "
+              "unpack %.0f us, issue %.0f us, total %.0f us\n", (long long)total, np, nthreads, (int)direct_out,
+              t_pack, t_wait, t_unpack, t_issue, since(t_start));
+  };
   for (int i = 0; i < np; i++) {
     const int64_t off = (int64_t)i * piece, len = std::min(piece, total - off);
+    auto t0 = std::chrono::steady_clock::now();
     if (i >= R) HIP_TRY(hipEventSynchronize(ev[3 * (i - R)]));  // slot i % R: its last H2D has read it
+    t_wait += since(t0);
+    t0 = std::chrono::steady_clock::now();
     host_copy(i, true);
+    t_pack += since(t0);
+    t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice,
                            st.h2d_stream));
     HIP_TRY(hipEventRecord(ev[3 * i], st.h2d_stream));
@@ -257,19 +277,32 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     char* d2h = direct_out ? flat + off : pin_out + (int64_t)(i % R) * piece;
     HIP_TRY(hipMemcpyAsync(d2h, dev + off, (size_t)len, hipMemcpyDeviceToHost, st.d2h_stream));
     HIP_TRY(hipEventRecord(ev[3 * i + 2], st.d2h_stream));
+    t_issue += since(t0);
     if (i >= lag) {
+      t0 = std::chrono::steady_clock::now();
       HIP_TRY(hipEventSynchronize(ev[3 * (i - lag) + 2]));
+      t_wait += since(t0);
+      t0 = std::chrono::steady_clock::now();
       host_copy(i - lag, false);
+      t_unpack += since(t0);
     }
   }
   if (direct_out) {
+    auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipStreamSynchronize(st.d2h_stream));
+    t_wait += since(t0);
+    report();
     return 0;
   }
   for (int j = std::max(0, np - lag); j < np; j++) {
+    auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventSynchronize(ev[3 * j + 2]));
+    t_wait += since(t0);
+    t0 = std::chrono::steady_clock::now();
     host_copy(j, false);
+    t_unpack += since(t0);
   }
+  report();
   return 0;
 }
 

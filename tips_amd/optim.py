@@ -51,11 +51,13 @@ class _GradBuckets(object):
 
     Ranks must issue the same allreduces in the same order. Buckets are therefore issued strictly
     in index order (a bucket whose gradients are ready waits for every earlier bucket), and the
-    layout depends only on the parameter list. synchronize() issues whatever backward did not
-    (parameters without a gradient contribute zeros), then makes the caller's stream wait for the
-    side streams. A group none of whose buckets was issued during backward (synchronize() called
-    without a backward, as bench.py's optimizer leg does) is reduced as one allreduce of its
-    whole flat buffer. `issue(flat_slice)` is the in-place allreduce (a test may pass its own)."""
+    layout depends only on the parameter list. synchronize() issues whatever backward did not,
+    bucket by bucket in index order (parameters without a gradient contribute zeros), then makes
+    the caller's stream wait for the side streams. How far the hooks got is rank-local (a parameter
+    may get no gradient on one rank only), so the bucket-by-bucket sequence is what keeps every
+    rank's allreduces paired. Only a caller that knows no backward ran on any rank (bench.py's
+    optimizer leg) may ask for whole_groups=True: one allreduce of each group's flat buffer.
+    `issue(flat_slice)` is the in-place allreduce (a test may pass its own)."""
 
     def __init__(self, params, bucket_bytes, passes, average, issue=None):
         import threading
@@ -215,21 +217,25 @@ class _GradBuckets(object):
         self._issue_range(key, s, e, b)
         self.issued[b] = True
 
-    def synchronize(self):
+    def synchronize(self, whole_groups=False):
         """Issue every bucket backward did not, in index order; the caller's streams then wait for
-        the side streams. Returns the parameters whose gradient came sparse (for allreduce_grads)."""
+        the side streams. Returns the parameters whose gradient came sparse (for allreduce_grads).
+        whole_groups=True (no backward ran on ANY rank since the last synchronize, so no bucket was
+        issued anywhere): one allreduce per group instead of one per bucket."""
         torch = self._torch
         err = self.error
         with self._lock:
             for p in self.params:
                 if id(p) not in self.seen:
                     self._adopt(p)  # no gradient: zeros; otherwise the view (copied in if needed)
-            touched = {self.buckets[b][0] for b in range(len(self.buckets)) if self.issued[b]}
+            if whole_groups and any(self.issued):
+                err = err or ("synchronize(whole_groups=True) after a backward that issued buckets: "
+                              "the ranks' allreduces would not pair")
             whole = set()
             for b in range(self.next, len(self.buckets)):
                 key = self.buckets[b][0]
-                if key not in touched:
-                    if key not in whole:  # nothing of this group issued yet: one allreduce of all of it
+                if whole_groups and not any(self.issued):
+                    if key not in whole:
                         whole.add(key)
                         self._issue_range(key, 0, self.groups[key]["n"], ("group", key))
                 elif not self.issued[b]:
@@ -269,7 +275,10 @@ class _DistributedOptimizer(object):
         if self._passes < 1:
             raise ValueError("backward_passes_per_step must be >= 1")
         self._buckets = None
-        self._synchronized = False
+        # synchronize() bookkeeping: the step count and gradient-event count it ran at. step() skips
+        # its own reduction only for a synchronize() of this very pass with no backward after it.
+        self._sync_at = None
+        self._grad_events = 0
         from . import Compression
         if (os.environ.get("TIPS_OVERLAP_BACKWARD", "1") != "0" and self._bucket_view
                 and self._compression is Compression.none and not sparse_as_dense):
@@ -283,6 +292,18 @@ class _DistributedOptimizer(object):
                 self._buckets = _GradBuckets(ps, max(1, int(mib * (1 << 20))), self._passes, self._average_aggregated)
                 self._buckets.active = self._overlap_active
                 self._buckets.final_pass = lambda: (self._calls + 1) % self._passes == 0
+        import weakref
+        ref = weakref.ref(self)
+
+        def count(p, _ref=ref):
+            o = _ref()
+            if o is not None:
+                o._grad_events += 1
+
+        self._count_handles = [p.register_post_accumulate_grad_hook(count)
+                               for p in {id(p): p for g in optimizer.param_groups for p in g["params"]
+                                         if p.requires_grad}.values()]
+        weakref.finalize(self, _remove_hooks, list(self._count_handles))
 
     @staticmethod
     def _overlap_active():
@@ -312,7 +333,7 @@ class _DistributedOptimizer(object):
     def _params_with_grad(self):
         return [p for g in self._optimizer.param_groups for p in g["params"] if p.grad is not None]
 
-    def synchronize(self):
+    def synchronize(self, whole_groups=False):
         """Allreduce every parameter's .grad (compute_gradients, __init__.py:296-310).
 
         Dense contiguous device gradients without compression are summed IN PLACE: with gradient
@@ -321,15 +342,25 @@ class _DistributedOptimizer(object):
         allreduce per bucket, unpack straight back into .grad - 4 x the gradient bytes of HBM
         traffic). With backward-overlapped buckets (_GradBuckets, the default at N > 1) most of
         that was issued during backward, and the end of backward already ordered the caller's
-        stream after it; this issues the rest and joins. step() does not reduce again in an
-        iteration where the caller already called synchronize() (to clip gradients, say)."""
+        stream after it; this issues the rest and joins, bucket by bucket (the same sequence on
+        every rank whatever its hooks reached). whole_groups=True is for a caller that knows no
+        backward ran on any rank since the last reduction (one allreduce per group).
+
+        step() does not reduce again when the caller called synchronize() in the final pass of this
+        step (to clip gradients, say) and no backward ran after it. A synchronize() in an earlier
+        accumulation pass, or one followed by another backward (an evaluation that never stepped),
+        does not excuse step(): it reduces, with a warning, as Horovod warns about synchronize()
+        without skip_synchronize()."""
         from . import Compression, _fusable, allreduce_grads, size
         from .ops import FusedList
-        self._synchronized = True
+        if self._sync_at == (self._calls, self._grad_events):
+            warnings.warn("DistributedOptimizer.synchronize() called again with no backward in between: "
+                          "the gradients are reduced a second time")
+        self._sync_at = (self._calls, self._grad_events)
         params = self._params_with_grad()
         if self._buckets is not None and size() > 1:
             # backward-overlapped buckets: the hooks issued what was ready; issue the rest in order
-            sparse = set(id(p) for p in self._buckets.synchronize())
+            sparse = set(id(p) for p in self._buckets.synchronize(whole_groups=whole_groups))
             managed = set(self._buckets.where)
             params = [p for p in params if id(p) not in managed or id(p) in sparse]
         if self._passes > 1 and self._average_aggregated:
@@ -396,9 +427,14 @@ class _DistributedOptimizer(object):
         self._calls += 1
         if self._calls % self._passes:
             return None
-        if not self._synchronized:  # (a caller that ran synchronize() itself, e.g. to clip, is not reduced twice)
+        sync_at, self._sync_at = self._sync_at, None
+        if sync_at != (self._calls - 1, self._grad_events):
+            if sync_at is not None:
+                warnings.warn("DistributedOptimizer.synchronize() ran %s: step() reduces the gradients again"
+                              % ("in an earlier accumulation pass" if sync_at[0] != self._calls - 1
+                                 else "before a later backward"))
             self.synchronize()
-        self._synchronized = False
+        self._sync_at = None
         return self._optimizer.step(closure) if closure is not None else self._optimizer.step()
 
 
