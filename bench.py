@@ -118,7 +118,7 @@ def cpu_baseline(bucket_elems):
 def cpu_ring_baseline(world, elems=16 << 20, iters=20):
     """N > 1: the reference's allreduce at the same rank count on host cores - MPI_Allreduce
     (MPI_FLOAT, MPI_SUM) under MPICH, mpirun -np N, one bounded 64 MiB bucket per rank (config 3's
-    1 GiB would take ~1 s per call at np = 8). Reported as `cpu_ring_baseline` in the
+    1 GiB would take ~1 s per call at np = 8). Reported as `cpu_baseline` in the
     same units as `value` (N x bucket bytes per second). Rank 0 runs it before anything touches
     the GPU; the other ranks wait for it in the bootstrap."""
     harness = os.path.join(REPO, "oracle", "build", "mpi_allreduce_ref")
@@ -617,39 +617,62 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
 ENV_VARIANTS = [("nchannels_per_peer_4", {"NCCL_NCHANNELS_PER_PEER": "4"})]
 
 
-def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=50):
-    """Per-call time of small allreduces (AUTO: one-shot up to 256 KiB, then direct), eager and as
-    replayed HIP graphs (TIPS_GRAPHS=1): the wall time of `calls` back-to-back calls on the same
-    buffers, slowest rank; where host cost, not bytes, bounds a call (config 1 is a 1 MiB bucket)."""
+SMALL_BUCKET_KIB = (16, 256, 512, 1024, 2048, 4096, 8192)
+
+
+def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BUCKET_KIB):
+    """Per-call time of small allreduces, 16 KiB - 8 MiB (config 1 is a 1 MiB bucket at p = 2), for
+    the path the library ships (AUTO with its default one-shot threshold and graph-replay limit)
+    and for each candidate beside it: direct eager, direct replayed as a HIP graph at any size,
+    one-shot eager and one-shot replayed. The wall time of `calls` back-to-back calls on the same
+    buffers, slowest rank; `best` names the fastest candidate and `shipped_vs_best` the ratio."""
     out = {"calls": calls, "unit": "us per call, slowest rank"}
-    saved = os.environ.get("TIPS_GRAPHS")
-    _lib.call("tips_set_algorithm", _lib.ALGO_AUTO)
+    keys = ("TIPS_GRAPHS", "TIPS_GRAPH_MAX_BYTES")
+    saved = {k: os.environ.get(k) for k in keys}
+    modes = [("shipped", _lib.ALGO_AUTO, {}),
+             ("direct_eager", _lib.ALGO_DIRECT, {"TIPS_GRAPHS": "0"}),
+             ("direct_graphs", _lib.ALGO_DIRECT, {"TIPS_GRAPHS": "1", "TIPS_GRAPH_MAX_BYTES": str(1 << 40)}),
+             ("oneshot_eager", _lib.ALGO_ONESHOT, {"TIPS_GRAPHS": "0"}),
+             ("oneshot_graphs", _lib.ALGO_ONESHOT, {"TIPS_GRAPHS": "1", "TIPS_GRAPH_MAX_BYTES": str(1 << 40)})]
+    world = dist.get_world_size()
     try:
-        for kib in (16, 256, 1024):
+        for kib in kibs:
             n = kib * 256
             x = torch.full((n,), float(rank + 1), device="cuda")
             y = torch.empty_like(x)
             row = {}
-            for mode in ("eager", "graphs"):
-                os.environ["TIPS_GRAPHS"] = "1" if mode == "graphs" else "0"
+            ok = True
+            for mode, algo, env in modes:
+                for k in keys:
+                    os.environ.pop(k, None)
+                os.environ.update(env)
+                _lib.call("tips_set_algorithm", algo)
+                y.zero_()
                 for _ in range(3):  # (a plan is captured on its second call)
                     L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, sp)
                 torch.cuda.synchronize()
+                ok = ok and bool(torch.all(y == world * (world + 1) / 2).item())
                 dist.barrier()
                 t0 = time.perf_counter()
                 for _ in range(calls):
                     L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, sp)
                 torch.cuda.synchronize()
                 row[mode] = round(max_over_ranks(dist, time.perf_counter() - t0) / calls * 1e6, 1)
-            world = dist.get_world_size()
-            ok = bool(torch.all(y == world * (world + 1) / 2).item())
-            row["check"] = "exact" if all_ranks_ok(dist, ok) else "FAIL on some rank"
+            cands = {k: v for k, v in row.items() if k != "shipped"}
+            best = min(cands, key=cands.get)
+            row["shipped_path"] = "%s%s" % (
+                "oneshot" if L.tips_resolve_algorithm(world, n * 4) == _lib.ALGO_ONESHOT else "direct",
+                " graphs" if n * 4 <= int(saved.get("TIPS_GRAPH_MAX_BYTES") or (1 << 20)) else " eager")
+            row["best"] = best
+            row["shipped_vs_best"] = round(row["shipped"] / cands[best], 3)
+            row["check"] = "exact (every mode)" if all_ranks_ok(dist, ok) else "FAIL on some rank"
             out["%d_KiB" % kib] = row
     finally:
-        if saved is None:
-            os.environ.pop("TIPS_GRAPHS", None)
-        else:
-            os.environ["TIPS_GRAPHS"] = saved
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return out
 
 
@@ -1117,8 +1140,8 @@ def bench_allreduce(args):
         line["gradient_api"] = gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, ms)
     if topo:
         line["gpu_topology"] = topo
-    if cpu_ring:
-        line["cpu_ring_baseline"] = cpu_ring
+    if cpu_ring:  # N > 1: the reference's MPI_Allreduce at the same rank count on host cores
+        line["cpu_baseline"] = cpu_ring
     if fallbacks:
         line["failed_schedules"] = fallbacks
     if workload == "negotiated1000":
@@ -1255,14 +1278,12 @@ def bench_allreduce(args):
                 line["xgmi_probe"] = link_probe(dist, rank, world)
             except Exception as e:  # noqa: BLE001
                 line["xgmi_probe"] = {"error": str(e)}
-        # Only in a job that spans every GPU of the node (the driver's last, N = 8, run) unless
-        # TIPS_BENCH_PEER=1: if the first cross-GPU run of these kernels faulted and took the
-        # GPUs down, no later bench run could be lost with it.
-        if world >= torch.cuda.device_count() or os.environ.get("TIPS_BENCH_PEER") == "1":
+        # Opt-in (TIPS_BENCH_PEER=1): the IPC peer schedules have not crossed real GPUs yet, so the
+        # driver's scaling runs do not start them (a fault there would cost the whole record).
+        if os.environ.get("TIPS_BENCH_PEER") == "1":
             run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"})])
-        elif workload == "bucket":
-            compare_check["peer"] = ("skipped: the IPC peer schedules run only when the job spans all %d GPUs of "
-                                     "the node (TIPS_BENCH_PEER=1 forces them)" % torch.cuda.device_count())
+        elif workload == "bucket" and world > 1:
+            compare_check["peer"] = "opt-in: TIPS_BENCH_PEER=1 (not yet run across real GPUs)"
         if world > 1 and workload == "bucket":
             note_progress("the small-bucket latency probe")
             try:
@@ -1274,14 +1295,21 @@ def bench_allreduce(args):
                 line["backward_overlap"] = overlap_probe(torch, dist, tips_amd, _lib, algo_names[args.algo])
             except Exception as e:  # noqa: BLE001
                 line["backward_overlap"] = {"error": str(e)}
-        run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
-                      ("ring_l2", "ring", {"TIPS_LANES": "2"}),
-                      ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
-                                                  "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
+        # Opt-in (TIPS_BENCH_LANES=1): transfer lanes split communicators that live to the end of
+        # the job; on the socket rehearsal they ran 10x slower and slowed every later call.
+        if os.environ.get("TIPS_BENCH_LANES") == "1":
+            run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
+                          ("ring_l2", "ring", {"TIPS_LANES": "2"}),
+                          ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
+                                                      "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
+        elif workload == "bucket" and world > 1:
+            compare_check["lanes"] = "opt-in: TIPS_BENCH_LANES=1"
     line["compare_check"] = compare_check
     line["compare_algbw_gib_s"] = compare
+    # Opt-in (TIPS_BENCH_ENV_VARIANTS=1): child jobs with other RCCL settings (one of them delivered
+    # wrong bytes in a probe, profiles/r02/rccl_nchannels_probe.txt)
     if world > 1 and workload == "bucket" and not args.no_compare and not args.no_env_variants \
-            and not os.environ.get("TIPS_NO_RCCL"):
+            and not os.environ.get("TIPS_NO_RCCL") and os.environ.get("TIPS_BENCH_ENV_VARIANTS") == "1":
         note_progress("the RCCL-setting child jobs")
         line["env_variants"] = env_variant_jobs(args, dist, rank, world)
     ring_algbw = algbw if algo == _lib.ALGO_RING else (compare.get("ring") or 0) * GIB

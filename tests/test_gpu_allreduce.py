@@ -386,7 +386,7 @@ def test_fused_host_flat_identity(gpu, monkeypatch, threads, piece):
         assert outs2[0].base.ctypes.data != base  # held: a new set
         for o, x, o2, x2 in zip(held, ins, outs2, ins2):
             assert same_bits(o, x, dtype) and same_bits(o2, x2, dtype)
-        del held, outs
+        del held, outs, o, o2  # (the loop variables hold views too)
         outs3 = gpu.fused_allreduce_host_flat(ins)
         assert outs3[0].base.ctypes.data == base  # released: reused
         for o, x in zip(outs3, ins):

@@ -324,21 +324,22 @@ class _HostFlatOutputs(object):
         self.offs = [int(o) for o in offs]
         self.sets = []
 
-    def _free(self, s):
+    def _refs(self, s):
+        """(references to the flat buffer, most references to one view) of set s. Measured the same
+        way when a set is made (its baseline) and when it is looked at again, so a set is free
+        exactly when nothing beyond the set itself refers to it: a view held, or an array / tensor
+        made from one (numpy collapses every view's .base to the owner; torch counts storage users)."""
         import sys
-        flat, views, c0, rc0 = s
         if self.is_torch:
             import torch
-            if torch._C._storage_Use_Count(flat.untyped_storage()._cdata) != c0:
-                return False
-        elif sys.getrefcount(flat) != c0:
-            return False
-        return max(map(sys.getrefcount, views), default=rc0) <= rc0
+            n = torch._C._storage_Use_Count(s[0].untyped_storage()._cdata)
+        else:
+            n = sys.getrefcount(s[0])
+        return n, max(map(sys.getrefcount, s[1]), default=0)
 
     def take(self):
-        import sys
         for s in self.sets:
-            if self._free(s):
+            if self._refs(s) == s[2]:
                 return s[0], s[1]
         if self.is_torch:
             import torch
@@ -354,13 +355,11 @@ class _HostFlatOutputs(object):
             # a kept set is page-locked for the life of the process (the device's D2H lands in it
             # directly); one past MAX_SETS is not (it is freed with its last output)
             _lib.call("tips_host_register", tensors.data_ptr(flat), self.total)
-            if self.is_torch:
-                import torch
-                c0 = torch._C._storage_Use_Count(flat.untyped_storage()._cdata)
-            else:
-                c0 = sys.getrefcount(flat)
-            self.sets.append((flat, views, c0, max(map(sys.getrefcount, views), default=0)))
-            return self.sets[-1][0:2]
+            st = [flat, views, None]
+            del flat, views  # (the baseline counts the set's own references only)
+            st[2] = self._refs(st)
+            self.sets.append(st)
+            return st[0], st[1]
         return flat, views
 
 
@@ -573,11 +572,19 @@ def allgather_async(tensor, name):
     box = {}
 
     torch_src = tensors.is_torch(src)
+    req_stream = None
+    if torch_src and src.is_cuda:
+        import torch
+        req_stream = torch.cuda.current_stream(src.device)  # the stream the request runs on
 
     def alloc(_ctx, nbytes):
         if torch_src:
+            import contextlib
             import torch
-            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=src.device)
+            # allocated on the negotiation thread, but the transfer writes it on the request's
+            # stream: allocate under that stream, so the caching allocator ties the block to it
+            with torch.cuda.stream(req_stream) if req_stream is not None else contextlib.nullcontext():
+                buf = torch.empty(int(nbytes), dtype=torch.uint8, device=src.device)
         else:
             buf = np.empty(int(nbytes), dtype=np.uint8)
         box["buf"] = buf

@@ -55,15 +55,36 @@ def link_rates(nbytes):
             fn()
         torch.cuda.synchronize()
         emit(what=name, bytes=nbytes, gib_s=round(5 * nbytes / (time.perf_counter() - t0) / GIB, 2))
+    def both(k):
+        for _ in range(k):
+            with torch.cuda.stream(s1):
+                d.copy_(h_in, non_blocking=True)
+            with torch.cuda.stream(s2):
+                h_out.copy_(d2, non_blocking=True)
+
+    both(2)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(5):
-        with torch.cuda.stream(s1):
-            d.copy_(h_in, non_blocking=True)
-        with torch.cuda.stream(s2):
-            h_out.copy_(d2, non_blocking=True)
+    both(5)
     torch.cuda.synchronize()
     emit(what="h2d+d2h", bytes=nbytes, gib_s_each=round(5 * nbytes / (time.perf_counter() - t0) / GIB, 2))
+    # D2H into host memory page-locked by hipHostRegister (the flat host outputs) vs hipHostMalloc
+    import tips_amd
+    from tips_amd import _lib
+    tips_amd.init()
+    reg = np.empty(nbytes, dtype=np.uint8)
+    reg[:] = 1
+    _lib.call("tips_host_register", reg.ctypes.data, nbytes)
+    reg_t = torch.from_numpy(reg)
+    for name, fn in [("d2h_registered", lambda: reg_t.copy_(d, non_blocking=True)),
+                     ("h2d_registered", lambda: d.copy_(reg_t, non_blocking=True))]:
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        emit(what=name, bytes=nbytes, gib_s=round(5 * nbytes / (time.perf_counter() - t0) / GIB, 2))
 
 
 def fused(sizes, label):
@@ -73,7 +94,7 @@ def fused(sizes, label):
     for _ in range(2):
         outs = tips_amd._reduce_grads(hg)
     ts = []
-    for _ in range(5):
+    for _ in range(8):
         t0 = time.perf_counter()
         outs = tips_amd._reduce_grads(hg)
         ts.append(time.perf_counter() - t0)
