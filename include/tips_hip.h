@@ -322,6 +322,10 @@ typedef void* (*tips_alloc_fn)(void* ctx, int64_t bytes);
  * gathers on `stream`. ndim >= 1. A host `in` gets a host output: alloc must then return host memory. */
 TIPS_API int64_t tips_enqueue_allgather(const char* name, const void* in, const int64_t* shape, int ndim, int dtype,
                                         void* stream, tips_alloc_fn alloc, void* ctx, int64_t* out_rows);
+/* Host-copy pool check (no GPU): `runs` back-to-back fork-join runs of njobs (every third run
+ * njobs / 2) on a pool of nthreads; TIPS_OK when every job of every run ran exactly once. For the
+ * CPU tests of the pool behind tips_fused_allreduce_host. */
+TIPS_API int tips_host_pool_selftest(int nthreads, int runs, int njobs);
 /* The negotiation protocol with an executor that only logs (no GPU): each
  * rank enqueues the newline-separated "name dtype count" lines of `requests`
  * ("@sleep ms" pauses, "@wait" blocks until every earlier request is

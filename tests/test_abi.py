@@ -327,3 +327,16 @@ def test_only_the_c_abi_is_exported():
                          capture_output=True, text=True, check=True).stdout
     text_syms = {l.split()[-1] for l in out.splitlines() if " T " in l}
     assert text_syms == set(header_functions())
+
+
+@pytest.mark.parametrize("threads,jobs", [(2, 2), (8, 8), (16, 5), (4, 64)])
+def test_host_pool_runs_every_job_once(threads, jobs):
+    """The host-copy pool behind tips_fused_allreduce_host (no GPU): 20000 back-to-back fork-join
+    runs, of two sizes in turn, each job exactly once. An earlier pool reset its job counter and
+    its pending count as two separate stores, so a thread still leaving one run could claim a job
+    of the next against the old count, and the caller waited forever (a GPU test with 256-B pieces,
+    ~800 runs per call, hung in it)."""
+    from tips_amd import _lib
+    L = _lib.lib()
+    rc = L.tips_host_pool_selftest(threads, 20000, jobs)
+    assert rc == 0, _lib.last_error()

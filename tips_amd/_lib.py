@@ -116,6 +116,7 @@ _SIGNATURES = [
     ("tips_enqueue_allgather", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
       ctypes.c_void_p, _c_i64_p]),
+    ("tips_host_pool_selftest", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tips_negotiation_selftest", ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),

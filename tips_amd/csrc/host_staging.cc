@@ -128,41 +128,52 @@ HostPool::~HostPool() {
   for (auto& t : th_) t.join();
 }
 
-void HostPool::grab() {  // take jobs until none is left (caller holds no lock)
-  for (int j; (j = next_.fetch_add(1)) < njobs_;) {
-    (*fn_)(j);
+void HostPool::grab(uint64_t gen) {  // claim jobs of run `gen` until none is left
+  uint64_t cur = ticket_.load();
+  // the ticket is (generation << 32 | jobs << 16 | next index): one atomic snapshot says whether
+  // this run still has a job, whatever a later run has written to fn_ / njobs_ meanwhile
+  while ((cur >> 32) == gen && (cur & 0xffff) < ((cur >> 16) & 0xffff)) {
+    if (!ticket_.compare_exchange_weak(cur, cur + 1)) continue;  // (cur reloaded)
+    (*fn_)((int)(cur & 0xffff));
     if (pending_.fetch_sub(1) == 1) {
       std::lock_guard<std::mutex> l(m_);
       done_cv_.notify_all();
     }
+    cur = ticket_.load();
   }
 }
 
 void HostPool::worker() {
   uint64_t seen = 0;
   while (true) {
+    uint64_t gen;
     {
       std::unique_lock<std::mutex> l(m_);
       cv_.wait(l, [&] { return stop_ || gen_ != seen; });
       if (stop_) return;
-      seen = gen_;
+      seen = gen = gen_;
     }
-    grab();
+    grab(gen);
   }
 }
 
 void HostPool::run(int njobs, const std::function<void(int)>& fn) {
   if (njobs <= 0) return;
+  if (njobs > 0xffff) {  // (the ticket holds 16 bits of job index; callers use one job per thread)
+    for (int j = 0; j < njobs; j += 0xffff)
+      run(std::min(0xffff, njobs - j), [&](int k) { fn(j + k); });
+    return;
+  }
+  uint64_t gen;
   {
     std::lock_guard<std::mutex> l(m_);
     fn_ = &fn;
-    njobs_ = njobs;
-    next_.store(0);
     pending_.store(njobs);
-    gen_++;
+    gen = ++gen_ & 0xffffffffull;
+    ticket_.store(gen << 32 | (uint64_t)njobs << 16);  // (published last: a claim of this run sees fn_, pending_)
   }
   if (njobs > 1) cv_.notify_all();
-  grab();
+  grab(gen);
   std::unique_lock<std::mutex> l(m_);
   done_cv_.wait(l, [&] { return pending_.load() == 0; });
 }
@@ -320,6 +331,22 @@ void host_release(State& st) {
 using namespace tips::rt;
 
 extern "C" {
+
+int tips_host_pool_selftest(int nthreads, int runs, int njobs) {
+  if (nthreads < 1 || nthreads > 64 || runs < 0 || njobs < 0) return fail(TIPS_ERR_INVALID_ARG, "bad arguments");
+  HostPool pool(nthreads);
+  std::vector<std::atomic<int>> hits((size_t)njobs);
+  for (int r = 0; r < runs; r++) {
+    for (auto& h : hits) h.store(0);
+    const int n = r % 3 == 2 ? njobs / 2 : njobs;  // (runs of different sizes back to back)
+    std::function<void(int)> fn = [&](int j) { hits[(size_t)j].fetch_add(1); };
+    pool.run(n, fn);
+    for (int j = 0; j < njobs; j++)
+      if (hits[(size_t)j].load() != (j < n ? 1 : 0))
+        return fail(TIPS_ERR_MISMATCH, "run %d: job %d ran %d times", r, j, hits[(size_t)j].load());
+  }
+  return 0;
+}
 
 int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype) {
   TRY(check_dtype(dtype));

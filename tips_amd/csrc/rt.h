@@ -138,8 +138,10 @@ struct PeerState;   // peer.cc
 struct FusionCache;  // fusion.cc: layouts and resolved segment tables of recent tensor lists
 struct PlanGraphs;   // schedules.cc: instantiated HIP graphs of recently replayed plans
 
-// host_staging.cc: a fork-join pool of host threads for packing / unpacking host tensors
-// (run(n, fn) calls fn(0..n-1) on the pool and the calling thread, returns when all are done).
+// host_staging.cc: fork-join pool for the host copies: run(n, fn) calls fn(0..n-1) on the pool's threads and the
+// caller's, and returns when all n are done. Jobs are claimed from one 64-bit ticket holding
+// (generation << 32 | jobs << 16 | next index), so a thread still leaving run k can never claim a job
+// of run k+1, nor one past run k's end: its compare-and-swap fails on the generation.
 class HostPool {
  public:
   explicit HostPool(int nthreads);
@@ -149,14 +151,14 @@ class HostPool {
 
  private:
   void worker();
-  void grab();
+  void grab(uint64_t gen);
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(int)>* fn_ = nullptr;
-  int njobs_ = 0;
-  std::atomic<int> next_{0}, pending_{0};
-  uint64_t gen_ = 0;
+  std::atomic<uint64_t> ticket_{0};
+  std::atomic<int> pending_{0};
+  uint64_t gen_ = 0;  // guarded by m_ (workers wait on it)
   bool stop_ = false;
 };
 
