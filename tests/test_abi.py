@@ -80,6 +80,12 @@ def test_algorithm_resolution():
     assert L.tips_resolve_algorithm(8, small) == _lib.ALGO_ONESHOT
     assert L.tips_resolve_algorithm(2, small) == _lib.ALGO_ONESHOT
     assert L.tips_resolve_algorithm(32, small) == _lib.ALGO_RING  # more ranks than the fold takes sources
+    # p = 2: a one-shot moves the ring's bytes in one step, so it takes buckets up to 8 MiB;
+    # p > 2: it moves (p - 1) x the all-pairs bytes per link, so only up to 256 KiB
+    assert L.tips_resolve_algorithm(2, 8 << 20) == _lib.ALGO_ONESHOT
+    assert L.tips_resolve_algorithm(2, (8 << 20) + 4) == _lib.ALGO_RING
+    assert L.tips_resolve_algorithm(4, 1 << 20) == _lib.ALGO_DIRECT
+    assert L.tips_resolve_algorithm(4, 256 << 10) == _lib.ALGO_ONESHOT
     L.tips_set_algorithm(_lib.ALGO_RING)
     assert L.tips_resolve_algorithm(8, small) == _lib.ALGO_RING
     L.tips_set_algorithm(_lib.ALGO_TUNE)  # measured per size class; small buckets stay one-shots

@@ -336,13 +336,15 @@ def test_fusion_caches_with_fresh_tensors(gpu, monkeypatch):
     assert s3["tables_built"] == s2["tables_built"] and s3["table_hits"] > s2["table_hits"]
 
 
-@pytest.mark.parametrize("piece", [256, 4096, 8 << 20])
-def test_fused_host_identity(gpu, monkeypatch, piece):
+@pytest.mark.parametrize("piece,first", [(256, 256), (4096, 4096), (8 << 20, 8 << 20), (65536, 1024), (16 << 20, 2 << 20)])
+def test_fused_host_identity(gpu, monkeypatch, piece, first):
     """tips_fused_allreduce_host at one rank (the identity after H2D -> HBM -> D2H): many host tensors
     of every dtype, pageable numpy and CPU torch, empty ones, pieces from 256 B (tensors span many
-    pieces; the copy threads split every piece) to 8 MiB; bit-exact, inputs unchanged."""
+    pieces; the copy threads split every piece) to 16 MiB, fixed or ramping up from `first` at the
+    head and down to it at the tail; bit-exact, inputs unchanged."""
     import torch
     monkeypatch.setenv("TIPS_HOST_FUSED_PIECE_BYTES", str(piece))
+    monkeypatch.setenv("TIPS_HOST_FUSED_FIRST_BYTES", str(first))
     rng = np.random.default_rng(piece % 977)
     for dtype in ALL_DTYPES:
         sizes = [int(round(2 ** rng.uniform(0, 14))) for _ in range(60)] + [0, 1, 3]

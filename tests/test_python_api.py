@@ -101,6 +101,8 @@ def _fake_two_ranks(monkeypatch):
     # dense host gradients go through the fused host path at N > 1: here each through the (faked)
     # tips_amd.allreduce, so the tests below see one reduction per gradient
     monkeypatch.setattr(tips_amd._ops, "fused_allreduce_host_flat", lambda ts: [tips_amd.allreduce(t) for t in ts])
+    # (a remembered plan calls the library directly: none here, so every call takes the fake)
+    monkeypatch.setattr(tips_amd, "_remember_plan", lambda grads, groups: None)
 
 
 def test_indexed_slices_take_the_allgather_branch(monkeypatch):

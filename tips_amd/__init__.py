@@ -134,8 +134,9 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
         buffer laid out as the fusion buckets, each bucket packed into it and allreduced in place
         (a layout depends on the counts only, so fresh gradient tensors every step hit the caches);
       - dense host gradients (numpy / CPU torch: the reference's op is a CPU op, ops.cc:118), per
-        dtype: fused_allreduce_host - packed into page-locked pieces by host threads, pipelined
-        H2D -> allreduce -> D2H, unpacked into new host tensors;
+        dtype: fused_allreduce_host_flat - packed into page-locked pieces by host threads,
+        pipelined H2D -> allreduce -> D2H straight into one page-locked flat host buffer, the
+        outputs views of it (reused as the device flat outputs are);
       - the rest (sparse) one by one, through the reference's allgather branch."""
     none = compression is Compression.none
     global _DATA_PTR
@@ -145,7 +146,10 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
     if fused and none:
         plan = _find_plan(grads)
         if plan is not None:  # the same tensor objects as a recent call: no per-tensor inspection
-            return plan.run(grads)
+            res = plan.run(grads)
+            if res is not None:
+                return res
+            _PLANS.remove(plan)
     out = list(grads)
     dev, host = {}, {}
     simple = fused and none  # only dense, contiguous device tensors: the split can be remembered
@@ -176,12 +180,23 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
         sums = _ops._flat_run(fo, ts, list(map(_DATA_PTR, ts)))
         for (i, _, ctx), s in zip(members, sums):
             out[i] = s if none else compression.decompress(s, ctx)
-        plan_groups.append(([i for i, _, _ in members], fo))
+        plan_groups.append(([i for i, _, _ in members], fo, None))
     for members in host.values():
-        sums = _ops.fused_allreduce_host_flat([c for _, c, _ in members])
+        ts = [c for _, c, _ in members]
+        sums = _ops.fused_allreduce_host_flat(ts)
+        if simple:
+            # a plan re-reads the pointers with the fast reader and re-checks shapes and dtypes:
+            # only for lists of the inputs themselves (contiguous, not copies) that it reads right
+            ok = all(c is grads[i] for i, c, _ in members) and \
+                _tensors.host_data_ptrs(ts) == [_tensors.data_ptr(t) for t in ts]
+            if ok:
+                plan_groups.append(([i for i, _, _ in members], _ops._host_flat_outputs(ts),
+                                    [(t.shape, t.dtype) for t in ts]))
+            else:
+                simple = False
         for (i, _, ctx), s in zip(members, sums):
             out[i] = s if none else compression.decompress(s, ctx)
-    if simple and not host:
+    if simple:
         _remember_plan(grads, plan_groups)
     return out
 
@@ -202,7 +217,9 @@ class _GradPlan(object):
         import weakref
         self.refs = [weakref.ref(g) if g is not None else _DEAD_REF for g in grads]
         self.n = len(grads)
-        self.groups = groups  # [(positions, _FlatOutputs)]
+        # [(positions, _FlatOutputs, None)] for device groups, [(positions, _HostFlatOutputs,
+        # [(shape, dtype)])] for host groups (numpy arrays can change shape or dtype in place)
+        self.groups = groups
         self.whole = len(groups) == 1 and groups[0][0] == list(range(self.n))
 
     def matches(self, grads):
@@ -211,10 +228,16 @@ class _GradPlan(object):
         return len(grads) == self.n and all(map(operator.is_, map(weakref.ref.__call__, self.refs), grads))
 
     def run(self, grads):
+        """The outputs, or None when a host tensor changed shape or dtype (the caller plans again)."""
         out = list(grads)
-        for pos, fo in self.groups:
+        for pos, fo, meta in self.groups:
             ts = grads if self.whole else [grads[i] for i in pos]
-            sums = _ops._flat_run(fo, ts, list(map(_DATA_PTR, ts)))
+            if meta is None:
+                sums = _ops._flat_run(fo, ts, list(map(_DATA_PTR, ts)))
+            else:
+                if any(t.shape != shp or t.dtype is not dt for t, (shp, dt) in zip(ts, meta)):
+                    return None
+                sums = _ops._host_flat_run(fo, _tensors.host_data_ptrs(ts))
             if self.whole:
                 return sums
             for i, s in zip(pos, sums):

@@ -178,6 +178,39 @@ void HostPool::run(int njobs, const std::function<void(int)>& fn) {
   done_cv_.wait(l, [&] { return pending_.load() == 0; });
 }
 
+// The pieces of a fused host stream of `total` bytes: at most `piece` bytes each, but ramping up
+// from `first` (doubling) at the start and back down to it at the end, so the first H2D starts
+// after a small pack and the last D2H is a short tail - with 16 MiB pieces throughout, the head
+// (one pack) and the tail (one D2H) cost 0.6 ms of a 3.3 ms config-5 call. A function of the sizes
+// alone: every rank cuts the same pieces (each piece is one allreduce). Offsets 256-B aligned.
+std::vector<Piece> host_pieces(int64_t total, int64_t piece, int64_t first) {
+  piece = std::max<int64_t>(kAlignBytes, round_up(piece, kAlignBytes));
+  first = std::min(piece, std::max<int64_t>(kAlignBytes, round_up(first, kAlignBytes)));
+  std::vector<int64_t> head, tail;
+  int64_t rest = total;
+  for (int64_t s = first; s < piece && rest > 0; s *= 2) {  // ramp up at the head, down at the tail
+    for (std::vector<int64_t>* v : {&head, &tail}) {
+      const int64_t take = std::min(s, rest);
+      if (take > 0) v->push_back(take);
+      rest -= take;
+    }
+  }
+  std::vector<Piece> out;
+  int64_t off = 0;
+  for (int64_t len : head) out.push_back(Piece{off, len}), off += len;
+  if (rest > 0) {
+    const int64_t n = (rest + piece - 1) / piece, per = round_up((rest + n - 1) / n, kAlignBytes);
+    for (int64_t k = 0; k < n && rest > 0; k++) {
+      const int64_t len = std::min(per, rest);
+      out.push_back(Piece{off, len});
+      off += len;
+      rest -= len;
+    }
+  }
+  for (auto it = tail.rbegin(); it != tail.rend(); ++it) out.push_back(Piece{off, *it}), off += *it;
+  return out;
+}
+
 namespace {
 
 struct HostSeg {
@@ -220,8 +253,9 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   std::sort(segs.begin(), segs.end(), [](const HostSeg& x, const HostSeg& y) { return x.off < y.off; });
   total = round_up(total, kAlignBytes);
   const int64_t piece = std::min<int64_t>(
-      total, round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_FUSED_PIECE_BYTES", 8 << 20)), kAlignBytes));
-  const int np = (int)((total + piece - 1) / piece);
+      total, round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_FUSED_PIECE_BYTES", 16 << 20)), kAlignBytes));
+  const std::vector<Piece> pieces = host_pieces(total, piece, env_i64("TIPS_HOST_FUSED_FIRST_BYTES", 2 << 20));
+  const int np = (int)pieces.size();
   const int R = 3;  // page-locked slots per direction; piece i uses slot i % R
   const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(64, env_i64("TIPS_HOST_THREADS", 8)));
   if (!st.host_pool || st.host_pool->size() != nthreads) {
@@ -244,7 +278,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   hipEvent_t* ev = st.pipe_ev.ev.data();  // [3i] H2D done, [3i+1] reduced, [3i+2] D2H done
   const int parts = nthreads;
   auto host_copy = [&](int i, bool pack) {
-    const int64_t p0 = (int64_t)i * piece, p1 = std::min(total, p0 + piece);
+    const int64_t p0 = pieces[(size_t)i].off, p1 = p0 + pieces[(size_t)i].len;
     char* buf = (pack ? pin_in : pin_out) + (int64_t)(i % R) * piece;
     const int64_t per = round_up((p1 - p0 + parts - 1) / parts, 64);
     st.host_pool->run(parts, [&](int j) {
@@ -262,14 +296,22 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   auto since = [](std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count();
   };
+  static hipEvent_t tev[3];  // (trace only) first H2D issued, last H2D done, last D2H done
+  if (trace && !tev[0])
+    for (auto& e : tev) HIP_TRY(hipEventCreate(&e));
   auto report = [&] {
-    if (trace)
-      fprintf(stderr, "[tips host] bytes %lld pieces %d threads %d direct_out %d: pack %.0f us, wait %.0f us, "
-              "unpack %.0f us, issue %.0f us, total %.0f us\n", (long long)total, np, nthreads, (int)direct_out,
-              t_pack, t_wait, t_unpack, t_issue, since(t_start));
+    if (!trace) return;
+    float h2d = 0, d2h = 0;
+    (void)hipEventSynchronize(tev[2]);
+    (void)hipEventElapsedTime(&h2d, tev[0], tev[1]);
+    (void)hipEventElapsedTime(&d2h, tev[0], tev[2]);
+    fprintf(stderr, "[tips host] bytes %lld pieces %d threads %d direct_out %d: pack %.0f us, wait %.0f us, "
+            "unpack %.0f us, issue %.0f us, total %.0f us; device: first H2D -> last H2D %.0f us "
+            "(%.1f GiB/s), -> last D2H %.0f us\n", (long long)total, np, nthreads, (int)direct_out, t_pack, t_wait,
+            t_unpack, t_issue, since(t_start), h2d * 1e3, total / (h2d * 1e-3) / 1073741824.0, d2h * 1e3);
   };
   for (int i = 0; i < np; i++) {
-    const int64_t off = (int64_t)i * piece, len = std::min(piece, total - off);
+    const int64_t off = pieces[(size_t)i].off, len = pieces[(size_t)i].len;
     auto t0 = std::chrono::steady_clock::now();
     if (i >= R) HIP_TRY(hipEventSynchronize(ev[3 * (i - R)]));  // slot i % R: its last H2D has read it
     t_wait += since(t0);
@@ -277,6 +319,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     host_copy(i, true);
     t_pack += since(t0);
     t0 = std::chrono::steady_clock::now();
+    if (trace && i == 0) HIP_TRY(hipEventRecord(tev[0], st.h2d_stream));
     HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice,
                            st.h2d_stream));
     HIP_TRY(hipEventRecord(ev[3 * i], st.h2d_stream));
@@ -288,6 +331,10 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     char* d2h = direct_out ? flat + off : pin_out + (int64_t)(i % R) * piece;
     HIP_TRY(hipMemcpyAsync(d2h, dev + off, (size_t)len, hipMemcpyDeviceToHost, st.d2h_stream));
     HIP_TRY(hipEventRecord(ev[3 * i + 2], st.d2h_stream));
+    if (trace && i == np - 1) {
+      HIP_TRY(hipEventRecord(tev[1], st.h2d_stream));
+      HIP_TRY(hipEventRecord(tev[2], st.d2h_stream));
+    }
     t_issue += since(t0);
     if (i >= lag) {
       t0 = std::chrono::steady_clock::now();

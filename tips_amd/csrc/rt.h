@@ -142,6 +142,11 @@ struct PlanGraphs;   // schedules.cc: instantiated HIP graphs of recently replay
 // caller's, and returns when all n are done. Jobs are claimed from one 64-bit ticket holding
 // (generation << 32 | jobs << 16 | next index), so a thread still leaving run k can never claim a job
 // of run k+1, nor one past run k's end: its compare-and-swap fails on the generation.
+struct Piece {
+  int64_t off, len;  // bytes of a fused host stream
+};
+std::vector<Piece> host_pieces(int64_t total, int64_t piece, int64_t first);
+
 class HostPool {
  public:
   explicit HostPool(int nthreads);

@@ -102,6 +102,16 @@ int join(hipStream_t waiter, hipStream_t src, hipEvent_t ev) {
   return 0;
 }
 
+// Buckets up to this go one-shot (one exchange + one fold kernel) under AUTO and TUNE. At p = 2
+// a one-shot moves the same bytes over the link as the ring (S each way) in one step instead of
+// two, so it wins at every size the fold's staging stays small for: 8 MiB (the p = 2 rehearsal,
+// profiles/r03/small_bucket_rehearsal_n2_before.json, measured it fastest at 16 KiB - 8 MiB). For p > 2 it
+// moves (p - 1) x the bytes of the all-pairs schedule per link, so it stays a latency tool: 256 KiB.
+// TIPS_ONESHOT_BYTES overrides both.
+int64_t oneshot_bytes(int p) {
+  return env_i64("TIPS_ONESHOT_BYTES", p == 2 ? (int64_t)8 << 20 : (int64_t)256 << 10);
+}
+
 int resolve_algo(int algo, int p, int64_t bytes) {
   if (algo == TIPS_ALGO_AUTO) {
     const char* e = getenv("TIPS_ALGO");
@@ -115,13 +125,13 @@ int resolve_algo(int algo, int p, int64_t bytes) {
     }
   }
   if (algo == TIPS_ALGO_TUNE) {  // measured per size class; small buckets stay latency-bound one-shots
-    if (p > 1 && p <= tips::kMaxSrcs && bytes <= env_i64("TIPS_ONESHOT_BYTES", 256 << 10)) return TIPS_ALGO_ONESHOT;
+    if (p > 1 && p <= tips::kMaxSrcs && bytes <= oneshot_bytes(p)) return TIPS_ALGO_ONESHOT;
     return TIPS_ALGO_TUNE;
   }
   if (algo != TIPS_ALGO_AUTO) return algo;
   // small buckets: one exchange + one kernel beats 2(p-1) pipelined steps (latency-bound);
   // large: ring on one link pair (p <= 2), all-pairs over every xGMI link otherwise
-  if (p > 1 && p <= tips::kMaxSrcs && bytes <= env_i64("TIPS_ONESHOT_BYTES", 256 << 10)) return TIPS_ALGO_ONESHOT;
+  if (p > 1 && p <= tips::kMaxSrcs && bytes <= oneshot_bytes(p)) return TIPS_ALGO_ONESHOT;
   return (p <= 2 || p > tips::kMaxSrcs) ? TIPS_ALGO_RING : TIPS_ALGO_DIRECT;
 }
 

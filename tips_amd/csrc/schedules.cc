@@ -213,11 +213,11 @@ void destroy_exec(State& st, hipGraphExec_t e) {
 // to replay correctly: RCCL >= 2.26 on a HIP runtime >= 7.0, i.e. torch's bundled ROCm 7.0.2 (a
 // Python process) and /opt/rocm's 7.2 (a C / cgo / JNI host) - tests/test_gpu_graphs.py and
 // test_gpu_rccl_procs.py::test_replayed_plans_in_python_processes - and for buckets up to
-// TIPS_GRAPH_MAX_BYTES (1 MiB), where a call's host cost, not its bytes, bounds it: the host time
-// of a call drops 126 -> 22 us (one-shot p = 2, Python) and a call takes 15-25 % less below 1 MiB
-// on the socket rehearsal, the same at 1 MiB (profiles/r02/graph_host_cost*.jsonl,
-// rehearsal_n2_small_buckets.jsonl). TIPS_GRAPHS=0 turns them off; 2 forces them on any runtime
-// (probing only).
+// TIPS_GRAPH_MAX_BYTES (8 MiB), where a call's host cost, not its bytes, bounds it: the host time
+// of a call drops 126 -> 22 us (one-shot p = 2, Python) (profiles/r02/graph_host_cost*.jsonl), and
+// on the p = 2 rehearsal a replayed one-shot was the fastest path at every size from 16 KiB to
+// 8 MiB, 4-30 % under the eager one (profiles/r03/small_bucket_rehearsal_n2_before.json; round 2 stopped
+// at 1 MiB). TIPS_GRAPHS=0 turns them off; 2 forces them on any runtime (probing only).
 bool graphs_supported() {
   static int ok = -1;
   if (ok < 0) {
@@ -232,7 +232,7 @@ bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
   if (st.graphs && st.graphs->off) return false;
   const int64_t want = env_i64("TIPS_GRAPHS", 1);
   if (want <= 0 || (want == 1 && !graphs_supported())) return false;
-  if (pl.n * tips::dtype_size(pl.dtype) > env_i64("TIPS_GRAPH_MAX_BYTES", 1 << 20)) return false;
+  if (pl.n * tips::dtype_size(pl.dtype) > env_i64("TIPS_GRAPH_MAX_BYTES", 8 << 20)) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(user, &cs) != hipSuccess) {
     (void)hipGetLastError();

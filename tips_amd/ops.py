@@ -323,6 +323,7 @@ class _HostFlatOutputs(object):
         self.es = _itemsize(dtype, is_torch)
         self.offs = [int(o) for o in offs]
         self.sets = []
+        self.last = (None, None)  # (pointer list, its ptr_array) of the previous call
 
     def _refs(self, s):
         """(references to the flat buffer, most references to one view) of set s. Measured the same
@@ -391,6 +392,12 @@ def fused_allreduce_host_flat(tensor_list):
         if tensors.dtype_code(t) != code:
             raise TypeError("fused_allreduce_host_flat needs one dtype per call")
         srcs.append(tensors.contiguous(t))
+    return _host_flat_run(_host_flat_outputs(srcs), [tensors.data_ptr(s) for s in srcs])
+
+
+def _host_flat_outputs(srcs):
+    """The _HostFlatOutputs of this host list's signature (dtype, numpy or torch, shapes); srcs are
+    contiguous host tensors of one dtype."""
     is_torch = tensors.is_torch(srcs[0])
     shapes = tuple(tuple(s.shape) for s in srcs)
     key = (str(srcs[0].dtype), is_torch, shapes)
@@ -398,10 +405,21 @@ def fused_allreduce_host_flat(tensor_list):
     if fo is None:
         if len(_HOST_FLAT) >= 16:
             _HOST_FLAT.pop(next(iter(_HOST_FLAT)))
-        fo = _HOST_FLAT[key] = _HostFlatOutputs(shapes, [tensors.numel(s) for s in srcs], code, srcs[0].dtype, is_torch)
+        fo = _HOST_FLAT[key] = _HostFlatOutputs(shapes, [tensors.numel(s) for s in srcs],
+                                                tensors.dtype_code(srcs[0]), srcs[0].dtype, is_torch)
+    return fo
+
+
+def _host_flat_run(fo, ptrs):
+    """tips_fused_allreduce_host_flat of the host tensors at `ptrs` into an output set of `fo`;
+    returns the outputs (views of the set's flat buffer)."""
+    if ptrs == fo.last[0]:
+        pp = fo.last[1]
+    else:
+        pp = _lib.ptr_array(ptrs)
+        fo.last = (ptrs, pp)
     flat, views = fo.take()
-    pi, _k1 = _lib.ptr_array([tensors.data_ptr(s) for s in srcs])
-    _lib.call("tips_fused_allreduce_host_flat", pi, fo.cp[0], len(srcs), code, tensors.data_ptr(flat))
+    _lib.call("tips_fused_allreduce_host_flat", pp[0], fo.cp[0], len(ptrs), fo.code, tensors.data_ptr(flat))
     return list(views)
 
 
