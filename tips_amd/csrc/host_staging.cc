@@ -2,6 +2,8 @@
 // on TF CPU tensors (tips/tensorflow/ops.cc:88-90), so gradients arrive in
 // host memory and must return there: this file moves them through HBM with
 // both PCIe directions and the device allreduce overlapped.
+#include <immintrin.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -213,6 +215,38 @@ std::vector<Piece> host_pieces(int64_t total, int64_t piece, int64_t first) {
 
 namespace {
 
+// Host copies of the fused path: bytes that the DMA engine (pack) or the caller (unpack) reads next,
+// not this thread. Streaming stores skip the read-for-ownership of every destination line and keep
+// the slots out of the caches; glibc's memcpy only streams above ~3/4 of the shared cache, far above
+// the per-thread share of a piece (16 MiB / 8 threads = 2 MiB). 32-B streaming stores after an
+// unaligned head; loads unaligned (numpy's buffers are 16-B aligned at best).
+__attribute__((target("avx2"))) void copy_stream_avx2(char* d, const char* s, size_t n) {
+  const size_t head = std::min(n, (size_t)((32 - ((uintptr_t)d & 31)) & 31));
+  memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+  }
+  for (; i + 32 <= n; i += 32)
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i)));
+  memcpy(d + i, s + i, n - i);
+  _mm_sfence();  // (streaming stores are weakly ordered: visible before the job reports done)
+}
+
+void copy_stream(char* d, const char* s, size_t n) {
+  static const bool ok = __builtin_cpu_supports("avx2") && env_i64("TIPS_HOST_STREAM_STORES", 1) != 0;
+  if (ok && n >= 4096) copy_stream_avx2(d, s, n);
+  else memcpy(d, s, n);
+}
+
 struct HostSeg {
   int64_t off, bytes;  // in the flat byte stream
   const char* in;
@@ -227,8 +261,8 @@ void copy_range(const std::vector<HostSeg>& segs, int64_t a, int64_t b, char* bu
   for (; it != segs.end() && it->off < b; ++it) {
     const int64_t s = std::max(a, it->off), e = std::min(b, it->off + it->bytes);
     if (e <= s) continue;
-    if (pack) memcpy(buf + (s - base), it->in + (s - it->off), (size_t)(e - s));
-    else memcpy(it->out + (s - it->off), buf + (s - base), (size_t)(e - s));
+    if (pack) copy_stream(buf + (s - base), it->in + (s - it->off), (size_t)(e - s));
+    else copy_stream(it->out + (s - it->off), buf + (s - base), (size_t)(e - s));
   }
 }
 
@@ -274,7 +308,9 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   char* dev = (char*)st.host_in.p;
   char* pin_in = (char*)st.hpin[0];
   char* pin_out = (char*)st.hpin[1];
-  const bool direct_out = flat && is_pinned_host(flat, total);  // D2H straight into the output
+  // D2H straight into the output (TIPS_HOST_DIRECT_OUT=0: through the page-locked slots, probing only)
+  const bool direct_out = flat && env_i64("TIPS_HOST_DIRECT_OUT", 1) != 0 && is_pinned_host(flat, total);
+
   hipEvent_t* ev = st.pipe_ev.ev.data();  // [3i] H2D done, [3i+1] reduced, [3i+2] D2H done
   const int parts = nthreads;
   auto host_copy = [&](int i, bool pack) {
@@ -284,7 +320,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     st.host_pool->run(parts, [&](int j) {
       const int64_t a = p0 + j * per, b = std::min(p1, a + per);
       if (a >= b) return;
-      if (!pack && flat) memcpy(flat + a, buf + (a - p0), (size_t)(b - a));  // (padding included: contiguous)
+      if (!pack && flat) copy_stream(flat + a, buf + (a - p0), (size_t)(b - a));  // (padding included: contiguous)
       else copy_range(segs, a, b, buf, p0, pack);
     });
   };
