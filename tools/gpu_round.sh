@@ -23,9 +23,9 @@ fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   if [ -n "${PYTEST_K:-}" ]; then
-    run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -m pytest tests -q -m gpu -k "$PYTEST_K"
+    run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -u -m pytest tests -q -m gpu --timeout 240 --timeout-method thread -k "$PYTEST_K"
   else
-    run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -m pytest tests -q -m gpu
+    run pytest_gpu "${PYTEST_TIMEOUT:-1100}" python -u -m pytest tests -q -m gpu --timeout 240 --timeout-method thread
   fi
   rc=$?; fatal $rc && exit $rc
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
