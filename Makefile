@@ -12,7 +12,17 @@ CRASH    := tools/lib/libcrashline.so
 
 REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe tools/_bin/op_body
 
-all: $(LIB) $(CRASH) $(REPRO) oracle
+FAST     := tips_amd/_fast$(shell python3 -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+TORCH    := $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
+PYINC    := $(shell python3 -c "import sysconfig; print(sysconfig.get_paths()['include'])")
+
+all: $(LIB) $(FAST) $(CRASH) $(REPRO) oracle
+
+# the Python mirror's list helper (tips_amd._fast: tensor pointers / counts in C++), torch headers
+$(FAST): tips_amd/csrc/pyfast.cc
+	g++ -O2 -std=c++17 -shared -fPIC -Wall -D_GLIBCXX_USE_CXX11_ABI=1 -I$(PYINC) -I$(TORCH)/include \
+	  -I$(TORCH)/include/torch/csrc/api/include -o $@ $< -L$(TORCH)/lib -ltorch_python -ltorch -lc10 \
+	  -Wl,-rpath,$(TORCH)/lib
 
 # bench.py's last-words hook (not part of the product library)
 $(CRASH): tools/crash_line.c

@@ -294,3 +294,36 @@ def test_distributed_gradient_tape(monkeypatch):
         tips_amd.DistributedGradientTape(num_groups=2)
     with pytest.raises(ValueError, match="gradient"):
         tips_amd.DistributedGradientTape(object())
+
+
+def test_fast_list_helper_reads_pointers_counts_and_shapes():
+    """tips_amd._fast (the list helper allreduce_grads' device path uses) on CPU tensors: data
+    pointers and counts as torch reports them, one hash per shape list, None for a list it must not
+    take (another dtype, a strided view, a non-tensor), and max_refcount as sys.getrefcount - 1."""
+    import ctypes
+    import sys
+    import torch
+    from tips_amd import _fast
+    flat = torch.zeros(4096)
+    ts = [flat[0:10].view(2, 5), flat[64:64 + 7], flat[128:128 + 300].view(3, 10, 10), torch.zeros(0)]
+    n = len(ts)
+    pa, na = (ctypes.c_int64 * n)(), (ctypes.c_int64 * n)()
+    a, b = ctypes.addressof(pa), ctypes.addressof(na)
+    st, dev, h = _fast.dev_list(ts, a, b, 0)
+    assert st == 6 and dev == -1  # c10::ScalarType::Float, CPU
+    assert list(pa) == [t.data_ptr() for t in ts] and list(na) == [t.numel() for t in ts]
+    # the hash follows the shapes, not only the counts
+    ts2 = [flat[0:10].view(5, 2)] + ts[1:]
+    assert _fast.dev_list(ts2, a, b, 0)[2] != h
+    assert _fast.dev_list(list(ts), a, b, 0)[2] == h
+    # lists it leaves to the general path
+    assert _fast.dev_list(ts, a, b, 1) is None                       # not device tensors
+    assert _fast.dev_list(ts[:2] + [torch.zeros(3, dtype=torch.float64)], a, b, 0) is None
+    assert _fast.dev_list([flat[::2]], a, b, 0) is None              # not contiguous
+    assert _fast.dev_list([flat[:4], None], a, b, 0) is None
+    assert _fast.dev_list([torch.zeros(3).to_sparse()], a, b, 0) is None
+    x = torch.zeros(3)
+    assert _fast.max_refcount([x]) == sys.getrefcount(x) - 1
+    keep = [x, x]
+    assert _fast.max_refcount([x]) == sys.getrefcount(x) - 1 and len(keep) == 2
+    assert _fast.max_refcount([]) == 0

@@ -143,7 +143,10 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
     if _DATA_PTR is None:
         import torch
         _DATA_PTR = torch.Tensor.data_ptr
-    if fused and none:
+    if fused and none and grads:
+        res = _ops._dev_list_flat(grads)  # (one dtype of dense device tensors: the common case)
+        if res is not None:
+            return res
         plan = _find_plan(grads)
         if plan is not None:  # the same tensor objects as a recent call: no per-tensor inspection
             res = plan.run(grads)

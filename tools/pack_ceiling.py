@@ -31,9 +31,11 @@ def main():
     import torch
 
     import bench
+    import tips_amd
     from tips_amd import _lib
     L = _lib.lib()
     torch.cuda.set_device(0)
+    tips_amd.init()
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     thr = 64 << 20
