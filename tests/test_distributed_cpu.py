@@ -204,3 +204,64 @@ def test_fusion_layout_mirror():
         if len(b) > 1:
             share = packed / len(b)
             assert all(f <= share + max(sizes) * 4 + 256 for f in fills)
+
+
+def _unused_param_worker(rank, world, port, q):
+    """One rank of test_unused_parameter_differs_by_rank: gloo all_reduce stands in for the bucket
+    allreduce (the same blocking pairing RCCL needs: every rank the same sequence of sizes)."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    from tips_amd.optim import _GradBuckets
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 8))
+    extra = torch.nn.Parameter(torch.ones(7))  # reversed order: in bucket 0, the first to issue
+    log = []
+
+    def issue(flat):
+        log.append(flat.numel())
+        dist.all_reduce(flat)
+
+    gb = _GradBuckets(list(m.parameters()) + [extra], 1024, 1, False, issue=issue)
+    g = torch.Generator().manual_seed(100 + rank)
+    loss = m(torch.randn(5, 16, generator=g)).pow(2).sum()
+    if rank % 2 == 1:  # only odd ranks use `extra`: whether bucket 0 fills during backward is rank-local
+        loss = loss + (extra * extra).sum()
+    loss.backward()
+    during = list(log)
+    gb.synchronize()
+    grads = [p.grad.clone() if p.grad is not None else None for p in list(m.parameters()) + [extra]]
+    view_extra = gb.view(extra).clone()
+    gb.remove()
+    dist.destroy_process_group()
+    q.put((rank, during, log, [x.tolist() if x is not None else None for x in grads], view_extra.tolist()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_unused_parameter_differs_by_rank(world):
+    """a parameter that gets a gradient on some ranks only. The ranks whose hooks could
+    not issue bucket 0 during backward issue every bucket from synchronize(), one by one, so every
+    rank sends the same sequence of bucket allreduces (sizes in order) and the sums agree - the
+    whole-group shortcut would have paired one group-sized allreduce with several bucket-sized ones."""
+    import torch.multiprocessing as tmp
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_unused_param_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    seqs = [log for _, _, log, _, _ in res]
+    assert all(s == seqs[0] for s in seqs) and len(seqs[0]) > 1
+    assert res[0][1] == [] and res[1][1] == seqs[0]  # rank 0 issued nothing during backward; rank 1 all
+    for r in range(1, world):
+        assert res[r][3][:-1] == res[0][3][:-1]  # identical sums on every rank
+        assert res[r][4] == res[0][4]
+    n_using = world // 2
+    assert res[0][4] == [2.0 * n_using] * 7  # d(extra . extra) = 2 extra, summed over the ranks that used it
