@@ -8,6 +8,8 @@ behind a spin so they run back to back, median of interleaved rounds:
   contig    the same kernel on a list of ONE tensor of the bucket's byte count (every tile on the
             one-segment fast path: no segment search, no ragged ends)
   memcpy    hipMemcpyAsync D2D of the same bytes (the copy engine path torch uses for copy_)
+  span_us   (launches of one bucket) one event pair around each launch instead of one pair around
+            20 back-to-back launches: the launch's own span, without the boundary to the next
   sizes     `contig` at 10-640 MiB, fitted to t = t0 + bytes / BW: t0 is the per-launch ramp and
             drain, BW the streaming rate; frac(S) = 2S / t(S) / 8 TB/s
 One JSON line per measurement to stdout.
@@ -52,6 +54,18 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / reps
+
+    def spans(fn, reps):
+        """one event pair around each call, all queued behind the gate: the calls' own spans,
+        without the boundary between one launch and the next"""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+        torch.cuda._sleep(12_000_000)
+        for k in range(reps):
+            ev[2 * k].record(stream)
+            fn(k)
+            ev[2 * k + 1].record(stream)
+        torch.cuda.synchronize()
+        return sum(ev[2 * k].elapsed_time(ev[2 * k + 1]) for k in range(reps)) * 1e3 / reps
 
     cases = {}
     sizes_only = os.environ.get("TIPS_FUSION_THRESHOLD") is not None  # (the configs' layouts would change)
@@ -103,9 +117,12 @@ def main():
         cases["size/contig_%dMiB" % mib] = (contig, 1, n1 * 4)
     torch.cuda.synchronize()
     res = {k: [] for k in cases}
+    spn = {k: [] for k in cases}
     for r in range(rounds):
         for k, (fn, per, _b) in cases.items():
             res[k].append(timed(fn, 20) / per)
+            if per == 1:
+                spn[k].append(spans(fn, 20))
     fit = []
     for k, (fn, per, b) in cases.items():
         us = statistics.median(res[k])
@@ -114,7 +131,8 @@ def main():
             fit.append((2 * b, us))
         print(json.dumps({"case": k, "bytes_per_launch": int(b), "us_per_launch": round(us, 2),
                           "GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
-                          "spread_us": [round(min(res[k]), 2), round(max(res[k]), 2)]}), flush=True)
+                          "spread_us": [round(min(res[k]), 2), round(max(res[k]), 2)],
+                          "span_us": round(statistics.median(spn[k]), 2) if spn[k] else None}), flush=True)
     if len(fit) >= 2:
         n = len(fit)
         mx = sum(x for x, _ in fit) / n
