@@ -346,8 +346,12 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
             "(%.1f GiB/s), -> last D2H %.0f us\n", (long long)total, np, nthreads, (int)direct_out, t_pack, t_wait,
             t_unpack, t_issue, since(t_start), h2d * 1e3, total / (h2d * 1e-3) / 1073741824.0, d2h * 1e3);
   };
+  // TIPS_HOST_H2D_STREAMS=2: odd pieces' H2D on a second stream (a second DMA queue), so the link
+  // does not idle between one piece's copy and the next while the runtime starts it
+  const bool two_h2d = env_i64("TIPS_HOST_H2D_STREAMS", 1) >= 2;
   for (int i = 0; i < np; i++) {
     const int64_t off = pieces[(size_t)i].off, len = pieces[(size_t)i].len;
+    hipStream_t hs = two_h2d && (i & 1) ? st.h2d_stream2 : st.h2d_stream;
     auto t0 = std::chrono::steady_clock::now();
     if (i >= R) HIP_TRY(hipEventSynchronize(ev[3 * (i - R)]));  // slot i % R: its last H2D has read it
     t_wait += since(t0);
@@ -355,10 +359,9 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     host_copy(i, true);
     t_pack += since(t0);
     t0 = std::chrono::steady_clock::now();
-    if (trace && i == 0) HIP_TRY(hipEventRecord(tev[0], st.h2d_stream));
-    HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice,
-                           st.h2d_stream));
-    HIP_TRY(hipEventRecord(ev[3 * i], st.h2d_stream));
+    if (trace && i == 0) HIP_TRY(hipEventRecord(tev[0], hs));
+    HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice, hs));
+    HIP_TRY(hipEventRecord(ev[3 * i], hs));
     HIP_TRY(hipStreamWaitEvent(st.io_stream, ev[3 * i], 0));
     TRY(allreduce_device(st, dev + off, dev + off, len / es, dtype, st.io_stream));
     HIP_TRY(hipEventRecord(ev[3 * i + 1], st.io_stream));
@@ -368,7 +371,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     HIP_TRY(hipMemcpyAsync(d2h, dev + off, (size_t)len, hipMemcpyDeviceToHost, st.d2h_stream));
     HIP_TRY(hipEventRecord(ev[3 * i + 2], st.d2h_stream));
     if (trace && i == np - 1) {
-      HIP_TRY(hipEventRecord(tev[1], st.h2d_stream));
+      HIP_TRY(hipEventRecord(tev[1], hs));
       HIP_TRY(hipEventRecord(tev[2], st.d2h_stream));
     }
     t_issue += since(t0);

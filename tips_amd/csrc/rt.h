@@ -174,6 +174,7 @@ struct State {
   ncclComm_t comm = nullptr;
   hipStream_t comm_stream = nullptr, comp_stream = nullptr, io_stream = nullptr;
   hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // host-memory pipeline (both PCIe directions)
+  hipStream_t h2d_stream2 = nullptr;  // fused host lists: odd pieces' H2D (TIPS_HOST_H2D_STREAMS=2)
   EventPool pipe_ev;
   hipStream_t fuse_stream = nullptr, bucket_stream = nullptr;  // fusion: pack/unpack || bucket allreduce
   EventPool fuse_ev;

@@ -67,6 +67,7 @@ int ensure_streams(State& st) {
   if (!st.io_stream) HIP_TRY(hipStreamCreateWithFlags(&st.io_stream, hipStreamNonBlocking));
   if (!st.h2d_stream) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream, hipStreamNonBlocking));
   if (!st.d2h_stream) HIP_TRY(hipStreamCreateWithFlags(&st.d2h_stream, hipStreamNonBlocking));
+  if (!st.h2d_stream2) HIP_TRY(hipStreamCreateWithFlags(&st.h2d_stream2, hipStreamNonBlocking));
   if (!st.fuse_stream) HIP_TRY(hipStreamCreateWithFlags(&st.fuse_stream, hipStreamNonBlocking));
   if (!st.bucket_stream) HIP_TRY(hipStreamCreateWithFlags(&st.bucket_stream, hipStreamNonBlocking));
   if (!st.ev_start) HIP_TRY(hipEventCreateWithFlags(&st.ev_start, hipEventDisableTiming));

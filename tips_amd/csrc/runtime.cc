@@ -139,7 +139,7 @@ void tips_shutdown(void) {
   st.fuse_ev.release();
   st.fusion_threshold = 0;
   for (hipStream_t* s : {&st.comm_stream, &st.comp_stream, &st.io_stream, &st.h2d_stream, &st.d2h_stream,
-                         &st.fuse_stream, &st.bucket_stream, &st.graph_stream})
+                         &st.h2d_stream2, &st.fuse_stream, &st.bucket_stream, &st.graph_stream})
     if (*s) {
       (void)hipStreamDestroy(*s);
       *s = nullptr;

@@ -117,26 +117,44 @@ def fused(sizes, label):
          ms=[round(t * 1e3, 3) for t in ts], gib_s_best=round(total / min(ts) / GIB, 2), ok=ok)
 
 
+VARIANTS = [[("TIPS_HOST_DIRECT_OUT", "0")], [("TIPS_HOST_THREADS", "4")], [("TIPS_HOST_THREADS", "16")],
+            [("TIPS_HOST_THREADS", "1")], [("TIPS_HOST_FUSED_PIECE_BYTES", str(4 << 20))],
+            [("TIPS_HOST_FUSED_PIECE_BYTES", str(8 << 20))], [("TIPS_HOST_FUSED_PIECE_BYTES", str(32 << 20))]]
+# --streams: the second H2D stream against one, at three piece sizes, rounds interleaved
+STREAM_VARIANTS = [[]] + [[("TIPS_HOST_H2D_STREAMS", "2")] + ([("TIPS_HOST_FUSED_PIECE_BYTES", str(p))] if p else [])
+                          for p in (0, 8 << 20, 32 << 20)] + [[("TIPS_HOST_FUSED_PIECE_BYTES", str(32 << 20))]]
+
+
+def run_variant(sizes, kv):
+    old = {k: os.environ.get(k) for k, _ in kv}
+    os.environ.update(dict(kv))
+    fused(sizes, ",".join("%s=%s" % x for x in kv) or "default")
+    for k, v in old.items():
+        if v is None:
+            del os.environ[k]
+        else:
+            os.environ[k] = v
+
+
 def main():
     import bench
     sizes = bench.resnet50_grad_sizes()
-    for th in (1, 4, 8, 16):
-        memcpy_rate(sum(sizes) * 4, th)
-    link_rates(8 << 20)
-    link_rates(64 << 20)
+    streams = "--streams" in sys.argv
+    if not streams:
+        for th in (1, 4, 8, 16):
+            memcpy_rate(sum(sizes) * 4, th)
+        link_rates(8 << 20)
+        link_rates(64 << 20)
     import tips_amd
     tips_amd.init()
-    fused(sizes, "default")
-    for k, v in [("TIPS_HOST_DIRECT_OUT", "0"), ("TIPS_HOST_THREADS", "4"), ("TIPS_HOST_THREADS", "16"), ("TIPS_HOST_THREADS", "1"),
-                 ("TIPS_HOST_FUSED_PIECE_BYTES", str(4 << 20)), ("TIPS_HOST_FUSED_PIECE_BYTES", str(16 << 20)),
-                 ("TIPS_HOST_FUSED_PIECE_BYTES", str(32 << 20))]:
-        old = os.environ.get(k)
-        os.environ[k] = v
-        fused(sizes, "%s=%s" % (k, v))
-        if old is None:
-            del os.environ[k]
-        else:
-            os.environ[k] = old
+    if streams:
+        for _ in range(3):
+            for kv in STREAM_VARIANTS:
+                run_variant(sizes, kv)
+    else:
+        fused(sizes, "default")
+        for kv in VARIANTS:
+            run_variant(sizes, kv)
     tips_amd.shutdown()
 
 
