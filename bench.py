@@ -1201,7 +1201,7 @@ def bench_allreduce(args):
         line["host_to_host_fused"] = {
             "ms_per_step": round(tf * 1e3, 3), "algbw_gib_s": round(total_elems * 4 / tf / GIB, 2),
             "steps": hsteps, "threads": int(os.environ.get("TIPS_HOST_THREADS", "8")),
-            "piece_bytes": int(os.environ.get("TIPS_HOST_FUSED_PIECE_BYTES", str(16 << 20))),  # (host_staging.cc's default)
+            "piece_bytes": int(os.environ.get("TIPS_HOST_FUSED_PIECE_BYTES", str(32 << 20))),  # (host_staging.cc's default)
             "h2d_streams": int(os.environ.get("TIPS_HOST_H2D_STREAMS", "1")),
             "vs_per_tensor": round(th / tf, 2),
             "check": "identity at one rank, bit-exact" if world == 1 and f_ok else ("FAIL" if not f_ok else "not checked"),

@@ -227,8 +227,9 @@ TIPS_API int tips_fusion_stats(int64_t* layouts_built, int64_t* layout_hits, int
                                int64_t* table_hits);
 /* Host tensors (numpy / CPU framework tensors, pageable or page-locked): outs[i] = SUM over ranks of
  * ins[i]. The list is packed by the library's host threads (TIPS_HOST_THREADS, 8) into page-locked
- * pieces of one byte stream (TIPS_HOST_FUSED_PIECE_BYTES, 8 MiB); each piece runs H2D -> allreduce in
- * HBM -> D2H pipelined on separate streams while the threads pack the next and unpack the previous.
+ * pieces of one byte stream (TIPS_HOST_FUSED_PIECE_BYTES, 32 MiB, ramped from 2 MiB at both ends);
+ * each piece runs H2D -> allreduce in HBM -> D2H pipelined on separate streams while the threads
+ * pack the next and unpack the previous.
  * The layout depends on the counts only. Blocks until every out is written (the reference's op is a
  * CPU op, ops.cc:118; its per-gradient loop, __init__.py:212-222, fused). */
 TIPS_API int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const int64_t* counts, int n,

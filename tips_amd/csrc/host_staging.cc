@@ -286,8 +286,11 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   if (segs.empty()) return 0;
   std::sort(segs.begin(), segs.end(), [](const HostSeg& x, const HostSeg& y) { return x.off < y.off; });
   total = round_up(total, kAlignBytes);
+  // 32 MiB middle pieces (between the 2 MiB ramps): config 5 host -> host 31-32 GiB/s best, 3.06-3.31 ms
+  // median, against 26-31 GiB/s / 3.38-4.25 ms at 16 MiB and 24-28 at 8 MiB (3 interleaved rounds on one
+  // box, profiles/r03/e_host_probe_streams.jsonl); a second H2D stream did not help reliably
   const int64_t piece = std::min<int64_t>(
-      total, round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_FUSED_PIECE_BYTES", 16 << 20)), kAlignBytes));
+      total, round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_FUSED_PIECE_BYTES", 32 << 20)), kAlignBytes));
   const std::vector<Piece> pieces = host_pieces(total, piece, env_i64("TIPS_HOST_FUSED_FIRST_BYTES", 2 << 20));
   const int np = (int)pieces.size();
   const int R = 3;  // page-locked slots per direction; piece i uses slot i % R

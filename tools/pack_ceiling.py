@@ -14,7 +14,7 @@ behind a spin so they run back to back, median of interleaved rounds:
             drain, BW the streaming rate; frac(S) = 2S / t(S) / 8 TB/s
 One JSON line per measurement to stdout.
 
-usage: python3 tools/pack_ceiling.py [rounds]
+usage: python3 tools/pack_ceiling.py [rounds] [--only=CASE_PREFIX ...]
        TIPS_FUSION_THRESHOLD=2147483648 python3 tools/pack_ceiling.py [rounds]   (the size series only, to 640 MiB)
 """
 import ctypes
@@ -26,10 +26,12 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PEAK = 8000.0  # GB/s
+ONLY = [a[len("--only="):] for a in sys.argv[1:] if a.startswith("--only=")]
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    args = [a for a in sys.argv[1:] if not a.startswith("--only=")]
+    rounds = int(args[0]) if args else 7
     import torch
 
     import bench
@@ -67,10 +69,17 @@ def main():
         torch.cuda.synchronize()
         return sum(ev[2 * k].elapsed_time(ev[2 * k + 1]) for k in range(reps)) * 1e3 / reps
 
+    only = ONLY
+
+    def want(name):
+        return not only or any(name.startswith(o) for o in only)
+
     cases = {}
     sizes_only = os.environ.get("TIPS_FUSION_THRESHOLD") is not None  # (the configs' layouts would change)
     workloads = () if sizes_only else (("config4", bench.fused1000_sizes()), ("config5", bench.resnet50_grad_sizes()))
     for wname, sizes in workloads:
+        if only and not any(o.startswith(wname + "/") or wname.startswith(o) for o in only):
+            continue
         sets = [[torch.randn(n, device="cuda") for n in sizes] for _ in range(4)]
         ptrs = [_lib.ptr_array([t.data_ptr() for t in s]) for s in sets]
         cp, _kc = _lib.i64_array(sizes)
@@ -89,6 +98,8 @@ def main():
                     raise _lib.TipsError("tips_fused_pack_bucket", int(rc), _lib.last_error())
         cases[wname + "/pack"] = (pack, nb, sum(payload) / nb)
         for b, pb in enumerate(payload):
+            if not want("%s/contig_b%d" % (wname, b)) and not want("%s/memcpy_b%d" % (wname, b)):
+                continue
             n1 = pb // 4
             one = [torch.randn(n1, device="cuda") for _ in range(4)]
             op = [_lib.ptr_array([t.data_ptr()]) for t in one]
@@ -103,6 +114,8 @@ def main():
             cases["%s/contig_b%d" % (wname, b)] = (contig, 1, pb)
             cases["%s/memcpy_b%d" % (wname, b)] = (memcpy, 1, pb)
     for mib in (10, 20, 40, 80, 160, 320, 640):
+        if not want("size/contig_%dMiB" % mib):
+            continue
         n1 = (mib << 20) // 4
         one = [torch.randn(n1, device="cuda") for _ in range(4)]
         big = torch.empty(n1, device="cuda")
@@ -115,6 +128,8 @@ def main():
             L.tips_fused_pack_bucket(op[k % 4][0], oc, 1, _lib.FLOAT32, 0, big.data_ptr(), sp)
         contig(0)
         cases["size/contig_%dMiB" % mib] = (contig, 1, n1 * 4)
+    if only:  # (PMC passes: only the named cases' launches)
+        cases = {k: v for k, v in cases.items() if any(k.startswith(o) for o in only)}
     torch.cuda.synchronize()
     res = {k: [] for k in cases}
     spn = {k: [] for k in cases}
