@@ -16,7 +16,7 @@ FAST     := tips_amd/_fast$(shell python3 -c "import sysconfig; print(sysconfig.
 TORCH    := $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
 PYINC    := $(shell python3 -c "import sysconfig; print(sysconfig.get_paths()['include'])")
 
-all: $(LIB) $(FAST) $(CRASH) $(REPRO) oracle
+all: $(LIB) $(FAST) $(CRASH) $(REPRO) oracle tsan
 
 # the Python mirror's list helper (tips_amd._fast: tensor pointers / counts in C++), torch headers
 $(FAST): tips_amd/csrc/pyfast.cc
@@ -56,6 +56,34 @@ tools/_bin/op_body: tests/c/op_body.c $(LIB) include/tips_hip.h oracle/build/lib
 oracle/build/liboracle.so: oracle/oracle.c oracle/oracle.h
 	$(MAKE) -C oracle build/liboracle.so
 
+# ThreadSanitizer build of the same sources (host code only: -fsanitize=thread after -Xarch_host;
+# device code unchanged) and its CPU driver - tests/test_tsan.py (the negotiation with threads and
+# callbacks, the host copy pool); tools/_bin/op_body_tsan runs the op-body test on the GPU box
+TSAN_OBJS := $(patsubst tips_amd/csrc/%,build/tsan/%.o,$(SRCS))
+TSAN_LIB  := tools/lib/libtips_hip_tsan.so
+CLANG     := /opt/rocm/lib/llvm/bin/clang
+
+build/tsan/%.o: tips_amd/csrc/% $(HDRS)
+	@mkdir -p build/tsan
+	$(HIPCC) --offload-arch=$(ARCH) -O1 -g -std=c++17 -fPIC -fno-gpu-flush-denormals-to-zero -fvisibility=hidden \
+	  -Xarch_host -fsanitize=thread -c -o $@ $<
+
+$(TSAN_LIB): $(TSAN_OBJS)
+	@mkdir -p tools/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(TSAN_OBJS) -lrccl
+
+tools/_bin/tsan_selftest: tools/tsan_selftest.c $(TSAN_LIB) include/tips_hip.h
+	@mkdir -p tools/_bin
+	$(CLANG) -O1 -g -fsanitize=thread -Iinclude -o $@ $< -Ltools/lib -ltips_hip_tsan -Wl,-rpath,'$$ORIGIN/../lib'
+
+tools/_bin/op_body_tsan: tests/c/op_body.c $(TSAN_LIB) include/tips_hip.h oracle/build/liboracle.so
+	@mkdir -p tools/_bin
+	$(CLANG) -O1 -g -fsanitize=thread -std=gnu11 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -Ioracle -o $@ $< \
+	  -Ltools/lib -ltips_hip_tsan -Loracle/build -loracle -L/opt/rocm/lib -lamdhip64 -lpthread \
+	  -Wl,-rpath,'$$ORIGIN/../lib' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -Wl,-rpath,/opt/rocm/lib
+
+tsan: tools/_bin/tsan_selftest tools/_bin/op_body_tsan
+
 tools/_bin/graph_probe: tools/graph_probe.cc
 	@mkdir -p tools/_bin
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -o $@ $< -lrccl
@@ -84,4 +112,4 @@ clean:
 	rm -f $(LIB) $(REPRO) tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle tools repro clean
+.PHONY: all oracle tools repro clean tsan

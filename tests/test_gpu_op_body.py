@@ -31,14 +31,26 @@ def _port():
 
 @pytest.mark.parametrize("p,tensors", [(3, 96), (2, 40)])
 def test_op_body_over_rccl(gpu, p, tensors):
-    exe = os.path.join(REPO, "tools", "_bin", "op_body")
-    assert os.path.exists(exe), "build it first: make tools/_bin/op_body (part of __graft_entry__.build())"
+    _run_op_body(p, tensors, "op_body")
+
+
+def test_op_body_under_tsan(gpu):
+    """The same over 3 RCCL ranks with the library's host code built -fsanitize=thread
+    (tools/_bin/op_body_tsan on tools/lib/libtips_hip_tsan.so, `make tsan`): the negotiation
+    thread, the completion thread, the issuing threads and the real executor's HIP / RCCL calls,
+    with any data race ThreadSanitizer sees in the library failing the test (halt_on_error)."""
+    _run_op_body(3, 48, "op_body_tsan", {"TSAN_OPTIONS": "halt_on_error=1 exitcode=66 report_signal_unsafe=0"})
+
+
+def _run_op_body(p, tensors, binary, extra_env=None):
+    exe = os.path.join(REPO, "tools", "_bin", binary)
+    assert os.path.exists(exe), "build it first: make tools/_bin/%s (part of __graft_entry__.build())" % binary
     port = _port()
     procs = []
     for r in range(p):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(p), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), TIPS_BOOTSTRAP_PORT=str(port), NCCL_HOSTID="tips-op-body-%d" % r,
-                   NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", OP_BODY_TENSORS=str(tensors))
+                   NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", OP_BODY_TENSORS=str(tensors), **(extra_env or {}))
         procs.append(subprocess.Popen([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = []
     try:
@@ -50,6 +62,7 @@ def test_op_body_over_rccl(gpu, p, tensors):
             if pr.poll() is None:
                 pr.kill()
     for rc, out, err in outs:
+        assert "ThreadSanitizer" not in err, err[-6000:]
         line = [l for l in out.splitlines() if l.startswith("{")]
         assert line, (rc, out[-2000:], err[-2000:])
         res = json.loads(line[-1])
