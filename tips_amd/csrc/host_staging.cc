@@ -3,8 +3,10 @@
 // host memory and must return there: this file moves them through HBM with
 // both PCIe directions and the device allreduce overlapped.
 #include <immintrin.h>
+#include <sched.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <condition_variable>
@@ -146,17 +148,39 @@ void HostPool::grab(uint64_t gen) {  // claim jobs of run `gen` until none is le
 }
 
 void HostPool::worker() {
-  uint64_t seen = 0;
+  uint64_t seen = 0, mask_seen = 0;
+  cpu_set_t start;
+  const bool have_start = sched_getaffinity(0, sizeof start, &start) == 0;
   while (true) {
     uint64_t gen;
+    std::vector<unsigned char> want;
+    bool remask = false;
     {
       std::unique_lock<std::mutex> l(m_);
       cv_.wait(l, [&] { return stop_ || gen_ != seen; });
       if (stop_) return;
       seen = gen = gen_;
+      if (mask_gen_.load() != mask_seen) {
+        mask_seen = mask_gen_.load();
+        want = mask_;
+        remask = true;
+      }
+    }
+    if (remask) {  // (best effort: a refused mask leaves the thread where it was)
+      if (want.size() == sizeof(cpu_set_t)) (void)sched_setaffinity(0, sizeof(cpu_set_t), (const cpu_set_t*)want.data());
+      else if (have_start) (void)sched_setaffinity(0, sizeof start, &start);
     }
     grab(gen);
   }
+}
+
+void HostPool::set_affinity(const void* cpus) {
+  std::lock_guard<std::mutex> l(m_);
+  std::vector<unsigned char> m;
+  if (cpus) m.assign((const unsigned char*)cpus, (const unsigned char*)cpus + sizeof(cpu_set_t));
+  if (m == mask_) return;
+  mask_ = std::move(m);
+  mask_gen_.fetch_add(1);
 }
 
 void HostPool::run(int njobs, const std::function<void(int)>& fn) {
@@ -214,6 +238,53 @@ std::vector<Piece> host_pieces(int64_t total, int64_t piece, int64_t first) {
 }
 
 namespace {
+
+bool read_cpulist(const std::string& path, cpu_set_t* set) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  char buf[4096] = {0};
+  const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+  fclose(f);
+  if (!ok) return false;
+  CPU_ZERO(set);
+  for (char* p = buf; *p && *p != '\n';) {
+    char* e = nullptr;
+    long a = strtol(p, &e, 10);
+    if (e == p) return false;
+    long b = a;
+    if (*e == '-') {
+      p = e + 1;
+      b = strtol(p, &e, 10);
+      if (e == p) return false;
+    }
+    for (long c = a; c <= b && c < CPU_SETSIZE; c++) CPU_SET((int)c, set);
+    p = *e == ',' ? e + 1 : e;
+  }
+  return true;
+}
+
+// The CPUs of the device's NUMA node that this process may run on (PCI sysfs): where the fused host
+// path's copy threads sit with TIPS_HOST_BIND=1, next to the root complex the DMA engines use.
+// False when the node is unknown or none of its CPUs is allowed.
+bool gpu_local_cpus(int device, cpu_set_t* out) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  for (char* c = bus; *c; c++) *c = (char)tolower((unsigned char)*c);
+  FILE* f = fopen((std::string("/sys/bus/pci/devices/") + bus + "/numa_node").c_str(), "r");
+  if (!f) return false;
+  int node = -1;
+  const int got = fscanf(f, "%d", &node);
+  fclose(f);
+  if (got != 1 || node < 0) return false;
+  cpu_set_t local, allowed;
+  if (!read_cpulist("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", &local)) return false;
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
+  CPU_AND(out, &local, &allowed);
+  return CPU_COUNT(out) > 0;
+}
 
 // Host copies of the fused path: bytes that the DMA engine (pack) or the caller (unpack) reads next,
 // not this thread. Streaming stores skip the read-for-ownership of every destination line and keep
@@ -298,6 +369,16 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   if (!st.host_pool || st.host_pool->size() != nthreads) {
     delete st.host_pool;
     st.host_pool = new HostPool(nthreads);
+  }
+  {  // TIPS_HOST_BIND=1: the pool's threads on the GPU's NUMA node (the caller's thread stays put)
+    static int local_ok = -1;
+    static cpu_set_t local;
+    if (env_i64("TIPS_HOST_BIND", 0) != 0) {
+      if (local_ok < 0) local_ok = gpu_local_cpus(st.device, &local) ? 1 : 0;
+      st.host_pool->set_affinity(local_ok == 1 ? &local : nullptr);
+    } else {
+      st.host_pool->set_affinity(nullptr);
+    }
   }
   if (st.hpin_bytes < (size_t)(R * piece)) {
     for (void*& p : st.hpin)

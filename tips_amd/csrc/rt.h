@@ -153,10 +153,15 @@ class HostPool {
   ~HostPool();
   void run(int njobs, const std::function<void(int)>& fn);
   int size() const { return (int)th_.size() + 1; }
+  // the CPUs the worker threads run on from their next job on: `cpus` (a cpu_set_t), or nullptr
+  // for the mask they started with (TIPS_HOST_BIND: the GPU's NUMA node)
+  void set_affinity(const void* cpus);
 
  private:
   void worker();
   void grab(uint64_t gen);
+  std::vector<unsigned char> mask_;  // guarded by m_: the wanted cpu_set_t bytes (empty: the start mask)
+  std::atomic<uint64_t> mask_gen_{0};
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
