@@ -116,6 +116,12 @@ TIPS_API int tips_bootstrap_broadcast(int rank, int size, const char* host, int 
  * connections a joining rank dropped because they reached itself (TCP simultaneous open), and
  * connections rank 0 dropped because the joiner never confirmed them (it gave up waiting). */
 TIPS_API int tips_net_stats(int64_t* self_connects_refused, int64_t* unconfirmed_joins_refused);
+/* Diagnostics (no reference counterpart): one line on what the negotiation's threads are doing now
+ * - the background thread's phase (waiting, exchanging cycle k, executing request i of a cycle's
+ * list), the completion thread's (which request's device work it waits for), the request queues and
+ * the names still waiting for other ranks. Never blocks on the library's locks: for a watchdog's
+ * hang report. */
+TIPS_API int tips_debug_state(char* out, int64_t cap);
 /* Message of the calling thread's last failed call ("" if none). */
 TIPS_API const char* tips_last_error(void);
 /* Library version string. */

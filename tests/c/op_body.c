@@ -168,21 +168,46 @@ static void* sync_caller(void* arg) {
   return NULL;
 }
 
-/* a watchdog: a hang ends the process with a line saying how far it got */
-static void on_alarm(int sig) {
-  (void)sig;
-  char b[256];
-  const int n = snprintf(b, sizeof b, "{\"rank\": %d, \"ok\": false, \"error\": \"watchdog: %d of %d callbacks\"}\n",
-                         g_rank, atomic_load(&g_callbacks), g_ntensors);
-  if (write(1, b, (size_t)n) < 0) _exit(5);
+/* a watchdog thread: while the run is not finished it reports at 60 and 120 s what the library's
+ * threads are doing (tips_debug_state) and which tensors are still open, and at 200 s ends the
+ * process with a JSON line saying how far it got and that report */
+static atomic_int g_finished;
+static void report(char* b, size_t cap) {
+  char st[3072];
+  tips_debug_state(st, sizeof st);
+  size_t l = (size_t)snprintf(b, cap, "callbacks %d of %d; state: %s; open:", atomic_load(&g_callbacks), g_ntensors, st);
+  int shown = 0;
+  for (int i = 0; i < g_ntensors && shown < 12 && l < cap - 64; i++)
+    if (!atomic_load(&g_t[i].done)) {
+      l += (size_t)snprintf(b + l, cap - l, " %d(kind %d)", i, g_t[i].kind);
+      shown++;
+    }
+  for (char* c = b; *c; c++)
+    if (*c == '"') *c = '\'';
+}
+
+static void* watchdog(void* arg) {
+  (void)arg;
+  static char b[4096];
+  for (int t = 1; t <= 200; t++) {
+    sleep(1);
+    if (atomic_load(&g_finished)) return NULL;
+    if (t == 60 || t == 120) {
+      report(b, sizeof b);
+      fprintf(stderr, "[op_body rank %d] t=%ds %s\n", g_rank, t, b);
+    }
+  }
+  report(b, sizeof b);
+  fprintf(stderr, "[op_body rank %d] t=200s %s\n", g_rank, b);
+  printf("{\"rank\": %d, \"ok\": false, \"error\": \"watchdog: %s\"}\n", g_rank, b);
+  fflush(stdout);
   _exit(4);
+  return NULL;
 }
 
 int main(void) {
   const char* nt = getenv("OP_BODY_TENSORS");
   g_ntensors = nt ? atoi(nt) : 96;
-  signal(SIGALRM, on_alarm);
-  alarm(200);
   tips_init();
   if (!tips_is_initialize()) {
     printf("{\"ok\": false, \"error\": \"tips_init: %s\"}\n", tips_last_error());
@@ -191,6 +216,8 @@ int main(void) {
   g_rank = tips_rank();
   g_size = tips_size();
   g_t = (Tensor*)calloc((size_t)g_ntensors, sizeof(Tensor));
+  pthread_t wd;
+  pthread_create(&wd, NULL, watchdog, NULL);
   for (int i = 0; i < g_ntensors; i++) {
     Tensor* t = &g_t[i];
     t->index = i;
@@ -284,6 +311,7 @@ int main(void) {
     free(exp);
   }
   tips_shutdown();
+  atomic_store(&g_finished, 1);
   const int ok = callbacks == g_ntensors && bad == 0 && !atomic_load(&g_sync_bad);
   printf("{\"rank\": %d, \"ok\": %s, \"callbacks\": %d, \"tensors\": %d, \"sync_calls\": %d, \"error\": \"", g_rank,
          ok ? "true" : "false", callbacks, g_ntensors, SYNC_CALLS);

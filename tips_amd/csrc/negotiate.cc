@@ -534,6 +534,7 @@ class Negotiator {
     while (true) {
       std::vector<std::shared_ptr<Req>> batch;
       bool stopping;
+      set_phase("waiting for requests");
       {
         std::unique_lock<std::mutex> l(m_);
         cv_.wait_for(l, cycle, [&] { return !fresh_.empty() || want_stop_; });
@@ -563,7 +564,12 @@ class Negotiator {
         w.str(r->name);
       }
       std::string resp;
+      set_phase("exchange (cycle " + std::to_string((long long)cycles_) + ", announcing " + std::to_string(batch.size()) + ")");
       if (!exchange(w.b, &resp)) break;
+      {
+        std::lock_guard<std::mutex> l(phase_mu_);
+        cycles_++;
+      }
       Reader rd(resp);
       const bool shutdown = rd.get<uint8_t>() != 0;
       const uint32_t n = rd.get<uint32_t>();
@@ -628,13 +634,16 @@ class Negotiator {
         msg = r->err;
       } else if (r->state == 2) {
         hipEvent_t ev = r->gev ? r->gev->ev : r->ev;
+        set_waiter_phase("hipEventSynchronize of " + r->name + (r->gev ? " (fused batch)" : ""));
         const hipError_t e = hipEventSynchronize(ev);
         if (e != hipSuccess) {
           status = TIPS_ERR_HIP;
           msg = std::string("request ") + r->name + ": " + hipGetErrorString(e);
         }
       }
+      set_waiter_phase("callback of " + r->name);
       r->cb(r->cb_ctx, status, msg.c_str());
+      set_waiter_phase("idle");
       release(r->handle, r);
       std::lock_guard<std::mutex> l(m_);
       cb_called_++;
@@ -747,6 +756,12 @@ class Negotiator {
         if (!reqs[i] || state[i] != 2) {
           i++;
           continue;
+        }
+        set_phase("execute " + std::to_string(i) + "/" + std::to_string(n) + ": " + reqs[i]->name +
+                  (reqs[i]->body ? " (routed call)" : reqs[i]->host ? " (host)" : reqs[i]->type != TIPS_REQ_ALLREDUCE ? " (other)" : ""));
+        {
+          std::lock_guard<std::mutex> l(phase_mu_);
+          executed_++;
         }
         if (reqs[i]->body) {  // a routed synchronous collective: its own call, here, in rank 0's order
           const int rc = reqs[i]->body();
@@ -919,8 +934,45 @@ class Negotiator {
 
   EventPool join_ev_;
 
+  // what the two threads are doing now (tips_debug_state): guarded by phase_mu_, never held across
+  // a blocking call, so a dump from a watchdog always gets through
+  std::mutex phase_mu_;
+  std::string phase_ = "start", waiter_phase_ = "idle";
+  int64_t cycles_ = 0, executed_ = 0;
+  void set_phase(std::string p) {
+    std::lock_guard<std::mutex> l(phase_mu_);
+    phase_ = std::move(p);
+  }
+  void set_waiter_phase(std::string p) {
+    std::lock_guard<std::mutex> l(phase_mu_);
+    waiter_phase_ = std::move(p);
+  }
+
  public:
   std::atomic<int64_t> sync_seq{0};  // routed synchronous collectives so far: their names
+
+  // one line of state for a hang report: the threads' phases, the cycle count and the request
+  // queues (try_lock on the request lock: a dump never waits for a thread that might be stuck)
+  std::string debug_state() {
+    std::string out;
+    {
+      std::lock_guard<std::mutex> l(phase_mu_);
+      out = "rank " + std::to_string(rank_) + " cycles " + std::to_string((long long)cycles_) + " executed " +
+            std::to_string((long long)executed_) + " | negotiation: " + phase_ + " | completion: " + waiter_phase_;
+    }
+    std::unique_lock<std::mutex> l(m_, std::try_to_lock);
+    if (!l.owns_lock()) return out + " | (request lock held)";
+    out += " | fresh " + std::to_string(fresh_.size()) + " pending " + std::to_string(by_name_.size()) + " handles " +
+           std::to_string(by_handle_.size()) + " done_q " + std::to_string(done_q_.size()) + " callbacks " +
+           std::to_string((long long)cb_called_);
+    int k = 0;
+    for (auto& kv : by_name_) {
+      if (k++ == 8) break;
+      out += (k == 1 ? " | waiting for other ranks: " : ", ") + kv.first + "(state " + std::to_string(kv.second->state) + ")";
+    }
+    if (!done_q_.empty()) out += " | next callback: " + done_q_.front()->name + "(state " + std::to_string(done_q_.front()->state) + ")";
+    return out;
+  }
 };
 
 std::mutex g_neg_mu;
@@ -1093,6 +1145,16 @@ int tips_on_done(int64_t handle, tips_done_fn fn, void* ctx) {
   auto n = current();
   if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
   return n->on_done(handle, fn, ctx);
+}
+
+int tips_debug_state(char* out, int64_t cap) {
+  if (!out || cap < 1) return fail(TIPS_ERR_INVALID_ARG, "tips_debug_state: no buffer");
+  std::string st = "no negotiation";
+  std::unique_lock<std::mutex> l(g_neg_mu, std::try_to_lock);
+  if (!l.owns_lock()) st = "(negotiation being started or stopped)";
+  else if (g_neg) st = g_neg->debug_state();
+  snprintf(out, (size_t)cap, "%s", st.c_str());
+  return 0;
 }
 
 int tips_net_stats(int64_t* self_connects_refused, int64_t* unconfirmed_joins_refused) {

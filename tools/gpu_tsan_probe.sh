@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT="$PWD/gpurun_out/${TAG:-tsan}"
 mkdir -p "$OUT"
-export TSAN_OPTIONS="halt_on_error=1 exitcode=66 report_signal_unsafe=0 ${TSAN_EXTRA:-}"
+export TSAN_OPTIONS="halt_on_error=1 exitcode=66 report_signal_unsafe=0 suppressions=$PWD/tools/tsan.supp ${TSAN_EXTRA:-}"
 run_ranks() {  # p tensors tag limit
   local p=$1 n=$2 tag=$3 lim=$4 port=$((29500 + RANDOM % 2000)) pids=() r rc=0
   for ((r = 0; r < p; r++)); do

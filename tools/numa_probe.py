@@ -56,6 +56,20 @@ def main():
     total = sum(sizes) * 4
     for _ in range(3):
         tips_amd._reduce_grads(hg)
+    # the same bytes as ONE host buffer through tips_amd.allreduce (the single-bucket host pipeline):
+    # what a list of this total size could reach at best
+    one = np.random.default_rng(7).random(sum(sizes), dtype=np.float32)
+    for _ in range(2):
+        tips_amd.allreduce(one)
+    ts = []
+    for _ in range(10):
+        t0 = time.perf_counter()
+        r = tips_amd.allreduce(one)
+        ts.append(time.perf_counter() - t0)
+    del r
+    ts.sort()
+    emit(what="one_host_buffer_same_bytes", median_ms=round(ts[5] * 1e3, 3), best_ms=round(ts[0] * 1e3, 3),
+         median_gib_s=round(total / ts[5] / 2 ** 30, 2))
     for rnd in range(3):
         for bind in ("0", "1"):
             os.environ["TIPS_HOST_BIND"] = bind
