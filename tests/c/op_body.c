@@ -17,8 +17,11 @@
  *
  * Build: make tools/_bin/op_body. Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (tips_init), and
  * OP_BODY_TENSORS (default 96). */
+#include <dirent.h>
+#include <execinfo.h>
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
+#include <sys/syscall.h>
 #include <signal.h>
 #include <stdatomic.h>
 #include <unistd.h>
@@ -186,6 +189,33 @@ static void report(char* b, size_t cap) {
     if (*c == '"') *c = '\'';
 }
 
+/* every thread's stack on stderr (module+offset frames; tools/symbolize_stacks.py names them):
+ * each thread of the process is sent SIGUSR1 in turn and prints its own backtrace */
+static void on_usr1(int sig) {
+  (void)sig;
+  void* fr[48];
+  const int n = backtrace(fr, 48);
+  char hdr[64];
+  const int l = snprintf(hdr, sizeof hdr, "--- thread %ld\n", (long)syscall(SYS_gettid));
+  if (write(2, hdr, (size_t)l) < 0) return;
+  backtrace_symbols_fd(fr, n, 2);
+}
+
+static void dump_stacks(void) {
+  signal(SIGUSR1, on_usr1);
+  const long self = (long)syscall(SYS_gettid);
+  DIR* d = opendir("/proc/self/task");
+  if (!d) return;
+  struct dirent* e;
+  while ((e = readdir(d)) != NULL) {
+    const long tid = atol(e->d_name);
+    if (tid <= 0 || tid == self) continue;
+    syscall(SYS_tgkill, (long)getpid(), tid, SIGUSR1);
+    usleep(50000);
+  }
+  closedir(d);
+}
+
 static void* watchdog(void* arg) {
   (void)arg;
   static char b[4096];
@@ -195,6 +225,7 @@ static void* watchdog(void* arg) {
     if (t == 60 || t == 120) {
       report(b, sizeof b);
       fprintf(stderr, "[op_body rank %d] t=%ds %s\n", g_rank, t, b);
+      if (t == 60) dump_stacks();
     }
   }
   report(b, sizeof b);
@@ -218,6 +249,7 @@ int main(void) {
   g_t = (Tensor*)calloc((size_t)g_ntensors, sizeof(Tensor));
   pthread_t wd;
   pthread_create(&wd, NULL, watchdog, NULL);
+  pthread_detach(wd);
   for (int i = 0; i < g_ntensors; i++) {
     Tensor* t = &g_t[i];
     t->index = i;
