@@ -253,3 +253,33 @@ def test_join_counts_a_rank_only_once_it_confirms():
         assert rc == 0, err
         assert lines(log) == ["a OK"]
     assert res[0][4][1] >= 1, res[0][4]  # rank 0 dropped at least one unconfirmed connection
+
+
+def test_debug_state_reports_the_threads():
+    """tips_debug_state (the hang report op_body's watchdog prints): while a one-rank dry-run
+    negotiation runs a script with a pause in it, another thread reads a line naming the
+    background thread's phase, the cycle count and the queues; outside a negotiation it says so."""
+    import ctypes
+    import threading
+    import time
+    from tips_amd import _lib
+    L = _lib.lib()
+    b = ctypes.create_string_buffer(4096)
+    assert L.tips_debug_state(b, len(b)) == 0 and b.value == b"no negotiation"
+    out = ctypes.create_string_buffer(1 << 16)
+    rc = []
+    t = threading.Thread(target=lambda: rc.append(L.tips_negotiation_selftest(
+        0, 1, b"127.0.0.1", _port(), b"a 0 4\n@sleep 400\nb 0 8\n@wait", out, len(out))))
+    t.start()
+    seen = []
+    deadline = time.time() + 20
+    while t.is_alive() and time.time() < deadline:
+        L.tips_debug_state(b, len(b))
+        seen.append(b.value.decode())
+        time.sleep(0.02)
+    t.join(30)
+    assert rc == [0], _lib.last_error()
+    live = [s for s in seen if s.startswith("rank 0 cycles")]
+    assert live, seen[:3]
+    assert all("| negotiation: " in s and "| completion: " in s for s in live)
+    assert any(" pending " in s for s in live)

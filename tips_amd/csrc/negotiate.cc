@@ -978,6 +978,7 @@ class Negotiator {
 std::mutex g_neg_mu;
 std::shared_ptr<Negotiator> g_neg;  // (shared: a caller waiting on a request keeps it alive through a shutdown)
 std::string g_neg_failed;           // a failed start's verdict: later named requests fail with it at once
+Negotiator* g_selftest_neg = nullptr;  // a running tips_negotiation_selftest's own (tips_debug_state)
 
 int negotiation_port() {
   return (int)env_i64("TIPS_NEGOTIATION_PORT", env_i64("MASTER_PORT", 29500) + 19);
@@ -1153,6 +1154,7 @@ int tips_debug_state(char* out, int64_t cap) {
   std::unique_lock<std::mutex> l(g_neg_mu, std::try_to_lock);
   if (!l.owns_lock()) st = "(negotiation being started or stopped)";
   else if (g_neg) st = g_neg->debug_state();
+  else if (g_selftest_neg) st = g_selftest_neg->debug_state();
   snprintf(out, (size_t)cap, "%s", st.c_str());
   return 0;
 }
@@ -1265,6 +1267,16 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   const bool cbs = per.size() > 1;
   Negotiator neg;
   TRY(neg.start(rank, size, (host && *host) ? host : "127.0.0.1", port, true, 120, 0, synccount));
+  struct Registered {  // visible to tips_debug_state while it runs
+    explicit Registered(Negotiator* n) {
+      std::lock_guard<std::mutex> l(g_neg_mu);
+      g_selftest_neg = n;
+    }
+    ~Registered() {
+      std::lock_guard<std::mutex> l(g_neg_mu);
+      g_selftest_neg = nullptr;
+    }
+  } registered(&neg);
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<SelftestCount> counts(per.size());
   std::vector<int> issued(per.size(), 0), rcs(per.size(), 0);
