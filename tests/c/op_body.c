@@ -51,6 +51,17 @@ typedef struct {
 } Tensor;
 
 static int g_rank, g_size, g_ntensors;
+/* OP_BODY_NONBLOCKING=1: the threads' streams are created non-blocking and the synchronous caller
+ * copies with hipMemcpyAsync + hipStreamSynchronize on its own stream (no legacy null stream) */
+static int g_nonblocking;
+static hipError_t make_stream(hipStream_t* s) {
+  return g_nonblocking ? hipStreamCreateWithFlags(s, hipStreamNonBlocking) : hipStreamCreate(s);
+}
+static hipError_t copy_sync(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s) {
+  if (!g_nonblocking) return hipMemcpy(dst, src, n, k);
+  hipError_t e = hipMemcpyAsync(dst, src, n, k, s);
+  return e != hipSuccess ? e : hipStreamSynchronize(s);
+}
 static Tensor* g_t;
 static atomic_int g_callbacks;
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
@@ -96,7 +107,7 @@ typedef struct {
 static void* executor(void* arg) {
   const Job* job = (const Job*)arg;
   hipStream_t s;
-  if (hipStreamCreate(&s) != hipSuccess) {
+  if (make_stream(&s) != hipSuccess) {
     note("%sthread %d: hipStreamCreate failed; ", "", job->thread);
     return NULL;
   }
@@ -140,7 +151,7 @@ static void* sync_caller(void* arg) {
   float* h = (float*)malloc(sizeof(float) * SYNC_N);
   float* exp = (float*)malloc(sizeof(float) * SYNC_N);
   float** all = (float**)malloc(sizeof(float*) * g_size);
-  if (hipStreamCreate(&s) != hipSuccess || hipMalloc((void**)&d, sizeof(float) * SYNC_N) != hipSuccess ||
+  if (make_stream(&s) != hipSuccess || hipMalloc((void**)&d, sizeof(float) * SYNC_N) != hipSuccess ||
       hipMalloc((void**)&o, sizeof(float) * SYNC_N) != hipSuccess) {
     atomic_store(&g_sync_bad, 1);
     return NULL;
@@ -149,9 +160,9 @@ static void* sync_caller(void* arg) {
   for (int c = 0; c < SYNC_CALLS; c++) {
     for (int r = 0; r < g_size; r++)
       for (int64_t j = 0; j < SYNC_N; j++) all[r][j] = f32_of(r, 100000 + c, j);
-    if (hipMemcpy(d, all[g_rank], sizeof(float) * SYNC_N, hipMemcpyHostToDevice) != hipSuccess ||
+    if (copy_sync(d, all[g_rank], sizeof(float) * SYNC_N, hipMemcpyHostToDevice, s) != hipSuccess ||
         tips_allreduce(d, o, SYNC_N, TIPS_FLOAT32, TIPS_OP_SUM, s) != TIPS_OK || hipStreamSynchronize(s) != hipSuccess ||
-        hipMemcpy(h, o, sizeof(float) * SYNC_N, hipMemcpyDeviceToHost) != hipSuccess) {
+        copy_sync(h, o, sizeof(float) * SYNC_N, hipMemcpyDeviceToHost, s) != hipSuccess) {
       note("sync call: %s (%d); ", tips_last_error(), c);
       atomic_store(&g_sync_bad, 1);
       break;
@@ -238,6 +249,7 @@ static void* watchdog(void* arg) {
 
 int main(void) {
   const char* nt = getenv("OP_BODY_TENSORS");
+  g_nonblocking = getenv("OP_BODY_NONBLOCKING") && atoi(getenv("OP_BODY_NONBLOCKING")) != 0;
   g_ntensors = nt ? atoi(nt) : 96;
   tips_init();
   if (!tips_is_initialize()) {
