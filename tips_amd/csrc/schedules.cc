@@ -36,11 +36,21 @@ int launch_psum(const PSum& s, char* const* base, int dtype, hipStream_t stream)
 
 // Eager plan work (and RCCL calls on the comm stream) after every replayed plan still in flight:
 // a replay reads and writes the same staging and issues RCCL work on the same communicator.
+// An eager RCCL call after a replay: on the device it waits for the replay (the comm stream joins
+// the graph stream); on the HOST it also waits until the replay has run (TIPS_REPLAY_HOST_ORDER,
+// default on). A replayed graph hands its transfers to RCCL's proxy thread only when the graph
+// starts on the device, an eager call hands them over when it is issued; issued while the replay
+// still waited in the queue, the eager call's transfers reached the proxy first, the proxy worked
+// on them, the device ran the replay first and waited for the replay's - on every rank. Seen as a
+// hang of the op-body test over 3 socket-transport RCCL ranks (1 run in 5, every rank in its
+// next eager call's hipStreamSynchronize, profiles/r03/k_op_body_hang.txt); gone with this wait.
 int order_after_replays(State& st) {
   if (!st.graph_pending) return 0;
   TRY(join(st.comm_stream, st.graph_stream, st.ev_graph[4]));
   HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_graph[4], 0));
   st.graph_pending = false;
+  static const bool host_order = env_i64("TIPS_REPLAY_HOST_ORDER", 1) != 0;
+  if (host_order) HIP_TRY(hipEventSynchronize(st.ev_graph[4]));
   return 0;
 }
 
