@@ -42,8 +42,9 @@ int launch_psum(const PSum& s, char* const* base, int dtype, hipStream_t stream)
 // starts on the device, an eager call hands them over when it is issued; issued while the replay
 // still waited in the queue, the eager call's transfers reached the proxy first, the proxy worked
 // on them, the device ran the replay first and waited for the replay's - on every rank. Seen as a
-// hang of the op-body test over 3 socket-transport RCCL ranks (1 run in 5, every rank in its
-// next eager call's hipStreamSynchronize, profiles/r03/k_op_body_hang.txt); gone with this wait.
+// hang of the op-body test over 3 socket-transport RCCL ranks: without this wait 3 of 10 runs hung,
+// every rank in an eager call's hipStreamSynchronize; with it 12 of 12 ran clean, as with replays
+// off (profiles/r03/k_op_body_hang.txt, k_hunt_summary.txt).
 int order_after_replays(State& st) {
   if (!st.graph_pending) return 0;
   TRY(join(st.comm_stream, st.graph_stream, st.ev_graph[4]));
