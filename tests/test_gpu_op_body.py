@@ -64,7 +64,8 @@ def _run_op_body(p, tensors, binary, extra_env=None):
                 pr.kill()
     bad = []  # every rank's story when any rank fails (a hang shows on all of them)
     for r, (rc, out, err) in enumerate(outs):
-        assert "ThreadSanitizer" not in err, err[-6000:]
+        k = err.find("WARNING: ThreadSanitizer")
+        assert k < 0, "rank %d: %s" % (r, err[k:k + 12000])
         line = [l for l in out.splitlines() if l.startswith("{")]
         res = json.loads(line[-1]) if line else None
         if rc != 0 or not res or not res["ok"]:

@@ -312,8 +312,17 @@ __attribute__((target("avx2"))) void copy_stream_avx2(char* d, const char* s, si
   _mm_sfence();  // (streaming stores are weakly ordered: visible before the job reports done)
 }
 
+// (the pool's threads reach this concurrently on their first job: the setting is an atomic, set by
+// whichever thread comes first - the same value every time - not a function-local static, whose
+// first use ThreadSanitizer reported as a race on the GPU box, profiles/r03/l_tsan_report.txt)
+std::atomic<int> g_stream_stores{-1};
+
 void copy_stream(char* d, const char* s, size_t n) {
-  static const bool ok = __builtin_cpu_supports("avx2") && env_i64("TIPS_HOST_STREAM_STORES", 1) != 0;
+  int ok = g_stream_stores.load(std::memory_order_relaxed);
+  if (ok < 0) {
+    ok = __builtin_cpu_supports("avx2") && env_i64("TIPS_HOST_STREAM_STORES", 1) != 0;
+    g_stream_stores.store(ok, std::memory_order_relaxed);
+  }
   if (ok && n >= 4096) copy_stream_avx2(d, s, n);
   else memcpy(d, s, n);
 }

@@ -50,8 +50,7 @@ int order_after_replays(State& st) {
   TRY(join(st.comm_stream, st.graph_stream, st.ev_graph[4]));
   HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_graph[4], 0));
   st.graph_pending = false;
-  static const bool host_order = env_i64("TIPS_REPLAY_HOST_ORDER", 1) != 0;
-  if (host_order) HIP_TRY(hipEventSynchronize(st.ev_graph[4]));
+  if (env_i64("TIPS_REPLAY_HOST_ORDER", 1) != 0) HIP_TRY(hipEventSynchronize(st.ev_graph[4]));
   return 0;
 }
 
@@ -230,13 +229,15 @@ void destroy_exec(State& st, hipGraphExec_t e) {
 // 8 MiB, 4-30 % under the eager one (profiles/r03/small_bucket_rehearsal_n2_before.json; round 2 stopped
 // at 1 MiB). TIPS_GRAPHS=0 turns them off; 2 forces them on any runtime (probing only).
 bool graphs_supported() {
-  static int ok = -1;
-  if (ok < 0) {
+  static std::atomic<int> ok{-1};  // (set once, by whichever thread asks first)
+  int v = ok.load(std::memory_order_relaxed);
+  if (v < 0) {
     int rv = 0, hv = 0;
-    ok = ncclGetVersion(&rv) == ncclSuccess && hipRuntimeGetVersion(&hv) == hipSuccess && rv >= 22600 && hv >= 70000000;
+    v = ncclGetVersion(&rv) == ncclSuccess && hipRuntimeGetVersion(&hv) == hipSuccess && rv >= 22600 && hv >= 70000000;
     (void)hipGetLastError();
+    ok.store(v, std::memory_order_relaxed);
   }
-  return ok == 1;
+  return v == 1;
 }
 
 bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
