@@ -327,3 +327,30 @@ def test_fast_list_helper_reads_pointers_counts_and_shapes():
     keep = [x, x]
     assert _fast.max_refcount([x]) == sys.getrefcount(x) - 1 and len(keep) == 2
     assert _fast.max_refcount([]) == 0
+
+
+def test_flat_output_sets_are_not_handed_out_twice():
+    """_FlatOutputs.take (allreduce_grads' output sets) returns the views in a new list, made before
+    the library call releases the GIL: while one call's outputs are referenced, a second take()
+    gets another set; once they are dropped, the first set comes back. (CPU tensors stand in for
+    device ones; tips_fused_layout is host-only.)"""
+    import gc
+    import torch
+    from tips_amd import _lib
+    from tips_amd.ops import _FlatOutputs
+    shapes = (torch.Size([3, 5]), torch.Size([7]), torch.Size([2, 2, 2]))
+    fo = _FlatOutputs(shapes, [15, 7, 8], _lib.FLOAT32, torch.float32, torch.device("cpu"))
+    f1, v1 = fo.take()
+    assert [v.shape for v in v1] == list(shapes)
+    f2, v2 = fo.take()
+    assert f2.data_ptr() != f1.data_ptr()  # set 1's views are still held
+    p1 = f1.data_ptr()
+    del v1, f1
+    gc.collect()
+    f3, v3 = fo.take()
+    assert f3.data_ptr() == p1 and v3[0].data_ptr() == p1
+    held = v3[1]
+    del v3, f3
+    f4, v4 = fo.take()
+    assert f4.data_ptr() != p1  # one view of set 1 is still held by the caller
+    del held

@@ -8,6 +8,7 @@ returns when the result is in host memory, like the reference's CPU op.
 """
 import os
 import re
+import threading
 
 from . import _fast  # (built in-tree by `make`: tips_amd/_fast*.so; no Python fallback)
 from . import _lib
@@ -210,18 +211,20 @@ class _FlatOutputs(object):
         return _fast.max_refcount(views) <= rc0
 
     def take(self):
-        """(flat buffer, views) for this call: a released set, or a new one."""
+        """(flat buffer, a new list of its views) for this call: a released set, or a new one. The
+        list is made here, before the library call releases the GIL, so another thread's take()
+        already sees the set's views referenced and does not hand it out twice."""
         import torch
         for s in self.sets:
             if self._free(s):
-                return s[0], s[1]
+                return s[0], list(s[1])
         flat = torch.empty(max(1, self.total // self.es), dtype=self.dtype, device=self.device)
         views = [flat[o:o + n].view(shp) for o, n, shp in zip(self.offs, self.numels, self.shapes)]
         if len(self.sets) < self.MAX_SETS:
             use0 = torch._C._storage_Use_Count(flat.untyped_storage()._cdata)
             rc0 = _fast.max_refcount(views)
             self.sets.append((flat, views, use0, rc0))
-        return flat, views
+        return flat, list(views)
 
 
 _FLAT_OUTPUTS = {}  # (dtype, device, shapes) -> _FlatOutputs (small LRU)
@@ -268,7 +271,7 @@ def _flat_run(fo, tensor_list, ptrs):
     t0 = tensor_list[0]
     _lib.call("tips_fused_allreduce_flat", pp[0], fo.cp[0], len(ptrs), fo.code, flat.data_ptr(),
               _torch_mod().cuda.current_stream(t0.device).cuda_stream)
-    return list(views)
+    return views
 
 
 def _torch_mod():
@@ -278,7 +281,8 @@ def _torch_mod():
 
 # c10::ScalarType -> tips dtype code (Float, Double, Int, Long, Half, BFloat16)
 _ST_CODES = {6: _lib.FLOAT32, 7: _lib.FLOAT64, 3: _lib.INT32, 4: _lib.INT64, 5: _lib.FLOAT16, 15: _lib.BFLOAT16}
-_LIST_BUFS = {}   # n -> (pointer array, count array, their addresses): reused call to call
+_LIST_BUFS = threading.local()  # .d: n -> (pointer array, count array, their addresses), per thread:
+                                # the library call releases the GIL while it reads them
 _FAST_FLAT = {}   # (scalar type, device, n, shape hash) -> (_FlatOutputs, count bytes)
 _CUR_STREAM = None
 
@@ -291,13 +295,16 @@ def _dev_list_flat(tensor_list):
     step; this costs tens of nanoseconds per tensor where reading them through Python cost ~0.2 us."""
     global _CUR_STREAM
     n = len(tensor_list)
-    bufs = _LIST_BUFS.get(n)
+    mine = getattr(_LIST_BUFS, "d", None)
+    if mine is None:
+        mine = _LIST_BUFS.d = {}
+    bufs = mine.get(n)
     if bufs is None:
         import ctypes
         pa, na = (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
-        if len(_LIST_BUFS) >= 16:
-            _LIST_BUFS.pop(next(iter(_LIST_BUFS)))
-        bufs = _LIST_BUFS[n] = (pa, na, ctypes.addressof(pa), ctypes.addressof(na))
+        if len(mine) >= 16:
+            mine.pop(next(iter(mine)))
+        bufs = mine[n] = (pa, na, ctypes.addressof(pa), ctypes.addressof(na))
     r = _fast.dev_list(tensor_list, bufs[2], bufs[3])
     if r is None or r[0] not in _ST_CODES:
         return None
@@ -317,7 +324,7 @@ def _dev_list_flat(tensor_list):
         _CUR_STREAM = torch.cuda.current_stream
     _lib.call("tips_fused_allreduce_flat", bufs[0], fo.cp[0], n, fo.code, flat.data_ptr(),
               _CUR_STREAM(tensor_list[0].device).cuda_stream)
-    return list(views)
+    return views
 
 
 def _flat_call(tensor_list, code, ptrs):
@@ -382,9 +389,11 @@ class _HostFlatOutputs(object):
         return n, max(map(sys.getrefcount, s[1]), default=0)
 
     def take(self):
+        """(flat buffer, a new list of its views): made before the library call releases the GIL,
+        as _FlatOutputs.take."""
         for s in self.sets:
             if self._refs(s) == s[2]:
-                return s[0], s[1]
+                return s[0], list(s[1])
         if self.is_torch:
             import torch
             flat = torch.empty(self.total, dtype=torch.uint8)
@@ -403,7 +412,7 @@ class _HostFlatOutputs(object):
             del flat, views  # (the baseline counts the set's own references only)
             st[2] = self._refs(st)
             self.sets.append(st)
-            return st[0], st[1]
+            return st[0], list(st[1])
         return flat, views
 
 
@@ -463,7 +472,7 @@ def _host_flat_run(fo, ptrs):
         fo.last = (ptrs, pp)
     flat, views = fo.take()
     _lib.call("tips_fused_allreduce_host_flat", pp[0], fo.cp[0], len(ptrs), fo.code, tensors.data_ptr(flat))
-    return list(views)
+    return views
 
 
 def fusion_stats():
