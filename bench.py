@@ -625,8 +625,10 @@ def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BU
     the path the library ships (AUTO with its default one-shot threshold and graph-replay limit)
     and for each candidate beside it: direct eager, direct replayed as a HIP graph at any size,
     one-shot eager and one-shot replayed. The wall time of `calls` back-to-back calls on the same
-    buffers, slowest rank; `best` names the fastest candidate and `shipped_vs_best` the ratio."""
-    out = {"calls": calls, "unit": "us per call, slowest rank"}
+    buffers (a quarter of them above 1 MiB), slowest rank; `best` names the fastest candidate and
+    `shipped_vs_best` the ratio. Sizes left when the probe has run TIPS_BENCH_PROBE_BUDGET_S (90 s)
+    are skipped, on every rank together."""
+    out = {"calls": calls, "calls_above_1MiB": max(5, calls // 4), "unit": "us per call, slowest rank"}
     keys = ("TIPS_GRAPHS", "TIPS_GRAPH_MAX_BYTES")
     saved = {k: os.environ.get(k) for k in keys}
     modes = [("shipped", _lib.ALGO_AUTO, {}),
@@ -643,8 +645,16 @@ def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BU
         os.environ.update(env)
         _lib.call("tips_set_algorithm", algo)
 
+    budget = float(os.environ.get("TIPS_BENCH_PROBE_BUDGET_S", "90"))
+    t_start = time.perf_counter()
     try:
         for kib in kibs:
+            # a time budget, decided together (the probe's calls are collectives): over sockets at
+            # N = 8 the 2-8 MiB sizes take minutes (profiles/r03/m_rehearsal_n8.jsonl), over xGMI seconds
+            if max_over_ranks(dist, time.perf_counter() - t_start) > budget:
+                out["%d_KiB" % kib] = "skipped: the probe's %.0f s budget was spent (TIPS_BENCH_PROBE_BUDGET_S)" % budget
+                continue
+            reps = calls if kib <= 1024 else max(5, calls // 4)
             n = kib * 256
             x = torch.full((n,), float(rank + 1), device="cuda")
             y = torch.empty_like(x)
@@ -663,10 +673,10 @@ def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BU
                     ok = ok and bool(torch.all(y == world * (world + 1) / 2).item())
                     dist.barrier()
                     t0 = time.perf_counter()
-                    for _ in range(calls):
+                    for _ in range(reps):
                         L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, _lib.FLOAT32, _lib.OP_SUM, sp)
                     torch.cuda.synchronize()
-                    us = round(max_over_ranks(dist, time.perf_counter() - t0) / calls * 1e6, 1)
+                    us = round(max_over_ranks(dist, time.perf_counter() - t0) / reps * 1e6, 1)
                     row[mode] = min(us, row.get(mode, us))
             cands = {k: v for k, v in row.items() if k != "shipped"}
             best = min(cands, key=cands.get)
