@@ -246,6 +246,32 @@ Layout* find_layout(State& st, FusionCache& fc, const int64_t* counts, int n, in
 
 // The resolved segment table(s) of this call's pointers: a cached one when this layout saw the
 // same pointers (and mode and base) recently, else built on the host and uploaded.
+// The order a launch's workgroups take a group's tiles in (a group: one bucket, or the region of
+// tensors reduced where they lie; launches cover whole groups). TIPS_COPY_ORDER=1: the tiles that
+// meet a tensor boundary (two or more segments, or a segment that does not cover the tile) first,
+// then the tiles inside one tensor - the slow tiles start while the queue is full instead of
+// trailing at the end of the launch; 0: tile order.
+std::vector<int> tile_order(const Layout& L) {
+  std::vector<int> order(L.ntiles);
+  for (int j = 0; j < L.ntiles; j++) order[j] = j;
+  if (env_i64("TIPS_COPY_ORDER", 1) == 0) return order;
+  const int64_t es = tips::dtype_size(L.dtype);
+  auto covered = [&](int j) {
+    if (L.tiles[2 * j + 1] != 1) return false;
+    const int i = L.seg_tensor[L.tiles[2 * j]];
+    return L.off[i] <= (int64_t)j * L.tile && L.off[i] + L.counts[i] * es >= (int64_t)(j + 1) * L.tile;
+  };
+  std::vector<int> bounds;
+  for (const Bucket& b : L.buckets) bounds.push_back(b.tile0);
+  bounds.push_back(L.buckets.empty() ? 0 : L.buckets.back().tile0 + L.buckets.back().ntiles);
+  bounds.push_back(L.ntiles);
+  for (size_t g = 0; g + 1 < bounds.size(); g++) {
+    const int g0 = bounds[g], g1 = std::min(bounds[g + 1], L.ntiles);
+    std::stable_partition(order.begin() + g0, order.begin() + std::max(g0, g1), [&](int j) { return !covered(j); });
+  }
+  return order;
+}
+
 Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchItem* items, int n,
                   const void* base) {
   uint64_t h = fnv(fnv(1469598103934665603ull, (uint64_t)mode), (uint64_t)(uintptr_t)base);
@@ -312,14 +338,19 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
     }
   }
   // tile records (two per tile): the segment itself when the tile meets one, both when it meets
-  // two (a tensor's end and the next one's start), else where its segments start
+  // two (a tensor's end and the next one's start), else where its segments start. Record slot q
+  // holds tile order[q]; the tile's byte offset travels in the second record (its begin when that
+  // record is unused; when it is the second segment, that segment begins in the tile, so the
+  // kernel rounds its begin down to the tile).
+  const std::vector<int> order = tile_order(L);
   for (int tb = 0; tb < ntab; tb++) {
     CopySeg* T = rec.data() + tb * per;
     const CopySeg* S = T + 2 * L.ntiles;
-    for (int j = 0; j < L.ntiles; j++) {
+    for (int q = 0; q < L.ntiles; q++) {
+      const int j = order[q];
       const int first = L.tiles[2 * j], cnt = L.tiles[2 * j + 1];
-      T[2 * j] = cnt <= 2 ? S[first] : CopySeg{first, cnt, 0, -1};
-      T[2 * j + 1] = cnt == 2 ? S[first + 1] : CopySeg{0, 0, 0, 0};
+      T[2 * q] = cnt <= 2 ? S[first] : CopySeg{first, cnt, 0, -1};
+      T[2 * q + 1] = cnt == 2 ? S[first + 1] : CopySeg{0, 0, (int64_t)j * L.tile, 0};
     }
   }
   t->stamp = ++fc.clock;

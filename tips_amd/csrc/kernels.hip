@@ -614,9 +614,10 @@ __device__ __forceinline__ void small_store(int64_t s, int64_t d, int len, const
   }
 }
 
-// tiles[2t], tiles[2t + 1]: the tile's segment and {0, 0, 0, 0}; or its two segments (the tensor
-// ending in it, the tensor starting in it); or {first segment, count, -, -1} and - when it meets
-// more than two (then staged from segs[] in LDS).
+// tiles[2t], tiles[2t + 1] (record slot t of the launch; fusion.cc puts a group's boundary tiles
+// first): the tile's segment and {0, 0, tile byte, 0}; or its two segments (the tensor ending in
+// it, the tensor starting in it); or {first segment, count, -, -1} and {0, 0, tile byte, 0} when
+// it meets more than two (then staged from segs[] in LDS).
 template <int U, int POL>
 __global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __restrict__ tiles,
                                                           const CopySeg* __restrict__ segs, int tile0, int ntiles) {
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __rest
   __shared__ CopySeg L[kMaxSeg];
   const int64_t tt = xcd_tile(blockIdx.x, gridDim.x);
   if (tt >= ntiles) return;  // (whole workgroup: before any barrier)
-  const int t = tile0 + (int)tt;
+  const int t = tile0 + (int)tt;  // the record slot (fusion.cc may order a group's tiles: slow ones first)
   // One (scalar) load of both records before the first data load. (A tile -> segment index
   // followed by the segment's record puts two dependent loads there: 17.5 against 14.1 us per
   // config-4 bucket, measured.)
@@ -635,7 +636,9 @@ __global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __rest
   const int64_t b_src = tr[4], b_dst = tr[5], b_beg = tr[6], b_end = tr[7];
   const int tid = threadIdx.x;
   const bool multi = a_end < 0, two = b_end > 0;
-  const int64_t tb = (int64_t)t * kTileBytes;
+  // the tile's first byte: the second record's begin, rounded down to the tile when that record is
+  // the segment starting inside the tile
+  const int64_t tb = two ? (b_beg & ~(kTileBytes - 1)) : b_beg;
   if (!multi && !two && a_beg <= tb && a_end >= tb + kTileBytes && ((a_src | a_dst) & 15) == 0) {
     // the tile lies inside one 16-B aligned tensor (most tiles): both sides are wave-uniform
     // contiguous ranges, moved as the round-2 kernel moved a whole tile - buffer loads nt, buffer
