@@ -209,6 +209,14 @@ TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int 
  * allreduce loop returns (tips/tensorflow/__init__.py:203-222), fused. */
 TIPS_API int tips_fused_allreduce_oop(const void* const* ins, void* const* outs, const int64_t* counts, int n,
                                       int dtype, void* stream);
+/* Test / diagnostics (no reference counterpart): the segment-copy records fusion.cc builds for
+ * one pointer set of a list - the layout of (counts, dtype) and the in -> out addresses given as
+ * integers - exactly as the device table of an out-of-place copy call holds them: 4 x int64 per
+ * record {src, dst, begin, end}, 2 per tile (in the launch's order) then one per segment. Host only,
+ * nothing is uploaded: tests/test_fusion_table.py runs copy_segs_kernel's per-lane rules over them
+ * on the CPU. Returns the record count (records may be NULL to ask) or < 0; *ntiles, *tile_bytes. */
+TIPS_API int64_t tips_fusion_tile_table(const int64_t* counts, int n, int dtype, const int64_t* ins, const int64_t* outs,
+                                       int64_t* records, int64_t cap, int64_t* ntiles, int64_t* tile_bytes);
 /* The byte offset of each tensor of a fused list in ONE flat buffer laid out as the fusion buckets
  * (offsets[i], 256-B aligned; may be NULL); returns the flat buffer's size in bytes (< 0 = error).
  * A pure host function of counts, dtype and TIPS_FUSION_THRESHOLD - the same on every rank. */

@@ -110,6 +110,8 @@ _SIGNATURES = [
     ("tips_on_done", ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     ("tips_net_stats", ctypes.c_int, [_c_i64_p, _c_i64_p]),
     ("tips_debug_state", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
+    ("tips_fusion_tile_table", ctypes.c_int64,
+     [_c_i64_p, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p, _c_i64_p, ctypes.c_int64, _c_i64_p, _c_i64_p]),
     ("tips_wait", ctypes.c_int, [ctypes.c_int64]),
     ("tips_enqueue_broadcast", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,

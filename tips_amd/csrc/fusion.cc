@@ -272,6 +272,51 @@ std::vector<int> tile_order(const Layout& L) {
   return order;
 }
 
+// One table's records for a pointer set: [2 per tile | one per segment] (twice for kSlot: pack,
+// then unpack). Host only: find_table uploads them; tips_fusion_tile_table returns them to the CPU
+// tests' interpreter of copy_segs_kernel.
+void fill_records(const Layout& L, int mode, const BatchItem* items, const void* base, std::vector<CopySeg>* dst) {
+  const int nseg = (int)L.seg_tensor.size();
+  const int ntab = mode == kSlot ? 2 : 1;
+  const size_t per = 2 * (size_t)L.ntiles + nseg;
+  const int64_t es = tips::dtype_size(L.dtype);
+  std::vector<CopySeg>& rec = *dst;
+  rec.assign(ntab * per, CopySeg{0, 0, 0, 0});
+  for (int k = 0; k < nseg; k++) {
+    const int i = L.seg_tensor[k];
+    const int64_t b = L.off[i], e = b + L.counts[i] * es;
+    const int64_t in = (int64_t)(uintptr_t)items[i].in - b, out = (int64_t)(uintptr_t)items[i].out - b;
+    CopySeg* r = rec.data() + 2 * L.ntiles + k;
+    if (mode == kSlot) {
+      const int bk = L.bucket[i];
+      // bucket bk lives in slot bk % 2: virtual byte v of it at slot + (v - bucket offset)
+      const int64_t slot = bk < 0 ? 0 : (int64_t)(uintptr_t)base + (int64_t)(bk % 2) * L.threshold - L.buckets[bk].off;
+      r[0] = CopySeg{in, slot, b, e};    // pack
+      r[per] = CopySeg{slot, out, b, e};  // unpack
+    } else if (mode == kCopy) {
+      r[0] = CopySeg{in, out, b, e};
+    } else {  // kFlat: straight into the flat output
+      r[0] = CopySeg{in, (int64_t)(uintptr_t)base, b, e};
+    }
+  }
+  // tile records (two per tile): the segment itself when the tile meets one, both when it meets
+  // two (a tensor's end and the next one's start), else where its segments start. Record slot q
+  // holds tile order[q]; the tile's byte offset travels in the second record (its begin when that
+  // record is unused; when it is the second segment, that segment begins in the tile, so the
+  // kernel rounds its begin down to the tile).
+  const std::vector<int> order = tile_order(L);
+  for (int tb = 0; tb < ntab; tb++) {
+    CopySeg* T = rec.data() + tb * per;
+    const CopySeg* S = T + 2 * L.ntiles;
+    for (int q = 0; q < L.ntiles; q++) {
+      const int j = order[q];
+      const int first = L.tiles[2 * j], cnt = L.tiles[2 * j + 1];
+      T[2 * q] = cnt <= 2 ? S[first] : CopySeg{first, cnt, 0, -1};
+      T[2 * q + 1] = cnt == 2 ? S[first + 1] : CopySeg{0, 0, (int64_t)j * L.tile, 0};
+    }
+  }
+}
+
 Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchItem* items, int n,
                   const void* base) {
   uint64_t h = fnv(fnv(1469598103934665603ull, (uint64_t)mode), (uint64_t)(uintptr_t)base);
@@ -318,41 +363,8 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
     t->ins[i] = items[i].in;
     t->outs[i] = items[i].out;
   }
-  const int64_t es = tips::dtype_size(L.dtype);
-  std::vector<CopySeg> rec(ntab * per);
-  for (int k = 0; k < nseg; k++) {
-    const int i = L.seg_tensor[k];
-    const int64_t b = L.off[i], e = b + L.counts[i] * es;
-    const int64_t in = (int64_t)(uintptr_t)items[i].in - b, out = (int64_t)(uintptr_t)items[i].out - b;
-    CopySeg* r = rec.data() + 2 * L.ntiles + k;
-    if (mode == kSlot) {
-      const int bk = L.bucket[i];
-      // bucket bk lives in slot bk % 2: virtual byte v of it at slot + (v - bucket offset)
-      const int64_t slot = bk < 0 ? 0 : (int64_t)(uintptr_t)base + (int64_t)(bk % 2) * L.threshold - L.buckets[bk].off;
-      r[0] = CopySeg{in, slot, b, e};    // pack
-      r[per] = CopySeg{slot, out, b, e};  // unpack
-    } else if (mode == kCopy) {
-      r[0] = CopySeg{in, out, b, e};
-    } else {  // kFlat: straight into the flat output
-      r[0] = CopySeg{in, (int64_t)(uintptr_t)base, b, e};
-    }
-  }
-  // tile records (two per tile): the segment itself when the tile meets one, both when it meets
-  // two (a tensor's end and the next one's start), else where its segments start. Record slot q
-  // holds tile order[q]; the tile's byte offset travels in the second record (its begin when that
-  // record is unused; when it is the second segment, that segment begins in the tile, so the
-  // kernel rounds its begin down to the tile).
-  const std::vector<int> order = tile_order(L);
-  for (int tb = 0; tb < ntab; tb++) {
-    CopySeg* T = rec.data() + tb * per;
-    const CopySeg* S = T + 2 * L.ntiles;
-    for (int q = 0; q < L.ntiles; q++) {
-      const int j = order[q];
-      const int first = L.tiles[2 * j], cnt = L.tiles[2 * j + 1];
-      T[2 * q] = cnt <= 2 ? S[first] : CopySeg{first, cnt, 0, -1};
-      T[2 * q + 1] = cnt == 2 ? S[first + 1] : CopySeg{0, 0, (int64_t)j * L.tile, 0};
-    }
-  }
+  std::vector<CopySeg> rec;
+  fill_records(L, mode, items, base, &rec);
   t->stamp = ++fc.clock;
   fc.tables_built++;
   if (upload(st, fc, t->dev, rec.data(), rec.size() * sizeof(CopySeg)) != 0) {
@@ -601,6 +613,31 @@ int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dt
 int tips_fused_allreduce_oop(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype,
                              void* stream) {
   return fused_entry(ins, outs, counts, n, dtype, stream);
+}
+
+int64_t tips_fusion_tile_table(const int64_t* counts, int n, int dtype, const int64_t* ins, const int64_t* outs,
+                               int64_t* records, int64_t cap, int64_t* ntiles, int64_t* tile_bytes) {
+  TRY(check_dtype(dtype));
+  if (n < 0 || (n > 0 && (!counts || !ins || !outs))) return fail(TIPS_ERR_INVALID_ARG, "bad list");
+  for (int i = 0; i < n; i++)
+    if (counts[i] < 0) return fail(TIPS_ERR_INVALID_ARG, "negative count %d", i);
+  Layout L;
+  L.dtype = dtype;
+  L.threshold = fusion_threshold_bytes();
+  L.tile = copy_tile_bytes();
+  L.balance = env_i64("TIPS_FUSION_BALANCE", 1) != 0;
+  build_layout(&L, counts, n);
+  std::vector<BatchItem> items((size_t)n);
+  for (int i = 0; i < n; i++) items[i] = BatchItem{(const void*)(uintptr_t)ins[i], (void*)(uintptr_t)outs[i], counts[i]};
+  std::vector<tips::CopySeg> rec;
+  fill_records(L, kCopy, items.data(), nullptr, &rec);
+  if (ntiles) *ntiles = L.ntiles;
+  if (tile_bytes) *tile_bytes = L.tile;
+  if (records) {
+    if (cap < (int64_t)rec.size()) return fail(TIPS_ERR_INVALID_ARG, "tips_fusion_tile_table: %zu records, room for %lld", rec.size(), (long long)cap);
+    memcpy(records, rec.data(), rec.size() * sizeof(tips::CopySeg));
+  }
+  return (int64_t)rec.size();
 }
 
 int64_t tips_fused_layout(const int64_t* counts, int n, int dtype, int64_t* offsets) {
