@@ -354,3 +354,42 @@ def test_flat_output_sets_are_not_handed_out_twice():
     f4, v4 = fo.take()
     assert f4.data_ptr() != p1  # one view of set 1 is still held by the caller
     del held
+
+
+def test_host_output_pool_reuses_only_released_outputs(monkeypatch):
+    """allreduce_op's host outputs of >= 1 MiB come from _HostOutPool: a released output is handed
+    out again (page-locked once, no fresh pages per call); one still referenced - directly, through
+    a numpy view, or through torch's .numpy() on its storage - is not; small outputs are fresh.
+    (tips_host_register is stubbed: no GPU here.)"""
+    import numpy as np
+    import torch
+    import tips_amd.ops as ops
+
+    class Stub:
+        def tips_host_register(self, p, n):
+            return 0
+    monkeypatch.setattr(ops._lib, "lib", lambda: Stub())
+    pool = ops._HostOutPool()
+    src = np.zeros(1 << 19, dtype=np.float32)  # 2 MiB
+    a = pool.take(src)
+    b = pool.take(src)
+    assert a is not b and a.shape == src.shape and a.dtype == src.dtype
+    pa = a.ctypes.data
+    del a
+    c = pool.take(src)
+    assert c.ctypes.data == pa
+    view = c[::2]
+    del c
+    assert pool.take(src).ctypes.data != pa and view.size == 1 << 18
+    small = np.zeros(100, dtype=np.float32)
+    pool.take(small)
+    assert (False, "float32", (100,)) not in pool.sets  # (under 1 MiB: a fresh output, not pooled)
+    t = torch.zeros(1 << 19)
+    x = pool.take(t)
+    px = x.data_ptr()
+    del x
+    y = pool.take(t)
+    assert y.data_ptr() == px
+    arr = y.numpy()
+    del y
+    assert pool.take(t).data_ptr() != px and arr.size == 1 << 19

@@ -54,7 +54,7 @@ def allreduce_op(tensor, name=None):
     basics.init()
     code = tensors.dtype_code(tensor)
     src = tensors.contiguous(tensor)
-    out = tensors.empty_like(src)
+    out = _HOST_OUT.take(src) if not tensors.is_device(src) else tensors.empty_like(src)
     n = tensors.numel(src)
     if _check:
         shape = _shape(src) or (1,)  # scalars travel as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
@@ -65,6 +65,61 @@ def allreduce_op(tensor, name=None):
         _lib.call("tips_allreduce", tensors.data_ptr(src), tensors.data_ptr(out), n, code, _lib.OP_SUM,
                   tensors.stream_of(src))
     return out
+
+
+class _HostOutPool(object):
+    """Outputs of host allreduces of at least 1 MiB (the reference's op works on CPU tensors,
+    ops.cc:118): kept page-locked (tips_host_register) and handed out again once the caller has
+    released them - no Python reference left and, for torch, no other tensor on the storage (numpy
+    views hold a reference to their base). A fresh numpy / torch array of that size is new pages every
+    call, and the D2H into it pays their first-touch faults: one 97.6 MiB numpy buffer took 16.7 ms
+    per allreduce that way (profiles/r03/p_numa_probe.jsonl). Up to PER_KEY outputs per (kind, dtype,
+    shape), TIPS_HOST_OUT_POOL_MIB (4096) page-locked in all; past that, fresh outputs as before."""
+
+    MIN_BYTES = 1 << 20
+    PER_KEY = 2
+
+    def __init__(self):
+        self.sets = {}
+        self.bytes = 0
+        self.lock = threading.Lock()
+
+    @staticmethod
+    def _free(e):
+        import sys
+        a = e[0]
+        if sys.getrefcount(a) > 3:  # (the entry, the local a, getrefcount's argument)
+            return False
+        if e[1] is not None:  # torch: no other tensor on the storage
+            import torch
+            return torch._C._storage_Use_Count(a.untyped_storage()._cdata) == e[1]
+        return True
+
+    def take(self, src):
+        is_t = tensors.is_torch(src)
+        nbytes = src.numel() * src.element_size() if is_t else src.nbytes
+        if nbytes < self.MIN_BYTES:
+            return tensors.empty_like(src)
+        key = (is_t, str(src.dtype), tuple(src.shape))
+        with self.lock:  # (the check and the hand-out together: another thread cannot get it too)
+            lst = self.sets.setdefault(key, [])
+            for e in lst:
+                if self._free(e):
+                    return e[0]
+            out = tensors.empty_like(src)
+            cap = int(os.environ.get("TIPS_HOST_OUT_POOL_MIB", "4096")) << 20
+            if len(lst) < self.PER_KEY and self.bytes + nbytes <= cap:
+                if _lib.lib().tips_host_register(tensors.data_ptr(out), nbytes) == 0:
+                    use0 = None
+                    if is_t:
+                        import torch
+                        use0 = torch._C._storage_Use_Count(out.untyped_storage()._cdata)
+                    lst.append((out, use0))
+                    self.bytes += nbytes
+            return out
+
+
+_HOST_OUT = _HostOutPool()
 
 
 def allgather_op(tensor, name=None):
