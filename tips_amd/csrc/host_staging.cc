@@ -264,7 +264,7 @@ bool read_cpulist(const std::string& path, cpu_set_t* set) {
 }
 
 // The CPUs of the device's NUMA node that this process may run on (PCI sysfs): where the fused host
-// path's copy threads sit with TIPS_HOST_BIND=1, next to the root complex the DMA engines use.
+// path's copy threads sit (TIPS_HOST_BIND, default on), next to the root complex the DMA engines use.
 // False when the node is unknown or none of its CPUs is allowed.
 bool gpu_local_cpus(int device, cpu_set_t* out) {
   char bus[64] = {0};
@@ -379,10 +379,12 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     delete st.host_pool;
     st.host_pool = new HostPool(nthreads);
   }
-  {  // TIPS_HOST_BIND=1: the pool's threads on the GPU's NUMA node (the caller's thread stays put)
+  {  // TIPS_HOST_BIND (default 1): the pool's threads on the GPU's NUMA node, as RCCL places its own
+     // threads (the caller's thread stays put). Config 5 host -> host: 0.5-1.5 % faster in each of 3
+     // interleaved rounds on a box whose process may run on both nodes (profiles/r03/p_numa_probe.jsonl)
     static int local_ok = -1;
     static cpu_set_t local;
-    if (env_i64("TIPS_HOST_BIND", 0) != 0) {
+    if (env_i64("TIPS_HOST_BIND", 1) != 0) {
       if (local_ok < 0) local_ok = gpu_local_cpus(st.device, &local) ? 1 : 0;
       st.host_pool->set_affinity(local_ok == 1 ? &local : nullptr);
     } else {
