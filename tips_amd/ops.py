@@ -179,7 +179,7 @@ def broadcast_op(tensor, root_rank=0, name=None):
     basics.init()
     code = tensors.dtype_code(tensor)
     src = tensors.contiguous(tensor)
-    out = tensors.empty_like(src)
+    out = _HOST_OUT.take(src) if not tensors.is_device(src) else tensors.empty_like(src)
     n = tensors.numel(src)
     if n:
         _lib.call("tips_broadcast", tensors.data_ptr(src), tensors.data_ptr(out), n, code, int(root_rank),
