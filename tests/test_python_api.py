@@ -393,3 +393,14 @@ def test_host_output_pool_reuses_only_released_outputs(monkeypatch):
     arr = y.numpy()
     del y
     assert pool.take(t).data_ptr() != px and arr.size == 1 << 19
+
+
+def test_fused_list_refuses_host_tensors():
+    """FusedList.allreduce_ reads pointers, counts and dtype in C++ (_fast.dev_list) and falls back
+    to the Python checks, with their error text, for a list it does not take: host tensors here."""
+    import torch
+    from tips_amd.ops import FusedList
+    fl = FusedList([3, 4])
+    with pytest.raises(ValueError, match="needs device tensors"):
+        fl.allreduce_([torch.zeros(3), torch.zeros(4)])
+    assert fl.allreduce_([]) == []

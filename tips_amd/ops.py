@@ -556,19 +556,32 @@ class FusedList(object):
         self._ptrs = None
         self._arrays = None
         self._cp = _lib.i64_array(self._counts)
+        self._count_bytes = self._cp[1].tobytes()  # (little-endian int64, as _fast.dev_list writes them)
+        self._tls = threading.local()  # per-thread scratch: the library call releases the GIL
 
     def allreduce_(self, tensor_list):
         if not tensor_list:
             return tensor_list
-        ptrs = [t.data_ptr() for t in tensor_list]
-        if ptrs != self._ptrs:
-            basics.init()
+        import ctypes
+        n = len(tensor_list)
+        sc = getattr(self._tls, "sc", None)
+        if sc is None or len(sc[0]) != n:
+            pa, na = (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
+            sc = self._tls.sc = (pa, na, ctypes.addressof(pa), ctypes.addressof(na))
+        # pointers, counts and dtype read in C++ (_fast.dev_list); the Python checks below only when
+        # the list is not one dtype of dense contiguous device tensors, or its pointers changed
+        r = _fast.dev_list(tensor_list, sc[2], sc[3])
+        cur = ctypes.string_at(sc[2], 8 * n) if r is not None else None
+        if r is None or cur != self._ptrs:
             code = _check_fusable(tensor_list, "fused_allreduce_")
-            if [t.numel() for t in tensor_list] != self._counts:
+            basics.init()
+            if len(tensor_list) != len(self._counts) or (r is not None and ctypes.string_at(sc[3], 8 * n) != self._count_bytes) \
+                    or (r is None and [t.numel() for t in tensor_list] != self._counts):
                 raise ValueError("FusedList: the tensors' element counts changed")
-            self._ptrs, self._arrays = ptrs, (code,) + _lib.ptr_array(ptrs)
+            ptrs = [t.data_ptr() for t in tensor_list]
+            self._ptrs, self._arrays = cur, (code,) + _lib.ptr_array(ptrs)
         code, pp = self._arrays[0], self._arrays[1]
-        _lib.call("tips_fused_allreduce", pp, self._cp[0], len(ptrs), code, tensors.stream_of(tensor_list[0]))
+        _lib.call("tips_fused_allreduce", pp, self._cp[0], n, code, tensors.stream_of(tensor_list[0]))
         return tensor_list
 
 
