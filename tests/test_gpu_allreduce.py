@@ -336,6 +336,36 @@ def test_fusion_caches_with_fresh_tensors(gpu, monkeypatch):
     assert s3["tables_built"] == s2["tables_built"] and s3["table_hits"] > s2["table_hits"]
 
 
+def test_fused_list_reuses_arrays_and_revalidates(gpu, monkeypatch):
+    """ops.FusedList (DistributedOptimizer's path without gradient bucket views): pointers read in
+    C++ every call; the same tensors reuse the cached arrays, a replaced tensor is picked up, a
+    count change or a second dtype is refused; one rank with the buckets kept (pack + unpack):
+    the tensors come back unchanged. allreduce_grads' C++ path with fresh outputs likewise."""
+    import torch
+    from tips_amd.ops import FusedList
+    monkeypatch.setenv("TIPS_FUSION_MEASURE_PACK", "1")
+    sizes = [4099, 17, 100000, 3, 65536]
+    ts = [torch.randn(n, device="cuda") for n in sizes]
+    ref = [t.clone() for t in ts]
+    fl = FusedList(sizes)
+    for _ in range(3):
+        fl.allreduce_(ts)
+    ts[1] = torch.randn(17, device="cuda")
+    ref[1] = ts[1].clone()
+    fl.allreduce_(ts)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(ts, ref))
+    with pytest.raises(ValueError, match="element counts changed"):
+        fl.allreduce_(ts[:-1] + [torch.randn(7, device="cuda")])
+    with pytest.raises(TypeError):
+        fl.allreduce_(ts[:-1] + [torch.randn(65536, device="cuda", dtype=torch.float64)])
+    g = [torch.randn(n, device="cuda") for n in sizes]
+    import tips_amd
+    outs = tips_amd._reduce_grads(g)
+    torch.cuda.synchronize()
+    assert [o.shape for o in outs] == [t.shape for t in g] and all(torch.equal(o, t) for o, t in zip(outs, g))
+
+
 @pytest.mark.parametrize("piece,first", [(256, 256), (4096, 4096), (8 << 20, 8 << 20), (65536, 1024), (16 << 20, 2 << 20)])
 def test_fused_host_identity(gpu, monkeypatch, piece, first):
     """tips_fused_allreduce_host at one rank (the identity after H2D -> HBM -> D2H): many host tensors
