@@ -757,11 +757,12 @@ class Negotiator {
           i++;
           continue;
         }
-        set_phase("execute " + std::to_string(i) + "/" + std::to_string(n) + ": " + reqs[i]->name +
-                  (reqs[i]->body ? " (routed call)" : reqs[i]->host ? " (host)" : reqs[i]->type != TIPS_REQ_ALLREDUCE ? " (other)" : ""));
-        {
+        {  // (the request itself is kept; debug_state formats the line only when asked)
           std::lock_guard<std::mutex> l(phase_mu_);
           executed_++;
+          exec_i_ = i;
+          exec_n_ = n;
+          exec_req_ = reqs[i];
         }
         if (reqs[i]->body) {  // a routed synchronous collective: its own call, here, in rank 0's order
           const int rc = reqs[i]->body();
@@ -939,9 +940,12 @@ class Negotiator {
   std::mutex phase_mu_;
   std::string phase_ = "start", waiter_phase_ = "idle";
   int64_t cycles_ = 0, executed_ = 0;
+  size_t exec_i_ = 0, exec_n_ = 0;
+  std::shared_ptr<Req> exec_req_;  // the request execute() is on (phase_ "execute")
   void set_phase(std::string p) {
     std::lock_guard<std::mutex> l(phase_mu_);
     phase_ = std::move(p);
+    exec_req_.reset();
   }
   void set_waiter_phase(std::string p) {
     std::lock_guard<std::mutex> l(phase_mu_);
@@ -957,8 +961,14 @@ class Negotiator {
     std::string out;
     {
       std::lock_guard<std::mutex> l(phase_mu_);
+      std::string ph = phase_;
+      if (exec_req_) {
+        const Req& r = *exec_req_;
+        ph = "execute " + std::to_string(exec_i_) + "/" + std::to_string(exec_n_) + ": " + r.name +
+             (r.body ? " (routed call)" : r.host ? " (host)" : r.type != TIPS_REQ_ALLREDUCE ? " (other)" : "");
+      }
       out = "rank " + std::to_string(rank_) + " cycles " + std::to_string((long long)cycles_) + " executed " +
-            std::to_string((long long)executed_) + " | negotiation: " + phase_ + " | completion: " + waiter_phase_;
+            std::to_string((long long)executed_) + " | negotiation: " + ph + " | completion: " + waiter_phase_;
     }
     std::unique_lock<std::mutex> l(m_, std::try_to_lock);
     if (!l.owns_lock()) return out + " | (request lock held)";
