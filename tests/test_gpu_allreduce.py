@@ -288,6 +288,14 @@ def test_fused_flat_outputs(gpu, monkeypatch, threshold, measure_pack):
             for o, t in zip(outs, ins):
                 assert o.shape == t.shape and o.dtype == t.dtype and torch.equal(o, t)
             del outs
+        # allreduce_grads' N > 1 body on the same list: its C++ list path (tips_amd._fast)
+        import tips_amd
+        for _ in range(2):
+            outs = tips_amd._reduce_grads(ins)
+            torch.cuda.synchronize()
+            for o, t in zip(outs, ins):
+                assert o.shape == t.shape and o.dtype == t.dtype and torch.equal(o, t)
+            del outs
 
 
 def test_fused_flat_output_reuse(gpu, monkeypatch):
