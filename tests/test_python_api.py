@@ -322,6 +322,12 @@ def test_fast_list_helper_reads_pointers_counts_and_shapes():
     assert _fast.dev_list([flat[::2]], a, b, 0) is None              # not contiguous
     assert _fast.dev_list([flat[:4], None], a, b, 0) is None
     assert _fast.dev_list([torch.zeros(3).to_sparse()], a, b, 0) is None
+    assert _fast.dev_list([torch.empty(3, device="meta")], a, b, 0) is None  # neither CPU nor device
+    # cap: the arrays hold n entries; a sequence of any other length is refused before any write
+    pa[0] = na[0] = -7
+    assert _fast.dev_list(ts + [flat[:1]], a, b, 0, n) is None
+    assert pa[0] == -7 and na[0] == -7
+    assert _fast.dev_list(ts, a, b, 0, n)[2] == h
     x = torch.zeros(3)
     assert _fast.max_refcount([x]) == sys.getrefcount(x) - 1
     keep = [x, x]

@@ -8,14 +8,15 @@
 // time (~0.2 ms) than the fused allreduce's device work. THPVariable_Unpack reads them in tens of
 // nanoseconds per tensor.
 //
-//   dev_list(seq, ptrs_addr, numels_addr[, on_device=1]) -> (scalar_type, device_index, shape_hash)
-//                                                            | None
+//   dev_list(seq, ptrs_addr, numels_addr[, on_device=1[, cap]]) -> (scalar_type, device_index,
+//                                                                  shape_hash) | None
 //       every item a dense, contiguous device (HIP) tensor - or, with on_device=0, CPU tensor - of
 //       one dtype on one device: writes its
 //       data pointer and element count into the int64 arrays at the two addresses (n entries each,
 //       allocated by the caller) and returns the dtype (c10::ScalarType as int), the device index
 //       and a 64-bit FNV-1a hash of every tensor's (ndim, sizes); None as soon as one item is not
-//       such a tensor (the caller takes its general path).
+//       such a tensor (the caller takes its general path), and None without writing anything when
+//       cap is given and the sequence does not hold exactly cap items (the arrays' size).
 //   max_refcount(seq) -> int: the largest reference count of the items (a flat output set is free
 //       again when no view of it is referenced outside the library's own lists).
 #include <Python.h>
@@ -29,8 +30,8 @@ namespace {
 inline uint64_t fnv(uint64_t h, uint64_t v) { return (h ^ v) * 1099511628211ull; }
 
 PyObject* dev_list(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-  if (nargs != 3 && nargs != 4) {
-    PyErr_SetString(PyExc_TypeError, "dev_list(seq, ptrs_addr, numels_addr[, on_device=1])");
+  if (nargs < 3 || nargs > 5) {
+    PyErr_SetString(PyExc_TypeError, "dev_list(seq, ptrs_addr, numels_addr[, on_device=1[, cap]])");
     return nullptr;
   }
   PyObject* seq = PySequence_Fast(args[0], "dev_list: a sequence of tensors");
@@ -38,6 +39,7 @@ PyObject* dev_list(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   const unsigned long long pa = PyLong_AsUnsignedLongLong(args[1]);
   const unsigned long long na = PyLong_AsUnsignedLongLong(args[2]);
   const bool on_device = nargs < 4 || PyObject_IsTrue(args[3]) == 1;
+  const long long cap = nargs < 5 ? -1 : PyLong_AsLongLong(args[4]);
   if (PyErr_Occurred()) {
     Py_DECREF(seq);
     return nullptr;
@@ -45,6 +47,10 @@ PyObject* dev_list(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   int64_t* ptrs = reinterpret_cast<int64_t*>(pa);
   int64_t* numels = reinterpret_cast<int64_t*>(na);
   const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  if (cap >= 0 && n != cap) {  // (a sequence whose len() and items disagree: never past the arrays)
+    Py_DECREF(seq);
+    Py_RETURN_NONE;
+  }
   PyObject** items = PySequence_Fast_ITEMS(seq);
   int st = -1, dev = -1;
   uint64_t h = 1469598103934665603ull;
@@ -55,7 +61,7 @@ PyObject* dev_list(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
       Py_RETURN_NONE;
     }
     const at::Tensor& t = THPVariable_Unpack(o);
-    if (!t.defined() || t.layout() != c10::kStrided || t.is_cuda() != on_device || !t.is_contiguous()) {
+    if (!t.defined() || t.layout() != c10::kStrided || !(on_device ? t.is_cuda() : t.is_cpu()) || !t.is_contiguous()) {
       Py_DECREF(seq);
       Py_RETURN_NONE;
     }
@@ -92,7 +98,7 @@ PyObject* max_refcount(PyObject*, PyObject* arg) {
 
 PyMethodDef kMethods[] = {
     {"dev_list", (PyCFunction)(void (*)(void))dev_list, METH_FASTCALL,
-     "dev_list(seq, ptrs_addr, numels_addr) -> (scalar_type, device, shape_hash) or None"},
+     "dev_list(seq, ptrs_addr, numels_addr[, on_device[, cap]]) -> (scalar_type, device, shape_hash) or None"},
     {"max_refcount", max_refcount, METH_O, "max_refcount(seq) -> the largest reference count of the items"},
     {nullptr, nullptr, 0, nullptr}};
 

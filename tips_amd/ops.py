@@ -360,7 +360,7 @@ def _dev_list_flat(tensor_list):
         if len(mine) >= 16:
             mine.pop(next(iter(mine)))
         bufs = mine[n] = (pa, na, ctypes.addressof(pa), ctypes.addressof(na))
-    r = _fast.dev_list(tensor_list, bufs[2], bufs[3])
+    r = _fast.dev_list(tensor_list, bufs[2], bufs[3], 1, n)
     if r is None or r[0] not in _ST_CODES:
         return None
     import ctypes
@@ -570,7 +570,7 @@ class FusedList(object):
             sc = self._tls.sc = (pa, na, ctypes.addressof(pa), ctypes.addressof(na))
         # pointers, counts and dtype read in C++ (_fast.dev_list); the Python checks below only when
         # the list is not one dtype of dense contiguous device tensors, or its pointers changed
-        r = _fast.dev_list(tensor_list, sc[2], sc[3])
+        r = _fast.dev_list(tensor_list, sc[2], sc[3], 1, n)
         cur = ctypes.string_at(sc[2], 8 * n) if r is not None else None
         if r is None or cur != self._ptrs:
             code = _check_fusable(tensor_list, "fused_allreduce_")
