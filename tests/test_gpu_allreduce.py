@@ -664,6 +664,41 @@ def test_named_async_many_single_rank(gpu, monkeypatch):
         gpu.allreduce_async_many([ts[0], ts[1].double()], ["a", "b"])
 
 
+def test_enqueue_n_classifies_each_pointer(gpu):
+    """tips_enqueue_allreduce_n remembers the device allocations it has met within one call
+    (negotiate.cc PtrRanges), so a list's later tensors skip the pointer queries. In one call:
+    slices of one allocation, a tensor of another, a host pair after them (still host: host memory
+    is never cached) and a device-in / host-out pair, refused as a single enqueue refuses it. At one
+    rank every accepted result is its input, bit for bit."""
+    import ctypes
+    import torch
+    from tips_amd import _lib
+    L = _lib.lib()
+    big = torch.randn(1 << 22, device="cuda")
+    dev_in = [big[0:1000], big[5000:9000], torch.randn(777, device="cuda"), big[(1 << 21):(1 << 21) + 3]]
+    dev_out = [torch.empty_like(t) for t in dev_in]
+    h_in = np.random.default_rng(1).random(5000).astype(np.float32)
+    h_out = np.empty_like(h_in)
+    items = [(t.data_ptr(), o.data_ptr(), t.numel()) for t, o in zip(dev_in, dev_out)]
+    items.insert(2, (h_in.ctypes.data, h_out.ctypes.data, h_in.size))
+    items.append((big[100:200].data_ptr(), h_out.ctypes.data, 100))
+    n = len(items)
+    names = (ctypes.c_char_p * n)(*[("ptr_ranges.%d" % i).encode() for i in range(n)])
+    ins, _k1 = _lib.ptr_array([a for a, _, _ in items])
+    outs, _k2 = _lib.ptr_array([b for _, b, _ in items])
+    cnt, _k3 = _lib.i64_array([c for _, _, c in items])
+    hs = (ctypes.c_int64 * n)()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = L.tips_enqueue_allreduce_n(names, ins, outs, cnt, n, _lib.FLOAT32, stream, hs)
+    assert rc < 0 and "one device and one host pointer" in _lib.last_error()
+    assert hs[n - 1] < 0 and all(h > 0 for h in hs[:n - 1])
+    assert L.tips_wait_n(hs, n - 1) == 0, _lib.last_error()
+    torch.cuda.synchronize()
+    for t, o in zip(dev_in, dev_out):
+        assert torch.equal(t, o)
+    assert np.array_equal(h_in, h_out)
+
+
 def test_sparse_allreduce_single_rank(gpu):
     """The reference's IndexedSlices branch (allgather of values and indices, __init__.py:59-74) through
     tips_allgatherv on one rank: device and host, IndexedSlices and torch sparse COO."""

@@ -82,6 +82,40 @@ thread_local bool tl_negotiation_thread = false;
 // every rank must have issued the same number when the negotiation starts (checked at the join).
 std::atomic<int64_t> g_sync_direct{0};
 
+// The device allocations one list call (tips_enqueue_allreduce_n / _shaped_n) has met so far: a
+// gradient list lies in a few of the caching allocator's segments, so after a segment's first
+// pointer (hipPointerGetAttributes, then hipMemGetAddressRange) the rest of its tensors are known
+// to be device memory without a HIP call - two calls per request otherwise, most of enqueue's cost.
+// Lives for one list call, during which the caller keeps every pointer of the list alive. Host
+// pointers are never cached: each takes its own hipPointerGetAttributes, as a single enqueue does.
+struct PtrRanges {
+  struct Range {
+    uintptr_t lo, len;
+  };
+  std::vector<Range> r;
+  size_t last = 0;
+  bool device_set = false;  // set_device done for this list (one thread, one device)
+  bool is_device(const void* p) {
+    const uintptr_t a = (uintptr_t)p;
+    if (last < r.size() && a - r[last].lo < r[last].len) return true;
+    for (size_t k = 0; k < r.size(); k++)
+      if (a - r[k].lo < r[k].len) {
+        last = k;
+        return true;
+      }
+    if (!is_device_ptr(p)) return false;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && size > 0) {
+      r.push_back(Range{(uintptr_t)base, (uintptr_t)size});
+      last = r.size() - 1;
+    } else {
+      (void)hipGetLastError();
+    }
+    return true;
+  }
+};
+
 // ---- wire format: flat little-endian records ----------------------------------
 struct Writer {
   std::string b;
@@ -373,7 +407,8 @@ class Negotiator {
 
   int64_t enqueue(const std::string& name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
                   hipStream_t s, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
-                  void* actx = nullptr, int64_t* out_rows = nullptr, std::function<int()> body = nullptr) {
+                  void* actx = nullptr, int64_t* out_rows = nullptr, std::function<int()> body = nullptr,
+                  PtrRanges* pr = nullptr) {
     if (ndim < 0 || ndim > TIPS_MAX_DIMS) return fail(TIPS_ERR_INVALID_ARG, "bad ndim %d", ndim);
     if (type == TIPS_REQ_ALLGATHER && ndim < 1) return fail(TIPS_ERR_INVALID_ARG, "An empty tensor found");
     auto r = std::make_shared<Req>();
@@ -398,12 +433,14 @@ class Negotiator {
     if (!dry_ && !r->body) {  // the real executor (the dry run touches no memory; a routed body checks its own)
       // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
       // st.device is fixed from init on)
-      TRY(set_device(S()));
+      if (!pr || !pr->device_set) TRY(set_device(S()));
+      if (pr) pr->device_set = true;
       // device tensors run stream-ordered on `s`; host tensors (the reference's MPIAllreduce is a
       // CPU op, ops.cc:118) run synchronously on the executor thread, staged through HBM as
       // tips_allreduce stages them. Both pointers of a request live on the same side.
       if (r->count > 0) {
-        const bool din = is_device_ptr(in), dout = type == TIPS_REQ_ALLGATHER ? din : is_device_ptr(out);
+        auto dev = [&](const void* q) { return pr ? pr->is_device(q) : is_device_ptr(q); };
+        const bool din = dev(in), dout = type == TIPS_REQ_ALLGATHER ? din : dev(out);
         if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "named request %s: one device and one host pointer", name.c_str());
         r->host = !din;
       }
@@ -1101,7 +1138,7 @@ std::shared_ptr<Negotiator> negotiator(int* code) {  // started by the first nam
 
 int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
                       void* stream, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
-                      void* actx = nullptr, int64_t* out_rows = nullptr) {
+                      void* actx = nullptr, int64_t* out_rows = nullptr, PtrRanges* pr = nullptr) {
   TRY(check_dtype(dtype));
   if (!name || !*name || ndim < 0 || ndim > TIPS_MAX_DIMS || (ndim > 0 && !shape))
     return fail(TIPS_ERR_INVALID_ARG, "bad named request");
@@ -1116,7 +1153,8 @@ int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t
   int code = TIPS_ERR_NOT_INITIALIZED;
   std::shared_ptr<Negotiator> n = negotiator(&code);
   if (!n) return code;
-  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, type, root, alloc, actx, out_rows);
+  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, type, root, alloc, actx, out_rows, nullptr,
+                    pr);
 }
 
 std::shared_ptr<Negotiator> current() {
@@ -1192,8 +1230,11 @@ int tips_enqueue_allreduce_n(const char* const* names, const void* const* ins, v
     return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce list");
   int rc = 0;
   std::string first_err;
+  PtrRanges pr;
   for (int i = 0; i < n; i++) {
-    handles[i] = tips_enqueue_allreduce(names[i], ins[i], outs[i], counts[i], dtype, stream);
+    handles[i] = counts[i] < 0 ? fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request")
+                               : enqueue_named(names[i], ins[i], outs[i], &counts[i], 1, dtype, stream,
+                                               TIPS_REQ_ALLREDUCE, 0, nullptr, nullptr, nullptr, &pr);
     if (handles[i] < 0 && rc == 0) {
       rc = (int)handles[i];
       first_err = last_error();
@@ -1210,11 +1251,13 @@ int tips_enqueue_allreduce_shaped_n(const char* const* names, const void* const*
   int rc = 0;
   std::string first_err;
   int64_t off = 0;
+  PtrRanges pr;
   for (int i = 0; i < n; i++) {
     if (ndims[i] < 0 || ndims[i] > TIPS_MAX_DIMS || (ndims[i] > 0 && !dims)) {
       handles[i] = fail(TIPS_ERR_INVALID_ARG, "bad ndim %d for %s", ndims[i], names[i] ? names[i] : "?");
     } else {
-      handles[i] = enqueue_named(names[i], ins[i], outs[i], dims ? dims + off : nullptr, ndims[i], dtype, stream);
+      handles[i] = enqueue_named(names[i], ins[i], outs[i], dims ? dims + off : nullptr, ndims[i], dtype, stream,
+                                 TIPS_REQ_ALLREDUCE, 0, nullptr, nullptr, nullptr, &pr);
       off += ndims[i];
     }
     if (handles[i] < 0 && rc == 0) {
