@@ -146,14 +146,19 @@ struct Reader {
     return v;
   }
   std::string str() {
+    std::string s;
+    str_into(s);
+    return s;
+  }
+  void str_into(std::string& s) {  // (into a reused string: no allocation once its capacity fits)
     const uint32_t n = get<uint32_t>();
     if (!ok || off + n > b.size()) {
       ok = false;
-      return std::string();
+      s.clear();
+      return;
     }
-    std::string s = b.substr(off, n);
+    s.assign(b.data() + off, n);
     off += n;
-    return s;
   }
 };
 
@@ -193,15 +198,32 @@ struct Table {
   int p = 1;
   std::unordered_map<std::string, Row> rows;
   std::vector<std::string> ready_q;
+  // Rows resolved in earlier cycles, kept with their map node, key and vectors: a new name reuses
+  // one instead of allocating all four (a 1000-gradient step resolves 1000 names a cycle).
+  std::vector<std::unordered_map<std::string, Row>::node_type> spare;
 
   void announce(int rank, const Announce& a) {
     auto it = rows.find(a.name);
     if (it == rows.end()) {
-      Row r;
-      r.rec.assign((size_t)p * TIPS_REQUEST_WORDS, 0);
-      r.seen.assign(p, 0);
-      r.roots.assign(p, 0);
-      it = rows.emplace(a.name, std::move(r)).first;
+      if (!spare.empty()) {
+        auto nh = std::move(spare.back());
+        spare.pop_back();
+        nh.key() = a.name;
+        Row& r = nh.mapped();
+        r.rec.assign((size_t)p * TIPS_REQUEST_WORDS, 0);
+        r.seen.assign(p, 0);
+        r.roots.assign(p, 0);
+        r.nseen = 0;
+        r.queued = false;
+        r.dup.clear();
+        it = rows.insert(std::move(nh)).position;
+      } else {
+        Row r;
+        r.rec.assign((size_t)p * TIPS_REQUEST_WORDS, 0);
+        r.seen.assign(p, 0);
+        r.roots.assign(p, 0);
+        it = rows.emplace(a.name, std::move(r)).first;
+      }
     }
     Row& r = it->second;
     if (r.seen[rank]) {
@@ -245,7 +267,8 @@ struct Table {
           for (int i = 0; i < p; i++) d.sizes.push_back(r.rec[(size_t)i * W + 3]);
         out.push_back(std::move(d));
       }
-      rows.erase(it);
+      if (spare.size() < 4096) spare.push_back(rows.extract(it));
+      else rows.erase(it);
     }
     ready_q.clear();
     return out;
@@ -731,8 +754,9 @@ class Negotiator {
       Reader rd(all[r]);
       everyone_stops &= rd.get<uint8_t>() != 0;
       const uint32_t n = rd.get<uint32_t>();
+      Announce a;  // (one, reused: its shape and name keep their allocations)
       for (uint32_t i = 0; i < n && rd.ok; i++) {
-        Announce a;
+        a.shape.clear();
         a.type = rd.get<int32_t>();
         a.root = rd.get<int32_t>();
         a.dtype = rd.get<int32_t>();
@@ -740,7 +764,7 @@ class Negotiator {
         const uint32_t ndim = rd.get<uint32_t>();
         if (ndim > TIPS_MAX_DIMS) rd.ok = false;
         for (uint32_t d = 0; d < ndim && rd.ok; d++) a.shape.push_back(rd.get<int64_t>());
-        a.name = rd.str();
+        rd.str_into(a.name);
         if (rd.ok) table_.announce(r, a);
       }
       if (!rd.ok) {
