@@ -10,13 +10,13 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals
 
 CRASH    := tools/lib/libcrashline.so
 
-REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe tools/_bin/op_body
+REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe tools/_bin/op_body tools/_bin/op_host tools/_bin/op_host_check
 
 FAST     := tips_amd/_fast$(shell python3 -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
 TORCH    := $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
 PYINC    := $(shell python3 -c "import sysconfig; print(sysconfig.get_paths()['include'])")
 
-all: $(LIB) $(FAST) $(CRASH) $(REPRO) oracle tsan
+all: $(LIB) $(FAST) $(CRASH) $(REPRO) oracle tsan tools/cpu_sum_bench
 
 # the Python mirror's list helper (tips_amd._fast: tensor pointers / counts in C++), torch headers
 $(FAST): tips_amd/csrc/pyfast.cc
@@ -52,6 +52,17 @@ tools/_bin/op_body: tests/c/op_body.c $(LIB) include/tips_hip.h oracle/build/lib
 	gcc -O2 -std=gnu11 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -Ioracle -o $@ $< \
 	  -Ltips_amd/lib -ltips_hip -Loracle/build -loracle -L/opt/rocm/lib -lamdhip64 -lpthread \
 	  -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -Wl,-rpath,/opt/rocm/lib
+
+# config 5 as 214 named host requests from TF-style executor threads (tools/op_host.c): bench.py's
+# leg links the product library only; the -m gpu test's build also checks against the oracle's fold
+tools/_bin/op_host: tools/op_host.c $(LIB) include/tips_hip.h
+	@mkdir -p tools/_bin
+	gcc -O2 -std=gnu11 -Wall -Iinclude -o $@ $< -Ltips_amd/lib -ltips_hip -lpthread -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib'
+
+tools/_bin/op_host_check: tools/op_host.c $(LIB) include/tips_hip.h oracle/build/liboracle.so
+	@mkdir -p tools/_bin
+	gcc -O2 -std=gnu11 -Wall -DOP_HOST_ORACLE -Iinclude -Ioracle -o $@ $< -Ltips_amd/lib -ltips_hip -Loracle/build -loracle \
+	  -lpthread -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib' -Wl,-rpath,'$$ORIGIN/../../oracle/build'
 
 oracle/build/liboracle.so: oracle/oracle.c oracle/oracle.h
 	$(MAKE) -C oracle build/liboracle.so

@@ -4,24 +4,36 @@
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...     (N > 1, one rank per GPU)
 
-N == 1 (BASELINE.json configs[1], the config the metric's first half is
-quoted on): one step = the device-resident sum of two 256 MiB fp32 gradient
-buffers, c = a + b (tips_bucket_sum: the per-chunk MPI_SUM of
-tips/core/collective/utils.h:60-65 as a gfx950 kernel). value = algorithmic
-bytes moved (2 reads + 1 write = 805,306,368 B per step) / time, GiB/s. Step i
-sums the (i % 4)-th of four such buffer triples, so every launch reads its
-operands from HBM, not from the 256 MiB Infinity Cache.
+One JSON line (rank 0). Its headline `value` is BASELINE.json's metric:
 
-N > 1 (configs[2]): one step = allreduce of one 1 GiB fp32 bucket per GPU
-(tips_allreduce: RCCL send/recv over xGMI + the sum kernels).
-value = N x 1 GiB / time (bucket bytes reduced by the whole job per second,
-GiB/s); algbw / busbw and the xGMI fraction are extra fields. Each rank checks
-its result against the fold of all ranks' seeded inputs after timing.
+N == 1 (configs[1], the config the metric's first half is quoted on): one step = the
+device-resident sum of two 256 MiB fp32 gradient buffers, c = a + b (tips_bucket_sum: the
+per-chunk MPI_SUM of tips/core/collective/utils.h:60-65 as a gfx950 kernel). value = algorithmic
+bytes moved (2 reads + 1 write = 805,306,368 B per step) / time, GiB/s. Step i sums the (i % 4)-th
+of four such buffer triples, so every launch reads its operands from HBM, not from the 256 MiB
+Infinity Cache.
 
-Inputs are synthetic seeded uniforms generated on the device and resident in
-HBM before the timed region. At N == 1, rank 0 also times the reference's CPU
-path (MPI_Allreduce, MPI_SUM under MPICH on host cores) on a bounded sample —
-a reported baseline, not the target.
+N > 1 (configs[2]): one step = allreduce of one 1 GiB fp32 bucket per GPU (tips_allreduce: RCCL
+send/recv over xGMI + the sum kernels). value = N x 1 GiB / time (bucket bytes reduced by the
+whole job per second, GiB/s); busbw and the xGMI fraction beside it. Each rank checks its result
+against the fold of all ranks' seeded inputs after timing.
+
+Beside the headline, the same line carries the other configs as sub-records (`configs`), each
+with its own steps, rate, roofline and parity check, at every N:
+  config3_bucket  (N == 1 only) config 3's 1 GiB bucket through tips_allreduce at one rank, value
+                  = N x bucket bytes / time: the same definition as the N > 1 headline, so a
+                  scaling curve starts from the workload it ends on;
+  config4_fused1000, config5_resnet50: the fusion path (tips_fused_allreduce) over the configs'
+                  gradient sets, busbw and xGMI fraction at N > 1, the pack kernel's HBM roofline
+                  at N == 1; config 5 also host -> host (the 214 gradients in host memory, fused),
+                  and at N == 1 as the reference's CPU op sees it: 214 named host requests from four
+                  executor threads (tools/op_host.c).
+Comparison schedules and probes follow, within a time budget all ranks agree on
+(TIPS_BENCH_BUDGET_S, 240 s from start); what the budget leaves out is named in the line.
+
+Inputs are synthetic seeded uniforms generated on the device and resident in HBM before the timed
+region. Rank 0 also times the reference's CPU path (MPI_Allreduce, MPI_SUM under MPICH on host
+cores) and an OpenMP c = a + b on a bounded sample — a reported baseline, not the target.
 """
 import argparse
 import json
@@ -39,8 +51,9 @@ GIB = float(1 << 30)
 # the exact instantiation tips_bucket_sum launches for f32 (kernels.hip kDef*): PMC traffic is only
 # reported from a profile of this kernel
 DEFAULT_SUM_KERNEL = "sum2_buf_kernel<0, 2, 16, 1, 256>"
-# N == 1 cycles over this many (a, b, c) triples of config 2's size (3 GiB at 4): see bench_sum
+# N == 1 cycles over this many (a, b, c) triples of config 2's size (3 GiB at 4): see sum_record
 ROTATING_SETS = 4
+SUB_WORKLOADS = ("fused1000", "resnet50")
 
 
 def parse():
@@ -48,31 +61,78 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--sub-steps", type=int, default=20, help="timed steps of each sub-record (configs 3-5)")
     ap.add_argument("--algo", default=os.environ.get("TIPS_ALGO", "tune"),
                     choices=["auto", "ring", "direct", "rccl", "oneshot", "peer", "tune"],
                     help="N>1 schedule; tune (default): the library times ring / direct at several pipeline "
                          "depths on the first call of a size class and keeps the fastest (TIPS_ALGO_TUNE)")
     ap.add_argument("--bucket-mib", type=int, default=None, help="override the bucket size (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-compare", action="store_true", help="N>1: skip the other-algorithm comparison runs")
+    ap.add_argument("--no-compare", action="store_true", help="skip the comparison schedules and probes")
+    ap.add_argument("--no-sub", action="store_true", help="the headline only: no config sub-records")
     ap.add_argument("--no-env-variants", action="store_true",
                     help="N>1: skip the child jobs that rerun direct under other RCCL settings")
     ap.add_argument("--no-extras", action="store_true",
-                    help="N=1: time the headline kernel only (no same-buffer, PCIe or host-memory legs), as under rocprofv3")
+                    help="N=1: time the headline kernel only (no same-buffer, PCIe or host-memory legs, no "
+                         "sub-records), as under rocprofv3")
     ap.add_argument("--workload", default="auto", choices=["auto", "sum", "bucket", "fused1000", "resnet50", "negotiated1000"],
-                    help="auto: config 2 (sum) at N=1, config 3 (bucket allreduce) at N>1")
+                    help="auto: config 2 (sum) at N=1, config 3 (bucket allreduce) at N>1, with the other configs "
+                         "as sub-records; any other: that workload alone as the headline")
     return ap.parse_args()
 
 
-# ----------------------------------------------------------------------------- CPU baseline (rank 0, N == 1)
+# ----------------------------------------------------------------------------- CPU baselines (rank 0)
+
+def host_info():
+    """The host the CPU baselines ran on: CPUs the OS shows, CPUs this process may run on, the
+    box's CPU share (OMP_NUM_THREADS, set to 16 per GPU on the GPU box), the CPU model."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "omp_num_threads": int(omp) if omp and omp.isdigit() else None,
+            "cpu_model": model}
+
+
+def openmp_sum(elems, threads, iters):
+    """tools/cpu_sum_bench: c = a + b over two `elems` fp32 buffers on `threads` OpenMP threads
+    (config 2's step on host cores, the loop libmpi's MPI_SUM runs per chunk). GiB/s of the same 3 x
+    bucket bytes as the GPU headline."""
+    exe = os.path.join(REPO, "tools", "cpu_sum_bench")
+    if not os.path.exists(exe):
+        return {"error": "tools/cpu_sum_bench not built"}
+    try:
+        r = subprocess.run([exe, str(elems), str(iters), str(threads)], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, OMP_PROC_BIND="spread", OMP_PLACES="cores"))
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    except Exception as e:  # noqa: BLE001 - a baseline leg never fails the bench
+        return {"error": repr(e)}
+    t = d["sec_per_call"]
+    return {"value": round(3 * elems * 4 / t / GIB, 3), "unit": "GiB/s", "cores": threads, "ms_per_call": round(t * 1e3, 3),
+            "check": "exact" if d.get("check") == 0 else "FAIL",
+            "sample": "tools/cpu_sum_bench: c = a + b, %d fp32 per buffer (%d MiB), %d timed calls after 1 warm-up, "
+                      "OpenMP static schedule, %d thread(s)" % (elems, elems * 4 >> 20, iters, threads)}
+
 
 def cpu_baseline(bucket_elems):
-    """Time the reference's data-path call on host cores: MPI_Allreduce(MPI_FLOAT, MPI_SUM) with
-    np=2, one 256 MiB fp32 bucket per rank, i.e. the reference computing config 2's c = a + b.
-    Runs BEFORE anything touches the GPU (it starts child processes)."""
+    """N == 1: the reference's data-path call on host cores - MPI_Allreduce(MPI_FLOAT, MPI_SUM) with
+    np = 2, one 256 MiB fp32 bucket per rank, i.e. the reference computing config 2's c = a + b
+    (`value`) - beside an OpenMP c = a + b on one core and on the box's CPU share, the
+    host's CPUs and model. Runs BEFORE anything touches the GPU (it starts child processes)."""
     harness = os.path.join(REPO, "oracle", "build", "mpi_allreduce_ref")
     mpirun = "/opt/conda/bin/mpirun"
-    out = {"value": None, "unit": "GiB/s", "cores": None, "kind": "reference", "sample": None}
+    host = host_info()
+    out = {"value": None, "unit": "GiB/s", "cores": None, "kind": "reference", "sample": None, "host": host}
     if os.path.exists(harness) and os.path.exists(mpirun):
         iters = 50  # about 8-10 s of host work on the GPU box (a bounded sample, contract ④)
         try:
@@ -92,7 +152,12 @@ def cpu_baseline(bucket_elems):
             out["error"] = "reference MPI baseline failed: %r" % (e,)
     else:
         out["error"] = "reference MPI baseline unavailable on box (no MPICH harness)"
-    # the oracle port (single thread, plain C loop) on a 64 Mi-element sample
+    share = host["omp_num_threads"] or host["affinity_cpus"] or 1
+    out["openmp_1_core"] = openmp_sum(bucket_elems, 1, 10)
+    out["openmp_all_cores"] = openmp_sum(bucket_elems, share, 30)
+    out["openmp_all_cores"]["cores_note"] = ("the box's CPU share (OMP_NUM_THREADS=%s of %s CPUs the OS shows)"
+                                             % (host["omp_num_threads"], host["nproc"]))
+    # the oracle port (single thread, plain C loop) on the same buffers
     try:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import numpy as np
@@ -123,16 +188,17 @@ def cpu_ring_baseline(world, elems=16 << 20, iters=20):
     the GPU; the other ranks wait for it in the bootstrap."""
     harness = os.path.join(REPO, "oracle", "build", "mpi_allreduce_ref")
     mpirun = "/opt/conda/bin/mpirun"
+    host = host_info()
     if not (os.path.exists(harness) and os.path.exists(mpirun)):
-        return {"error": "reference MPI baseline unavailable on box (no MPICH harness)"}
+        return {"error": "reference MPI baseline unavailable on box (no MPICH harness)", "host": host}
     try:
         r = subprocess.run([mpirun, "-np", str(world), harness, "bench", "0", str(elems), str(iters)],
                            capture_output=True, text=True, timeout=150)
         t = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["sec_per_call"]
     except Exception as e:  # noqa: BLE001 - never fail the bench on the baseline leg
-        return {"error": "reference MPI baseline failed: %r" % (e,)}
+        return {"error": "reference MPI baseline failed: %r" % (e,), "host": host}
     return {"value": round(world * elems * 4 / t / GIB, 3), "unit": "GiB/s", "cores": world, "kind": "reference",
-            "ms_per_call": round(t * 1e3, 3),
+            "ms_per_call": round(t * 1e3, 3), "host": host,
             "sample": "MPI_Allreduce(in,out,%d,MPI_FLOAT,MPI_SUM,MPI_COMM_WORLD) as in tips/core/collective/"
                       "utils.h:60-65, MPICH 3.3.2, mpirun -np %d (1 core each), one %d MiB fp32 bucket per rank, "
                       "%d timed calls after 1 warm-up; value = %d x bucket bytes / time, as the GPU line's"
@@ -155,150 +221,8 @@ def pmc_traffic(kernel_substr, file_pattern="*pmc*.json"):
     return None
 
 
-# ----------------------------------------------------------------------------- N == 1: bucket sum
 
-def bench_sum(args):
-    steps = args.steps if args.steps is not None else 200
-    warmup = args.warmup if args.warmup is not None else 20
-    n = (args.bucket_mib or 256) * (1 << 20) // 4
-    cpu = None if args.no_cpu_baseline else cpu_baseline(n)
-
-    import torch
-    import tips_amd
-    from tips_amd import _lib
-    L = _lib.lib()
-    torch.cuda.set_device(0)
-    g = torch.Generator(device="cuda")
-    stream = torch.cuda.current_stream()
-    sp = stream.cuda_stream
-    # ROTATING_SETS (a, b, c) triples, 768 MiB each: step i sums triple i % ROTATING_SETS, so 2.25 GiB
-    # of other traffic separates two uses of a buffer and no launch finds its operands in the
-    # 256 MiB Infinity Cache: the timed rate is HBM's. Triple 0 is config 2's seeded pair (seeds 1, 2).
-    sets = []
-    for k in range(ROTATING_SETS):
-        x_, y_, z_ = (torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(3))
-        g.manual_seed(1 if k == 0 else 10 + 2 * k)
-        x_.uniform_(-1.0, 1.0, generator=g)
-        g.manual_seed(2 if k == 0 else 11 + 2 * k)
-        y_.uniform_(-1.0, 1.0, generator=g)
-        sets.append((x_, y_, z_))
-    a, b, c = sets[0]
-
-    def step(i=0):
-        x_, y_, z_ = sets[i % len(sets)]
-        rc = L.tips_bucket_sum(z_.data_ptr(), x_.data_ptr(), y_.data_ptr(), n, _lib.FLOAT32, sp)
-        if rc:
-            raise _lib.TipsError("tips_bucket_sum", rc, _lib.last_error())
-
-    def timed(k, same_buffers):
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for i in range(k):
-            step(0 if same_buffers else i)
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        return ev0.elapsed_time(ev1) / k, time.perf_counter() - t0  # HIP events on the kernel's stream
-
-    for i in range(warmup):
-        step(i)
-    torch.cuda.synchronize()
-    ms, wall = timed(steps, same_buffers=False)
-    ok = all(bool(torch.equal(z_, x_ + y_)) for x_, y_, z_ in sets)  # one IEEE add per element: bit-exact
-
-    same = None
-    if not args.no_extras:
-        # the same kernel re-reading ONE triple (the literal config-2 loop): part of each launch's
-        # operands is still in the Infinity Cache from the launch before, so this is not an HBM rate
-        step(0)
-        ms_same, _ = timed(steps, same_buffers=True)
-        same = {"us_per_launch": round(ms_same * 1e3, 2), "achieved_GBps": round(3 * n * 4 / (ms_same / 1e3) / 1e9, 1),
-                "note": "tips_bucket_sum on the same (a, b, c) every launch: the 256 MiB Infinity Cache serves part "
-                        "of the 768 MiB working set from the previous launch, so this exceeds the HBM-only rate above"}
-    del sets[1:]  # (the PCIe leg below uses triple 0)
-
-    t_host, host_rates, host_ok = None, {}, True
-    if not args.no_extras:  # (skipped under rocprofv3: its kernel stats then hold only the timed launches)
-        # PCIe-inclusive rate (the path starts and ends in host memory): pinned H2D a,b + sum + D2H c
-        ha, hb, hc = (torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(3))
-        ha.copy_(a)
-        hb.copy_(b)
-        torch.cuda.synchronize()
-        reps = 3
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            a.copy_(ha, non_blocking=True)
-            b.copy_(hb, non_blocking=True)
-            step()
-            hc.copy_(c, non_blocking=True)
-        torch.cuda.synchronize()
-        t_host = (time.perf_counter() - t1) / reps
-
-        # host-memory leg of the drop-in path: tips_allreduce on host buffers (1 rank: H2D, device copy, D2H)
-        host_rates = {}
-        import numpy as np
-        pinned_in = torch.empty(n, dtype=torch.float32, pin_memory=True)
-        pinned_out = torch.empty(n, dtype=torch.float32, pin_memory=True)
-        pageable_in = np.random.default_rng(1).random(n, dtype=np.float32)
-        pageable_out = np.empty_like(pageable_in)
-        tips_amd.init()
-        reg_in = np.random.default_rng(2).random(n, dtype=np.float32)
-        reg_out = np.empty_like(reg_in)
-        _lib.call("tips_host_register", reg_in.ctypes.data, reg_in.nbytes)
-        _lib.call("tips_host_register", reg_out.ctypes.data, reg_out.nbytes)
-        for label, src, dst in (("pageable_numpy", pageable_in.ctypes.data, pageable_out.ctypes.data),
-                                ("pinned", pinned_in.data_ptr(), pinned_out.data_ptr()),
-                                ("registered_numpy", reg_in.ctypes.data, reg_out.ctypes.data)):
-            _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)  # warm (allocates staging)
-            ts = []
-            for _ in range(5):
-                t2 = time.perf_counter()
-                _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)
-                ts.append(time.perf_counter() - t2)
-            host_rates[label] = round(n * 4 / sorted(ts)[2] / GIB, 3)  # median of 5 calls
-            host_rates[label + "_calls_ms"] = [round(t * 1e3, 3) for t in ts]
-        host_ok = bool(np.array_equal(pageable_out, pageable_in)) and bool(np.array_equal(reg_out, reg_in))
-        _lib.call("tips_host_unregister", reg_in.ctypes.data)
-        _lib.call("tips_host_unregister", reg_out.ctypes.data)
-        del pinned_in, pinned_out, pageable_in, pageable_out, reg_in, reg_out
-
-    moved = 3 * n * 4
-    t_s = ms / 1e3
-    achieved = moved / t_s / 1e9
-    tr = pmc_traffic(DEFAULT_SUM_KERNEL)
-    line = {
-        "metric": METRIC, "value": round(moved / t_s / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
-        "warmup": warmup, "ms_per_step": round(ms, 6), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: fp32 U[-1,1), torch cuda generator seeds 1 and 2 (+ %d more seeded pairs), resident in HBM"
-                % (ROTATING_SETS - 1),
-        "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
-                   "bucket_bytes": n * 4, "elements": n, "rotating_sets": ROTATING_SETS,
-                   "timing": "HIP events over the timed launches; launch i sums triple i %% %d (HBM-only: no launch "
-                             "finds its operands in the 256 MiB Infinity Cache)" % ROTATING_SETS, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, XCD-contiguous order, buffer_load/store_dwordx4)",
-                   "parallelism": "single GPU"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": (tr["bytes"] if tr else None)},
-        "cpu_baseline": cpu,
-        "same_buffers_repeated": same,
-        "input_bucket_gib_s": round(n * 4 / t_s / GIB, 2),
-        "algorithmic_bytes_per_step": moved,
-        "pcie_inclusive_gib_s": round(n * 4 / t_host / GIB, 3) if t_host else None,
-        "pcie_inclusive_note": "pinned H2D of a and b + kernel + D2H of c, bucket bytes / wall time",
-        "host_allreduce_gib_s": host_rates,
-        "host_allreduce_note": "tips_allreduce(host in, host out) on one rank, 256 MiB: staged H2D + device + D2H, "
-                               "bucket bytes / median wall time of 5 calls (all 5 listed)" + ("" if host_ok else " (RESULT MISMATCH)"),
-        "check": "bit-exact vs torch a+b" if ok else "FAIL",
-        "wall_s_timed_region": round(wall, 4),
-    }
-    if tr:
-        line["roofline"]["traffic_source"] = tr["source"]
-    print(json.dumps(line), flush=True)
-    return 0 if ok else 1
-
-
-# ----------------------------------------------------------------------------- N > 1: allreduce
+# ----------------------------------------------------------------------------- workloads, probes
 
 def fused1000_sizes():
     """Config 4: 1000 fp32 gradients, sizes round(2**U(8,17)) from default_rng(20261015)."""
@@ -620,14 +544,14 @@ ENV_VARIANTS = [("nchannels_per_peer_4", {"NCCL_NCHANNELS_PER_PEER": "4"})]
 SMALL_BUCKET_KIB = (16, 256, 512, 1024, 2048, 4096, 8192)
 
 
-def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BUCKET_KIB):
+def small_bucket_latency(job, torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BUCKET_KIB):
     """Per-call time of small allreduces, 16 KiB - 8 MiB (config 1 is a 1 MiB bucket at p = 2), for
     the path the library ships (AUTO with its default one-shot threshold and graph-replay limit)
     and for each candidate beside it: direct eager, direct replayed as a HIP graph at any size,
     one-shot eager and one-shot replayed. The wall time of `calls` back-to-back calls on the same
     buffers (a quarter of them above 1 MiB), slowest rank; `best` names the fastest candidate and
-    `shipped_vs_best` the ratio. Sizes left when the probe has run TIPS_BENCH_PROBE_BUDGET_S (90 s)
-    are skipped, on every rank together."""
+    `shipped_vs_best` the ratio. Sizes left when the probe has run TIPS_BENCH_PROBE_BUDGET_S (90 s),
+    or the job's budget is spent, are skipped, on every rank together."""
     out = {"calls": calls, "calls_above_1MiB": max(5, calls // 4), "unit": "us per call, slowest rank"}
     keys = ("TIPS_GRAPHS", "TIPS_GRAPH_MAX_BYTES")
     saved = {k: os.environ.get(k) for k in keys}
@@ -651,7 +575,7 @@ def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BU
         for kib in kibs:
             # a time budget, decided together (the probe's calls are collectives): over sockets at
             # N = 8 the 2-8 MiB sizes take minutes (profiles/r03/m_rehearsal_n8.jsonl), over xGMI seconds
-            if max_over_ranks(dist, time.perf_counter() - t_start) > budget:
+            if max_over_ranks(dist, time.perf_counter() - t_start) > budget or job.left() < 10:
                 out["%d_KiB" % kib] = "skipped: the probe's %.0f s budget was spent (TIPS_BENCH_PROBE_BUDGET_S)" % budget
                 continue
             reps = calls if kib <= 1024 else max(5, calls // 4)
@@ -695,14 +619,16 @@ def small_bucket_latency(torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BU
     return out
 
 
-def overlap_probe(torch, dist, tips_amd, _lib, algo_code, steps=10):
+def overlap_probe(torch, dist, tips_amd, _lib, algo_code, job, steps=10):
     """A training step with DistributedOptimizer, its allreduces issued after backward vs during it
     (TIPS_OVERLAP_BACKWARD: post-accumulate hooks issue each <= 25 MiB gradient bucket as it
     completes, on a side stream). The model is 6 fp32 Linear(2048, 2048) layers, 25.2 M parameters
     (ResNet-50 has 25.6 M), on a 2048-row synthetic batch; wall time per step, slowest rank.
     `backward_only` is the same step without the optimizer (no allreduce): the floor overlap can
     approach. The reference's per-gradient async ops overlap backward the same way
-    (__init__.py:212-222)."""
+    (__init__.py:212-222). `replay_host_waits` per variant: how often an eager RCCL call found a
+    replayed plan pending and blocked the host until it had run (tips_replay_order_stats), and the
+    host time it cost per step."""
     saved = os.environ.get("TIPS_OVERLAP_BACKWARD")
     _lib.call("tips_set_algorithm", algo_code)
     out = {"model": "6 x Linear(2048, 2048) + ReLU, fp32, 25.2 M parameters, batch 2048", "steps": steps,
@@ -730,10 +656,14 @@ def overlap_probe(torch, dist, tips_amd, _lib, algo_code, steps=10):
             run(3)
             torch.cuda.synchronize()
             dist.barrier()
+            w0 = job.replay_waits()
             t0 = time.perf_counter()
             run(steps)
             torch.cuda.synchronize()
             out[name] = round(max_over_ranks(dist, time.perf_counter() - t0) / steps * 1e3, 3)
+            w1 = job.replay_waits()
+            out.setdefault("replay_host_waits", {})[name] = {
+                "per_step": round((w1[0] - w0[0]) / steps, 2), "ms_per_step": round((w1[1] - w0[1]) / steps / 1e6, 4)}
             if overlap:
                 out["buckets"] = len(opt._buckets.buckets) if opt._buckets is not None else 0
             del m, opt, layers
@@ -861,7 +791,756 @@ def start_watchdog(seconds, rank):
     return t
 
 
-def bench_allreduce(args):
+
+# ----------------------------------------------------------------------------- the job
+
+class Job(object):
+    """What every measurement of one run shares: torch, the gloo group the ranks time and agree
+    through, the library, this rank's stream, and the time budget of the optional legs."""
+
+    def __init__(self, args, torch, dist, tips_amd, _lib):
+        self.args, self.torch, self.dist, self.tips_amd, self._lib = args, torch, dist, tips_amd, _lib
+        self.L = _lib.lib()
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.stream = torch.cuda.current_stream()
+        self.sp = self.stream.cuda_stream
+        self.algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT,
+                           "rccl": _lib.ALGO_RCCL, "oneshot": _lib.ALGO_ONESHOT, "peer": _lib.ALGO_PEER,
+                           "tune": _lib.ALGO_TUNE}
+        self.inv = {v: k for k, v in self.algo_names.items()}
+        self.budget_s = float(os.environ.get("TIPS_BENCH_BUDGET_S", "240"))
+        self.skipped = []
+
+    def left(self):
+        """Seconds of the budget left, the same number on every rank (slowest rank's clock): a
+        collective, so every rank asks at the same points."""
+        return self.budget_s - max_over_ranks(self.dist, time.time() - _T0)
+
+    def afford(self, what, need_s):
+        """True when `need_s` seconds of the budget are left (decided together); else notes `what`."""
+        if self.left() >= need_s:
+            return True
+        self.skipped.append(what)
+        progress(self.rank, "budget: skipping %s" % what)
+        return False
+
+    def replay_waits(self):
+        import ctypes
+        w, ns = ctypes.c_int64(), ctypes.c_int64()
+        self._lib.call("tips_replay_order_stats", ctypes.byref(w), ctypes.byref(ns))
+        return w.value, ns.value
+
+
+# ----------------------------------------------------------------------------- N == 1: config 2's bucket sum
+
+def sum_record(args, cpu):
+    """Config 2, the N == 1 headline: tips_bucket_sum over 4 rotating 256 MiB triples."""
+    steps = args.steps if args.steps is not None else 200
+    warmup = args.warmup if args.warmup is not None else 20
+    n = (args.bucket_mib or 256) * (1 << 20) // 4
+
+    import torch
+    import tips_amd
+    from tips_amd import _lib
+    L = _lib.lib()
+    torch.cuda.set_device(0)
+    g = torch.Generator(device="cuda")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    # ROTATING_SETS (a, b, c) triples, 768 MiB each: step i sums triple i % ROTATING_SETS, so 2.25 GiB
+    # of other traffic separates two uses of a buffer and no launch finds its operands in the
+    # 256 MiB Infinity Cache: the timed rate is HBM's. Triple 0 is config 2's seeded pair (seeds 1, 2).
+    sets = []
+    for k in range(ROTATING_SETS):
+        x_, y_, z_ = (torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(3))
+        g.manual_seed(1 if k == 0 else 10 + 2 * k)
+        x_.uniform_(-1.0, 1.0, generator=g)
+        g.manual_seed(2 if k == 0 else 11 + 2 * k)
+        y_.uniform_(-1.0, 1.0, generator=g)
+        sets.append((x_, y_, z_))
+    a, b, c = sets[0]
+
+    def step(i=0):
+        x_, y_, z_ = sets[i % len(sets)]
+        rc = L.tips_bucket_sum(z_.data_ptr(), x_.data_ptr(), y_.data_ptr(), n, _lib.FLOAT32, sp)
+        if rc:
+            raise _lib.TipsError("tips_bucket_sum", rc, _lib.last_error())
+
+    def timed(k, same_buffers):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(k):
+            step(0 if same_buffers else i)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / k, time.perf_counter() - t0  # HIP events on the kernel's stream
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ms, wall = timed(steps, same_buffers=False)
+    ok = all(bool(torch.equal(z_, x_ + y_)) for x_, y_, z_ in sets)  # one IEEE add per element: bit-exact
+
+    same = None
+    if not args.no_extras:
+        # the same kernel re-reading ONE triple (the literal config-2 loop): part of each launch's
+        # operands is still in the Infinity Cache from the launch before, so this is not an HBM rate
+        step(0)
+        ms_same, _ = timed(steps, same_buffers=True)
+        same = {"us_per_launch": round(ms_same * 1e3, 2), "achieved_GBps": round(3 * n * 4 / (ms_same / 1e3) / 1e9, 1),
+                "note": "tips_bucket_sum on the same (a, b, c) every launch: the 256 MiB Infinity Cache serves part "
+                        "of the 768 MiB working set from the previous launch, so this exceeds the HBM-only rate above"}
+    del sets[1:]  # (the PCIe leg below uses triple 0)
+
+    t_host, host_rates, host_ok = None, {}, True
+    if not args.no_extras:  # (skipped under rocprofv3: its kernel stats then hold only the timed launches)
+        # PCIe-inclusive rate (the path starts and ends in host memory): pinned H2D a,b + sum + D2H c
+        ha, hb, hc = (torch.empty(n, dtype=torch.float32, pin_memory=True) for _ in range(3))
+        ha.copy_(a)
+        hb.copy_(b)
+        torch.cuda.synchronize()
+        reps = 3
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            a.copy_(ha, non_blocking=True)
+            b.copy_(hb, non_blocking=True)
+            step()
+            hc.copy_(c, non_blocking=True)
+        torch.cuda.synchronize()
+        t_host = (time.perf_counter() - t1) / reps
+        del ha, hb, hc
+
+        # host-memory leg of the drop-in path: tips_allreduce on host buffers (1 rank: H2D, device copy, D2H)
+        import numpy as np
+        pinned_in = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        pinned_out = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        pageable_in = np.random.default_rng(1).random(n, dtype=np.float32)
+        pageable_out = np.empty_like(pageable_in)
+        tips_amd.init()
+        reg_in = np.random.default_rng(2).random(n, dtype=np.float32)
+        reg_out = np.empty_like(reg_in)
+        _lib.call("tips_host_register", reg_in.ctypes.data, reg_in.nbytes)
+        _lib.call("tips_host_register", reg_out.ctypes.data, reg_out.nbytes)
+        for label, src, dst in (("pageable_numpy", pageable_in.ctypes.data, pageable_out.ctypes.data),
+                                ("pinned", pinned_in.data_ptr(), pinned_out.data_ptr()),
+                                ("registered_numpy", reg_in.ctypes.data, reg_out.ctypes.data)):
+            _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)  # warm (allocates staging)
+            ts = []
+            for _ in range(5):
+                t2 = time.perf_counter()
+                _lib.call("tips_allreduce", src, dst, n, _lib.FLOAT32, _lib.OP_SUM, None)
+                ts.append(time.perf_counter() - t2)
+            host_rates[label] = round(n * 4 / sorted(ts)[2] / GIB, 3)  # median of 5 calls
+            host_rates[label + "_calls_ms"] = [round(t * 1e3, 3) for t in ts]
+        host_ok = bool(np.array_equal(pageable_out, pageable_in)) and bool(np.array_equal(reg_out, reg_in))
+        _lib.call("tips_host_unregister", reg_in.ctypes.data)
+        _lib.call("tips_host_unregister", reg_out.ctypes.data)
+        del pinned_in, pinned_out, pageable_in, pageable_out, reg_in, reg_out
+    del sets, a, b, c
+    torch.cuda.empty_cache()
+
+    moved = 3 * n * 4
+    t_s = ms / 1e3
+    achieved = moved / t_s / 1e9
+    tr = pmc_traffic(DEFAULT_SUM_KERNEL)
+    line = {
+        "metric": METRIC, "value": round(moved / t_s / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(ms, 6), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: fp32 U[-1,1), torch cuda generator seeds 1 and 2 (+ %d more seeded pairs), resident in HBM"
+                % (ROTATING_SETS - 1),
+        "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
+                   "bucket_bytes": n * 4, "elements": n, "rotating_sets": ROTATING_SETS,
+                   "timing": "HIP events over the timed launches; launch i sums triple i %% %d (HBM-only: no launch "
+                             "finds its operands in the 256 MiB Infinity Cache)" % ROTATING_SETS, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, XCD-contiguous order, buffer_load/store_dwordx4)",
+                   "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": (tr["bytes"] if tr else None)},
+        "cpu_baseline": cpu,
+        "same_buffers_repeated": same,
+        "input_bucket_gib_s": round(n * 4 / t_s / GIB, 2),
+        "algorithmic_bytes_per_step": moved,
+        "pcie_inclusive_gib_s": round(n * 4 / t_host / GIB, 3) if t_host else None,
+        "pcie_inclusive_note": "pinned H2D of a and b + kernel + D2H of c, bucket bytes / wall time",
+        "host_allreduce_gib_s": host_rates,
+        "host_allreduce_note": "tips_allreduce(host in, host out) on one rank, 256 MiB: staged H2D + device + D2H, "
+                               "bucket bytes / median wall time of 5 calls (all 5 listed)" + ("" if host_ok else " (RESULT MISMATCH)"),
+        "check": "bit-exact vs torch a+b" if ok else "FAIL",
+        "wall_s_timed_region": round(wall, 4),
+    }
+    if tr:
+        line["roofline"]["traffic_source"] = tr["source"]
+    return line, ok
+
+
+# ----------------------------------------------------------------------------- one allreduce workload
+
+class Workload(object):
+    """One workload through the library at this job's N: config 3's bucket (tips_allreduce), configs
+    4 / 5 fused (tips_fused_allreduce over the gradient set's views), or config 4 as 1000 named
+    requests (negotiated1000). setup -> warm (schedules tuned) -> timed -> parity -> record; the
+    headline's comparison schedules reuse its buffers (compare)."""
+
+    def __init__(self, job, workload, steps, warmup):
+        self.job, self.workload, self.steps, self.warmup = job, workload, steps, warmup
+        torch, L, _lib, world, rank = job.torch, job.L, job._lib, job.world, job.rank
+        self.measure_pack = world == 1 and workload in SUB_WORKLOADS
+        # one rank: the library does no bucket work at all (the allreduce is the identity); pack and
+        # unpack the buckets anyway, as at N > 1, so this record measures the fusion's per-step HBM cost
+        self._saved_pack = os.environ.get("TIPS_FUSION_MEASURE_PACK")
+        if self.measure_pack:
+            os.environ["TIPS_FUSION_MEASURE_PACK"] = "1"
+        self.g = torch.Generator(device="cuda")
+        if workload == "bucket":
+            sizes = [(job.args.bucket_mib or 1024) * (1 << 20) // 4]
+            seed0, desc = 3000, "config 3: allreduce of one 1 GiB fp32 bucket per GPU over xGMI"
+        elif workload == "fused1000":
+            sizes, seed0 = fused1000_sizes(), 4000
+            desc = "config 4: 1000 fp32 grads (2^U(8,17) elems) fused into 64 MiB buckets, allreduced in place"
+        elif workload == "negotiated1000":
+            sizes, seed0 = fused1000_sizes(), 4000
+            desc = ("config 4 without fusion: 1000 fp32 grads, one named allreduce each through the negotiated "
+                    "path (tips_enqueue_allreduce/tips_wait), the reference's per-tensor structure")
+        else:
+            sizes, seed0 = resnet50_grad_sizes(), 5000
+            desc = "config 5: ResNet-50 gradient set (214 tensors, 25.6 M fp32) fused into 64 MiB buckets, in place"
+        self.sizes, self.seed0, self.desc = sizes, seed0, desc
+        # the schedule the (largest) reduced buffer gets: the bucket itself, or a <= 64 MiB fusion bucket
+        self.qbytes = sizes[0] * 4 if workload == "bucket" else max(sizes) * 4 if workload == "negotiated1000" else 64 << 20
+        self.algo = L.tips_resolve_algorithm(world, self.qbytes)
+        # every tensor at a 256-B aligned offset of one flat buffer, 256 B apart at least, as separate
+        # allocations of a caching allocator lie: the fusion path packs them (its layout depends only on
+        # the counts). (A flat gradient buffer allreduced as one tensor is the gradient_api "optimizer" leg.)
+        offs, total = [], 0
+        gap = 64 if workload in SUB_WORKLOADS else 0
+        for k in sizes:
+            offs.append(total)
+            total += (k + 63) // 64 * 64 + gap
+        if workload == "bucket":
+            total = sizes[0]  # the parity check compares the whole output buffer
+        self.offs, self.total, self.total_elems = offs, total, sum(sizes)
+        self.x = torch.empty(total, dtype=torch.float32, device="cuda")
+        self.fill(self.x, rank)
+        self.y = torch.empty_like(self.x) if workload == "bucket" else self.x
+        views = [self.x[o:o + k] for o, k in zip(offs, sizes)]
+        pp, keep1 = _lib.ptr_array([v.data_ptr() for v in views])
+        self.cp, self._keep2 = _lib.i64_array(sizes)
+        # The fused workloads cycle over ROTATING_SETS gradient sets (step i reduces set i % R): the
+        # 83-102 MB of one set would otherwise stay in the 256 MiB Infinity Cache from one step to the
+        # next, and a one-rank record (pack + unpack only) would not be an HBM rate.
+        self.rot = ROTATING_SETS if workload in SUB_WORKLOADS else 1
+        self.rot_sets = [(self.x, pp, keep1)]
+        for k in range(1, self.rot):
+            xk = torch.empty(total, dtype=torch.float32, device="cuda")
+            self.fill(xk, rank + 100 * k)
+            self.rot_sets.append((xk,) + _lib.ptr_array([xk[o:o + n_].data_ptr() for o, n_ in zip(offs, sizes)]))
+        self.ctr = 0
+        import ctypes
+        self.names = [("grad.%d" % i).encode() for i in range(len(sizes))]
+        self.view_ptrs = [v.data_ptr() for v in views]
+        self.host_t = {"enqueue": 0.0, "wait": 0.0}
+        self.per_call = False
+        self.name_arr = (ctypes.c_char_p * len(self.names))(*self.names)
+        self.h_arr = (ctypes.c_int64 * len(sizes))()
+        self.fallbacks = []
+        self.tuned = None
+
+    def fill(self, t, r):
+        self.g.manual_seed(self.seed0 + r)
+        t.uniform_(0.5, 1.5, generator=self.g)
+
+    def step(self):
+        job, L, _lib = self.job, self.job.L, self.job._lib
+        w = self.workload
+        if w == "bucket":
+            rc = L.tips_allreduce(self.x.data_ptr(), self.y.data_ptr(), self.sizes[0], _lib.FLOAT32, _lib.OP_SUM, job.sp)
+        elif w == "negotiated1000" and self.per_call:  # one ctypes call per tensor (Python-bound)
+            t0 = time.perf_counter()
+            hs = [L.tips_enqueue_allreduce(nm, p_, p_, k, _lib.FLOAT32, job.sp)
+                  for nm, p_, k in zip(self.names, self.view_ptrs, self.sizes)]
+            t1 = time.perf_counter()
+            rc = next((int(h) for h in hs if h < 0), 0)
+            for h in hs:
+                if h > 0:
+                    wr = L.tips_wait(h)
+                    rc = rc or (wr if wr < 0 else 0)
+            self.host_t["enqueue"] += t1 - t0
+            self.host_t["wait"] += time.perf_counter() - t1
+        elif w == "negotiated1000":  # the same 1000 named requests, one library call each way
+            t0 = time.perf_counter()
+            rc = L.tips_enqueue_allreduce_n(self.name_arr, self.rot_sets[0][1], self.rot_sets[0][1], self.cp,
+                                            len(self.sizes), _lib.FLOAT32, job.sp, self.h_arr)
+            t1 = time.perf_counter()
+            if rc == 0:
+                rc = L.tips_wait_n(self.h_arr, len(self.sizes))
+            self.host_t["enqueue"] += t1 - t0
+            self.host_t["wait"] += time.perf_counter() - t1
+        else:
+            rc = L.tips_fused_allreduce(self.rot_sets[self.ctr % self.rot][1], self.cp, len(self.sizes),
+                                        _lib.FLOAT32, job.sp)
+            self.ctr += 1
+        if rc:
+            raise _lib.TipsError("allreduce", rc, _lib.last_error())
+
+    def timed(self, k):
+        job = self.job
+        job.dist.barrier()
+        job.torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            self.step()
+        job.torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        job.dist.barrier()
+        return max_over_ranks(job.dist, dt)
+
+    def warm(self):
+        """The warm-up steps (the tuner measures the schedules on its first call of a size class). A
+        schedule that fails outright on this node (an error on every rank, not a hang) must not cost
+        the record: the next one is measured instead and the failure is reported."""
+        job, _lib = self.job, self.job._lib
+        while True:
+            try:
+                for _ in range(self.warmup):
+                    self.step()
+                job.torch.cuda.synchronize()
+                break
+            except _lib.TipsError as e:
+                nxt = {_lib.ALGO_DIRECT: _lib.ALGO_RING, _lib.ALGO_PEER: _lib.ALGO_DIRECT, _lib.ALGO_TUNE: _lib.ALGO_DIRECT,
+                       _lib.ALGO_ONESHOT: _lib.ALGO_RING, _lib.ALGO_RING: _lib.ALGO_RCCL}.get(self.algo)
+                if self.workload == "negotiated1000" or nxt is None:
+                    raise
+                self.fallbacks.append({"algorithm": job.inv.get(self.algo, str(self.algo)), "error": str(e)})
+                self.algo = nxt
+                _lib.call("tips_set_algorithm", self.algo)
+        if self.algo == _lib.ALGO_TUNE:  # the warm-up measured the schedules; report (and check) the one kept
+            import ctypes
+            ta, td, tl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            if job.L.tips_tuned_schedule(self.qbytes, ctypes.byref(ta), ctypes.byref(td), ctypes.byref(tl)) == 1:
+                self.tuned = {"algorithm": job.inv.get(ta.value, str(ta.value)), "pipeline_depth": td.value,
+                              "lanes": tl.value}
+                self.algo = ta.value
+
+    def parity(self, algo_now):
+        """One fresh call, then fold all ranks' seeded inputs on this device (rank order) and compare."""
+        torch, _lib, world = self.job.torch, self.job._lib, self.job.world
+        self.fill(self.x, self.job.rank)
+        self.ctr = 0  # (the fused workloads: reduce set 0, i.e. x)
+        self.step()
+        torch.cuda.synchronize()
+        tmp = torch.empty_like(self.x)
+        ref = None
+        for r in range(world):
+            self.fill(tmp, r)
+            ref = tmp.clone() if ref is None else ref + tmp
+        w = self.workload
+        got = torch.cat([self.y[o:o + k] for o, k in zip(self.offs, self.sizes)]) if w != "bucket" else self.y
+        exp = torch.cat([ref[o:o + k] for o, k in zip(self.offs, self.sizes)]) if w != "bucket" else ref
+        if algo_now in (_lib.ALGO_DIRECT, _lib.ALGO_PEER, _lib.ALGO_ONESHOT) or world == 1:
+            good = bool(torch.equal(got, exp))
+            msg = "bit-exact vs rank-order fold of all ranks' inputs" if good else "FAIL (not bit-exact)"
+        else:
+            rel = ((got.double() - exp.double()).abs() / exp.double()).max().item()
+            good = rel <= 1e-6
+            msg = ("max rel err %.2e vs rank-order fold (bound 1e-6)" % rel) if good else ("FAIL rel %.2e" % rel)
+        del ref, tmp, got, exp
+        return good, msg
+
+    def run(self):
+        """Warm, time `steps` steps (max over ranks), check parity on every rank: the record."""
+        job = self.job
+        self.warm()
+        progress(job.rank, "%s: warm-up done" % self.workload)
+        self.host_t.update(enqueue=0.0, wait=0.0)
+        w0 = job.replay_waits()
+        t = self.timed(self.steps)
+        w1 = job.replay_waits()
+        self.host_split = dict(self.host_t)
+        self.ms = t / self.steps * 1e3
+        progress(job.rank, "%s: %.3f ms per step" % (self.workload, self.ms))
+        ok, check = self.parity(self.algo)
+        self.ok = all_ranks_ok(job.dist, ok)
+        progress(job.rank, "%s parity: %s" % (self.workload, check))
+        return self.record(check, (w1[0] - w0[0], w1[1] - w0[1]))
+
+    def record(self, check, waits):
+        job, world, _lib = self.job, self.job.world, self.job._lib
+        ms = self.ms
+        algbw = self.total_elems * 4 / (ms / 1e3)  # bytes/s per rank
+        busbw = algbw * 2 * (world - 1) / world
+        links = 1 if self.algo == _lib.ALGO_RING else max(1, world - 1)
+        rec = {
+            "value": round(world * self.total_elems * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
+            "value_definition": "N x bytes per rank / time (bytes reduced by the whole job per second)",
+            "n_gpus": world, "steps": self.steps, "warmup": self.warmup, "ms_per_step": round(ms, 4),
+            "workload": self.desc, "tensors": len(self.sizes), "bytes_per_rank": self.total_elems * 4,
+            "algorithm": job.inv.get(self.algo, str(self.algo)) if world > 1 else "none (1 rank)",
+            "selection": ("TIPS_ALGO_TUNE: measured on the first call, kept: %s" % self.tuned) if self.tuned else job.args.algo,
+            "rotating_sets": self.rot,
+            "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % self.seed0,
+            "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
+            "roofline": {"bound": "xgmi", "achieved": round(busbw / 1e9, 1), "peak": XGMI_LINK_GBPS * links,
+                         "unit": "GB/s", "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None,
+                         "links_used": links, "frac_of_one_link": round(busbw / 1e9 / XGMI_LINK_GBPS, 4),
+                         "note": "multi-GPU: the ring/all-pairs transfer, not the sum kernel, bounds the step"},
+            "replay_host_waits": {"count": waits[0], "ms_total": round(waits[1] / 1e6, 3)},
+            "check": check if self.ok else "FAIL on some rank",
+        }
+        if self.fallbacks:
+            rec["failed_schedules"] = self.fallbacks
+        if world == 1:  # one rank: no link carries anything; the step is HBM work on this GPU
+            # bucket: the allreduce is a copy (read + write); fused: pack + unpack (2 reads + 2 writes)
+            moved = (2 if self.workload == "bucket" else 4) * self.total_elems * 4
+            rec["roofline"] = {"bound": "hbm", "achieved": round(moved / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                               "unit": "GB/s", "frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                               "traffic": None,
+                               "note": "one rank: the allreduce of a bucket is the identity; %s" % (
+                                   "in -> out copy (hipMemcpyAsync D2D)" if self.workload == "bucket" else
+                                   "algorithmic bytes = pack + unpack of every tensor (2 reads + 2 writes); step i "
+                                   "reduces gradient set i %% %d, so no step finds its gradients in the 256 MiB "
+                                   "Infinity Cache" % self.rot)}
+            del rec["busbw_GBps"]
+            if self.measure_pack:  # the dominant kernel (fusion pack / unpack) timed per launch; the step beside it
+                rec["fusion_one_rank"] = ("TIPS_FUSION_MEASURE_PACK=1: buckets packed and unpacked as at N > 1 (the "
+                                          "default one-rank path does no bucket work)")
+                rec["step_roofline"] = rec["roofline"]
+                rec["step_roofline"]["note"] = "whole eager step (launches, stream joins, table lookup)" + \
+                    rec["step_roofline"]["note"][len("one rank"):]
+                rec["roofline"], rec["graph_replayed_step"] = fusion_one_rank_kernels(
+                    job.torch, job.L, _lib, self.sizes, self.offs, self.rot_sets, self.cp, job.stream, moved)
+                rec["eager_vs_graph_replayed"] = round(ms * 1e3 / rec["graph_replayed_step"]["us_per_step"], 3)
+                tr = pmc_traffic("copy_segs_kernel", "*pmc_%s.json" % self.workload)  # this workload's PMC passes
+                if tr:
+                    rec["roofline"]["traffic"] = round(tr["bytes"])
+                    rec["roofline"]["traffic_source"] = tr["source"]
+        if self.workload == "negotiated1000":
+            rec["per_tensor_us"] = round(ms * 1e3 / len(self.sizes), 2)
+            rec["host_us_per_tensor"] = {k: round(v / self.steps / len(self.sizes) * 1e6, 2) for k, v in self.host_split.items()}
+            rec["api"] = "tips_enqueue_allreduce_n + tips_wait_n (1000 named requests, one call each way)"
+            self.per_call = True  # the same requests through one ctypes call per tensor, for comparison
+            for _ in range(2):
+                self.step()
+            self.host_t.update(enqueue=0.0, wait=0.0)
+            tpc = self.timed(self.steps)
+            rec["per_call_api_per_tensor_us"] = round(tpc / self.steps / len(self.sizes) * 1e6, 2)
+            rec["per_call_api_host_us_per_tensor"] = {k: round(v / self.steps / len(self.sizes) * 1e6, 2)
+                                                      for k, v in self.host_t.items()}
+            self.per_call = False
+        return rec
+
+    def reduce_kernel_roofline(self):
+        """The reduce kernel of this schedule, timed alone at its per-launch shape (HBM roofline)."""
+        job, torch, _lib, world = self.job, self.job.torch, self.job._lib, self.job.world
+        if not (world > 1 and self.workload == "bucket" and self.algo in (_lib.ALGO_RING, _lib.ALGO_DIRECT)):
+            return None
+        import ctypes
+        depth, sub = ctypes.c_int(), ctypes.c_int64()
+        _lib.call("tips_schedule_shape", self.sizes[0], world, _lib.FLOAT32, ctypes.byref(depth), ctypes.byref(sub))
+        m = sub.value
+        nsrc = world if self.algo == _lib.ALGO_DIRECT else 2
+        bufs = torch.empty((nsrc + 1) * m, dtype=torch.float32, device="cuda").uniform_(0.5, 1.5)
+        srcs = [bufs[j * m:(j + 1) * m] for j in range(nsrc)]
+        dst = bufs[nsrc * m:]
+        sp_arr, _keep3 = _lib.ptr_array([t.data_ptr() for t in srcs])
+
+        def kern():
+            if nsrc == 2:
+                _lib.call("tips_bucket_sum", dst.data_ptr(), srcs[0].data_ptr(), srcs[1].data_ptr(), m, _lib.FLOAT32, job.sp)
+            else:
+                _lib.call("tips_multi_sum", dst.data_ptr(), sp_arr, nsrc, m, _lib.FLOAT32, job.sp)
+
+        for _ in range(3):
+            kern()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(job.stream)
+        for _ in range(50):
+            kern()
+        e1.record(job.stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 50 * 1e3
+        kbytes = (nsrc + 1) * m * 4
+        roof = {"kernel": "multi_sum_buf_kernel" if nsrc > 2 else "sum2_buf_kernel", "sources": nsrc,
+                "elements_per_launch": m, "launches_per_step": depth.value * (world - 1 if nsrc == 2 else 1),
+                "bound": "hbm", "achieved": round(kbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(kbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": kbytes,
+                "note": "one launch of the schedule's sub-chunk shape, timed alone on re-read buffers "
+                        "(Infinity Cache assisted: in the schedule a freshly received slot may be on-die too)"}
+        if nsrc > 2:  # HBM bytes from the committed PMC passes over the fold (8 x 32 MiB, rotating sets)
+            try:
+                with open(os.path.join(REPO, "profiles", "r02", "pmc_multi_sum.json")) as f:
+                    k = next(iter(json.load(f)["kernels"].values()))
+                roof["traffic_over_algorithmic_pmc"] = round(k["traffic_over_algorithmic"], 5)
+                roof["traffic_source"] = "profiles/r02/pmc_multi_sum.json (8 x 32 MiB sources)"
+            except Exception:  # noqa: BLE001
+                pass
+        del bufs, srcs, dst
+        return roof
+
+    def close(self):
+        if self.measure_pack:
+            if self._saved_pack is None:
+                os.environ.pop("TIPS_FUSION_MEASURE_PACK", None)
+            else:
+                os.environ["TIPS_FUSION_MEASURE_PACK"] = self._saved_pack
+        del self.rot_sets, self.x, self.y
+        self.job.torch.cuda.synchronize()
+        self.job.torch.cuda.empty_cache()
+
+
+def host_legs(job, w, line):
+    """Config 5 host -> host (the gradients in host memory, as the reference's CPU op has them):
+    one tips_amd.allreduce per numpy gradient (the reference's per-op structure), and the same
+    gradients through allreduce_grads' N > 1 body (one fused host call)."""
+    import numpy as np
+    tips_amd, world, sizes = job.tips_amd, job.world, w.sizes
+    hg = [np.random.default_rng(w.seed0 + job.rank * 1000 + i).random(k, dtype=np.float32) for i, k in enumerate(sizes)]
+    for gr in hg:
+        tips_amd.allreduce(gr)
+    hsteps = max(3, w.steps // 4)
+    job.dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(hsteps):
+        for gr in hg:  # each result consumed at once, as the optimizer would (no 100 MB of live outputs)
+            tips_amd.allreduce(gr)
+    th = max_over_ranks(job.dist, time.perf_counter() - t0) / hsteps
+    outs = [tips_amd.allreduce(gr) for gr in hg]
+    h_ok = world > 1 or all(np.array_equal(o, gr) for o, gr in zip(outs, hg))
+    line["host_to_host_python"] = {
+        "ms_per_step": round(th * 1e3, 3), "algbw_gib_s": round(w.total_elems * 4 / th / GIB, 2),
+        "us_per_tensor": round(th * 1e6 / len(sizes), 2), "steps": hsteps,
+        "check": "identity at one rank" if world == 1 and h_ok else ("FAIL" if not h_ok else "not checked"),
+        "note": "214 numpy gradients, one tips_amd.allreduce each (host staged), the reference's per-op structure"}
+    # The same 214 numpy gradients through allreduce_grads' N > 1 body: one fused host call
+    # (tips_fused_allreduce_host_flat: host threads pack page-locked pieces, H2D -> allreduce -> D2H
+    # pipelined per piece, straight into a page-locked flat output).
+    for _ in range(2):
+        outs = tips_amd._reduce_grads(hg)
+    # each call timed on its own (max over ranks per call): the host side of the box is shared
+    # with other jobs, and one call in ten can take 2-3 x the others (profiles/r03/b_host_probe.txt);
+    # the median is the rate, the mean and the best are reported beside it
+    fsteps = max(hsteps, 15)
+    per = []
+    for _ in range(fsteps):
+        job.dist.barrier()
+        t0 = time.perf_counter()
+        outs = tips_amd._reduce_grads(hg)
+        per.append(max_over_ranks(job.dist, time.perf_counter() - t0))
+    tf = sorted(per)[len(per) // 2]
+    f_ok = all(np.array_equal(o, gr) for o, gr in zip(outs, hg)) if world == 1 else None
+    if world > 1:  # the fused host result against the fold of every rank's regenerated inputs
+        exp = None
+        for r in range(world):
+            xs = [np.random.default_rng(w.seed0 + r * 1000 + i).random(k, dtype=np.float32) for i, k in enumerate(sizes)]
+            exp = xs if exp is None else [e + x for e, x in zip(exp, xs)]
+        f_ok = all_ranks_ok(job.dist, all(np.array_equal(o, e) for o, e in zip(outs, exp)))
+    line["host_to_host_fused"] = {
+        "ms_per_step": round(tf * 1e3, 3), "algbw_gib_s": round(w.total_elems * 4 / tf / GIB, 2),
+        "statistic": "median of %d calls, each timed alone" % fsteps,
+        "ms_mean": round(sum(per) / len(per) * 1e3, 3), "ms_best": round(min(per) * 1e3, 3),
+        "best_gib_s": round(w.total_elems * 4 / min(per) / GIB, 2),
+        "steps": fsteps, "threads": int(os.environ.get("TIPS_HOST_THREADS", "8")),
+        "piece_bytes": int(os.environ.get("TIPS_HOST_FUSED_PIECE_BYTES", str(32 << 20))),  # (host_staging.cc's default)
+        "vs_per_tensor": round(th / tf, 2),
+        "check": ("identity at one rank, bit-exact" if world == 1 else "bit-exact vs rank-order fold of all ranks' inputs")
+        if f_ok else "FAIL",
+        "note": "the same 214 numpy gradients through allreduce_grads' N > 1 body (tips_fused_allreduce_host_flat): "
+                "one call, outputs views of a page-locked flat buffer, pageable inputs; at one rank the round trip "
+                "through HBM is kept"}
+    del hg, outs
+
+
+def op_host_leg(steps=20, warmup=3):
+    """Config 5 as the reference's TF op sees it, at one rank: tools/_bin/op_host (a plain-C host on
+    the product library alone) issues the 214 gradients as named HOST requests,
+    tips_enqueue_allreduce_shaped + tips_on_done, from four executor threads per step, as TF's
+    executor runs MPIAllreduce's ComputeAsync (ops.cc:86-118, coordinator.cc:223-241). A child
+    process (its own tips_init at one rank); median step of `steps`."""
+    import socket
+    exe = os.path.join(REPO, "tools", "_bin", "op_host")
+    if not os.path.exists(exe):
+        return {"error": "tools/_bin/op_host not built"}
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                                                              "MASTER_PORT", "TIPS_BOOTSTRAP_PORT",
+                                                              "TIPS_FUSION_MEASURE_PACK")}
+    env.update(OP_HOST_STEPS=str(steps), OP_HOST_WARMUP=str(warmup), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=120)
+        d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    except Exception as e:  # noqa: BLE001 - a leg never costs the line
+        return {"error": repr(e)}
+    d.pop("rank", None)
+    d["statistic"] = "median step of %d (each step: 214 enqueues from %d threads, then every callback)" % (
+        steps, d.get("threads", 4))
+    d["note"] = ("tools/op_host.c: 214 named host requests per step (pageable TF-style host tensors, outputs "
+                 "reused), tips_enqueue_allreduce_shaped + tips_on_done from executor threads; the negotiation "
+                 "fuses each cycle's host requests into one tips_fused_allreduce_host call")
+    return d
+
+# ----------------------------------------------------------------------------- comparisons (after the sub-records)
+
+def comparisons(job, w, line, last_words):
+    """The headline bucket on the other schedules, RCCL's own allreduce and the probes, each only
+    while the budget lasts (a skipped one is named in line["budget_skipped"]). A hang here is caught
+    by the watchdog, which then still prints the line; a crash by last_words."""
+    _lib, algo_names = job._lib, job.algo_names
+    compare, compare_check = {}, {}
+
+    def note_progress(what):
+        """What rank 0 prints if a fatal signal ends the process during `what`."""
+        progress(job.rank, what)
+        if last_words:
+            last_words(json.dumps(dict(line, compare_algbw_gib_s=compare, compare_check=compare_check,
+                                       compare_error="process ended by a signal during %s" % what)))
+
+    def _one_call_s():
+        job.torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        w.step()
+        job.torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    def run_variants(variants):
+        kc = max(3, w.steps // 4)
+        for label, name, env in variants:
+            if (label == name and algo_names[name] == w.algo) or (name == "peer" and w.workload != "bucket") or \
+                    (env and w.workload != "bucket"):
+                continue
+            # a variant costs about kc + 4 headline steps (slower schedules more): ask for 3x that
+            if not job.afford("comparison %s" % label, 15 + 3 * (kc + 4) * w.ms / 1e3):
+                continue
+            note_progress("comparison %r" % label)
+            saved = {k: os.environ.get(k) for k in env}
+            try:
+                os.environ.update(env)
+                _lib.call("tips_set_algorithm", algo_names[name])
+                for _ in range(2):
+                    w.step()
+                job.torch.cuda.synchronize()
+                # a variant far slower than the main line (the socket rehearsal saw 100x for the
+                # transfer lanes) is priced from one call, so it cannot eat the budget; every rank
+                # takes the same branch (the slowest rank's time decides)
+                t1 = max_over_ranks(job.dist, _one_call_s())
+                if t1 > 20 * max(w.ms, 1e-3) / 1e3:
+                    compare[label] = round(w.total_elems * 4 / t1 / GIB, 2)
+                    compare_check[label] = "priced from one call (%.1f ms, > 20 x the main line); no parity run" % (t1 * 1e3)
+                    continue
+                tc = w.timed(kc)
+                compare[label] = round(w.total_elems * 4 / (tc / kc) / GIB, 2)
+                good, msg = w.parity(algo_names[name])
+                compare_check[label] = msg if all_ranks_ok(job.dist, good) else "FAIL on some rank (%s here)" % msg
+            except Exception as e:  # noqa: BLE001 - a comparison point never costs the main line
+                compare[label] = None
+                compare_check[label] = "error: %s" % (e,)
+            finally:
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+        _lib.call("tips_set_algorithm", w.algo if w.fallbacks else algo_names[job.args.algo])
+
+    # (oneshot targets small buckets only.) The _k entries re-run a schedule at another sub-chunk
+    # pipeline depth (read per call). Order: RCCL's allreduce and the other schedules, the link probe,
+    # the probes; then the opt-in legs (IPC peer schedules, transfer lanes).
+    run_variants([("rccl", "rccl", {}), ("ring", "ring", {}), ("direct", "direct", {}),
+                  ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
+                  ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
+                  ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
+                  # the same plan captured once and replayed as a HIP graph (TIPS_GRAPHS)
+                  ("direct_graphs", "direct", {"TIPS_GRAPHS": "1", "TIPS_GRAPH_MAX_BYTES": str(1 << 40)})])
+    if job.world > 1 and not os.environ.get("TIPS_NO_RCCL") and job.afford("the xGMI link probe", 30):
+        note_progress("the xGMI link probe")
+        try:
+            line["xgmi_probe"] = link_probe(job.dist, job.rank, job.world)
+        except Exception as e:  # noqa: BLE001
+            line["xgmi_probe"] = {"error": str(e)}
+    if job.world > 1 and job.afford("the backward-overlap probe", 45):
+        note_progress("the backward-overlap probe")
+        try:
+            line["backward_overlap"] = overlap_probe(job.torch, job.dist, job.tips_amd, _lib, algo_names[job.args.algo], job)
+        except Exception as e:  # noqa: BLE001
+            line["backward_overlap"] = {"error": str(e)}
+    if job.world > 1 and job.afford("the small-bucket latency probe", 40):
+        note_progress("the small-bucket latency probe")
+        try:
+            line["small_bucket_latency"] = small_bucket_latency(job, job.torch, job.dist, _lib, job.L, job.rank, job.sp)
+        except Exception as e:  # noqa: BLE001
+            line["small_bucket_latency"] = {"error": str(e)}
+    # Opt-in (TIPS_BENCH_PEER=1): the IPC peer schedules have not crossed real GPUs yet, so the
+    # driver's scaling runs do not start them (a fault there would cost the whole record).
+    if os.environ.get("TIPS_BENCH_PEER") == "1":
+        run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"})])
+    elif job.world > 1:
+        compare_check["peer"] = "opt-in: TIPS_BENCH_PEER=1 (not yet run across real GPUs)"
+    # Opt-in (TIPS_BENCH_LANES=1): transfer lanes split communicators that live to the end of
+    # the job; on the socket rehearsal they ran 10x slower and slowed every later call.
+    if os.environ.get("TIPS_BENCH_LANES") == "1":
+        run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
+                      ("ring_l2", "ring", {"TIPS_LANES": "2"}),
+                      ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
+                                                  "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
+    elif job.world > 1:
+        compare_check["lanes"] = "opt-in: TIPS_BENCH_LANES=1"
+    line["compare_check"] = compare_check
+    line["compare_algbw_gib_s"] = compare
+    # Opt-in (TIPS_BENCH_ENV_VARIANTS=1): child jobs with other RCCL settings (one of them delivered
+    # wrong bytes in a probe, profiles/r02/rccl_nchannels_probe.txt)
+    if job.world > 1 and not job.args.no_env_variants and not os.environ.get("TIPS_NO_RCCL") \
+            and os.environ.get("TIPS_BENCH_ENV_VARIANTS") == "1":
+        note_progress("the RCCL-setting child jobs")
+        line["env_variants"] = env_variant_jobs(job.args, job.dist, job.rank, job.world)
+    ring_algbw = w.total_elems * 4 / (w.ms / 1e3) if w.algo == _lib.ALGO_RING else (compare.get("ring") or 0) * GIB
+    if job.world > 1 and ring_algbw:  # the north star's ring target: >= 70 % of one xGMI link
+        rb = ring_algbw * 2 * (job.world - 1) / job.world
+        line["ring_xgmi"] = {"busbw_GBps": round(rb / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS,
+                             "frac_of_one_link": round(rb / 1e9 / XGMI_LINK_GBPS, 4), "target_frac": 0.70}
+
+
+# ----------------------------------------------------------------------------- the run
+
+def sub_records(job, line, steps):
+    """The other configs at this N, each a record of its own in line["configs"]."""
+    subs = line.setdefault("configs", {})
+    order = ([("config3_bucket", "bucket")] if job.world == 1 else []) + \
+        [("config4_fused1000", "fused1000"), ("config5_resnet50", "resnet50")]
+    for key, wl in order:
+        # a record costs its tuning + warm-up + steps: at N = 8 over the socket rehearsal ~20 s each
+        if not job.afford(key, 30):
+            subs[key] = {"skipped": "time budget (TIPS_BENCH_BUDGET_S)"}
+            continue
+        progress(job.rank, "sub-record %s" % key)
+        w = Workload(job, wl, steps, 5 if wl != "bucket" else 3)
+        try:
+            rec = w.run()
+            if wl in SUB_WORKLOADS and job.afford("%s gradient_api legs" % key, 25):
+                rec["gradient_api"] = gradient_api_legs(job.torch, job.dist, job.tips_amd, job.world, w.sizes, w.offs,
+                                                        w.rot_sets, min(steps, 10), w.ms)
+            if wl == "resnet50" and job.afford("config5 host legs", 40):
+                host_legs(job, w, rec)
+                if job.world == 1:
+                    rec["op_host_named"] = op_host_leg()
+                    fused = rec.get("host_to_host_fused", {}).get("algbw_gib_s")
+                    if fused and rec["op_host_named"].get("algbw_gib_s"):
+                        rec["op_host_named"]["vs_host_to_host_fused"] = round(
+                            rec["op_host_named"]["algbw_gib_s"] / fused, 3)
+            subs[key] = rec
+            line["sub_records_ok"] = line.get("sub_records_ok", True) and w.ok
+        except Exception as e:  # noqa: BLE001 - a sub-record never costs the headline
+            subs[key] = {"error": "%s: %s" % (type(e).__name__, e)}
+            line["sub_records_ok"] = False
+        finally:
+            w.close()
+    return subs
+
+
+def bench_job(args):
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
@@ -874,483 +1553,82 @@ def bench_allreduce(args):
         os.environ["NCCL_HOSTID"] = "tips-bench-rank-%d" % rank
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     wd = start_watchdog(int(os.environ.get("TIPS_BENCH_WATCHDOG", "420")), rank)
+    workload = args.workload if args.workload != "auto" else ("sum" if world == 1 else "bucket")
+    headline_sum = workload == "sum"
+    # CPU baselines first, on rank 0, before this process touches the GPU (they start child processes)
     topo = gpu_topology() if rank == 0 and world > 1 else None
-    cpu_ring = None
-    if rank == 0 and world > 1 and not args.no_cpu_baseline and args.workload in ("auto", "bucket"):
-        cpu_ring = cpu_ring_baseline(world)  # (child processes: before this process touches the GPU)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        if headline_sum:
+            cpu = cpu_baseline((args.bucket_mib or 256) * (1 << 20) // 4)
+        elif workload == "bucket":
+            cpu = cpu_ring_baseline(world) if world > 1 else None
+    sum_ok = True
+    if headline_sum:
+        line, sum_ok = sum_record(args, cpu)
+        progress(rank, "config 2: %.2f GiB/s (%.4f of HBM)" % (line["value"], line["roofline"]["frac"]))
+        if args.no_extras or args.no_sub:
+            print(json.dumps(line), flush=True)
+            wd.cancel()
+            return 0 if sum_ok else 1
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))  # (several ranks per GPU only under TIPS_NO_RCCL)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import tips_amd
     from tips_amd import _lib
     tips_amd.init()  # unique id through the gloo group, one RCCL communicator per GPU
     progress(rank, "initialised: %d ranks" % world)
-    L = _lib.lib()
-    algo_names = {"auto": _lib.ALGO_AUTO, "ring": _lib.ALGO_RING, "direct": _lib.ALGO_DIRECT, "rccl": _lib.ALGO_RCCL,
-                  "oneshot": _lib.ALGO_ONESHOT, "peer": _lib.ALGO_PEER, "tune": _lib.ALGO_TUNE}
-    inv = {v: k for k, v in algo_names.items()}
-    _lib.call("tips_set_algorithm", algo_names[args.algo])
-
-    workload = args.workload if args.workload != "auto" else "bucket"
-    measure_pack = world == 1 and workload in ("fused1000", "resnet50")
-    if measure_pack:
-        # one rank: the library does no bucket work at all (the allreduce is the identity); pack and
-        # unpack the buckets anyway, as at N > 1, so this line measures the fusion's per-step HBM cost
-        os.environ["TIPS_FUSION_MEASURE_PACK"] = "1"
-    steps = args.steps if args.steps is not None else 20
-    warmup = args.warmup if args.warmup is not None else 5
-    g = torch.Generator(device="cuda")
-    stream = torch.cuda.current_stream()
-    sp = stream.cuda_stream
-
-    if workload == "bucket":
-        sizes = [(args.bucket_mib or 1024) * (1 << 20) // 4]
-        seed0, desc = 3000, "config 3: allreduce of one 1 GiB fp32 bucket per GPU over xGMI"
-    elif workload == "fused1000":
-        sizes, seed0 = fused1000_sizes(), 4000
-        desc = "config 4: 1000 fp32 grads (2^U(8,17) elems) fused into 64 MiB buckets, allreduced in place"
-    elif workload == "negotiated1000":
-        sizes, seed0 = fused1000_sizes(), 4000
-        desc = ("config 4 without fusion: 1000 fp32 grads, one named allreduce each through the negotiated "
-                "path (tips_enqueue_allreduce/tips_wait), the reference's per-tensor structure")
-    else:
-        sizes, seed0 = resnet50_grad_sizes(), 5000
-        desc = "config 5: ResNet-50 gradient set (214 tensors, 25.6 M fp32) fused into 64 MiB buckets, in place"
-    # the schedule the (largest) reduced buffer gets: the bucket itself, or a <= 64 MiB fusion bucket
-    algo = L.tips_resolve_algorithm(world, sizes[0] * 4 if workload == "bucket" else
-                                    max(sizes) * 4 if workload == "negotiated1000" else 64 << 20)
-    # every tensor at a 256-B aligned offset of one flat buffer, 256 B apart at least, as separate
-    # allocations of a caching allocator lie: the fusion path packs them (its layout depends only on
-    # the counts). (A flat gradient buffer allreduced as one tensor is the gradient_api
-    # "optimizer" leg.)
-    offs, total = [], 0
-    gap = 64 if workload in ("fused1000", "resnet50") else 0  # (the bucket / named workloads: no gap)
-    for k in sizes:
-        offs.append(total)
-        total += (k + 63) // 64 * 64 + gap
-    if workload == "bucket":
-        total = sizes[0]  # the parity check compares the whole output buffer
-    total_elems = sum(sizes)
-
-    def fill(t, r):
-        g.manual_seed(seed0 + r)
-        t.uniform_(0.5, 1.5, generator=g)
-
-    x = torch.empty(total, dtype=torch.float32, device="cuda")
-    fill(x, rank)
-    y = torch.empty_like(x) if workload == "bucket" else x
-    views = [x[o:o + k] for o, k in zip(offs, sizes)]
-    pp, _keep1 = _lib.ptr_array([v.data_ptr() for v in views])
-    cp, _keep2 = _lib.i64_array(sizes)
-    # The fused workloads cycle over ROTATING_SETS gradient sets (step i reduces set i % R): the
-    # 83-102 MB of one set would otherwise stay in the 256 MiB Infinity Cache from one step to the
-    # next, and a one-rank line (pack + unpack only) would not be an HBM rate.
-    rot = ROTATING_SETS if workload in ("fused1000", "resnet50") else 1
-    rot_sets = [(x, pp, _keep1)]
-    for k in range(1, rot):
-        xk = torch.empty(total, dtype=torch.float32, device="cuda")
-        fill(xk, rank + 100 * k)
-        rot_sets.append((xk,) + _lib.ptr_array([xk[o:o + n_].data_ptr() for o, n_ in zip(offs, sizes)]))
-    ctr = [0]
-
-    names = [("grad.%d" % i).encode() for i in range(len(sizes))]
-    view_ptrs = [v.data_ptr() for v in views]
-    host_t = {"enqueue": 0.0, "wait": 0.0}
-    per_call = [False]
-    import ctypes
-    name_arr = (ctypes.c_char_p * len(names))(*names)
-    vp_arr = pp
-    h_arr = (ctypes.c_int64 * len(sizes))()
-
-    def step():
-        if workload == "bucket":
-            rc = L.tips_allreduce(x.data_ptr(), y.data_ptr(), sizes[0], _lib.FLOAT32, _lib.OP_SUM, sp)
-        elif workload == "negotiated1000" and per_call[0]:  # one ctypes call per tensor (Python-bound)
-            t0 = time.perf_counter()
-            hs = [L.tips_enqueue_allreduce(nm, p_, p_, k, _lib.FLOAT32, sp) for nm, p_, k in zip(names, view_ptrs, sizes)]
-            t1 = time.perf_counter()
-            rc = next((int(h) for h in hs if h < 0), 0)
-            for h in hs:
-                if h > 0:
-                    w = L.tips_wait(h)
-                    rc = rc or (w if w < 0 else 0)
-            host_t["enqueue"] += t1 - t0
-            host_t["wait"] += time.perf_counter() - t1
-        elif workload == "negotiated1000":  # the same 1000 named requests, one library call each way
-            t0 = time.perf_counter()
-            rc = L.tips_enqueue_allreduce_n(name_arr, vp_arr, vp_arr, cp, len(sizes), _lib.FLOAT32, sp, h_arr)
-            t1 = time.perf_counter()
-            if rc == 0:
-                rc = L.tips_wait_n(h_arr, len(sizes))
-            host_t["enqueue"] += t1 - t0
-            host_t["wait"] += time.perf_counter() - t1
-        else:
-            rc = L.tips_fused_allreduce(rot_sets[ctr[0] % rot][1], cp, len(sizes), _lib.FLOAT32, sp)
-            ctr[0] += 1
-        if rc:
-            raise _lib.TipsError("allreduce", rc, _lib.last_error())
-
-    def timed(k):
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(k):
-            step()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        dist.barrier()
-        return max_over_ranks(dist, dt)
-
-    # A schedule that fails outright on this node (an error on every rank, not a hang) must not
-    # cost the whole line: the next one is measured instead and the failure is reported.
-    fallbacks = []
-    while True:
-        try:
-            for _ in range(warmup):
-                step()
-            torch.cuda.synchronize()
-            break
-        except _lib.TipsError as e:
-            nxt = {_lib.ALGO_DIRECT: _lib.ALGO_RING, _lib.ALGO_PEER: _lib.ALGO_DIRECT, _lib.ALGO_TUNE: _lib.ALGO_DIRECT,
-                   _lib.ALGO_ONESHOT: _lib.ALGO_RING, _lib.ALGO_RING: _lib.ALGO_RCCL}.get(algo)
-            if workload == "negotiated1000" or nxt is None:
-                raise
-            fallbacks.append({"algorithm": inv.get(algo, str(algo)), "error": str(e)})
-            algo = nxt
-            _lib.call("tips_set_algorithm", algo)
-    progress(rank, "warm-up done (schedule measured when tuning)")
-    tuned = None
-    if algo == _lib.ALGO_TUNE:  # the warm-up measured the schedules; report (and check) the one kept
-        import ctypes
-        ta, td, tl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        qbytes = sizes[0] * 4 if workload == "bucket" else max(sizes) * 4 if workload == "negotiated1000" else 64 << 20
-        if L.tips_tuned_schedule(qbytes, ctypes.byref(ta), ctypes.byref(td), ctypes.byref(tl)) == 1:
-            tuned = {"algorithm": inv.get(ta.value, str(ta.value)), "pipeline_depth": td.value, "lanes": tl.value}
-            algo = ta.value
-    host_t.update(enqueue=0.0, wait=0.0)
-    t = timed(steps)
-    host_split = dict(host_t)
-    ms = t / steps * 1e3
-
-    # parity: one fresh call, then fold all ranks' seeded inputs on this device (rank order) and compare
-    def parity(algo_now):
-        fill(x, rank)
-        ctr[0] = 0  # (the fused workloads: reduce set 0, i.e. x)
-        step()
-        torch.cuda.synchronize()
-        tmp = torch.empty_like(x)
-        ref = None
-        for r in range(world):
-            fill(tmp, r)
-            ref = tmp.clone() if ref is None else ref + tmp
-        got = torch.cat([y[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else y
-        exp = torch.cat([ref[o:o + k] for o, k in zip(offs, sizes)]) if workload != "bucket" else ref
-        if algo_now in (_lib.ALGO_DIRECT, _lib.ALGO_PEER) or world == 1:
-            good = bool(torch.equal(got, exp))
-            msg = "bit-exact vs rank-order fold of all ranks' inputs" if good else "FAIL (not bit-exact)"
-        else:
-            rel = ((got.double() - exp.double()).abs() / exp.double()).max().item()
-            good = rel <= 1e-6
-            msg = ("max rel err %.2e vs rank-order fold (bound 1e-6)" % rel) if good else ("FAIL rel %.2e" % rel)
-        del ref, tmp, got, exp
-        return good, msg
-
-    progress(rank, "timed: %.3f ms per step" % ms)
-    ok, check = parity(algo)
-    all_ok = all_ranks_ok(dist, ok)
-    progress(rank, "parity: %s" % check)
-
-    # the reduce kernel of this schedule, timed alone at its per-launch shape (HBM roofline)
-    kernel_roof = None
-    if world > 1 and workload == "bucket" and algo in (_lib.ALGO_RING, _lib.ALGO_DIRECT):
-        import ctypes
-        depth, sub = ctypes.c_int(), ctypes.c_int64()
-        _lib.call("tips_schedule_shape", sizes[0], world, _lib.FLOAT32, ctypes.byref(depth), ctypes.byref(sub))
-        m = sub.value
-        nsrc = world if algo == _lib.ALGO_DIRECT else 2
-        bufs = torch.empty((nsrc + 1) * m, dtype=torch.float32, device="cuda").uniform_(0.5, 1.5)
-        srcs = [bufs[j * m:(j + 1) * m] for j in range(nsrc)]
-        dst = bufs[nsrc * m:]
-        sp_arr, _keep3 = _lib.ptr_array([t.data_ptr() for t in srcs])
-
-        def kern():
-            if nsrc == 2:
-                _lib.call("tips_bucket_sum", dst.data_ptr(), srcs[0].data_ptr(), srcs[1].data_ptr(), m, _lib.FLOAT32, sp)
-            else:
-                _lib.call("tips_multi_sum", dst.data_ptr(), sp_arr, nsrc, m, _lib.FLOAT32, sp)
-
-        for _ in range(3):
-            kern()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(50):
-            kern()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / 50 * 1e3
-        kbytes = (nsrc + 1) * m * 4
-        kernel_roof = {"kernel": "multi_sum_buf_kernel" if nsrc > 2 else "sum2_buf_kernel", "sources": nsrc,
-                       "elements_per_launch": m, "launches_per_step": depth.value * (world - 1 if nsrc == 2 else 1),
-                       "bound": "hbm", "achieved": round(kbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS,
-                       "unit": "GB/s", "frac": round(kbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
-                       "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": kbytes,
-                       "note": "one launch of the schedule's sub-chunk shape, timed alone on re-read buffers "
-                               "(Infinity Cache assisted: in the schedule a freshly received slot may be on-die too)"}
-        if nsrc > 2:  # HBM bytes from the committed PMC passes over the fold (8 x 32 MiB, rotating sets)
-            try:
-                with open(os.path.join(REPO, "profiles", "r02", "pmc_multi_sum.json")) as f:
-                    k = next(iter(json.load(f)["kernels"].values()))
-                kernel_roof["traffic_over_algorithmic_pmc"] = round(k["traffic_over_algorithmic"], 5)
-                kernel_roof["traffic_source"] = "profiles/r02/pmc_multi_sum.json (8 x 32 MiB sources)"
-            except Exception:  # noqa: BLE001
-                pass
-        del bufs, srcs, dst
-
-    algbw = total_elems * 4 / (ms / 1e3)  # bytes/s per rank
-    busbw = algbw * 2 * (world - 1) / world
-    links = 1 if algo == _lib.ALGO_RING else max(1, world - 1)
-    line = {
-        "metric": METRIC, "value": round(world * total_elems * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s",
-        "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: fp32 U[0.5,1.5), torch cuda generator seed %d+rank, resident in HBM" % seed0,
-        "config": {"workload": desc, "tensors": len(sizes), "bytes_per_rank": total_elems * 4,
-                   "algorithm": inv.get(algo, str(algo)) if world > 1 else "none (1 rank)",
-                   "selection": ("TIPS_ALGO_TUNE: measured on the first call, kept: %s" % tuned) if tuned else args.algo,
-                   "rotating_sets": rot,
-                   "fusion_one_rank": ("TIPS_FUSION_MEASURE_PACK=1: buckets packed and unpacked as at N > 1 (the "
-                                       "default one-rank path does no bucket work)") if measure_pack else None,
-                   "parallelism": "dp%d (one process per GPU, %s)" % (
-                       world, "our kernels through IPC-mapped peer memory over xGMI" if algo == _lib.ALGO_PEER
-                       else "ncclAllReduce" if algo == _lib.ALGO_RCCL else "RCCL p2p over xGMI")
-                   if world > 1 else "single GPU: no link carries anything (the allreduce of one rank is the identity)"},
-        "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
-        "xgmi": {"busbw_GBps": round(busbw / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS, "links_used": links,
-                 "frac_of_links_used": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4),
-                 "frac_of_one_link": round(busbw / 1e9 / XGMI_LINK_GBPS, 4)},
-        "roofline": {"bound": "xgmi", "achieved": round(busbw / 1e9, 1), "peak": XGMI_LINK_GBPS * links,
-                     "unit": "GB/s", "frac": round(busbw / 1e9 / (XGMI_LINK_GBPS * links), 4), "traffic": None,
-                     "note": "multi-GPU: the ring/all-pairs transfer, not the sum kernel, bounds the step"},
-        "cpu_baseline": None,
-        "reduce_kernel_roofline": kernel_roof,
-        "check": check if all_ok else "FAIL on some rank",
-    }
-    if world == 1:  # one rank: no link carries anything; the step is HBM work on this GPU
-        # bucket: the allreduce is a copy (read + write); fused: pack + unpack (2 reads + 2 writes)
-        moved = (2 if workload == "bucket" else 4) * total_elems * 4
-        line["roofline"] = {"bound": "hbm", "achieved": round(moved / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
-                            "unit": "GB/s", "frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                            "note": "one rank: the allreduce of a bucket is the identity; %s" % (
-                                "in -> out copy" if workload == "bucket" else
-                                "algorithmic bytes = pack + unpack of every tensor (2 reads + 2 writes); step i "
-                                "reduces gradient set i %% %d, so no step finds its gradients in the 256 MiB "
-                                "Infinity Cache" % rot)}
-        del line["xgmi"]
-        if measure_pack:  # the dominant kernel (fusion pack / unpack) timed per launch; the step's rate beside it
-            line["step_roofline"] = line["roofline"]
-            line["step_roofline"]["note"] = "whole step (host-bound: launches and stream joins)" + \
-                line["step_roofline"]["note"][len("one rank"):]
-            line["roofline"], line["graph_replayed_step"] = fusion_one_rank_kernels(
-                torch, L, _lib, sizes, offs, rot_sets, cp, stream, moved)
-            tr = pmc_traffic("copy_segs_kernel", "*pmc_%s.json" % workload)  # this workload's PMC passes
-            if tr:
-                line["roofline"]["traffic"] = round(tr["bytes"])
-                line["roofline"]["traffic_source"] = tr["source"]
-    if workload in ("fused1000", "resnet50"):
-        line["gradient_api"] = gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps, ms)
-    if topo:
-        line["gpu_topology"] = topo
-    if cpu_ring:  # N > 1: the reference's MPI_Allreduce at the same rank count on host cores
-        line["cpu_baseline"] = cpu_ring
-    if fallbacks:
-        line["failed_schedules"] = fallbacks
-    if workload == "negotiated1000":
-        line["per_tensor_us"] = round(ms * 1e3 / len(sizes), 2)
-        line["host_us_per_tensor"] = {k: round(v / steps / len(sizes) * 1e6, 2) for k, v in host_split.items()}
-        line["api"] = "tips_enqueue_allreduce_n + tips_wait_n (1000 named requests, one call each way)"
-        per_call[0] = True  # the same requests through one ctypes call per tensor, for comparison
-        for _ in range(2):
-            step()
-        host_t.update(enqueue=0.0, wait=0.0)
-        tpc = timed(steps)
-        line["per_call_api_per_tensor_us"] = round(tpc / steps / len(sizes) * 1e6, 2)
-        line["per_call_api_host_us_per_tensor"] = {k: round(v / steps / len(sizes) * 1e6, 2) for k, v in host_t.items()}
-        per_call[0] = False
-    if workload == "resnet50":
-        # Config 5 host -> host through the Python surface, as the reference's op sees it: every
-        # gradient a host (numpy) array, one tips_amd.allreduce per tensor (__init__.py:212-222),
-        # each staged H2D -> device allreduce -> D2H. Bytes reduced per second of the whole step.
-        import numpy as np
-        hg = [np.random.default_rng(seed0 + rank * 1000 + i).random(k, dtype=np.float32) for i, k in enumerate(sizes)]
-        for gr in hg:
-            tips_amd.allreduce(gr)
-        hsteps = max(3, steps // 4)
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(hsteps):
-            for gr in hg:  # each result consumed at once, as the optimizer would (no 100 MB of live outputs)
-                tips_amd.allreduce(gr)
-        th = max_over_ranks(dist, time.perf_counter() - t0) / hsteps
-        outs = [tips_amd.allreduce(gr) for gr in hg]
-        h_ok = world > 1 or all(np.array_equal(o, gr) for o, gr in zip(outs, hg))
-        line["host_to_host_python"] = {
-            "ms_per_step": round(th * 1e3, 3), "algbw_gib_s": round(total_elems * 4 / th / GIB, 2),
-            "us_per_tensor": round(th * 1e6 / len(sizes), 2), "steps": hsteps,
-            "check": "identity at one rank" if world == 1 and h_ok else ("FAIL" if not h_ok else "not checked"),
-            "note": "214 numpy gradients, one tips_amd.allreduce each (host staged), the reference's per-op structure"}
-        # The same 214 numpy gradients through allreduce_grads' N > 1 body: one fused host call
-        # (tips_fused_allreduce_host: host threads pack page-locked pieces, H2D -> allreduce -> D2H
-        # pipelined per piece, unpack into new numpy arrays).
-        for _ in range(2):
-            outs = tips_amd._reduce_grads(hg)
-        # each call timed on its own (max over ranks per call): the host side of the box is shared
-        # with other jobs, and one call in ten can take 2-3 x the others (profiles/r03/b_host_probe.txt);
-        # the median is the rate, the mean and the best are reported beside it
-        fsteps = max(hsteps, 15)
-        per = []
-        for _ in range(fsteps):
-            dist.barrier()
-            t0 = time.perf_counter()
-            outs = tips_amd._reduce_grads(hg)
-            per.append(max_over_ranks(dist, time.perf_counter() - t0))
-        tf = sorted(per)[len(per) // 2]
-        f_ok = world > 1 or all(np.array_equal(o, gr) for o, gr in zip(outs, hg))
-        line["host_to_host_fused"] = {
-            "ms_per_step": round(tf * 1e3, 3), "algbw_gib_s": round(total_elems * 4 / tf / GIB, 2),
-            "statistic": "median of %d calls, each timed alone" % fsteps,
-            "ms_mean": round(sum(per) / len(per) * 1e3, 3), "ms_best": round(min(per) * 1e3, 3),
-            "best_gib_s": round(total_elems * 4 / min(per) / GIB, 2),
-            "steps": fsteps, "threads": int(os.environ.get("TIPS_HOST_THREADS", "8")),
-            "piece_bytes": int(os.environ.get("TIPS_HOST_FUSED_PIECE_BYTES", str(32 << 20))),  # (host_staging.cc's default)
-            "h2d_streams": int(os.environ.get("TIPS_HOST_H2D_STREAMS", "1")),
-            "vs_per_tensor": round(th / tf, 2),
-            "check": "identity at one rank, bit-exact" if world == 1 and f_ok else ("FAIL" if not f_ok else "not checked"),
-            "note": "the same 214 numpy gradients through allreduce_grads' N > 1 body (tips_fused_allreduce_host): "
-                    "one call, new numpy outputs, pageable inputs; at one rank the round trip through HBM is kept"}
-        del hg, outs
+    job = Job(args, torch, dist, tips_amd, _lib)
+    _lib.call("tips_set_algorithm", job.algo_names[args.algo])
+    w = None
+    all_ok = sum_ok
+    if not headline_sum:
+        steps = args.steps if args.steps is not None else 20
+        warmup = args.warmup if args.warmup is not None else 5
+        w = Workload(job, workload, steps, warmup)
+        rec = w.run()
+        all_ok = w.ok
+        line = {"metric": METRIC, "value": rec.pop("value"), "unit": rec.pop("unit"), "n_gpus": world, "steps": steps,
+                "warmup": warmup, "ms_per_step": rec.pop("ms_per_step"), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f32", "data": rec.pop("data"),
+                "config": {"workload": rec.pop("workload"), "tensors": rec.pop("tensors"),
+                           "bytes_per_rank": rec.pop("bytes_per_rank"), "algorithm": rec.pop("algorithm"),
+                           "selection": rec.pop("selection"), "rotating_sets": rec.pop("rotating_sets"),
+                           "parallelism": "dp%d (one process per GPU, %s)" % (
+                               world, "our kernels through IPC-mapped peer memory over xGMI" if w.algo == _lib.ALGO_PEER
+                               else "ncclAllReduce" if w.algo == _lib.ALGO_RCCL else "RCCL p2p over xGMI")
+                           if world > 1 else "single GPU: no link carries anything (the allreduce of one rank is the identity)"},
+                "cpu_baseline": cpu}
+        line.update(rec)
+        kr = w.reduce_kernel_roofline()
+        if kr:
+            line["reduce_kernel_roofline"] = kr
+        if workload in SUB_WORKLOADS:
+            line["gradient_api"] = gradient_api_legs(torch, dist, tips_amd, world, w.sizes, w.offs, w.rot_sets, steps, w.ms)
+            if workload == "resnet50":
+                host_legs(job, w, line)
+                if world == 1:
+                    line["op_host_named"] = op_host_leg()
+        if topo:
+            line["gpu_topology"] = topo
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True
+    if args.workload == "auto" and not args.no_sub:
+        sub_records(job, line, args.sub_steps)
+        _RESULT["line"] = line if rank == 0 else None
     last_words = crash_line() if rank == 0 and not args.no_compare else None
-
-    def note_progress(what):
-        """What rank 0 prints if a fatal signal ends the process during `what`."""
-        progress(rank, what)
-        if last_words:
-            last_words(json.dumps(dict(line, compare_algbw_gib_s=compare, compare_check=compare_check,
-                                       compare_error="process ended by a signal during %s" % what)))
-
-    # comparison points on the same workload: the other schedules and ncclAllReduce (optional; a hang
-    # here is caught by the watchdog, which then still prints the line above; a crash by last_words)
-    compare, compare_check = {}, {}
-
-    def _one_call_s():
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        step()
-        torch.cuda.synchronize()
-        return time.perf_counter() - t0
-
-    def run_variants(variants):
-        kc = max(3, steps // 4)
-        for label, name, env in variants:
-            if (label == name and algo_names[name] == algo) or (name == "peer" and workload != "bucket") or \
-                    (env and workload != "bucket"):
-                continue
-            note_progress("comparison %r" % label)
-            saved = {k: os.environ.get(k) for k in env}
-            try:
-                os.environ.update(env)
-                _lib.call("tips_set_algorithm", algo_names[name])
-                for _ in range(2):
-                    step()
-                torch.cuda.synchronize()
-                # a variant far slower than the main line (the socket rehearsal saw 100x for the
-                # transfer lanes) is priced from one call, so it cannot eat the watchdog's budget;
-                # every rank takes the same branch (the slowest rank's time decides)
-                t1 = max_over_ranks(dist, _one_call_s())
-                if t1 > 20 * max(ms, 1e-3) / 1e3:
-                    compare[label] = round(total_elems * 4 / t1 / GIB, 2)
-                    compare_check[label] = "priced from one call (%.1f ms, > 20 x the main line); no parity run" % (t1 * 1e3)
-                    continue
-                tc = timed(kc)
-                compare[label] = round(total_elems * 4 / (tc / kc) / GIB, 2)
-                good, msg = parity(algo_names[name])
-                compare_check[label] = msg if all_ranks_ok(dist, good) else "FAIL on some rank (%s here)" % msg
-            except Exception as e:  # noqa: BLE001 - a comparison point never costs the main line
-                compare[label] = None
-                compare_check[label] = "error: %s" % (e,)
-            finally:
-                for k, v in saved.items():
-                    if v is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = v
-        _lib.call("tips_set_algorithm", algo if fallbacks else algo_names[args.algo])
-
-    if not args.no_compare:
-        # (oneshot targets small buckets only.) The _k entries re-run a schedule at another sub-chunk
-        # pipeline depth, the _l entries on more transfer lanes (both read per call). Order:
-        # RCCL-moved schedules, the link probe, the schedules whose bytes our own kernels move
-        # through IPC-mapped peer memory (measured here, on the driver's 8-GPU run, before either
-        # can be a default), and last the transfer lanes, whose split communicators live on to the
-        # end of the job (on the socket rehearsal their existence slowed every later RCCL call).
-        # A fault or a hang in one of them costs only what comes after it: last_words / the
-        # watchdog print the numbers gathered before.
-        run_variants([("ring", "ring", {}), ("direct", "direct", {}), ("rccl", "rccl", {}),
-                      ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
-                      ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
-                      ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
-                      # the same plan captured once and replayed as a HIP graph (TIPS_GRAPHS)
-                      ("direct_graphs", "direct", {"TIPS_GRAPHS": "1", "TIPS_GRAPH_MAX_BYTES": str(1 << 40)})])
-        if world > 1 and not os.environ.get("TIPS_NO_RCCL"):
-            note_progress("the xGMI link probe")
-            try:
-                line["xgmi_probe"] = link_probe(dist, rank, world)
-            except Exception as e:  # noqa: BLE001
-                line["xgmi_probe"] = {"error": str(e)}
-        # Opt-in (TIPS_BENCH_PEER=1): the IPC peer schedules have not crossed real GPUs yet, so the
-        # driver's scaling runs do not start them (a fault there would cost the whole record).
-        if os.environ.get("TIPS_BENCH_PEER") == "1":
-            run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"})])
-        elif workload == "bucket" and world > 1:
-            compare_check["peer"] = "opt-in: TIPS_BENCH_PEER=1 (not yet run across real GPUs)"
-        if world > 1 and workload == "bucket":
-            note_progress("the small-bucket latency probe")
-            try:
-                line["small_bucket_latency"] = small_bucket_latency(torch, dist, _lib, L, rank, sp)
-            except Exception as e:  # noqa: BLE001
-                line["small_bucket_latency"] = {"error": str(e)}
-            note_progress("the backward-overlap probe")
-            try:
-                line["backward_overlap"] = overlap_probe(torch, dist, tips_amd, _lib, algo_names[args.algo])
-            except Exception as e:  # noqa: BLE001
-                line["backward_overlap"] = {"error": str(e)}
-        # Opt-in (TIPS_BENCH_LANES=1): transfer lanes split communicators that live to the end of
-        # the job; on the socket rehearsal they ran 10x slower and slowed every later call.
-        if os.environ.get("TIPS_BENCH_LANES") == "1":
-            run_variants([("direct_l2", "direct", {"TIPS_LANES": "2"}),
-                          ("ring_l2", "ring", {"TIPS_LANES": "2"}),
-                          ("direct_k8_l4", "direct", {"TIPS_LANES": "4", "TIPS_PIPELINE_DEPTH": "8",
-                                                      "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)})])
-        elif workload == "bucket" and world > 1:
-            compare_check["lanes"] = "opt-in: TIPS_BENCH_LANES=1"
-    line["compare_check"] = compare_check
-    line["compare_algbw_gib_s"] = compare
-    # Opt-in (TIPS_BENCH_ENV_VARIANTS=1): child jobs with other RCCL settings (one of them delivered
-    # wrong bytes in a probe, profiles/r02/rccl_nchannels_probe.txt)
-    if world > 1 and workload == "bucket" and not args.no_compare and not args.no_env_variants \
-            and not os.environ.get("TIPS_NO_RCCL") and os.environ.get("TIPS_BENCH_ENV_VARIANTS") == "1":
-        note_progress("the RCCL-setting child jobs")
-        line["env_variants"] = env_variant_jobs(args, dist, rank, world)
-    ring_algbw = algbw if algo == _lib.ALGO_RING else (compare.get("ring") or 0) * GIB
-    if world > 1 and workload == "bucket" and ring_algbw:  # the north star's ring target: >= 70 % of one xGMI link
-        rb = ring_algbw * 2 * (world - 1) / world
-        line["ring_xgmi"] = {"busbw_GBps": round(rb / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS,
-                             "frac_of_one_link": round(rb / 1e9 / XGMI_LINK_GBPS, 4), "target_frac": 0.70}
+    if w is not None and workload == "bucket" and world > 1 and not args.no_compare:
+        comparisons(job, w, line, last_words)
+    if job.skipped:
+        line["budget_skipped"] = {"legs": job.skipped, "budget_s": job.budget_s,
+                                  "note": "TIPS_BENCH_BUDGET_S: optional legs start only while the budget lasts"}
+    line["wall_s"] = round(time.time() - _T0, 1)
     if rank == 0:
         if last_words:
             last_words(None)
         print(json.dumps(line), flush=True)
     _RESULT["printed"] = True  # the watchdog must not print a second line
+    if w is not None:
+        w.close()
     dist.barrier()
     wd.cancel()
     tips_amd.shutdown()
@@ -1367,21 +1645,18 @@ def main():
                "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29511"),
                os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
-    if world > 1 or args.workload in ("bucket", "fused1000", "resnet50", "negotiated1000"):
-        if world == 1:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29512")
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
-        try:
-            return bench_allreduce(args)
-        except Exception as e:  # one diagnosable line instead of a bare traceback
-            if int(os.environ.get("RANK", "0")) == 0 and not _RESULT.get("printed"):
-                line = _RESULT.get("line") or {"metric": METRIC, "value": None, "unit": "GiB/s",
-                                               "n_gpus": world}
-                print(json.dumps(dict(line, error="%s: %s" % (type(e).__name__, e))), flush=True)
-            raise
-    return bench_sum(args)
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29512")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    try:
+        return bench_job(args)
+    except Exception as e:  # one diagnosable line instead of a bare traceback
+        if int(os.environ.get("RANK", "0")) == 0 and not _RESULT.get("printed"):
+            line = _RESULT.get("line") or {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world}
+            print(json.dumps(dict(line, error="%s: %s" % (type(e).__name__, e))), flush=True)
+        raise
 
 
 if __name__ == "__main__":

@@ -374,6 +374,11 @@ TIPS_API int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lane
  * Returns 0 (graphs on), 1 (a failed capture turned them off for the job), 2 (off: not asked
  * for, or an older runtime), < 0 on error. */
 TIPS_API int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached);
+/* The cost of keeping RCCL's order after replays: how many times an eager RCCL call (a larger
+ * bucket, a fused call, a synchronous collective) found a replay still pending and blocked the
+ * calling host thread until it had run (TIPS_REPLAY_HOST_ORDER, default 1), and the host time those
+ * waits took in total (ns). Counts since tips_init. */
+TIPS_API int tips_replay_order_stats(int64_t* host_waits, int64_t* host_wait_ns);
 
 /* ---- single-GPU harnesses (tests and benchmarks) ---- */
 

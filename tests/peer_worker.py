@@ -605,8 +605,11 @@ def graphs_case(c, rank, size, L, _lib, sp):
                   "call_us": round((time.perf_counter() - t0) / c["time_calls"] * 1e6, 2)}
     cap, rep, cached = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     off = L.tips_graph_stats(ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(cached))
+    waits, wait_ns = ctypes.c_int64(), ctypes.c_int64()
+    _lib.call("tips_replay_order_stats", ctypes.byref(waits), ctypes.byref(wait_ns))
     return dict({"case": {"graphs": len(specs)}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:5]),
-                 "captured": cap.value, "replayed": rep.value, "cached": cached.value, "graphs_off": off}, **timing)
+                 "captured": cap.value, "replayed": rep.value, "cached": cached.value, "graphs_off": off,
+                 "replay_host_waits": waits.value, "replay_host_wait_us": round(wait_ns.value / 1e3, 1)}, **timing)
 
 
 def golden_case(c, rank, size, L, _lib, sp):

@@ -277,3 +277,33 @@ def interpret(plans, ins, dtype, inplace=False):
                     res = oracle_bind.fold(srcs, code=dtype, wide_acc=True)
                 view(r, u["dst"][0], u["dst"][1], u["count"])[:] = res
     return outs
+
+
+def proxy_order(calls, host_wait="end"):
+    """RCCL's proxy thread works through the operations of one communicator in the order they are
+    POSTED; the device runs the groups in stream order. A replayed plan's group posts its
+    operations from a host node of the graph when the device reaches that group; an eager group
+    posts them when the host issues it. `calls` = [("replay" | "eager", number of groups)] in
+    issue order; the device is taken to lag the host as far as it can (it runs nothing until the
+    host waits for it). host_wait is what schedules.cc order_after_replays does before an eager
+    call while a replay is pending: "end" (wait until the replay has run), "start" (until its first
+    group has begun) or "none". Returns (posting order, device order) of (call, group) pairs: a
+    schedule is safe when they are equal (else the proxy waits on work the device has not reached
+    while the device waits on the proxy - the hang of profiles/r03/k_op_body_hang.txt)."""
+    from collections import deque
+    device = [(c, k) for c, (_, ng) in enumerate(calls) for k in range(ng)]
+    posted, deferred = [], deque()  # deferred: replay groups the device has not reached, device order
+    for c, (mode, ng) in enumerate(calls):
+        if mode == "replay":
+            deferred.extend((c, k) for k in range(ng))
+            continue
+        if deferred and host_wait == "end":
+            while deferred:
+                posted.append(deferred.popleft())
+        elif deferred and host_wait == "start":
+            last = deferred[-1][0]  # the pending replay: the device has reached its first group
+            while deferred and (deferred[0][0] < last or deferred[0] == (last, 0)):
+                posted.append(deferred.popleft())
+        posted.extend((c, k) for k in range(ng))
+    posted.extend(deferred)
+    return posted, device

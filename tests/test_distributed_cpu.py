@@ -265,3 +265,54 @@ def test_unused_parameter_differs_by_rank(world):
         assert res[r][4] == res[0][4]
     n_using = world // 2
     assert res[0][4] == [2.0 * n_using] * 7  # d(extra . extra) = 2 extra, summed over the ranks that used it
+
+
+def test_cpu_baseline_reports_the_host_and_openmp_legs():
+    """bench.cpu_baseline's host half (SURVEY §8d): the CPUs and model it ran on, and config 2's
+    c = a + b as an OpenMP loop on one core and on the box's CPU share (tools/cpu_sum_bench), here on
+    a tiny bucket."""
+    sys.path.insert(0, REPO)
+    import bench
+    h = bench.host_info()
+    assert h["nproc"] >= 1 and h["affinity_cpus"] >= 1 and set(h) >= {"cpu_model", "omp_num_threads"}
+    one = bench.openmp_sum(1 << 16, 1, 3)
+    if "error" in one:
+        pytest.skip(one["error"])
+    two = bench.openmp_sum(1 << 16, 2, 3)
+    assert one["value"] > 0 and one["cores"] == 1 and one["check"] == "exact"
+    assert two["value"] > 0 and two["cores"] == 2 and two["check"] == "exact"
+
+
+def _budget_worker(rank, world, port, q):
+    import time
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    job = object.__new__(bench.Job)  # (no GPU: only the budget half of a Job)
+    job.dist, job.rank, job.skipped = dist, rank, []
+    bench._T0 = time.time() - (50 if rank == world - 1 else 0)  # the last rank's clock started 50 s earlier
+    job.budget_s = 60.0
+    got = [job.afford("a", 5), job.afford("b", 20), job.afford("c", 9)]
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, got, job.skipped))
+
+
+def test_bench_budget_is_decided_together():
+    """bench.Job.afford: an optional leg starts only while the budget lasts on the SLOWEST rank's
+    clock, so every rank takes the same branch (the legs are collectives)."""
+    import torch.multiprocessing as tmp
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_budget_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+    for rank, got, skipped in res:
+        assert got == [True, False, True], (rank, got)
+        assert skipped == ["b"]

@@ -74,3 +74,35 @@ def _run_op_body(p, tensors, binary, extra_env=None):
     for rc, out, err in outs:
         res = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
         assert res["callbacks"] == tensors
+
+
+def test_op_host_config5_over_rccl(gpu):
+    """Config 5 as the reference's CPU op sees it (tools/op_host.c): the 214 ResNet-50 gradients as
+    named HOST allreduces (tips_enqueue_allreduce_shaped with their TF shapes + tips_on_done), issued
+    by four executor threads per rank in a per-rank shuffled order, step after step, over 3 real RCCL
+    ranks; every output of the last step bit-exact against the oracle's rank-order fold of all ranks'
+    regenerated inputs (ops.cc:86-118, coordinator.cc:223-241). bench.py times the same binary's
+    product-only build at one rank (op_host_named)."""
+    exe = os.path.join(REPO, "tools", "_bin", "op_host_check")
+    assert os.path.exists(exe), "build it first: make tools/_bin/op_host_check (part of __graft_entry__.build())"
+    port = _port()
+    procs = []
+    for r in range(3):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), TIPS_BOOTSTRAP_PORT=str(port), NCCL_HOSTID="tips-op-host-%d" % r,
+                   NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", OP_HOST_STEPS="3", OP_HOST_WARMUP="1")
+        procs.append(subprocess.Popen([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            out, err = pr.communicate(timeout=240)
+            outs.append((pr.returncode, out, err))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    for r, (rc, out, err) in enumerate(outs):
+        line = [l for l in out.splitlines() if l.startswith("{")]
+        res = json.loads(line[-1]) if line else None
+        assert rc == 0 and res and res["ok"], "rank %d rc %s: %s\n%s" % (r, rc, out[-1500:], err[-3000:])
+        assert res["tensors"] == 214 and res["elements"] == 25583592 and res["check"].startswith("bit-exact"), res

@@ -122,7 +122,9 @@ def test_replayed_plans_in_python_processes(gpu, algo, p):
     (ROCm 7.0.2, RCCL 2.26): the groups are captured on the graph's origin stream (a group captured
     on a forked stream crashes that runtime, tools/graph_probe.py mode 3). Buffers reduced round
     after round from two streams, one reallocated half way, interleaved with an eager bucket
-    over the replay limit: replays happen and every result is bit-exact."""
+    over the replay limit: replays happen and every result is bit-exact. Every eager bucket that
+    follows a replay takes order_after_replays' host wait (tips_replay_order_stats counts them;
+    tests/test_plans.py::test_eager_after_replay_takes_the_host_wait shows why it must)."""
     env = rccl_env(algo)
     env.update(TIPS_GRAPHS="1", TIPS_GRAPH_MAX_BYTES=str(2 << 20))
     bufs = [[F32, 300007, False, False], [I64, 70001, True, False], [BF16, 4099, False, True],
@@ -132,6 +134,8 @@ def test_replayed_plans_in_python_processes(gpu, algo, p):
     for res in results:
         c = res["results"][0]
         assert c["graphs_off"] == 0 and c["captured"] >= 3 and c["replayed"] >= 9, c
+        # each round from the third on: replays of buffers 0-2, then the eager 3 MiB bucket
+        assert c["replay_host_waits"] >= 4, c
 
 
 @pytest.mark.parametrize("p", [2, 3])

@@ -211,3 +211,28 @@ def test_counts_past_int32(algo, p, n, dtype):
                 covered += e - max(s, end)
                 end = e
         assert covered == n * es and end == n * es, (r, covered, n * es)
+
+
+def _groups(algo, p, n, K):
+    """Transfer groups (one ncclGroupStart/End each) of rank 0's plan."""
+    return sum(1 for s in pu.dump(algo, p, 0, n, F32, K)["steps"] if s["xfers"])
+
+
+@pytest.mark.parametrize("seq", [("replay", "eager"), ("eager", "replay", "eager", "replay", "replay", "eager"),
+                                 ("replay", "replay", "eager", "eager"), ("replay", "eager", "replay", "eager")])
+@pytest.mark.parametrize("algo,p,n,K", [(pu.ONESHOT, 2, 65536, 1), (pu.DIRECT, 8, 262147, 2), (pu.RING, 4, 100003, 3)])
+def test_eager_after_replay_takes_the_host_wait(seq, algo, p, n, K):
+    """RCCL's proxy order (plan_util.proxy_order): with order_after_replays' host wait until the
+    pending replay has RUN, every group's operations reach the proxy in the device's order, for any
+    mix of replayed and eager calls of real plans (a replayed small bucket, an eager large one);
+    without the wait an eager call after a replay is posted ahead of the replay's groups; waiting
+    only for the replay's START leaves a multi-group plan's later groups behind the eager call
+    (why schedules.cc waits for the end and counts the waits: tips_replay_order_stats)."""
+    ng = _groups(algo, p, n, K)
+    calls = [(m, ng) for m in seq]
+    posted, device = pu.proxy_order(calls, "end")
+    assert posted == device
+    posted, device = pu.proxy_order(calls, "none")
+    assert posted != device  # every sequence here has an eager call after a pending replay
+    posted, device = pu.proxy_order(calls, "start")
+    assert (posted == device) == (ng == 1)

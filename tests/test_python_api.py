@@ -410,3 +410,124 @@ def test_fused_list_refuses_host_tensors():
     with pytest.raises(ValueError, match="needs device tensors"):
         fl.allreduce_([torch.zeros(3), torch.zeros(4)])
     assert fl.allreduce_([]) == []
+
+
+def test_evicted_host_flat_sets_unregister_after_last_use(monkeypatch):
+    """_HOST_FLAT keeps 16 host list signatures; a set evicted from it stays page-locked only while
+    an output of it is alive, and is unregistered once the last one goes (numpy views and
+    torch.from_numpy storages both hold the page-locked array). Cycles through 20 signatures.
+    (tips_host_register / _unregister are stubbed: no GPU here.)"""
+    import gc
+    import torch
+    import tips_amd.ops as ops
+
+    live = {}
+
+    class Stub:
+        def tips_host_register(self, p, n):
+            assert p not in live, "address registered twice"
+            live[p] = n
+            return 0
+
+        def tips_host_unregister(self, p):
+            assert p in live
+            del live[p]
+            return 0
+
+        def tips_fused_layout(self, cp, n, code, offs):
+            return ops._lib.lib().tips_fused_layout(cp, n, code, offs)
+    real = ops._lib.lib
+    monkeypatch.setattr(ops._lib, "lib", lambda: Stub())
+    monkeypatch.setattr(ops._lib, "call", lambda name, *a: getattr(Stub(), name)(*a))
+    monkeypatch.setattr(Stub, "tips_fused_layout", lambda self, *a: real().tips_fused_layout(*a))
+    monkeypatch.setattr(ops, "_HOST_FLAT", {})
+    held = []
+    for k in range(20):
+        srcs = [np.zeros(k + 3, np.float32), np.zeros(7, np.float32)] if k % 2 else \
+            [torch.zeros(k + 3), torch.zeros(5)]
+        fo = ops._host_flat_outputs(srcs)
+        flat, views = fo.take()
+        if k == 0:
+            held.append(views[1])  # an output of the first (torch) set outlives its eviction
+        del flat, views
+    gc.collect()
+    assert len(ops._HOST_FLAT) == 16
+    kept = {tensors_ptr(s[0]) for fo in ops._HOST_FLAT.values() for s in fo.sets}
+    # every registration still live belongs to a kept set, or to the output still held
+    assert set(live) - kept == {held[0].untyped_storage().data_ptr()}
+    del held[:]
+    gc.collect()
+    assert set(live) == kept
+
+
+def tensors_ptr(x):
+    from tips_amd import tensors
+    return tensors.data_ptr(x)
+
+
+def test_grad_plan_never_matches_a_dead_gradient_or_a_changed_tensor(monkeypatch):
+    """_GradPlan (allreduce_grads' remembered split): a gradient that died does not pass for a
+    None in the same position, and a None position must stay None; a plan's run() re-checks its
+    device groups through the checking reader (here: _dev_list_flat refuses the changed list)."""
+    import gc
+    import torch
+    import tips_amd
+    a, b = torch.zeros(3), torch.zeros(4)
+    plan = tips_amd._GradPlan([a, None, b], [([0, 2], None, None)])
+    assert plan.matches([a, None, b])
+    assert not plan.matches([a, b, b]) and not plan.matches([a, None])
+    del a
+    gc.collect()
+    assert plan.dead and not plan.matches([None, None, b])
+    c = torch.zeros(2)
+    plan2 = tips_amd._GradPlan([c], [([0], None, None)])
+    calls = []
+    monkeypatch.setattr(tips_amd._ops, "_dev_list_flat", lambda ts: calls.append(ts) or None)
+    assert plan2.run([c]) is None and calls == [[c]]
+
+
+def test_flat_output_keys_follow_the_layout_settings(monkeypatch):
+    """A fusion layout depends on TIPS_FUSION_THRESHOLD / TIPS_COPY_TILE_BYTES / TIPS_FUSION_BALANCE
+    as well as the counts: the cached flat-output sets are keyed on them, so a changed setting gets
+    offsets of its own layout."""
+    import torch
+    import tips_amd.ops as ops
+    monkeypatch.setattr(ops, "_FLAT_OUTPUTS", {})
+    ts = [torch.zeros(300 << 10), torch.zeros(300 << 10)]  # 1.2 MiB each
+    fo1 = ops._flat_outputs(ts, ops._lib.FLOAT32)
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(1 << 20))
+    fo2 = ops._flat_outputs(ts, ops._lib.FLOAT32)
+    assert fo2 is not fo1
+    monkeypatch.delenv("TIPS_FUSION_THRESHOLD")
+    assert ops._flat_outputs(ts, ops._lib.FLOAT32) is fo1
+
+
+def test_flat_output_take_is_exclusive_across_threads():
+    """_FlatOutputs.take from many threads at once: no set is handed to two holders at a time (the
+    free check and the hand-out run under the object's lock)."""
+    import threading
+    import torch
+    from tips_amd import _lib
+    from tips_amd.ops import _FlatOutputs
+    fo = _FlatOutputs((torch.Size([8]), torch.Size([3])), [8, 3], _lib.FLOAT32, torch.float32, torch.device("cpu"))
+    owners = {}
+    bad = []
+    lock = threading.Lock()
+
+    def worker(k):
+        for _ in range(300):
+            flat, views = fo.take()
+            p = flat.data_ptr()
+            with lock:
+                if owners.get(p) is not None:
+                    bad.append((p, owners[p], k))
+                owners[p] = k
+            with lock:
+                owners[p] = None
+            del flat, views
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not bad

@@ -183,7 +183,7 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
         sums = _ops._flat_run(fo, ts, list(map(_DATA_PTR, ts)))
         for (i, _, ctx), s in zip(members, sums):
             out[i] = s if none else compression.decompress(s, ctx)
-        plan_groups.append(([i for i, _, _ in members], fo, None))
+        plan_groups.append(([i for i, _, _ in members], None, None))
     for members in host.values():
         ts = [c for _, c, _ in members]
         sums = _ops.fused_allreduce_host_flat(ts)
@@ -209,34 +209,49 @@ _PLANS = []       # recent _GradPlans, most recent first
 
 
 class _GradPlan(object):
-    """How _reduce_grads split one list of dense device gradients, kept for a later call with the
-    SAME tensor objects (a training loop whose .grad tensors persist, or a set of gradient buffers
-    used in turn): such a call is recognised through weak references - a tensor that died or was
-    replaced never matches - and skips the per-tensor inspection (kind, dtype, contiguity, shape),
-    which costs more host time for 1000 gradients than the fused allreduce's device work. Only the
-    data pointers are read again (a tensor's storage can be swapped in place)."""
+    """How _reduce_grads split one list of dense gradients, kept for a later call with the SAME
+    tensor objects (a training loop whose .grad tensors persist, or a set of gradient buffers used
+    in turn): such a call is recognised through weak references and skips the per-tensor Python
+    inspection (kind, dtype, contiguity, shape), which costs more host time for 1000 gradients than
+    the fused allreduce's device work. A plan whose tensors one has died never matches again (a
+    weak-reference callback marks it), and a position that was None must be None again: a dead
+    gradient cannot pass for a None one. Tensors can still change in place (.data =, set_, resize_,
+    a numpy array's shape), so every call re-reads each group through the checking readers: device
+    groups through _ops._dev_list_flat (pointers, counts, dtype, contiguity in C++), host groups
+    through their recorded shapes and dtypes; any difference plans again."""
 
     def __init__(self, grads, groups):
         import weakref
-        self.refs = [weakref.ref(g) if g is not None else _DEAD_REF for g in grads]
+        self.dead = False
+
+        def died(_ref, plan=weakref.ref(self)):
+            p = plan()
+            if p is not None:
+                p.dead = True
+        self.refs = [weakref.ref(g, died) if g is not None else _NONE_REF for g in grads]
         self.n = len(grads)
-        # [(positions, _FlatOutputs, None)] for device groups, [(positions, _HostFlatOutputs,
-        # [(shape, dtype)])] for host groups (numpy arrays can change shape or dtype in place)
+        # [(positions, None, None)] for device groups, [(positions, _HostFlatOutputs,
+        # [(shape, dtype)])] for host groups
         self.groups = groups
         self.whole = len(groups) == 1 and groups[0][0] == list(range(self.n))
 
     def matches(self, grads):
         import operator
         import weakref
-        return len(grads) == self.n and all(map(operator.is_, map(weakref.ref.__call__, self.refs), grads))
+        if self.dead or len(grads) != self.n:
+            return False
+        # a live tensor's reference returns it; a None position's returns None (_NONE_REF)
+        return all(map(operator.is_, map(weakref.ref.__call__, self.refs), grads))
 
     def run(self, grads):
-        """The outputs, or None when a host tensor changed shape or dtype (the caller plans again)."""
+        """The outputs, or None when a tensor changed in place (the caller plans again)."""
         out = list(grads)
         for pos, fo, meta in self.groups:
             ts = grads if self.whole else [grads[i] for i in pos]
             if meta is None:
-                sums = _ops._flat_run(fo, ts, list(map(_DATA_PTR, ts)))
+                sums = _ops._dev_list_flat(ts)  # (None: not one dtype of dense contiguous device tensors now)
+                if sums is None:
+                    return None
             else:
                 if any(t.shape != shp or t.dtype is not dt for t, (shp, dt) in zip(ts, meta)):
                     return None
@@ -257,7 +272,7 @@ def _dead():
     return weakref.ref(_Gone())  # (the object is gone at once: the reference reads None, as a None gradient)
 
 
-_DEAD_REF = _dead()
+_NONE_REF = _dead()  # the reference of a position that held None (only a plan's None positions use it)
 
 
 def _find_plan(grads):

@@ -130,6 +130,7 @@ _SIGNATURES = [
                                            ctypes.POINTER(ctypes.c_int)]),
     ("tips_graph_stats", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    ("tips_replay_order_stats", ctypes.c_int, [_c_i64_p, _c_i64_p]),
     ("tips_ring_simulate", ctypes.c_int,
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_oneshot_simulate", ctypes.c_int,

@@ -692,6 +692,8 @@ int64_t tips_fused_pack_bucket(const void* const* ins, const int64_t* counts, in
   if (!t) return TIPS_ERR_HIP;
   if (fc.tables_built != built) TRY(join((hipStream_t)stream, st.fuse_stream, st.ev_done));  // the upload first
   TRY(copy_tiles(*L, *t, 0, bk.tile0, bk.ntiles, (hipStream_t)stream));
+  // the table's later reuse (an upload into it, hipFreeAsync) is ordered on fuse_stream: after this read
+  TRY(join(st.fuse_stream, (hipStream_t)stream, st.ev_start));
   int64_t payload = 0;
   for (int i = 0; i < n; i++)
     if (L->bucket[i] == bucket) payload += counts[i] * tips::dtype_size(dtype);

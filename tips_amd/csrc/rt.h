@@ -214,6 +214,8 @@ struct State {
   bool graph_pending = false;  // a replay may still run on graph_stream: eager plan work waits for it
   bool eager_pending = false;  // eager plan work was queued on comm / comp since the last replay
   int64_t graphs_captured = 0, graphs_replayed = 0;
+  // order_after_replays' host waits (eager RCCL work issued while a replay was pending) and their time
+  int64_t replay_host_waits = 0, replay_host_wait_ns = 0;
 };
 
 State& S();

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <tuple>
 
 #include "plan.h"
@@ -38,19 +39,29 @@ int launch_psum(const PSum& s, char* const* base, int dtype, hipStream_t stream)
 // a replay reads and writes the same staging and issues RCCL work on the same communicator.
 // An eager RCCL call after a replay: on the device it waits for the replay (the comm stream joins
 // the graph stream); on the HOST it also waits until the replay has run (TIPS_REPLAY_HOST_ORDER,
-// default on). A replayed graph hands its transfers to RCCL's proxy thread only when the graph
-// starts on the device, an eager call hands them over when it is issued; issued while the replay
-// still waited in the queue, the eager call's transfers reached the proxy first, the proxy worked
-// on them, the device ran the replay first and waited for the replay's - on every rank. Seen as a
-// hang of the op-body test over 3 socket-transport RCCL ranks: without this wait 3 of 10 runs hung,
-// every rank in an eager call's hipStreamSynchronize; with it 12 of 12 ran clean, as with replays
-// off (profiles/r03/k_op_body_hang.txt, k_hunt_summary.txt).
+// default on). RCCL posts a replayed group's proxy operations from a host node of the graph, when
+// the device reaches that group; an eager group posts its own when it is issued. Issued while a
+// replay still waited in the queue (or between two of its groups), the eager call's operations
+// reached the proxy first, the proxy worked on them, the device ran the replay first and waited for
+// the replay's - on every rank. Seen as a hang of the op-body test over 3 socket-transport RCCL
+// ranks: without this wait 3 of 10 runs hung, every rank in an eager call's hipStreamSynchronize;
+// with it 12 of 12 ran clean, as with replays off (profiles/r03/k_op_body_hang.txt,
+// k_hunt_summary.txt). Waiting for the replay's start would not do: a multi-step plan posts each
+// group's operations when the device reaches that group, so only the end of the replay covers its
+// last group. tests/plan_util.py proxy_order() models the hazard; tips_replay_order_stats counts
+// the waits and their host time.
 int order_after_replays(State& st) {
   if (!st.graph_pending) return 0;
   TRY(join(st.comm_stream, st.graph_stream, st.ev_graph[4]));
   HIP_TRY(hipStreamWaitEvent(st.comp_stream, st.ev_graph[4], 0));
   st.graph_pending = false;
-  if (env_i64("TIPS_REPLAY_HOST_ORDER", 1) != 0) HIP_TRY(hipEventSynchronize(st.ev_graph[4]));
+  if (env_i64("TIPS_REPLAY_HOST_ORDER", 1) != 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipEventSynchronize(st.ev_graph[4]));
+    st.replay_host_waits++;
+    st.replay_host_wait_ns +=
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  }
   return 0;
 }
 
@@ -580,6 +591,7 @@ void graphs_release(State& st) {
   }
   st.graph_pending = st.eager_pending = false;
   st.graphs_captured = st.graphs_replayed = 0;
+  st.replay_host_waits = st.replay_host_wait_ns = 0;
 }
 
 namespace {
@@ -784,6 +796,15 @@ int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached) {
   if (st.graphs && st.graphs->off) return 1;
   const int64_t want = env_i64("TIPS_GRAPHS", 1);
   return (want <= 0 || (want == 1 && !graphs_supported())) ? 2 : 0;
+}
+
+int tips_replay_order_stats(int64_t* host_waits, int64_t* host_wait_ns) {
+  if (!host_waits || !host_wait_ns) return fail(TIPS_ERR_INVALID_ARG, "bad replay-order query");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  *host_waits = st.replay_host_waits;
+  *host_wait_ns = st.replay_host_wait_ns;
+  return 0;
 }
 
 int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, int depth, int64_t* out, int64_t cap) {

@@ -257,6 +257,7 @@ class _FlatOutputs(object):
         self.offs = [int(o) // self.es for o in offs]
         self.shapes, self.dtype, self.device = shapes, dtype, device
         self.sets = []
+        self.lock = threading.Lock()  # (the free check and the hand-out together, as _HostOutPool)
 
     def _free(self, s):
         flat, views, use0, rc0 = s
@@ -270,19 +271,27 @@ class _FlatOutputs(object):
         list is made here, before the library call releases the GIL, so another thread's take()
         already sees the set's views referenced and does not hand it out twice."""
         import torch
-        for s in self.sets:
-            if self._free(s):
-                return s[0], list(s[1])
-        flat = torch.empty(max(1, self.total // self.es), dtype=self.dtype, device=self.device)
-        views = [flat[o:o + n].view(shp) for o, n, shp in zip(self.offs, self.numels, self.shapes)]
-        if len(self.sets) < self.MAX_SETS:
-            use0 = torch._C._storage_Use_Count(flat.untyped_storage()._cdata)
-            rc0 = _fast.max_refcount(views)
-            self.sets.append((flat, views, use0, rc0))
-        return flat, list(views)
+        with self.lock:  # another thread's take() cannot see a set free between the check and the copy
+            for s in self.sets:
+                if self._free(s):
+                    return s[0], list(s[1])
+            flat = torch.empty(max(1, self.total // self.es), dtype=self.dtype, device=self.device)
+            views = [flat[o:o + n].view(shp) for o, n, shp in zip(self.offs, self.numels, self.shapes)]
+            if len(self.sets) < self.MAX_SETS:
+                use0 = torch._C._storage_Use_Count(flat.untyped_storage()._cdata)
+                rc0 = _fast.max_refcount(views)
+                self.sets.append((flat, views, use0, rc0))
+            return flat, list(views)
 
 
-_FLAT_OUTPUTS = {}  # (dtype, device, shapes) -> _FlatOutputs (small LRU)
+_FLAT_OUTPUTS = {}  # (dtype, device, shapes, layout settings) -> _FlatOutputs (small LRU)
+
+
+def _layout_settings():
+    """The settings a fusion layout depends on besides the counts (fusion.cc reads them per call):
+    part of every flat-output cache key, so a changed setting never reuses offsets of another layout."""
+    env = os.environ
+    return (env.get("TIPS_FUSION_THRESHOLD"), env.get("TIPS_COPY_TILE_BYTES"), env.get("TIPS_FUSION_BALANCE"))
 
 
 def fused_allreduce_flat(tensor_list):
@@ -302,7 +311,7 @@ def _flat_outputs(tensor_list, code):
     """The _FlatOutputs of this list's signature (dtype, device, shapes)."""
     t0 = tensor_list[0]
     shapes = tuple(t.shape for t in tensor_list)
-    key = (t0.dtype, t0.device, shapes)
+    key = (t0.dtype, t0.device, shapes, _layout_settings())
     fo = _FLAT_OUTPUTS.get(key)
     if fo is None:
         if len(_FLAT_OUTPUTS) >= 16:
@@ -317,8 +326,9 @@ def _flat_outputs(tensor_list, code):
 def _flat_run(fo, tensor_list, ptrs):
     """tips_fused_allreduce_flat of `tensor_list` (whose data pointers are `ptrs`) into an output set
     of `fo`; returns the outputs."""
-    if ptrs == fo.last[0]:
-        pp = fo.last[1]
+    last = fo.last  # (one read: another thread may replace it)
+    if ptrs == last[0]:
+        pp = last[1]
     else:
         pp = _lib.ptr_array(ptrs)
         fo.last = (ptrs, pp)
@@ -338,7 +348,7 @@ def _torch_mod():
 _ST_CODES = {6: _lib.FLOAT32, 7: _lib.FLOAT64, 3: _lib.INT32, 4: _lib.INT64, 5: _lib.FLOAT16, 15: _lib.BFLOAT16}
 _LIST_BUFS = threading.local()  # .d: n -> (pointer array, count array, their addresses), per thread:
                                 # the library call releases the GIL while it reads them
-_FAST_FLAT = {}   # (scalar type, device, n, shape hash) -> (_FlatOutputs, count bytes)
+_FAST_FLAT = {}   # (scalar type, device, n, shape hash, layout settings) -> (_FlatOutputs, count bytes)
 _CUR_STREAM = None
 
 
@@ -364,7 +374,7 @@ def _dev_list_flat(tensor_list):
     if r is None or r[0] not in _ST_CODES:
         return None
     import ctypes
-    key = (r[0], r[1], n, r[2])
+    key = (r[0], r[1], n, r[2], _layout_settings())
     hit = _FAST_FLAT.get(key)
     counts = ctypes.string_at(bufs[3], 8 * n)
     if hit is None or hit[1] != counts:
@@ -429,6 +439,7 @@ class _HostFlatOutputs(object):
         self.offs = [int(o) for o in offs]
         self.sets = []
         self.last = (None, None)  # (pointer list, its ptr_array) of the previous call
+        self.lock = threading.Lock()
 
     def _refs(self, s):
         """(references to the flat buffer, most references to one view) of set s. Measured the same
@@ -445,30 +456,53 @@ class _HostFlatOutputs(object):
 
     def take(self):
         """(flat buffer, a new list of its views): made before the library call releases the GIL,
-        as _FlatOutputs.take."""
-        for s in self.sets:
-            if self._refs(s) == s[2]:
-                return s[0], list(s[1])
-        if self.is_torch:
-            import torch
-            flat = torch.empty(self.total, dtype=torch.uint8)
-            views = [flat[o:o + n * self.es].view(self.dtype).view(shp)
-                     for o, n, shp in zip(self.offs, self.numels, self.shapes)]
-        else:
+        as _FlatOutputs.take, under the object's lock."""
+        with self.lock:
+            for s in self.sets:
+                if self._refs(s) == s[2]:
+                    return s[0], list(s[1])
             import numpy as np
-            flat = np.empty(self.total, dtype=np.uint8)
-            views = [flat[o:o + n * self.es].view(self.dtype).reshape(shp)
-                     for o, n, shp in zip(self.offs, self.numels, self.shapes)]
-        if len(self.sets) < self.MAX_SETS:
-            # a kept set is page-locked for the life of the process (the device's D2H lands in it
-            # directly); one past MAX_SETS is not (it is freed with its last output)
-            _lib.call("tips_host_register", tensors.data_ptr(flat), self.total)
-            st = [flat, views, None]
-            del flat, views  # (the baseline counts the set's own references only)
-            st[2] = self._refs(st)
-            self.sets.append(st)
-            return st[0], list(st[1])
-        return flat, views
+            mem = np.empty(self.total, dtype=np.uint8)
+            if self.is_torch:
+                import torch
+                flat = torch.from_numpy(mem)  # (the storage keeps `mem` alive: see _register_until_freed)
+                views = [flat[o:o + n * self.es].view(self.dtype).view(shp)
+                         for o, n, shp in zip(self.offs, self.numels, self.shapes)]
+            else:
+                flat = mem
+                views = [flat[o:o + n * self.es].view(self.dtype).reshape(shp)
+                         for o, n, shp in zip(self.offs, self.numels, self.shapes)]
+            if len(self.sets) < self.MAX_SETS:
+                # a kept set is page-locked while its memory lives (the device's D2H lands in it
+                # directly); one past MAX_SETS is not (it is freed with its last output)
+                _register_until_freed(mem, self.total)
+                del mem
+                st = [flat, views, None]
+                del flat, views  # (the baseline counts the set's own references only)
+                st[2] = self._refs(st)
+                self.sets.append(st)
+                return st[0], list(st[1])
+            return flat, views
+
+
+def _register_until_freed(mem, nbytes):
+    """Page-lock a numpy host buffer (tips_host_register) and unregister it just before its memory
+    is freed: numpy views hold their base, and a torch tensor made by torch.from_numpy holds the
+    array from its storage, so the array dies with the last output that uses its memory. A set
+    evicted from _HOST_FLAT is therefore unregistered once its last output is released - never while
+    a call writes into it (the call holds the buffer) - and no later allocation at the same address
+    finds a stale registration."""
+    import weakref
+    ptr = mem.ctypes.data
+    _lib.call("tips_host_register", ptr, nbytes)
+    weakref.finalize(mem, _unregister, ptr).atexit = False  # (at exit the process's pages go anyway)
+
+
+def _unregister(ptr):
+    try:
+        _lib.lib().tips_host_unregister(ptr)
+    except Exception:  # noqa: BLE001 - at interpreter exit the library may be gone
+        pass
 
 
 def _itemsize(dtype, is_torch):
@@ -479,7 +513,7 @@ def _itemsize(dtype, is_torch):
     return np.dtype(dtype).itemsize
 
 
-_HOST_FLAT = {}  # (dtype, torch?, shapes) -> _HostFlatOutputs
+_HOST_FLAT = {}  # (dtype, torch?, shapes, layout settings) -> _HostFlatOutputs
 
 
 def fused_allreduce_host_flat(tensor_list):
@@ -507,7 +541,7 @@ def _host_flat_outputs(srcs):
     contiguous host tensors of one dtype."""
     is_torch = tensors.is_torch(srcs[0])
     shapes = tuple(tuple(s.shape) for s in srcs)
-    key = (str(srcs[0].dtype), is_torch, shapes)
+    key = (str(srcs[0].dtype), is_torch, shapes, _layout_settings())
     fo = _HOST_FLAT.get(key)
     if fo is None:
         if len(_HOST_FLAT) >= 16:
@@ -520,8 +554,9 @@ def _host_flat_outputs(srcs):
 def _host_flat_run(fo, ptrs):
     """tips_fused_allreduce_host_flat of the host tensors at `ptrs` into an output set of `fo`;
     returns the outputs (views of the set's flat buffer)."""
-    if ptrs == fo.last[0]:
-        pp = fo.last[1]
+    last = fo.last  # (one read: another thread may replace it)
+    if ptrs == last[0]:
+        pp = last[1]
     else:
         pp = _lib.ptr_array(ptrs)
         fo.last = (ptrs, pp)
