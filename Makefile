@@ -1,11 +1,15 @@
-# Top-level build: the product library (libtips_hip.so, gfx950 only) and the oracle checkers.
+# Top-level build: the product library (libtips_hip.so, gfx950 only: exactly the C-ABI of
+# include/tips_hip.h), the development library (tools/lib/libtips_hip_dev.so: the same runtime plus
+# include/tips_hip_dev.h's simulators, self-tests and tuning sweeps, -DTIPS_DEV) and the oracle checkers.
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 LIB      := tips_amd/lib/libtips_hip.so
 SRCS     := tips_amd/csrc/kernels.hip tips_amd/csrc/runtime.cc tips_amd/csrc/rt_common.cc tips_amd/csrc/plan.cc tips_amd/csrc/schedules.cc \
             tips_amd/csrc/fusion.cc tips_amd/csrc/host_staging.cc tips_amd/csrc/control.cc tips_amd/csrc/negotiate.cc tips_amd/csrc/peer.cc \
             tips_amd/csrc/bootstrap.cc
-HDRS     := tips_amd/csrc/kernels.h tips_amd/csrc/rt.h tips_amd/csrc/net.h tips_amd/csrc/plan.h include/tips_hip.h
+HDRS     := tips_amd/csrc/kernels.h tips_amd/csrc/rt.h tips_amd/csrc/net.h tips_amd/csrc/plan.h include/tips_hip.h \
+            include/tips_hip_dev.h
+DEVLIB   := tools/lib/libtips_hip_dev.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-result -fvisibility=hidden
 
 CRASH    := tools/lib/libcrashline.so
@@ -16,7 +20,7 @@ FAST     := tips_amd/_fast$(shell python3 -c "import sysconfig; print(sysconfig.
 TORCH    := $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
 PYINC    := $(shell python3 -c "import sysconfig; print(sysconfig.get_paths()['include'])")
 
-all: $(LIB) $(FAST) $(CRASH) $(REPRO) oracle tsan tools/cpu_sum_bench
+all: $(LIB) $(DEVLIB) $(FAST) $(CRASH) $(REPRO) oracle tsan tools/cpu_sum_bench
 
 # the Python mirror's list helper (tips_amd._fast: tensor pointers / counts in C++), torch headers
 $(FAST): tips_amd/csrc/pyfast.cc
@@ -36,9 +40,21 @@ build/obj/%.o: tips_amd/csrc/% $(HDRS)
 	@mkdir -p build/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+# -Bsymbolic: each library calls its own entry points (the development library is loaded beside the
+# product one in test processes, RTLD_LOCAL: its internal calls must not bind to the product's copies)
 $(LIB): $(OBJS)
 	@mkdir -p tips_amd/lib
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -lrccl
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-Bsymbolic -o $@ $(OBJS) -lrccl
+
+DEV_OBJS := $(patsubst tips_amd/csrc/%,build/dev/%.o,$(SRCS))
+
+build/dev/%.o: tips_amd/csrc/% $(HDRS)
+	@mkdir -p build/dev
+	$(HIPCC) $(HIPFLAGS) -DTIPS_DEV -c -o $@ $<
+
+$(DEVLIB): $(DEV_OBJS)
+	@mkdir -p tools/lib
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-Bsymbolic -o $@ $(DEV_OBJS) -lrccl
 
 # replayed-plan checks through the C-ABI on /opt/rocm's runtime (tests/test_gpu_graphs.py)
 tools/_bin/graph_repro: tools/graph_repro.cc $(LIB) include/tips_hip.h
@@ -77,7 +93,7 @@ CLANG     := /opt/rocm/lib/llvm/bin/clang
 build/tsan/%.o: tips_amd/csrc/% $(HDRS)
 	@mkdir -p build/tsan
 	$(HIPCC) --offload-arch=$(ARCH) -O1 -g -std=c++17 -fPIC -fno-gpu-flush-denormals-to-zero -fvisibility=hidden \
-	  -Xarch_host -fsanitize=thread -c -o $@ $<
+	  -DTIPS_DEV -Xarch_host -fsanitize=thread -c -o $@ $<
 
 $(TSAN_LIB): $(TSAN_OBJS)
 	@mkdir -p tools/lib
@@ -106,8 +122,8 @@ oracle:
 
 tools: tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
 
-tools/peer_mem_probe: tools/peer_mem_probe.cc $(LIB)
-	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../tips_amd/lib'
+tools/peer_mem_probe: tools/peer_mem_probe.cc $(DEVLIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Iinclude -o $@ $< -Ltools/lib -ltips_hip_dev -Wl,-rpath,'$$ORIGIN/lib'
 
 tools/ipc_probe: tools/ipc_probe.cc
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -o $@ $<
@@ -115,12 +131,12 @@ tools/ipc_probe: tools/ipc_probe.cc
 tools/cpu_sum_bench: tools/cpu_sum_bench.c
 	gcc -O3 -fopenmp -o $@ $<
 
-tools/sum_sweep: tools/sum_sweep.cc $(LIB)
-	$(HIPCC) -O2 -std=c++17 -o $@ $< -Itips_amd -Ltips_amd/lib -ltips_hip -Wl,-rpath,'$$ORIGIN/../tips_amd/lib'
+tools/sum_sweep: tools/sum_sweep.cc $(DEVLIB)
+	$(HIPCC) -O2 -std=c++17 -o $@ $< -Iinclude -Ltools/lib -ltips_hip_dev -Wl,-rpath,'$$ORIGIN/lib'
 
 clean:
-	rm -rf build/obj
-	rm -f $(LIB) $(REPRO) tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
+	rm -rf build/obj build/dev
+	rm -f $(LIB) $(DEVLIB) $(REPRO) tools/sum_sweep tools/cpu_sum_bench tools/peer_mem_probe tools/ipc_probe
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle tools repro clean tsan

@@ -69,17 +69,19 @@ def stream():
 
 
 def simulate(kind, ins, dtype, inplace=False, transport=0):
+    """p virtual ranks' plans on this one GPU through the development library's simulators
+    (include/tips_hip_dev.h): the same plans, kernels and stream order as the RCCL executor."""
     import torch
     from tips_amd import _lib
-    _lib.call("tips_set_sim_transport", transport)
+    _lib.dev_call("tips_set_sim_transport", transport)
     devs = [to_dev(x) for x in ins]
     outs = devs if inplace else [torch.empty_like(d) for d in devs]
     pi, _k1 = _lib.ptr_array([d.data_ptr() for d in devs])
     po, _k2 = _lib.ptr_array([o.data_ptr() for o in outs])
     fn = {"ring": "tips_ring_simulate", "direct": "tips_direct_simulate", "oneshot": "tips_oneshot_simulate"}[kind]
     try:
-        _lib.call(fn, po, pi, len(ins), ins[0].size, dtype, stream())
+        _lib.dev_call(fn, po, pi, len(ins), ins[0].size, dtype, stream())
         torch.cuda.synchronize()
     finally:
-        _lib.call("tips_set_sim_transport", 0)
+        _lib.dev_call("tips_set_sim_transport", 0)
     return [from_dev(o, dtype) for o in outs]

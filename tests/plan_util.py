@@ -27,7 +27,7 @@ RING, DIRECT, ONESHOT = 0, 1, 3
 
 def dump(algo, p, rank, n, dtype, depth=0):
     from tips_amd import _lib
-    L = _lib.lib()
+    L = _lib.dev()
     need = L.tips_schedule_plan(algo, p, rank, n, dtype, depth, None, 0)
     assert need > 0, _lib.last_error()
     buf = (ctypes.c_int64 * need)()

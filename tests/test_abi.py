@@ -1,5 +1,6 @@
 """The C-ABI boundary without a GPU: the library loads, exports every symbol
-include/tips_hip.h declares, the Python binding declares each of them, and the
+include/tips_hip.h declares and nothing else, the Python binding declares each of them, the
+development library (include/tips_hip_dev.h) exports the product symbols plus its own, and the
 argument / lifecycle error paths behave (no compute calls here)."""
 import ctypes
 import multiprocessing as mp
@@ -13,10 +14,11 @@ import pytest
 from conftest import REPO
 
 HEADER = os.path.join(REPO, "include", "tips_hip.h")
+DEV_HEADER = os.path.join(REPO, "include", "tips_hip_dev.h")
 
 
-def header_functions():
-    src = open(HEADER).read()
+def header_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(tips_\w+)\s*\(", src)))
 
@@ -40,6 +42,44 @@ def test_python_binding_declares_every_symbol():
     from tips_amd import _lib
     declared = {n for n, _, _ in _lib._SIGNATURES}
     assert set(header_functions()) == declared
+    assert set(header_functions(DEV_HEADER)) == {n for n, _, _ in _lib._DEV_SIGNATURES}
+
+
+def _exported(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if " T " in l}
+
+
+def test_product_and_development_exports():
+    """The product library exports exactly include/tips_hip.h (the drop-in boundary: the reference's
+    five lifecycle symbols of operations.h:7-21 plus the data path); the simulators, self-tests and
+    tuning sweeps live in tools/lib/libtips_hip_dev.so only, which exports the product symbols too
+    (one complete runtime) and loads beside the product library without touching it."""
+    import shutil
+    if not shutil.which("nm"):
+        pytest.skip("no nm")
+    prod = _exported(os.path.join(REPO, "tips_amd", "lib", "libtips_hip.so"))
+    dev = _exported(os.path.join(REPO, "tools", "lib", "libtips_hip_dev.so"))
+    dev_only = set(header_functions(DEV_HEADER))
+    assert prod == set(header_functions())
+    assert not prod & dev_only
+    assert dev == prod | dev_only
+    assert len(dev_only) == 12  # simulators (4), self-tests (2), sweeps (4), tips_schedule_plan, tile table
+    from tips_amd import _lib
+    D, L = _lib.dev(), _lib.lib()
+    assert D is not L and not hasattr_c(L, "tips_ring_simulate") and hasattr_c(D, "tips_ring_simulate")
+    # separate runtimes: the development library's state is its own
+    assert D.tips_size() == -1 and L.tips_set_algorithm(_lib.ALGO_RING) == 0 and D.tips_get_algorithm() != _lib.ALGO_RING
+    L.tips_set_algorithm(_lib.ALGO_AUTO)
+
+
+def hasattr_c(handle, name):
+    try:
+        getattr(handle, name)
+        return True
+    except AttributeError:
+        return False
 
 
 def test_lifecycle_before_init():
@@ -343,6 +383,4 @@ def test_host_pool_runs_every_job_once(threads, jobs):
     of the next against the old count, and the caller waited forever (a GPU test with 256-B pieces,
     ~800 runs per call, hung in it)."""
     from tips_amd import _lib
-    L = _lib.lib()
-    rc = L.tips_host_pool_selftest(threads, 20000, jobs)
-    assert rc == 0, _lib.last_error()
+    assert _lib.dev_call("tips_host_pool_selftest", threads, 20000, jobs) == 0

@@ -21,7 +21,7 @@ LANES = 256
 
 def table(counts, ins, outs, dtype):
     from tips_amd import _lib
-    L = _lib.lib()
+    L = _lib.dev()
     n = len(counts)
     c = (ctypes.c_int64 * n)(*counts)
     pi = (ctypes.c_int64 * n)(*ins)

@@ -127,7 +127,7 @@ def test_empty_and_single_rank(gpu, oracle):
     assert np.array_equal(simulate("direct", [x], F32)[0], x)
     from tips_amd import _lib
     pp, _k = _lib.ptr_array([0, 0])
-    assert _lib.lib().tips_ring_simulate(pp, pp, 2, 0, F32, None) == 0
+    assert _lib.dev().tips_ring_simulate(pp, pp, 2, 0, F32, None) == 0
 
 
 @pytest.mark.slow
@@ -581,7 +581,7 @@ def test_config3_full_size_8ranks(gpu, kind):
     pi, _k1 = _lib.ptr_array([x.data_ptr() for x in ins])
     po, _k2 = _lib.ptr_array([o.data_ptr() for o in outs])
     fn = "tips_ring_simulate" if kind == "ring" else "tips_direct_simulate"
-    _lib.call(fn, po, pi, p, n, F32, torch.cuda.current_stream().cuda_stream)
+    _lib.dev_call(fn, po, pi, p, n, F32, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     exp = torch.empty_like(ins[0])
     if kind == "ring":

@@ -81,7 +81,7 @@ def test_every_sum_variant_is_exact(gpu, oracle, mode, unroll, nt, threads):
     a, b = rand(F32, n, rng), rand(F32, n, rng)
     da, db = to_dev(a), to_dev(b)
     dc = torch.empty_like(da)
-    _lib.call("tips_sum_variant", dc.data_ptr(), da.data_ptr(), db.data_ptr(), n, F32, mode, unroll, nt, 512,
+    _lib.dev_call("tips_sum_variant", dc.data_ptr(), da.data_ptr(), db.data_ptr(), n, F32, mode, unroll, nt, 512,
               threads, stream())
     torch.cuda.synchronize()
     assert same_bits(from_dev(dc, F32), oracle.sum2(a, b), F32)
@@ -171,7 +171,7 @@ def test_xfer_segments(gpu, nseg, shift):
     pd, _k1 = _lib.ptr_array([dst.data_ptr() + x for x in offs])
     ps, _k2 = _lib.ptr_array([src.data_ptr() + x for x in offs])
     pb, _k3 = _lib.i64_array(sizes)
-    _lib.call("tips_xfer", pd, ps, pb, nseg, stream())
+    _lib.dev_call("tips_xfer", pd, ps, pb, nseg, stream())
     torch.cuda.synchronize()
     d, s = dst.cpu().numpy(), src.cpu().numpy()
     mask = np.zeros(len(d), dtype=bool)

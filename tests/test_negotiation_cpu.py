@@ -24,7 +24,7 @@ def _worker(rank, size, port, requests, q, env=None, delay=0.0, stats=None):
     os.environ.update(env or {})  # (the join's test knobs are read once, at the first join)
     time.sleep(delay)
     from tips_amd import _lib
-    L = _lib.lib()
+    L = _lib.dev()  # (tips_negotiation_selftest: the development library, tips_hip_dev.h)
     out = ctypes.create_string_buffer(1 << 16)
     rc = L.tips_negotiation_selftest(rank, size, b"127.0.0.1", port, requests.encode(), out, len(out))
     a, b = ctypes.c_int64(), ctypes.c_int64()
@@ -263,7 +263,7 @@ def test_debug_state_reports_the_threads():
     import threading
     import time
     from tips_amd import _lib
-    L = _lib.lib()
+    L = _lib.dev()  # (tips_negotiation_selftest: the development library, tips_hip_dev.h)
     b = ctypes.create_string_buffer(4096)
     assert L.tips_debug_state(b, len(b)) == 0 and b.value == b"no negotiation"
     out = ctypes.create_string_buffer(1 << 16)

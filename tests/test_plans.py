@@ -143,7 +143,7 @@ def test_interpreted_plans_match_oracle(oracle, algo, dtype, p, n, K):
 
 def test_plan_argument_errors():
     from tips_amd import _lib
-    L = _lib.lib()
+    L = _lib.dev()
     assert L.tips_schedule_plan(pu.DIRECT, 17, 0, 100, F32, 1, None, 0) == -1  # fold takes <= 16 sources
     assert L.tips_schedule_plan(pu.RING, 1, 0, 100, F32, 1, None, 0) == -1
     assert L.tips_schedule_plan(pu.RING, 4, 4, 100, F32, 1, None, 0) == -1

@@ -12,6 +12,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TIPS_HIP_LIB", os.path.join(_HERE, "lib", "libtips_hip.so"))
+# the development library (include/tips_hip_dev.h): tests, tuning sweeps and probes only
+DEV_LIB_PATH = os.environ.get("TIPS_HIP_DEV_LIB", os.path.join(os.path.dirname(_HERE), "tools", "lib",
+                                                                 "libtips_hip_dev.so"))
 
 # dtype codes (include/tips_hip.h enum tips_dtype; 0-3 = collective_messages.fbs:17-23)
 FLOAT32, FLOAT64, INT32, INT64, FLOAT16, BFLOAT16 = 0, 1, 2, 3, 4, 5
@@ -110,8 +113,6 @@ _SIGNATURES = [
     ("tips_on_done", ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     ("tips_net_stats", ctypes.c_int, [_c_i64_p, _c_i64_p]),
     ("tips_debug_state", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
-    ("tips_fusion_tile_table", ctypes.c_int64,
-     [_c_i64_p, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p, _c_i64_p, ctypes.c_int64, _c_i64_p, _c_i64_p]),
     ("tips_wait", ctypes.c_int, [ctypes.c_int64]),
     ("tips_enqueue_broadcast", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -119,9 +120,6 @@ _SIGNATURES = [
     ("tips_enqueue_allgather", ctypes.c_int64,
      [ctypes.c_char_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
       ctypes.c_void_p, _c_i64_p]),
-    ("tips_host_pool_selftest", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
-    ("tips_negotiation_selftest", ctypes.c_int,
-     [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
     ("tips_set_algorithm", ctypes.c_int, [ctypes.c_int]),
     ("tips_get_algorithm", ctypes.c_int, []),
     ("tips_resolve_algorithm", ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),
@@ -131,6 +129,21 @@ _SIGNATURES = [
     ("tips_graph_stats", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     ("tips_replay_order_stats", ctypes.c_int, [_c_i64_p, _c_i64_p]),
+    ("tips_schedule_shape", ctypes.c_int,
+     [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), _c_i64_p]),
+    ("tips_chunk_bounds", ctypes.c_int,
+     [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p]),
+    ("tips_bootstrap_broadcast", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
+]
+
+# include/tips_hip_dev.h: libtips_hip_dev.so's entry points beyond the product C-ABI (tests, sweeps)
+_DEV_SIGNATURES = [
+    ("tips_fusion_tile_table", ctypes.c_int64,
+     [_c_i64_p, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p, _c_i64_p, ctypes.c_int64, _c_i64_p, _c_i64_p]),
+    ("tips_host_pool_selftest", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("tips_negotiation_selftest", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
     ("tips_ring_simulate", ctypes.c_int,
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_oneshot_simulate", ctypes.c_int,
@@ -146,14 +159,8 @@ _SIGNATURES = [
     ("tips_xfer", ctypes.c_int, [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_void_p]),
     ("tips_copy_tiles_variant", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]),
-    ("tips_schedule_shape", ctypes.c_int,
-     [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), _c_i64_p]),
-    ("tips_chunk_bounds", ctypes.c_int,
-     [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p]),
     ("tips_schedule_plan", ctypes.c_int64,
      [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _c_i64_p, ctypes.c_int64]),
-    ("tips_bootstrap_broadcast", ctypes.c_int,
-     [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
 ]
 
 
@@ -196,6 +203,43 @@ def lib():
                 fn.argtypes = args
             _lib = handle
     return _lib
+
+
+_dev = None
+
+
+def dev():
+    """The development library (include/tips_hip_dev.h: simulators, self-tests, tuning sweeps),
+    loaded once beside the product library. It is a second, complete copy of the runtime with
+    state of its own, loaded RTLD_LOCAL and linked -Bsymbolic, so nothing in it binds to the
+    product library's symbols or they to it: tests call its extra entry points through it
+    (dev_call), never a job's collectives."""
+    global _dev
+    if _dev is not None:
+        return _dev
+    _share_torch_runtime()
+    with _lock:
+        if _dev is None:
+            if not os.path.exists(DEV_LIB_PATH):
+                raise TipsLibraryError("libtips_hip_dev.so not found at %s — build it with `make`" % DEV_LIB_PATH)
+            try:
+                handle = ctypes.CDLL(DEV_LIB_PATH, mode=ctypes.RTLD_LOCAL)
+            except OSError as e:
+                raise TipsLibraryError("cannot load %s: %s" % (DEV_LIB_PATH, e)) from e
+            for name, res, args in _SIGNATURES + _DEV_SIGNATURES:
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _dev = handle
+    return _dev
+
+
+def dev_call(name, *args):
+    """Call development-library function `name` and raise on a negative status (its own last error)."""
+    code = getattr(dev(), name)(*args)
+    if code < 0:
+        raise TipsError(name, code, dev().tips_last_error().decode(errors="replace"))
+    return code
 
 
 def last_error():

@@ -22,10 +22,15 @@
 // through a page-locked ring - unless this layout saw the same pointer set recently
 // (LRU of 16 per layout), in which case nothing is uploaded. tips_fusion_stats counts both caches.
 //
-// Streams: every device operation of a call runs on the two fusion streams (pack / unpack on
-// fuse_stream, bucket allreduces on bucket_stream), joined with the caller's stream at entry and
-// exit, so calls from different caller streams never write a shared bucket slot concurrently.
-// Nothing here synchronises the device.
+// Streams: a call's pack / unpack launches and table uploads run on the CALLER's stream (the
+// "work stream"; TIPS_FUSION_CALLER_STREAM=0: on the library's fuse_stream, joined with the caller
+// both ways as rounds 1-3 did), its bucket allreduces at N > 1 on bucket_stream, forked from and
+// joined back to the work stream. The slots and tables are shared by every call, so the calls form
+// one chain: each records an event at its end on its work stream, and a call from another stream
+// first waits for it (fusion_enter / fusion_leave). A step from one stream then crosses no queue
+// at all at one rank (the two joins per call cost ~25 us of cross-queue latency per step: config 4
+// eager 87 us vs 62 us replayed as one graph, profiles/r03/r_bench_fused1000.jsonl). Nothing here
+// synchronises the device.
 #include <string.h>
 
 #include <algorithm>
@@ -178,8 +183,26 @@ struct FusionCache {
 
 namespace {
 
+// the chain's event, recorded now if the last call left it unrecorded (see fusion_leave)
+int chain_event(State& st) {
+  if (st.fuse_chain_lazy) {
+    HIP_TRY(hipEventRecord(st.ev_fuse_chain, st.fuse_chain_stream));
+    st.fuse_chain_lazy = false;
+  }
+  return 0;
+}
+
+// Table memory (hipMallocAsync, the uploads, hipFreeAsync) lives on the library's fuse_stream, behind
+// every earlier fused call (the chain's event): a table freed or refilled there was last read by an
+// earlier call. A call that built a table waits for the upload on its work stream (find_table).
+// Only cache misses touch fuse_stream, so a call that finds its table crosses no queue.
+hipStream_t table_stream(State& st) {
+  if (st.fuse_chain_valid && chain_event(st) == 0) (void)hipStreamWaitEvent(st.fuse_stream, st.ev_fuse_chain, 0);
+  return st.fuse_stream;
+}
+
 void free_table(State& st, Table* t) {
-  if (t->dev) (void)hipFreeAsync(t->dev, st.fuse_stream);  // behind its last use on fuse_stream
+  if (t->dev) (void)hipFreeAsync(t->dev, table_stream(st));  // behind its last use: the chain
   delete t;
 }
 
@@ -188,7 +211,7 @@ void free_layout(State& st, Layout* L) {
   delete L;
 }
 
-// Host -> device on fuse_stream through a page-locked slot (the pageable path would block).
+// Host -> device on the work stream through a page-locked slot (the pageable path would block).
 // A slot is reused once the copy that last read it has run; with 4 slots that wait is rare.
 int upload(State& st, FusionCache& fc, void* dev, const void* src, size_t bytes) {
   FusionCache::Upload& u = fc.up[fc.next_up];
@@ -204,8 +227,9 @@ int upload(State& st, FusionCache& fc, void* dev, const void* src, size_t bytes)
   }
   if (!u.done) HIP_TRY(hipEventCreateWithFlags(&u.done, hipEventDisableTiming));
   memcpy(u.host, src, bytes);
-  HIP_TRY(hipMemcpyAsync(dev, u.host, bytes, hipMemcpyHostToDevice, st.fuse_stream));
-  HIP_TRY(hipEventRecord(u.done, st.fuse_stream));
+  const hipStream_t ws = table_stream(st);
+  HIP_TRY(hipMemcpyAsync(dev, u.host, bytes, hipMemcpyHostToDevice, ws));
+  HIP_TRY(hipEventRecord(u.done, ws));
   u.used = true;
   return 0;
 }
@@ -342,12 +366,17 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
       L.tables.erase(lru);
     }
   }
+  if (st.fuse_capturing) {
+    fail(TIPS_ERR_INVALID_ARG, "fusion: a fused call under stream capture must find its pointer table built: make "
+                               "the same call once before the capture");
+    return nullptr;
+  }
   const int nseg = (int)L.seg_tensor.size();
   const int ntab = mode == kSlot ? 2 : 1;
   const size_t per = 2 * (size_t)L.ntiles + nseg;  // one table: [2 records per tile | segment records]
   if (!t) {
     t = new Table();
-    if (hipMallocAsync((void**)&t->dev, ntab * per * sizeof(CopySeg), st.fuse_stream) != hipSuccess) {
+    if (hipMallocAsync((void**)&t->dev, ntab * per * sizeof(CopySeg), table_stream(st)) != hipSuccess) {
       delete t;
       fail(TIPS_ERR_HIP, "fusion: hipMallocAsync of a segment table failed");
       return nullptr;
@@ -367,7 +396,8 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
   fill_records(L, mode, items, base, &rec);
   t->stamp = ++fc.clock;
   fc.tables_built++;
-  if (upload(st, fc, t->dev, rec.data(), rec.size() * sizeof(CopySeg)) != 0) {
+  if (upload(st, fc, t->dev, rec.data(), rec.size() * sizeof(CopySeg)) != 0 ||
+      (st.fuse_in_call && join(st.fuse_ws, st.fuse_stream, st.ev_fuse_table) != 0)) {  // the launches after it
     t->hash = 0;  // (a failed upload must never be matched)
     t->ins.clear();
     return nullptr;
@@ -380,6 +410,10 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
 // after the fusion streams have finished with them.
 int ensure_slots(State& st, FusionCache& fc, int64_t threshold) {
   if (threshold == st.fusion_threshold && st.fusion.p) return 0;
+  if (st.fuse_chain_valid) {
+    TRY(chain_event(st));
+    HIP_TRY(hipEventSynchronize(st.ev_fuse_chain));
+  }
   HIP_TRY(hipStreamSynchronize(st.fuse_stream));
   HIP_TRY(hipStreamSynchronize(st.bucket_stream));
   for (Layout* L : fc.layouts) {
@@ -404,6 +438,63 @@ int copy_tiles(const Layout& L, const Table& t, int table, int tile0, int ntiles
   return 0;
 }
 
+// A fused call's entry: the work stream (the caller's, or fuse_stream under
+// TIPS_FUSION_CALLER_STREAM=0) after the chain's previous call and after the caller's own work.
+// A call captured into a graph (torch.cuda.graph around it) stays out of the chain: the capture
+// may not wait for an event recorded outside it, and an event recorded inside it is a graph node,
+// not a point later calls could wait for; the graph's replays are ordered by the stream they are
+// launched on. Such a call must find its tables built (the same call made once before the
+// capture, as CUDA-graph users warm up), since uploading them would be captured too.
+int fusion_enter(State& st, hipStream_t user, hipStream_t* ws) {
+  if (!st.ev_fuse_chain) HIP_TRY(hipEventCreateWithFlags(&st.ev_fuse_chain, hipEventDisableTiming));
+  *ws = env_i64("TIPS_FUSION_CALLER_STREAM", 1) != 0 ? user : st.fuse_stream;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(user, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    cs = hipStreamCaptureStatusNone;
+  }
+  st.fuse_capturing = cs != hipStreamCaptureStatusNone;
+  if (!st.fuse_capturing && st.fuse_chain_valid && st.fuse_chain_stream != *ws) {
+    TRY(chain_event(st));
+    HIP_TRY(hipStreamWaitEvent(*ws, st.ev_fuse_chain, 0));
+  }
+  if (*ws != user) TRY(join(*ws, user, st.ev_start));
+  st.fuse_ws = *ws;
+  st.fuse_in_call = true;
+  return 0;
+}
+
+// ... and its exit: the caller after the work stream, the chain's event at the end of the call.
+// lazy (tips_fused_pack_bucket, a measurement entry whose launches are timed back to back): the
+// event is recorded only when a later call needs it - a call from another stream, a table freed
+// behind the chain, new slots - on the stream this call used, which must then still exist.
+int fusion_leave(State& st, hipStream_t user, bool lazy = false) {
+  const hipStream_t ws = st.fuse_ws;
+  st.fuse_ws = nullptr;
+  st.fuse_in_call = false;
+  if (ws != user) TRY(join(user, ws, st.ev_done));
+  if (st.fuse_capturing) {
+    st.fuse_capturing = false;
+    return 0;
+  }
+  st.fuse_chain_stream = ws;
+  st.fuse_chain_valid = true;
+  st.fuse_chain_lazy = lazy && ws == user;
+  if (!st.fuse_chain_lazy) HIP_TRY(hipEventRecord(st.ev_fuse_chain, ws));
+  return 0;
+}
+
+// fusion_enter ... fusion_leave around `body(ws)`; the exit runs on failure too (the chain's event
+// then covers whatever the body queued)
+template <typename F>
+int in_fusion(State& st, hipStream_t user, F body, bool lazy = false) {
+  hipStream_t ws = nullptr;
+  TRY(fusion_enter(st, user, &ws));
+  const int rc = body(ws);
+  const int rc2 = fusion_leave(st, user, lazy);
+  return rc ? rc : rc2;
+}
+
 }  // namespace
 
 int64_t fusion_threshold_bytes() {
@@ -412,6 +503,12 @@ int64_t fusion_threshold_bytes() {
 
 void fusion_release(State& st) {
   FusionCache* fc = st.fusion_cache;
+  if (st.ev_fuse_chain) {
+    if (st.fuse_chain_valid && chain_event(st) == 0) (void)hipEventSynchronize(st.ev_fuse_chain);
+    (void)hipEventDestroy(st.ev_fuse_chain);
+    st.ev_fuse_chain = nullptr;
+    st.fuse_chain_valid = false;
+  }
   if (!fc) return;
   for (Layout* L : fc->layouts) free_layout(st, L);
   if (st.fuse_stream) (void)hipStreamSynchronize(st.fuse_stream);
@@ -459,60 +556,60 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
   if (identity && in_place) return 0;
   std::vector<int64_t> counts((size_t)n);
   for (int i = 0; i < n; i++) counts[i] = items[i].count;
-  TRY(join(st.fuse_stream, user, st.ev_start));  // inputs ready (the bucket stream waits for it too)
-  if (st.size > 1) HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
-  Layout* L = find_layout(st, fc, counts.data(), n, dtype, threshold, copy_tile_bytes(),
-                          env_i64("TIPS_FUSION_BALANCE", 1) != 0);
-  if (!L) return TIPS_ERR_HIP;
-  if (L->seg_tensor.empty()) return join(user, st.fuse_stream, st.ev_done);
-  const int64_t es = tips::dtype_size(dtype);
-  if (identity) {  // one rank, out of place: every tensor copied in -> out, one launch over the whole space
-    Table* t = find_table(st, fc, *L, kCopy, items, n, nullptr);
-    if (!t) return TIPS_ERR_HIP;
-    TRY(copy_tiles(*L, *t, 0, 0, L->ntiles, st.fuse_stream));
-    return join(user, st.fuse_stream, st.ev_done);
-  }
-  const int B = (int)L->buckets.size();
-  Table* t = B ? find_table(st, fc, *L, kSlot, items, n, st.fusion.p) : nullptr;
-  if (B && !t) return TIPS_ERR_HIP;
-  auto pack = [&](int b) { return copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, st.fuse_stream); };
-  auto unpack = [&](int b) { return copy_tiles(*L, *t, 1, L->buckets[b].tile0, L->buckets[b].ntiles, st.fuse_stream); };
-  auto slot = [&](int b) { return (char*)st.fusion.p + (int64_t)(b % 2) * threshold; };
-  if (st.size == 1) {  // TIPS_FUSION_MEASURE_PACK: pack, (identity), unpack, in stream order
-    for (int b = 0; b < B; b++) {
+  return in_fusion(st, user, [&](hipStream_t ws) -> int {
+    if (st.size > 1) {  // inputs ready for the bucket stream too (the direct tensors start at once)
+      HIP_TRY(hipEventRecord(st.ev_start, ws));
+      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
+    }
+    Layout* L = find_layout(st, fc, counts.data(), n, dtype, threshold, copy_tile_bytes(),
+                            env_i64("TIPS_FUSION_BALANCE", 1) != 0);
+    if (!L) return TIPS_ERR_HIP;
+    if (L->seg_tensor.empty()) return 0;
+    const int64_t es = tips::dtype_size(dtype);
+    if (identity) {  // one rank, out of place: every tensor copied in -> out, one launch over the whole space
+      Table* t = find_table(st, fc, *L, kCopy, items, n, nullptr);
+      if (!t) return TIPS_ERR_HIP;
+      return copy_tiles(*L, *t, 0, 0, L->ntiles, ws);
+    }
+    const int B = (int)L->buckets.size();
+    Table* t = B ? find_table(st, fc, *L, kSlot, items, n, st.fusion.p) : nullptr;
+    if (B && !t) return TIPS_ERR_HIP;
+    auto pack = [&](int b) { return copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, ws); };
+    auto unpack = [&](int b) { return copy_tiles(*L, *t, 1, L->buckets[b].tile0, L->buckets[b].ntiles, ws); };
+    auto slot = [&](int b) { return (char*)st.fusion.p + (int64_t)(b % 2) * threshold; };
+    if (st.size == 1) {  // TIPS_FUSION_MEASURE_PACK: pack, (identity), unpack, in stream order
+      for (int b = 0; b < B; b++) {
+        TRY(pack(b));
+        TRY(unpack(b));
+      }
+      for (int i : L->direct) TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, ws));
+      return 0;
+    }
+    // bucket stream: the direct tensors first (nothing to pack: their exchange starts at once and
+    //                overlaps pack(0)), then allreduce(b) after pack(b)
+    // work stream:   pack(0) pack(1) | unpack(0) pack(2) | unpack(1) pack(3) | ... unpack(B-1);
+    //                unpack(b) after allreduce(b); pack(b+2) reuses slot b % 2 after unpack(b)
+    for (int i : L->direct) TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, st.bucket_stream));
+    TRY(st.fuse_ev.ensure(2 * (size_t)B));
+    hipEvent_t* packed = st.fuse_ev.ev.data();
+    hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
+    for (int b = 0; b < std::min(B, 2); b++) {
       TRY(pack(b));
+      HIP_TRY(hipEventRecord(packed[b], ws));
+    }
+    for (int b = 0; b < B; b++) {
+      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[b], 0));
+      TRY(allreduce_device(st, slot(b), slot(b), L->buckets[b].bytes / es, dtype, st.bucket_stream));
+      HIP_TRY(hipEventRecord(reduced[b], st.bucket_stream));
+      HIP_TRY(hipStreamWaitEvent(ws, reduced[b], 0));
       TRY(unpack(b));
+      if (b + 2 < B) {
+        TRY(pack(b + 2));
+        HIP_TRY(hipEventRecord(packed[b + 2], ws));
+      }
     }
-    for (int i : L->direct)
-      TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, st.fuse_stream));
-    return join(user, st.fuse_stream, st.ev_done);
-  }
-  // bucket stream: the direct tensors first (nothing to pack: their exchange starts at once and
-  //                overlaps pack(0)), then allreduce(b) after pack(b)
-  // fuse stream:   pack(0) pack(1) | unpack(0) pack(2) | unpack(1) pack(3) | ... unpack(B-1);
-  //                unpack(b) after allreduce(b); pack(b+2) reuses slot b % 2 after unpack(b)
-  for (int i : L->direct) TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, st.bucket_stream));
-  TRY(st.fuse_ev.ensure(2 * (size_t)B));
-  hipEvent_t* packed = st.fuse_ev.ev.data();
-  hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
-  for (int b = 0; b < std::min(B, 2); b++) {
-    TRY(pack(b));
-    HIP_TRY(hipEventRecord(packed[b], st.fuse_stream));
-  }
-  for (int b = 0; b < B; b++) {
-    HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[b], 0));
-    TRY(allreduce_device(st, slot(b), slot(b), L->buckets[b].bytes / es, dtype, st.bucket_stream));
-    HIP_TRY(hipEventRecord(reduced[b], st.bucket_stream));
-    HIP_TRY(hipStreamWaitEvent(st.fuse_stream, reduced[b], 0));
-    TRY(unpack(b));
-    if (b + 2 < B) {
-      TRY(pack(b + 2));
-      HIP_TRY(hipEventRecord(packed[b + 2], st.fuse_stream));
-    }
-  }
-  TRY(join(user, st.fuse_stream, st.ev_done));
-  TRY(join(user, st.bucket_stream, st.ev_comp_done));
-  return 0;
+    return join(ws, st.bucket_stream, st.ev_comp_done);  // (the direct tensors' allreduces too)
+  });
 }
 
 // flat = SUM over ranks of the inputs, tensor i at its layout offset: pack(b) straight into the
@@ -524,37 +621,38 @@ int fused_allreduce_flat(State& st, const BatchItem* items, int n, int dtype, vo
   const int64_t threshold = fusion_threshold_bytes();
   std::vector<int64_t> counts((size_t)n);
   for (int i = 0; i < n; i++) counts[i] = items[i].count;
-  TRY(join(st.fuse_stream, user, st.ev_start));
-  if (st.size > 1) HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
-  Layout* L = find_layout(st, fc, counts.data(), n, dtype, threshold, copy_tile_bytes(),
-                          env_i64("TIPS_FUSION_BALANCE", 1) != 0);
-  if (!L) return TIPS_ERR_HIP;
-  if (L->seg_tensor.empty()) return join(user, st.fuse_stream, st.ev_done);
-  Table* t = find_table(st, fc, *L, kFlat, items, n, flat);
-  if (!t) return TIPS_ERR_HIP;
-  const int64_t es = tips::dtype_size(dtype);
-  const bool measure = st.size == 1 && env_i64("TIPS_FUSION_MEASURE_PACK", 0);
-  if (st.size == 1 && !measure) {  // one rank: the identity - every tensor copied into place, one launch
-    TRY(copy_tiles(*L, *t, 0, 0, L->ntiles, st.fuse_stream));
-    return join(user, st.fuse_stream, st.ev_done);
-  }
-  const int B = (int)L->buckets.size();
-  hipStream_t red = st.size > 1 ? st.bucket_stream : st.fuse_stream;
-  for (int i : L->direct)
-    TRY(allreduce_device(st, items[i].in, (char*)flat + L->off[i], items[i].count, dtype, red));
-  TRY(st.fuse_ev.ensure((size_t)B));
-  for (int b = 0; b < B; b++) {
-    TRY(copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, st.fuse_stream));
+  return in_fusion(st, user, [&](hipStream_t ws) -> int {
     if (st.size > 1) {
-      HIP_TRY(hipEventRecord(st.fuse_ev.ev[b], st.fuse_stream));
-      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.fuse_ev.ev[b], 0));
-      char* p = (char*)flat + L->buckets[b].off;
-      TRY(allreduce_device(st, p, p, L->buckets[b].bytes / es, dtype, st.bucket_stream));
+      HIP_TRY(hipEventRecord(st.ev_start, ws));
+      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
     }
-  }
-  TRY(join(user, st.fuse_stream, st.ev_done));
-  if (st.size > 1) TRY(join(user, st.bucket_stream, st.ev_comp_done));
-  return 0;
+    Layout* L = find_layout(st, fc, counts.data(), n, dtype, threshold, copy_tile_bytes(),
+                            env_i64("TIPS_FUSION_BALANCE", 1) != 0);
+    if (!L) return TIPS_ERR_HIP;
+    if (L->seg_tensor.empty()) return 0;
+    Table* t = find_table(st, fc, *L, kFlat, items, n, flat);
+    if (!t) return TIPS_ERR_HIP;
+    const int64_t es = tips::dtype_size(dtype);
+    const bool measure = st.size == 1 && env_i64("TIPS_FUSION_MEASURE_PACK", 0);
+    if (st.size == 1 && !measure)  // one rank: the identity - every tensor copied into place, one launch
+      return copy_tiles(*L, *t, 0, 0, L->ntiles, ws);
+    const int B = (int)L->buckets.size();
+    hipStream_t red = st.size > 1 ? st.bucket_stream : ws;
+    for (int i : L->direct)
+      TRY(allreduce_device(st, items[i].in, (char*)flat + L->off[i], items[i].count, dtype, red));
+    TRY(st.fuse_ev.ensure((size_t)B));
+    for (int b = 0; b < B; b++) {
+      TRY(copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, ws));
+      if (st.size > 1) {
+        HIP_TRY(hipEventRecord(st.fuse_ev.ev[b], ws));
+        HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.fuse_ev.ev[b], 0));
+        char* p = (char*)flat + L->buckets[b].off;
+        TRY(allreduce_device(st, p, p, L->buckets[b].bytes / es, dtype, st.bucket_stream));
+      }
+    }
+    if (st.size > 1) TRY(join(ws, st.bucket_stream, st.ev_comp_done));
+    return 0;
+  });
 }
 
 }  // namespace rt
@@ -615,6 +713,7 @@ int tips_fused_allreduce_oop(const void* const* ins, void* const* outs, const in
   return fused_entry(ins, outs, counts, n, dtype, stream);
 }
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int64_t tips_fusion_tile_table(const int64_t* counts, int n, int dtype, const int64_t* ins, const int64_t* outs,
                                int64_t* records, int64_t cap, int64_t* ntiles, int64_t* tile_bytes) {
   TRY(check_dtype(dtype));
@@ -639,6 +738,7 @@ int64_t tips_fusion_tile_table(const int64_t* counts, int n, int dtype, const in
   }
   return (int64_t)rec.size();
 }
+#endif  // TIPS_DEV
 
 int64_t tips_fused_layout(const int64_t* counts, int n, int dtype, int64_t* offsets) {
   TRY(check_dtype(dtype));
@@ -687,13 +787,13 @@ int64_t tips_fused_pack_bucket(const void* const* ins, const int64_t* counts, in
   if (bucket >= B || !dst) return fail(TIPS_ERR_INVALID_ARG, "bucket %d of %d", bucket, B);
   const Bucket& bk = L->buckets[bucket];
   for (auto& it : items) it.out = (char*)dst - bk.off;
-  const int64_t built = fc.tables_built;
-  Table* t = find_table(st, fc, *L, kFlat, items.data(), n, (char*)dst - bk.off);
-  if (!t) return TIPS_ERR_HIP;
-  if (fc.tables_built != built) TRY(join((hipStream_t)stream, st.fuse_stream, st.ev_done));  // the upload first
-  TRY(copy_tiles(*L, *t, 0, bk.tile0, bk.ntiles, (hipStream_t)stream));
-  // the table's later reuse (an upload into it, hipFreeAsync) is ordered on fuse_stream: after this read
-  TRY(join(st.fuse_stream, (hipStream_t)stream, st.ev_start));
+  // in the fusion chain like any fused call (the table's upload and later reuse stay ordered), with
+  // the chain's event left to the next call that needs it: no marker between back-to-back launches
+  TRY(in_fusion(st, (hipStream_t)stream, [&](hipStream_t ws) -> int {
+    Table* t = find_table(st, fc, *L, kFlat, items.data(), n, (char*)dst - bk.off);
+    if (!t) return TIPS_ERR_HIP;
+    return copy_tiles(*L, *t, 0, bk.tile0, bk.ntiles, ws);
+  }, /*lazy=*/true));
   int64_t payload = 0;
   for (int i = 0; i < n; i++)
     if (L->bucket[i] == bucket) payload += counts[i] * tips::dtype_size(dtype);

@@ -119,7 +119,18 @@ int allreduce_host_pipelined(State& st, const char* in, char* out, int64_t n, in
 // aligned offsets), and each piece runs H2D -> allreduce in place in HBM -> D2H on three streams
 // while the threads pack the next piece and unpack the previous one.
 
-HostPool::HostPool(int nthreads) {
+// A fused host call runs its pool once per piece and direction, 20 fork-joins for config 5, each
+// a few hundred microseconds apart: a worker that blocked on the condition variable between them
+// pays a futex wake-up and a reschedule every time. Workers (and the caller waiting for its jobs)
+// therefore spin for TIPS_HOST_SPIN_US (300 us) before they block, which keeps them hot through one
+// call and idle between calls.
+namespace {
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+HostPool::HostPool(int nthreads) : spin_ns_(std::max<int64_t>(0, env_i64("TIPS_HOST_SPIN_US", 300)) * 1000) {
   for (int i = 1; i < nthreads; i++) th_.emplace_back([this] { worker(); });
 }
 
@@ -127,6 +138,7 @@ HostPool::~HostPool() {
   {
     std::lock_guard<std::mutex> l(m_);
     stop_ = true;
+    stop_pub_.store(true, std::memory_order_release);
   }
   cv_.notify_all();
   for (auto& t : th_) t.join();
@@ -155,6 +167,12 @@ void HostPool::worker() {
     uint64_t gen;
     std::vector<unsigned char> want;
     bool remask = false;
+    if (spin_ns_ > 0) {  // the next run of this call is usually a few hundred microseconds away
+      const int64_t t0 = now_ns();
+      while (gen_pub_.load(std::memory_order_acquire) == seen && !stop_pub_.load(std::memory_order_acquire) &&
+             now_ns() - t0 < spin_ns_)
+        _mm_pause();
+    }
     {
       std::unique_lock<std::mutex> l(m_);
       cv_.wait(l, [&] { return stop_ || gen_ != seen; });
@@ -197,9 +215,14 @@ void HostPool::run(int njobs, const std::function<void(int)>& fn) {
     pending_.store(njobs);
     gen = ++gen_ & 0xffffffffull;
     ticket_.store(gen << 32 | (uint64_t)njobs << 16);  // (published last: a claim of this run sees fn_, pending_)
+    gen_pub_.store(gen_, std::memory_order_release);
   }
   if (njobs > 1) cv_.notify_all();
   grab(gen);
+  if (spin_ns_ > 0) {  // the other workers' last jobs are usually microseconds from done
+    const int64_t t0 = now_ns();
+    while (pending_.load(std::memory_order_acquire) != 0 && now_ns() - t0 < spin_ns_) _mm_pause();
+  }
   std::unique_lock<std::mutex> l(m_);
   done_cv_.wait(l, [&] { return pending_.load() == 0; });
 }
@@ -513,6 +536,7 @@ using namespace tips::rt;
 
 extern "C" {
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int tips_host_pool_selftest(int nthreads, int runs, int njobs) {
   if (nthreads < 1 || nthreads > 64 || runs < 0 || njobs < 0) return fail(TIPS_ERR_INVALID_ARG, "bad arguments");
   HostPool pool(nthreads);
@@ -528,6 +552,7 @@ int tips_host_pool_selftest(int nthreads, int runs, int njobs) {
   }
   return 0;
 }
+#endif  // TIPS_DEV
 
 int tips_fused_allreduce_host(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype) {
   TRY(check_dtype(dtype));

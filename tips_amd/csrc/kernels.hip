@@ -229,6 +229,7 @@ __global__ __launch_bounds__(BLOCK) void sum2_buf_kernel(u32x4* __restrict__ dst
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
 template <int U>
 __global__ __launch_bounds__(256) void sum2_lds_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
                                                        const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
@@ -262,12 +263,14 @@ __global__ __launch_bounds__(256) void sum2_lds_kernel(u32x4* __restrict__ dst, 
   }
   if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
 }
+#endif  // TIPS_DEV
 
 // Persistent streaming 2-input sum (tuning sweep only, f32): gridDim = 256 CUs x WPC
 // workgroups, each owning one contiguous range of the bucket (XCD-contiguous order), walked
 // 4 KiB per operand at a time with the next tile's loads issued before the current tile's add
 // and sc1 store (2-deep software pipeline). Tests whether long sequential runs per CU beat one
 // short tile per workgroup on DRAM efficiency.
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
 __global__ __launch_bounds__(256) void sum2_stream_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
                                                           const u32x4* __restrict__ b, int64_t nvec,
                                                           int64_t tail_begin, int64_t n) {
@@ -301,6 +304,7 @@ __global__ __launch_bounds__(256) void sum2_stream_kernel(u32x4* __restrict__ ds
   }
   if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
 }
+#endif  // TIPS_DEV
 
 // Unaligned fallback (any pointer not 16-B aligned): one element per lane.
 template <int DT>
@@ -487,6 +491,7 @@ __global__ __launch_bounds__(kBlock) void multi_sum_scalar_kernel(void* dst, Src
 // ---------------------------------------------------------------------------
 // Batched copy (fusion pack / unpack)
 
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
 __global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __restrict__ tiles, int ntiles) {
   const int64_t ti = xcd_tile(blockIdx.x, gridDim.x);
   if (ti >= ntiles) return;
@@ -514,6 +519,7 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __re
     for (int64_t i = tid; i < t.bytes; i += kBlock) t.dst[i] = t.src[i];
   }
 }
+#endif  // TIPS_DEV
 
 // Grouped variant (tuning sweep, tools/copy_sweep.py): each workgroup copies G consecutive tiles
 // of at most 256 x U x 16 B. The G descriptors are read up front (independent scalar loads, one
@@ -522,6 +528,7 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_kernel(const CopyTile* __re
 // whose ends are 16-B aligned moves its whole 16-B vectors through buffer ops (range = those
 // vectors, so lanes past them fall off) and its < 16 trailing bytes bytewise; a misaligned tile
 // goes bytewise whole.
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
 template <int G, int U, int LAUX, int SAUX>
 __global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __restrict__ tiles, int ntiles) {
   const int64_t t0 = xcd_tile(blockIdx.x, gridDim.x) * G;
@@ -550,6 +557,7 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __
     for (int64_t i = vec[g] + tid; i < d[g].bytes; i += kBlock) d[g].dst[i] = d[g].src[i];
   }
 }
+#endif  // TIPS_DEV
 
 // ---------------------------------------------------------------------------
 // Segment copy (fusion pack / unpack / identity copy since round 3; fusion.cc)
@@ -778,6 +786,7 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     hipLaunchKernelGGL((sum2_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, a, b, n);
     return hipGetLastError();
   }
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
   if (mode == 5) {  // persistent streaming, f32, 256 threads; unroll = workgroups per CU (grid = 256 x unroll)
     if constexpr (DT == kF32) {
       if (threads == 256 && (unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8)) {
@@ -811,6 +820,7 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     }
     return hipErrorInvalidValue;
   }
+#endif  // TIPS_DEV
 #define TIPS_SUM2_CASE(M, U, NTV, L, S_, B)                      \
   if (mode == M && unroll == U && nt == NTV && threads == B) \
     return run_sum2<DT, M, U, L, S_, B>(dst, a, b, n, blocks, s);
@@ -829,6 +839,7 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     return hipGetLastError();                                                                              \
   }
     TIPS_BUF_CASE(1, 2, 16, 1, 256)  // the product default: nt loads, sc1 stores, 1 x 16 B per lane, 256 lanes
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
     if constexpr (DT == kF32) {
       TIPS_BUF_CASE(0, 2, 0, 1, 256)
       TIPS_BUF_CASE(2, 2, 17, 1, 256)
@@ -856,9 +867,11 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
       TIPS_BUF_CASE(12, 2, 1, 1, 256)
       TIPS_BUF_CASE(13, 2, 3, 1, 256)
     }
+#endif  // TIPS_DEV
 #undef TIPS_BUF_CASE
     return hipErrorInvalidValue;
   }
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
   // global_load/store forms: the tuning sweep's other variants (f32 only)
   if constexpr (DT == kF32) {
     TIPS_SUM2_CASE(2, 1, 2, true, false, 256)
@@ -906,6 +919,7 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     TIPS_SUM2_CASE(1, 4, 1, true, true, 128)
     TIPS_SUM2_CASE(1, 8, 1, true, true, 64)
   }
+#endif  // TIPS_DEV
 #undef TIPS_SUM2_CASE
   return hipErrorInvalidValue;
 }
@@ -940,6 +954,7 @@ hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
 // Sweep entry (f32; nsrc 2, 4, 8): 0 = global nt loads (U 2 for nsrc <= 4, else 1),
 // 1 = buffer nt loads U 1, 2 = buffer nt loads U 2, 3 = buffer plain loads U 1, 4 = buffer nt loads U 4.
 template <int NSRC>
@@ -989,6 +1004,7 @@ hipError_t run_multi_variant(void* dst, const SrcList& sl, int64_t n, int varian
   }
   return hipGetLastError();
 }
+#endif  // TIPS_DEV
 
 template <int DT>
 hipError_t multi_dispatch(void* dst, const void* const* srcs, int nsrc, int64_t n, hipStream_t s) {
@@ -1064,6 +1080,7 @@ hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_
   }
 }
 
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
 hipError_t launch_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, int variant,
                                    hipStream_t s) {
   if (n <= 0) return hipSuccess;
@@ -1080,7 +1097,9 @@ hipError_t launch_multi_sum_variant(void* dst, const void* const* srcs, int nsrc
     default: return hipErrorInvalidValue;
   }
 }
+#endif  // TIPS_DEV
 
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
 hipError_t launch_copy_tiles(const CopyTile* tiles_dev, int ntiles, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
   const unsigned grid = (unsigned)((ntiles + 7) / 8 * 8);
@@ -1129,6 +1148,7 @@ hipError_t launch_pack_tiles(const CopyTile* tiles_dev, int ntiles, int64_t max_
   if (max_tile_bytes > 16384) return launch_copy_tiles(tiles_dev, ntiles, s);
   return launch_copy_tiles_variant(tiles_dev, ntiles, 1, max_tile_bytes, s);
 }
+#endif  // TIPS_DEV
 
 namespace {
 

@@ -1307,6 +1307,7 @@ int tips_wait_n(const int64_t* handles, int n) {
   return rc ? fail(rc, "%s", first_err.c_str()) : 0;
 }
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 namespace {
 
 struct SelftestCount {
@@ -1434,5 +1435,6 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   snprintf(out, (size_t)cap, "%s", log.c_str());
   return rc;
 }
+#endif  // TIPS_DEV
 
 }  // extern "C"

@@ -19,7 +19,11 @@
 #include <unordered_map>
 #include <vector>
 
+#ifdef TIPS_DEV
+#include "../../include/tips_hip_dev.h"
+#else
 #include "../../include/tips_hip.h"
+#endif
 #include "kernels.h"
 
 namespace tips {
@@ -170,6 +174,11 @@ class HostPool {
   std::atomic<int> pending_{0};
   uint64_t gen_ = 0;  // guarded by m_ (workers wait on it)
   bool stop_ = false;
+  // the same two, readable without m_: workers (and run's wait for its jobs) spin on them for up to
+  // spin_ns_ before blocking (TIPS_HOST_SPIN_US)
+  std::atomic<uint64_t> gen_pub_{0};
+  std::atomic<bool> stop_pub_{false};
+  int64_t spin_ns_ = 0;
 };
 
 struct State {
@@ -183,6 +192,16 @@ struct State {
   EventPool pipe_ev;
   hipStream_t fuse_stream = nullptr, bucket_stream = nullptr;  // fusion: pack/unpack || bucket allreduce
   EventPool fuse_ev;
+  // fusion.cc: the stream of the fused call in progress (its pack / unpack / table work) and the chain
+  // that orders every fused call after the previous one: an event at the end of each call, on the
+  // stream it ran on, which a call from another stream waits for first
+  hipStream_t fuse_ws = nullptr, fuse_chain_stream = nullptr;
+  hipEvent_t ev_fuse_chain = nullptr;
+  hipEvent_t ev_fuse_table = nullptr;  // a table uploaded on fuse_stream: the work stream waits for it
+  bool fuse_chain_valid = false;
+  bool fuse_chain_lazy = false;  // the last call (tips_fused_pack_bucket) left its event unrecorded
+  bool fuse_capturing = false;   // the call in progress is being captured into a graph (no chain)
+  bool fuse_in_call = false;     // fuse_ws is set (it may be the legacy null stream, i.e. nullptr)
   int64_t fusion_threshold = 0;  // the fusion slots' size (2 slots of it in `fusion`)
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr, ev_comp_prev = nullptr;
   EventPool recv_ev, sum_ev;

@@ -74,6 +74,7 @@ int ensure_streams(State& st) {
   if (!st.ev_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_done, hipEventDisableTiming));
   if (!st.ev_comp_done) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_done, hipEventDisableTiming));
   if (!st.ev_comp_prev) HIP_TRY(hipEventCreateWithFlags(&st.ev_comp_prev, hipEventDisableTiming));
+  if (!st.ev_fuse_table) HIP_TRY(hipEventCreateWithFlags(&st.ev_fuse_table, hipEventDisableTiming));
   return 0;
 }
 

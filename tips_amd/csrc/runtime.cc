@@ -173,6 +173,7 @@ int tips_set_algorithm(int algo) {
 
 int tips_get_algorithm(void) { return S().algo; }
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int tips_set_sim_transport(int transport) {
   if (transport != 0 && transport != 1) return fail(TIPS_ERR_INVALID_ARG, "bad sim transport %d", transport);
   State& st = S();
@@ -180,6 +181,7 @@ int tips_set_sim_transport(int transport) {
   st.sim_transport = transport;
   return 0;
 }
+#endif  // TIPS_DEV
 
 int tips_resolve_algorithm(int nranks, int64_t bytes) { return resolve_algo(S().algo, nranks, bytes); }
 
@@ -192,6 +194,7 @@ int tips_bucket_sum(void* dst, const void* a, const void* b, int64_t count, int 
   return 0;
 }
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int dtype, int mode, int unroll, int nt,
                      int blocks, int threads, void* stream) {
   TRY(check_dtype(dtype));
@@ -199,7 +202,9 @@ int tips_sum_variant(void* dst, const void* a, const void* b, int64_t count, int
   HIP_TRY(tips::launch_sum2_variant(dst, a, b, count, dtype, mode, unroll, nt, blocks, threads, (hipStream_t)stream));
   return 0;
 }
+#endif  // TIPS_DEV
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int tips_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, int variant,
                            void* stream) {
   TRY(check_dtype(dtype));
@@ -208,6 +213,7 @@ int tips_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t
   HIP_TRY(tips::launch_multi_sum_variant(dst, srcs, nsrc, count, dtype, variant, (hipStream_t)stream));
   return 0;
 }
+#endif  // TIPS_DEV
 
 int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, void* stream) {
   TRY(check_dtype(dtype));
@@ -218,6 +224,7 @@ int tips_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t count, 
   return 0;
 }
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int tips_copy_tiles_variant(const void* tiles, int ntiles, int variant, int64_t max_tile_bytes, void* stream) {
   if (ntiles < 0 || (ntiles > 0 && !tiles) || max_tile_bytes < 1 || max_tile_bytes > tips::kCopyTileBytes)
     return fail(TIPS_ERR_INVALID_ARG, "bad copy-tile arguments");
@@ -225,7 +232,9 @@ int tips_copy_tiles_variant(const void* tiles, int ntiles, int variant, int64_t 
                                           (hipStream_t)stream));
   return 0;
 }
+#endif  // TIPS_DEV
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int tips_xfer(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, void* stream) {
   if (n < 0 || n > tips::kMaxXferSegs || (n > 0 && (!dsts || !srcs || !bytes)))
     return fail(TIPS_ERR_INVALID_ARG, "tips_xfer takes 0..%d segments", tips::kMaxXferSegs);
@@ -237,6 +246,7 @@ int tips_xfer(void* const* dsts, const void* const* srcs, const int64_t* bytes, 
   HIP_TRY(tips::launch_xfer(segs, n, (hipStream_t)stream));
   return 0;
 }
+#endif  // TIPS_DEV
 
 int tips_allreduce(const void* in, void* out, int64_t count, int dtype, int op, void* stream) {
   TRY(check_dtype(dtype));

@@ -594,6 +594,7 @@ void graphs_release(State& st) {
   st.replay_host_waits = st.replay_host_wait_ns = 0;
 }
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 namespace {
 
 // Peer transfers of the single-GPU simulator, batched per plan step: device-to-device
@@ -729,6 +730,7 @@ int simulate(int algo, void* const* outs, const void* const* ins, int p, int64_t
 }
 
 }  // namespace
+#endif  // TIPS_DEV
 
 }  // namespace rt
 }  // namespace tips
@@ -807,6 +809,7 @@ int tips_replay_order_stats(int64_t* host_waits, int64_t* host_wait_ns) {
   return 0;
 }
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, int depth, int64_t* out, int64_t cap) {
   TRY(check_dtype(dtype));
   if (cap < 0 || (cap > 0 && !out)) return fail(TIPS_ERR_INVALID_ARG, "bad plan buffer");
@@ -824,7 +827,9 @@ int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, 
   if ((int64_t)w.size() <= cap) std::copy(w.begin(), w.end(), out);
   return (int64_t)w.size();
 }
+#endif  // TIPS_DEV
 
+#ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
 // ---------------------------------------------------------------------------
 // single-GPU schedule simulators (test harnesses): the plans of all p ranks, on one device
 
@@ -839,5 +844,6 @@ int tips_direct_simulate(void* const* outs, const void* const* ins, int p, int64
 int tips_oneshot_simulate(void* const* outs, const void* const* ins, int p, int64_t n, int dtype, void* stream) {
   return simulate(TIPS_ALGO_ONESHOT, outs, ins, p, n, dtype, stream);
 }
+#endif  // TIPS_DEV
 
 }  // extern "C"

@@ -21,7 +21,7 @@ def main():
 
     import bench
     from tips_amd import _lib
-    L = _lib.lib()
+    L = _lib.dev()  # (include/tips_hip_dev.h)
     torch.cuda.set_device(0)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream

@@ -38,7 +38,7 @@ def _port():
 def _worker(rank, size, port, requests, q):
     import ctypes
     from tips_amd import _lib
-    L = _lib.lib()
+    L = _lib.dev()  # (include/tips_hip_dev.h)
     out = ctypes.create_string_buffer(1 << 20)
     rc = L.tips_negotiation_selftest(rank, size, b"127.0.0.1", port, requests.encode(), out, len(out))
     log = out.value.decode().splitlines()

@@ -96,9 +96,17 @@ def report(d, label):
             mx = union(xfer)
             comp_busy = sum(e - s for s, e in union(comp))
             under = sum(overlap_len(s, e, mx) for s, e in union(comp))
+            allk = union(xfer + comp)
+            span = max(e for _, e in allk) - min(s for s, _ in allk)
+            busy = sum(e - s for s, e in allk)
+            # the same split over the timed steps only: the last `steps` (5) of the 7 optimizer steps,
+            # cut at the SGD kernels' ends is fragile, so the whole trace is split per its wall span
             out["processes"].append({"trace": f, "compute_kernels": len(comp), "transfer_kernels": len(xfer),
                                      "compute_busy_ms": round(comp_busy / 1e6, 3),
                                      "transfer_busy_ms": round(sum(e - s for s, e in mx) / 1e6, 3),
+                                     "transfer_not_under_compute_ms": round((busy - comp_busy) / 1e6, 3),
+                                     "idle_ms": round((span - busy) / 1e6, 3), "span_ms": round(span / 1e6, 3),
+                                     "mean_transfer_kernel_us": round(sum(e - s for s, e in xfer) / max(1, len(xfer)) / 1e3, 1),
                                      "compute_under_transfer_frac": round(under / max(1, comp_busy), 4)})
     print(json.dumps(out))
 

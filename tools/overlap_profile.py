@@ -41,12 +41,12 @@ def main():
     po, _k2 = _lib.ptr_array([o.data_ptr() for o in outs])
     sp = torch.cuda.current_stream().cuda_stream
     fn = {"ring": "tips_ring_simulate", "direct": "tips_direct_simulate"}[kind]
-    _lib.call("tips_set_sim_transport", transport)
-    _lib.call(fn, po, pi, p, n, _lib.FLOAT32, sp)  # warm-up (staging, events, RCCL connections)
+    _lib.dev_call("tips_set_sim_transport", transport)
+    _lib.dev_call(fn, po, pi, p, n, _lib.FLOAT32, sp)  # warm-up (staging, events, RCCL connections)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        _lib.call(fn, po, pi, p, n, _lib.FLOAT32, sp)
+        _lib.dev_call(fn, po, pi, p, n, _lib.FLOAT32, sp)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / reps
     depth, sub = ctypes.c_int(), ctypes.c_int64()

@@ -10,7 +10,7 @@
 //          one of the kind.
 // Variants interleaved over rounds in one process; median ms and GB/s of
 // algorithmic bytes. One JSON line per variant.
-//   hipcc --offload-arch=gfx950 -O2 -o tools/peer_mem_probe tools/peer_mem_probe.cc -Ltips_amd/lib -ltips_hip
+//   hipcc --offload-arch=gfx950 -O2 -o tools/peer_mem_probe tools/peer_mem_probe.cc -Iinclude -Ltools/lib -ltips_hip_dev
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -19,7 +19,7 @@
 #include <string>
 #include <vector>
 
-#include "../include/tips_hip.h"
+#include "../include/tips_hip_dev.h"
 
 #define CHECK(x)                                                                         \
   do {                                                                                   \

@@ -38,7 +38,7 @@ def main():
     reps = 3
     for fn in ("tips_ring_simulate", "tips_direct_simulate"):
         for _ in range(reps):
-            _lib.call(fn, po, pi, p, n, _lib.FLOAT32, sp)
+            _lib.dev_call(fn, po, pi, p, n, _lib.FLOAT32, sp)
         torch.cuda.synchronize()
     m = sub.value
     print(json.dumps({"p": p, "elements_per_rank": n, "pipeline_depth": depth.value, "sub_chunk_elements": m,

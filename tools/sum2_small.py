@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, ".")
 from tips_amd import _lib  # noqa: E402
 
-L = _lib.lib()
+L = _lib.dev()  # (the tuning sweep entry points: include/tips_hip_dev.h)
 torch.cuda.set_device(0)
 s = torch.cuda.current_stream()
 for mib in (1, 2, 4, 8, 16, 32):

@@ -14,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "../include/tips_hip.h"
+#include "../include/tips_hip_dev.h"
 
 #define CHECK(x)                                                                              \
   do {                                                                                        \

@@ -11,7 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "tips_hip.h"
+#include "tips_hip_dev.h"
 
 static char* slurp(const char* path) {
   FILE* f = fopen(path, "rb");
