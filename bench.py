@@ -621,8 +621,9 @@ def small_bucket_latency(job, torch, dist, _lib, L, rank, sp, calls=40, kibs=SMA
 
 def overlap_probe(torch, dist, tips_amd, _lib, algo_code, job, steps=10):
     """A training step with DistributedOptimizer, its allreduces issued after backward vs during it
-    (TIPS_OVERLAP_BACKWARD: post-accumulate hooks issue each <= 25 MiB gradient bucket as it
-    completes, on a side stream). The model is 6 fp32 Linear(2048, 2048) layers, 25.2 M parameters
+    (TIPS_OVERLAP_BACKWARD=1: post-accumulate hooks issue each <= 25 MiB gradient bucket as it
+    completes, on a side stream), and the optimizer's default, the measured choice between the two
+    (=auto: its trial steps run first, untimed; measured_choice_detail has what it measured and kept). The model is 6 fp32 Linear(2048, 2048) layers, 25.2 M parameters
     (ResNet-50 has 25.6 M), on a 2048-row synthetic batch; wall time per step, slowest rank.
     `backward_only` is the same step without the optimizer (no allreduce): the floor overlap can
     approach. The reference's per-gradient async ops overlap backward the same way
@@ -636,9 +637,9 @@ def overlap_probe(torch, dist, tips_amd, _lib, algo_code, job, steps=10):
     g = torch.Generator(device="cuda").manual_seed(77)
     x = torch.randn(2048, 2048, device="cuda", generator=g)
     try:
-        for name, overlap, sync in (("backward_only", False, False), ("allreduce_after_backward", False, True),
-                                    ("allreduce_during_backward", True, True)):
-            os.environ["TIPS_OVERLAP_BACKWARD"] = "1" if overlap else "0"
+        for name, overlap, sync in (("backward_only", "0", False), ("allreduce_after_backward", "0", True),
+                                    ("allreduce_during_backward", "1", True), ("measured_choice", "auto", True)):
+            os.environ["TIPS_OVERLAP_BACKWARD"] = overlap
             torch.manual_seed(5)
             layers = []
             for _ in range(6):
@@ -653,7 +654,7 @@ def overlap_probe(torch, dist, tips_amd, _lib, algo_code, job, steps=10):
                     if sync:
                         opt.step()
 
-            run(3)
+            run(3 if overlap != "auto" else 10)  # (auto: 2 warm-up + 2 x 3 trial steps decide first)
             torch.cuda.synchronize()
             dist.barrier()
             w0 = job.replay_waits()
@@ -664,8 +665,10 @@ def overlap_probe(torch, dist, tips_amd, _lib, algo_code, job, steps=10):
             w1 = job.replay_waits()
             out.setdefault("replay_host_waits", {})[name] = {
                 "per_step": round((w1[0] - w0[0]) / steps, 2), "ms_per_step": round((w1[1] - w0[1]) / steps / 1e6, 4)}
-            if overlap:
+            if overlap == "1":
                 out["buckets"] = len(opt._buckets.buckets) if opt._buckets is not None else 0
+            if overlap == "auto":
+                out["measured_choice_detail"] = opt.overlap_choice
             del m, opt, layers
     finally:
         if saved is None:
@@ -1291,28 +1294,31 @@ class Workload(object):
 
 
 def host_legs(job, w, line):
-    """Config 5 host -> host (the gradients in host memory, as the reference's CPU op has them):
-    one tips_amd.allreduce per numpy gradient (the reference's per-op structure), and the same
-    gradients through allreduce_grads' N > 1 body (one fused host call)."""
+    """Config 5 host -> host (the gradients in host memory, as the reference's CPU op has them): the
+    gradients through allreduce_grads' N > 1 body (one fused host call), and at one rank also one
+    tips_amd.allreduce per numpy gradient (the reference's per-op structure; at N > 1 that leg would
+    cost the rehearsal's budget minutes, and the fused one is what allreduce_grads runs)."""
     import numpy as np
     tips_amd, world, sizes = job.tips_amd, job.world, w.sizes
     hg = [np.random.default_rng(w.seed0 + job.rank * 1000 + i).random(k, dtype=np.float32) for i, k in enumerate(sizes)]
-    for gr in hg:
-        tips_amd.allreduce(gr)
     hsteps = max(3, w.steps // 4)
-    job.dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(hsteps):
-        for gr in hg:  # each result consumed at once, as the optimizer would (no 100 MB of live outputs)
+    th = None
+    if world == 1:
+        for gr in hg:
             tips_amd.allreduce(gr)
-    th = max_over_ranks(job.dist, time.perf_counter() - t0) / hsteps
-    outs = [tips_amd.allreduce(gr) for gr in hg]
-    h_ok = world > 1 or all(np.array_equal(o, gr) for o, gr in zip(outs, hg))
-    line["host_to_host_python"] = {
-        "ms_per_step": round(th * 1e3, 3), "algbw_gib_s": round(w.total_elems * 4 / th / GIB, 2),
-        "us_per_tensor": round(th * 1e6 / len(sizes), 2), "steps": hsteps,
-        "check": "identity at one rank" if world == 1 and h_ok else ("FAIL" if not h_ok else "not checked"),
-        "note": "214 numpy gradients, one tips_amd.allreduce each (host staged), the reference's per-op structure"}
+        job.dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(hsteps):
+            for gr in hg:  # each result consumed at once, as the optimizer would (no 100 MB of live outputs)
+                tips_amd.allreduce(gr)
+        th = max_over_ranks(job.dist, time.perf_counter() - t0) / hsteps
+        outs = [tips_amd.allreduce(gr) for gr in hg]
+        h_ok = all(np.array_equal(o, gr) for o, gr in zip(outs, hg))
+        line["host_to_host_python"] = {
+            "ms_per_step": round(th * 1e3, 3), "algbw_gib_s": round(w.total_elems * 4 / th / GIB, 2),
+            "us_per_tensor": round(th * 1e6 / len(sizes), 2), "steps": hsteps,
+            "check": "identity at one rank" if h_ok else "FAIL",
+            "note": "214 numpy gradients, one tips_amd.allreduce each (host staged), the reference's per-op structure"}
     # The same 214 numpy gradients through allreduce_grads' N > 1 body: one fused host call
     # (tips_fused_allreduce_host_flat: host threads pack page-locked pieces, H2D -> allreduce -> D2H
     # pipelined per piece, straight into a page-locked flat output).
@@ -1321,7 +1327,7 @@ def host_legs(job, w, line):
     # each call timed on its own (max over ranks per call): the host side of the box is shared
     # with other jobs, and one call in ten can take 2-3 x the others (profiles/r03/b_host_probe.txt);
     # the median is the rate, the mean and the best are reported beside it
-    fsteps = max(hsteps, 15)
+    fsteps = max(hsteps, 15) if world == 1 else 5
     per = []
     for _ in range(fsteps):
         job.dist.barrier()
@@ -1343,7 +1349,7 @@ def host_legs(job, w, line):
         "best_gib_s": round(w.total_elems * 4 / min(per) / GIB, 2),
         "steps": fsteps, "threads": int(os.environ.get("TIPS_HOST_THREADS", "8")),
         "piece_bytes": int(os.environ.get("TIPS_HOST_FUSED_PIECE_BYTES", str(32 << 20))),  # (host_staging.cc's default)
-        "vs_per_tensor": round(th / tf, 2),
+        "vs_per_tensor": round(th / tf, 2) if th else None,
         "check": ("identity at one rank, bit-exact" if world == 1 else "bit-exact vs rank-order fold of all ranks' inputs")
         if f_ok else "FAIL",
         "note": "the same 214 numpy gradients through allreduce_grads' N > 1 body (tips_fused_allreduce_host_flat): "

@@ -115,11 +115,18 @@ def overlap_case(c, rank, size, L, _lib, sp):
     optimizer steps (the second after zero_grad(set_to_none=True): gradients copied into the views
     again). Checks: every bucket was issued before step() (by the hooks), the summed gradients
     equal the rank-order sum of all ranks' (averaged) local gradients bit for bit (AUTO at p > 2:
-    one-shot / direct, the rank-order fold), and the parameters equal p - lr * sum."""
+    one-shot / direct, the rank-order fold), and the parameters equal p - lr * sum.
+    mode "auto" (c["mode"]): the measured choice (optim._OverlapChoice) over 2 warm-up + 2 x 2
+    trial steps and 2 more: every step's sums still bit-exact, the hooks issue every bucket exactly
+    in the steps run during backward, and every rank ends with the same choice."""
     import torch
     import tips_amd
     passes, avg = int(c.get("passes", 1)), bool(c.get("average", False))
+    mode = c.get("mode", "1")
     os.environ["TIPS_GRAD_BUCKET_MIB"] = str(c.get("bucket_kib", 8) / 1024.0)
+    os.environ["TIPS_OVERLAP_BACKWARD"] = mode
+    os.environ["TIPS_OVERLAP_TRIAL_STEPS"] = "2"
+    steps = 8 if mode == "auto" else 2
 
     def model():
         torch.manual_seed(c["seed"])
@@ -139,8 +146,11 @@ def overlap_case(c, rank, size, L, _lib, sp):
                                         average_aggregated_gradients=avg)
     if opt._buckets is None or len(opt._buckets.buckets) < 3:
         return {"case": {"overlap": c["seed"]}, "rc": 0, "ok": False, "error": "no overlapped buckets"}
-    for it in range(2):
+    choices = []
+    for it in range(steps):
         sums = None
+        during = opt.overlap_choice["current"] == "during"
+        choices.append(during)
         for r in range(size):
             ref.zero_grad(set_to_none=True)
             for k in range(passes):
@@ -153,14 +163,16 @@ def overlap_case(c, rank, size, L, _lib, sp):
             if k < passes - 1:
                 opt.step()  # counts the pass only
         issued = list(opt._buckets.issue_log)
-        if issued != list(range(len(opt._buckets.buckets))):
-            bad.append("it %d: hooks issued %s of %d buckets" % (it, issued, len(opt._buckets.buckets)))
+        if issued != (list(range(len(opt._buckets.buckets))) if during else []):
+            bad.append("it %d: hooks issued %s of %d buckets (during: %s)" % (it, issued, len(opt._buckets.buckets),
+                                                                           during))
         # right after backward, work on the caller's stream already sees the reduced gradients
         # (the end-of-backward callback ordered it after the side stream), before any synchronize
-        snap = [p.grad.clone() for p in m.parameters()]
-        for i, (g, s) in enumerate(zip(snap, sums)):
-            if not torch.equal(g, s):
-                bad.append("it %d: grad %d read after backward differs" % (it, i))
+        if during:
+            snap = [p.grad.clone() for p in m.parameters()]
+            for i, (g, s) in enumerate(zip(snap, sums)):
+                if not torch.equal(g, s):
+                    bad.append("it %d: grad %d read after backward differs" % (it, i))
         with torch.no_grad():
             exp = [p - lr * s for p, s in zip(ref.parameters(), sums)]
         if it == 1:
@@ -175,7 +187,11 @@ def overlap_case(c, rank, size, L, _lib, sp):
         with torch.no_grad():  # keep the replica in step with the updated parameters
             for pr, p in zip(ref.parameters(), m.parameters()):
                 pr.copy_(p)
-    return {"case": {"overlap": c["seed"], "passes": passes}, "rc": 0, "ok": not bad, "error": "; ".join(bad[:4])}
+    res = {"case": {"overlap": c["seed"], "passes": passes, "mode": mode}, "rc": 0, "ok": not bad,
+           "error": "; ".join(bad[:4]), "choices": choices, "overlap_choice": opt.overlap_choice}
+    if mode == "auto" and "chosen" not in opt.overlap_choice:
+        res.update(ok=False, error="no overlap choice after %d steps" % steps)
+    return res
 
 
 def named_collectives_case(c, rank, size, L, _lib, sp):

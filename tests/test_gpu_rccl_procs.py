@@ -222,14 +222,24 @@ def test_counts_past_int32_over_rccl(gpu, algo, p):
 
 @pytest.mark.parametrize("p", [2, 3])
 def test_overlapped_optimizer_over_rccl(gpu, p):
-    """DistributedOptimizer's backward-overlapped buckets over real RCCL ranks: the post-accumulate
+    """DistributedOptimizer's backward-overlapped buckets (TIPS_OVERLAP_BACKWARD=1, and the measured
+    choice, =auto) over real RCCL ranks: the post-accumulate
     hooks issue every bucket's in-place allreduce during backward (8 KiB and 64 KiB buckets, so a
     small MLP makes many), in bucket order on every rank; one and two backward passes per step,
     averaged; summed gradients bit-exact against the rank-order sum (p = 2 takes the one-shot for
     these sizes, p = 3 the one-shot / direct fold), parameters p - lr * sum."""
     cases = [{"overlap": True, "seed": 21, "bucket_kib": 8},
-             {"overlap": True, "seed": 22, "bucket_kib": 64, "passes": 2, "average": True}]
-    check(run_job(p, cases, timeout=600, **rccl_env("auto")))
+             {"overlap": True, "seed": 22, "bucket_kib": 64, "passes": 2, "average": True},
+             {"overlap": True, "seed": 23, "bucket_kib": 8, "mode": "auto"}]
+    results = run_job(p, cases, timeout=600, **rccl_env("auto"))
+    check(results)
+    # the measured choice (optim._OverlapChoice): warm-up steps during backward, then the trial
+    # alternating during / after, then one choice - the same on every rank
+    first = results[0]["results"][2]
+    assert first["choices"][:6] == [True, True, True, False, True, False], first
+    for res in results:
+        c = res["results"][2]
+        assert c["choices"] == first["choices"] and c["overlap_choice"]["chosen"] == first["overlap_choice"]["chosen"]
 
 
 @pytest.mark.parametrize("p", [3, 4])

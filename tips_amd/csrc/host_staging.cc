@@ -396,7 +396,11 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
       total, round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_HOST_FUSED_PIECE_BYTES", 32 << 20)), kAlignBytes));
   const std::vector<Piece> pieces = host_pieces(total, piece, env_i64("TIPS_HOST_FUSED_FIRST_BYTES", 2 << 20));
   const int np = (int)pieces.size();
-  const int R = 3;  // page-locked slots per direction; piece i uses slot i % R
+  // page-locked slots per direction (piece i uses slot i % R), and how many pieces behind the one
+  // being packed the unpack runs: with lag 2 the thread unpacks a piece whose D2H finished while
+  // the previous piece was packed, instead of waiting for the one just sent (TIPS_HOST_SLOTS,
+  // TIPS_HOST_UNPACK_LAG; lag <= R - 1, since D2H(i + 1) reuses the slot unpack(i + 1 - R) freed)
+  const int R = (int)std::max<int64_t>(2, std::min<int64_t>(8, env_i64("TIPS_HOST_SLOTS", 4)));
   const int nthreads = (int)std::max<int64_t>(1, std::min<int64_t>(64, env_i64("TIPS_HOST_THREADS", 8)));
   if (!st.host_pool || st.host_pool->size() != nthreads) {
     delete st.host_pool;
@@ -442,7 +446,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
       else copy_range(segs, a, b, buf, p0, pack);
     });
   };
-  const int lag = direct_out ? np : 1;  // piece i - lag is unpacked while piece i is on the link
+  const int lag = direct_out ? np : (int)std::max<int64_t>(1, std::min<int64_t>(R - 1, env_i64("TIPS_HOST_UNPACK_LAG", 2)));
   // TIPS_HOST_TRACE=1: where one call's time goes (stderr), for tuning the piece and thread counts
   static const bool trace = env_i64("TIPS_HOST_TRACE", 0) != 0;
   double t_pack = 0, t_wait = 0, t_unpack = 0, t_issue = 0;

@@ -600,10 +600,17 @@ class Negotiator {
   void loop() {
     const auto cycle = std::chrono::microseconds(std::max<int64_t>(50, env_i64("TIPS_CYCLE_TIME_US", 1000)));
     const auto linger = std::chrono::microseconds(std::max<int64_t>(0, env_i64("TIPS_BATCH_LINGER_US", 30)));
+    // TIPS_NEG_TRACE=1: per cycle with requests, on stderr: the batch, and how long the linger, the
+    // exchange with rank 0 and the execution took (microseconds)
+    const bool trace = env_i64("TIPS_NEG_TRACE", 0) != 0;
+    auto us_since = [](std::chrono::steady_clock::time_point t) {
+      return (long long)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
+    };
     while (true) {
       std::vector<std::shared_ptr<Req>> batch;
       bool stopping;
       set_phase("waiting for requests");
+      long long t_linger = 0;
       {
         std::unique_lock<std::mutex> l(m_);
         cv_.wait_for(l, cycle, [&] { return !fresh_.empty() || want_stop_; });
@@ -619,7 +626,9 @@ class Negotiator {
         fresh_.clear();
         for (auto& r : batch) r->state = 1;
         stopping = want_stop_;
+        t_linger = us_since(t0);
       }
+      const auto t_x = std::chrono::steady_clock::now();
       Writer w;
       w.put<uint8_t>(stopping ? 1 : 0);
       w.put<uint32_t>((uint32_t)batch.size());
@@ -656,7 +665,12 @@ class Negotiator {
         set_loop_error("negotiation: malformed response");
         break;
       }
+      const long long t_exchange = us_since(t_x);
+      const auto t_e = std::chrono::steady_clock::now();
       execute(ds);
+      if (trace && (!batch.empty() || !ds.empty()))
+        fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us, exchange %lld us, "
+                "execute %lld us\n", rank_, (long long)cycles_, batch.size(), ds.size(), t_linger, t_exchange, us_since(t_e));
       if (shutdown) break;
     }
     std::lock_guard<std::mutex> l(m_);
@@ -686,38 +700,49 @@ class Negotiator {
 
   // The completion thread: in the order requests finished, wait for a device request's work, call
   // its callback (without the lock: a callback may enqueue more requests) and release its handle.
+  // The completion thread: takes every queued request at once (a fused batch of host requests is
+  // queued together: config 5's 214 in one go), runs each callback - for device work after its
+  // event - and releases the batch's handles with one lock. Its phase for tips_debug_state is the
+  // request it is at, formatted only when asked (a string per request cost ~1 ms per config-5 step).
   void waiter_loop() {
+    std::deque<std::shared_ptr<Req>> batch;
     while (true) {
-      std::shared_ptr<Req> r;
       {
         std::unique_lock<std::mutex> l(m_);
         done_cv_.wait(l, [&] { return !done_q_.empty() || waiter_stop_; });
         if (done_q_.empty()) return;
-        r = done_q_.front();
-        done_q_.pop_front();
+        batch.swap(done_q_);
       }
-      int status = 0;
-      std::string msg;
-      if (r->state < 0) {
-        status = r->code;
-        msg = r->err;
-      } else if (r->state == 2 && !(r->gev && r->gev->done.load(std::memory_order_acquire))) {
-        hipEvent_t ev = r->gev ? r->gev->ev : r->ev;
-        set_waiter_phase("hipEventSynchronize of " + r->name + (r->gev ? " (fused batch)" : ""));
-        const hipError_t e = hipEventSynchronize(ev);
-        if (e != hipSuccess) {
-          status = TIPS_ERR_HIP;
-          msg = std::string("request ") + r->name + ": " + hipGetErrorString(e);
-        } else if (r->gev) {
-          r->gev->done.store(true, std::memory_order_release);
+      for (auto& r : batch) {
+        int status = 0;
+        std::string msg;
+        if (r->state < 0) {
+          status = r->code;
+          msg = r->err;
+        } else if (r->state == 2 && !(r->gev && r->gev->done.load(std::memory_order_acquire))) {
+          set_waiter_req(r, true);
+          hipEvent_t ev = r->gev ? r->gev->ev : r->ev;
+          const hipError_t e = hipEventSynchronize(ev);
+          if (e != hipSuccess) {
+            status = TIPS_ERR_HIP;
+            msg = std::string("request ") + r->name + ": " + hipGetErrorString(e);
+          } else if (r->gev) {
+            r->gev->done.store(true, std::memory_order_release);
+          }
         }
+        set_waiter_req(r, false);
+        r->cb(r->cb_ctx, status, msg.c_str());
       }
-      set_waiter_phase("callback of " + r->name);
-      r->cb(r->cb_ctx, status, msg.c_str());
-      set_waiter_phase("idle");
-      release(r->handle, r);
+      set_waiter_req(nullptr, false);
       std::lock_guard<std::mutex> l(m_);
-      cb_called_++;
+      for (auto& r : batch) {  // (release() for the whole batch)
+        if (r->ev) ev_pool_.push_back(r->ev);
+        r->ev = nullptr;
+        r->gev.reset();
+        by_handle_.erase(r->handle);
+      }
+      cb_called_ += (int64_t)batch.size();
+      batch.clear();
     }
   }
 
@@ -1010,7 +1035,9 @@ class Negotiator {
   // what the two threads are doing now (tips_debug_state): guarded by phase_mu_, never held across
   // a blocking call, so a dump from a watchdog always gets through
   std::mutex phase_mu_;
-  std::string phase_ = "start", waiter_phase_ = "idle";
+  std::string phase_ = "start";
+  std::shared_ptr<Req> waiter_req_;  // the request the completion thread is at (null: idle)
+  bool waiter_syncing_ = false;      // ... waiting for its device work (else: in its callback)
   int64_t cycles_ = 0, executed_ = 0;
   size_t exec_i_ = 0, exec_n_ = 0;
   std::shared_ptr<Req> exec_req_;  // the request execute() is on (phase_ "execute")
@@ -1019,9 +1046,10 @@ class Negotiator {
     phase_ = std::move(p);
     exec_req_.reset();
   }
-  void set_waiter_phase(std::string p) {
+  void set_waiter_req(const std::shared_ptr<Req>& r, bool syncing) {
     std::lock_guard<std::mutex> l(phase_mu_);
-    waiter_phase_ = std::move(p);
+    waiter_req_ = r;
+    waiter_syncing_ = syncing;
   }
 
  public:
@@ -1040,7 +1068,10 @@ class Negotiator {
              (r.body ? " (routed call)" : r.host ? " (host)" : r.type != TIPS_REQ_ALLREDUCE ? " (other)" : "");
       }
       out = "rank " + std::to_string(rank_) + " cycles " + std::to_string((long long)cycles_) + " executed " +
-            std::to_string((long long)executed_) + " | negotiation: " + ph + " | completion: " + waiter_phase_;
+            std::to_string((long long)executed_) + " | negotiation: " + ph + " | completion: " +
+            (!waiter_req_ ? std::string("idle")
+                          : waiter_syncing_ ? "hipEventSynchronize of " + waiter_req_->name + (waiter_req_->gev ? " (fused batch)" : "")
+                                            : "callback of " + waiter_req_->name);
     }
     std::unique_lock<std::mutex> l(m_, std::try_to_lock);
     if (!l.owns_lock()) return out + " | (request lock held)";

@@ -8,10 +8,15 @@ optimizer applies them, optionally after backward_passes_per_step local
 accumulations (LocalGradientAggregationHelper, gradient_aggregation.py). Here
 the wrapped object is a torch.optim.Optimizer: the parameters' .grad tensors
 are summed over ranks in place and then the wrapped optimizer steps. Dense
-device gradients are views of per-dtype flat buffers whose buckets are
-allreduced during backward as they complete (_GradBuckets, as the reference's
-async per-gradient ops overlap backward); the rest go through
-tips_amd.allreduce_grads in step().
+device gradients are views of per-dtype flat buffers cut into <= 25 MiB buckets,
+allreduced in place either during backward as each bucket completes
+(_GradBuckets, as the reference's async per-gradient ops overlap backward) or
+after it, in step(). Which one is measured, not assumed (TIPS_OVERLAP_BACKWARD=
+auto, the default): the first optimizer steps alternate the two, every rank
+times them on the device, the ranks agree on the slowest rank's means and all
+keep the faster (_OverlapChoice). Round 3's default was "during"; rehearsals on
+one shared GPU measured it both faster and slower. =1 / =0 fix
+the choice. The rest go through tips_amd.allreduce_grads.
 
 As in the reference, op / prescale / postscale never reach the reduction
 (__init__.py:82-87, 194-201): the gradients are SUMMED over ranks, op=Average
@@ -255,6 +260,61 @@ class _GradBuckets(object):
         return sparse
 
 
+class _OverlapChoice(object):
+    """Whether DistributedOptimizer's gradient buckets are allreduced during backward or after it,
+    per optimizer step. mode "1" / "0": always / never. "auto": optimizer steps [W, W + 2M) alternate
+    during / after (TIPS_OVERLAP_TRIAL_WARMUP W = 2 steps first, TIPS_OVERLAP_TRIAL_STEPS M = 3 of
+    each), each step timed on the device from the end of the step before it to its own end (events
+    on the caller's stream: forward, backward, the allreduces, the optimizer); after the last trial
+    step every rank reports its mean per mode, the ranks take the slowest rank's (one small
+    allgather, at the same step on every rank) and every rank keeps the faster mode from then on.
+    The two modes issue the same bucket allreduces, so the trial changes no result."""
+
+    def __init__(self, mode):
+        import os
+        self.mode = mode if mode in ("0", "1", "auto") else "auto"
+        self.warm = max(0, int(os.environ.get("TIPS_OVERLAP_TRIAL_WARMUP", "2")))
+        self.trials = max(1, int(os.environ.get("TIPS_OVERLAP_TRIAL_STEPS", "3")))
+        self.chosen = {"0": False, "1": True}.get(self.mode)
+        self.events = {}   # optimizer step -> event recorded at its end (trial window only)
+        self.report = {"mode": self.mode}
+
+    def on(self, s):
+        """During backward for optimizer step s (0-based)?"""
+        if self.chosen is not None:
+            return self.chosen
+        k = s - self.warm
+        return k < 0 or k % 2 == 0  # (warm-up steps overlap, as round 3 did)
+
+    def stepped(self, s):
+        """After optimizer step s: time it (trial window) and decide after the last trial step."""
+        if self.chosen is not None:
+            return
+        import torch
+        if s >= self.warm - 1:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.events[s] = ev
+        last = self.warm + 2 * self.trials - 1
+        if s < last:
+            return
+        self.events[last].synchronize()
+        per = {True: [], False: []}
+        for t in range(self.warm, last + 1):
+            per[self.on(t)].append(self.events[t - 1].elapsed_time(self.events[t]))
+        mine = [int(sum(v) / len(v) * 1000) for v in (per[True], per[False])]  # us, during / after
+        from .ops import _allgather_i64
+        from . import basics
+        allv = _allgather_i64(mine)
+        n = basics.size()
+        slow_on = max(allv[2 * r] for r in range(n))
+        slow_off = max(allv[2 * r + 1] for r in range(n))
+        self.chosen = slow_on < slow_off
+        self.events = {}
+        self.report.update(trial_steps_each=self.trials, during_backward_ms=slow_on / 1e3,
+                           after_backward_ms=slow_off / 1e3, chosen="during" if self.chosen else "after")
+
+
 class _DistributedOptimizer(object):
     """Wraps a torch.optim.Optimizer; step() allreduces the gradients first (__init__.py:252-335)."""
 
@@ -279,8 +339,10 @@ class _DistributedOptimizer(object):
         # its own reduction only for a synchronize() of this very pass with no backward after it.
         self._sync_at = None
         self._grad_events = 0
+        self._in_step = False
         from . import Compression
-        if (os.environ.get("TIPS_OVERLAP_BACKWARD", "1") != "0" and self._bucket_view
+        self._overlap = _OverlapChoice(os.environ.get("TIPS_OVERLAP_BACKWARD", "auto").lower())
+        if (self._overlap.mode != "0" and self._bucket_view
                 and self._compression is Compression.none and not sparse_as_dense):
             import torch
             ps = [p for g in optimizer.param_groups for p in g["params"]
@@ -305,12 +367,17 @@ class _DistributedOptimizer(object):
                                          if p.requires_grad}.values()]
         weakref.finalize(self, _remove_hooks, list(self._count_handles))
 
-    @staticmethod
-    def _overlap_active():
+    def _overlap_active(self):
         """Hooks issue allreduces only once TiPS runs with more than one rank (never initialise
-        TiPS from inside backward: synchronize() issues what the hooks did not)."""
+        TiPS from inside backward: synchronize() issues what the hooks did not), and only for a
+        step _OverlapChoice runs during backward."""
         from . import basics
-        return basics.is_initialized() and basics.size() > 1
+        return basics.is_initialized() and basics.size() > 1 and self._overlap.on(self._step_index())
+
+    @property
+    def overlap_choice(self):
+        """{mode, and once decided: the trial's slowest-rank step means and the mode kept}."""
+        return dict(self._overlap.report, current="during" if self._overlap.on(self._step_index()) else "after")
 
     # the wrapped optimizer's surface
     @property
@@ -340,10 +407,11 @@ class _DistributedOptimizer(object):
         bucket views (default) as one allreduce of the flat buffer they are views of, no copies;
         with TIPS_GRAD_BUCKET_VIEW=0 through the fusion buckets (tips_fused_allreduce: pack, one
         allreduce per bucket, unpack straight back into .grad - 4 x the gradient bytes of HBM
-        traffic). With backward-overlapped buckets (_GradBuckets, the default at N > 1) most of
-        that was issued during backward, and the end of backward already ordered the caller's
-        stream after it; this issues the rest and joins, bucket by bucket (the same sequence on
-        every rank whatever its hooks reached). whole_groups=True is for a caller that knows no
+        traffic). In a step run during backward (_GradBuckets at N > 1: TIPS_OVERLAP_BACKWARD=1, or
+        auto's choice) most of that was issued during backward, and the end of backward already
+        ordered the caller's stream after it; this issues the rest and joins, bucket by bucket (the
+        same sequence on every rank whatever its hooks reached); in a step run after backward, one
+        allreduce per group. whole_groups=True is for a caller that knows no
         backward ran on any rank since the last reduction (one allreduce per group).
 
         step() does not reduce again when the caller called synchronize() in the final pass of this
@@ -359,8 +427,11 @@ class _DistributedOptimizer(object):
         self._sync_at = (self._calls, self._grad_events)
         params = self._params_with_grad()
         if self._buckets is not None and size() > 1:
-            # backward-overlapped buckets: the hooks issued what was ready; issue the rest in order
-            sparse = set(id(p) for p in self._buckets.synchronize(whole_groups=whole_groups))
+            # backward-overlapped buckets: the hooks issued what was ready; issue the rest in order.
+            # A step _OverlapChoice runs after backward issued nothing on any rank (the choice is
+            # the same on every rank): one allreduce per group's flat buffer instead of per bucket
+            after = not self._overlap.on(self._step_index())
+            sparse = set(id(p) for p in self._buckets.synchronize(whole_groups=whole_groups or after))
             managed = set(self._buckets.where)
             params = [p for p in params if id(p) not in managed or id(p) in sparse]
         if self._passes > 1 and self._average_aggregated:
@@ -433,9 +504,26 @@ class _DistributedOptimizer(object):
                 warnings.warn("DistributedOptimizer.synchronize() ran %s: step() reduces the gradients again"
                               % ("in an earlier accumulation pass" if sync_at[0] != self._calls - 1
                                  else "before a later backward"))
-            self.synchronize()
+            self._in_step = True
+            try:
+                self.synchronize()
+            finally:
+                self._in_step = False
         self._sync_at = None
-        return self._optimizer.step(closure) if closure is not None else self._optimizer.step()
+        out = self._optimizer.step(closure) if closure is not None else self._optimizer.step()
+        if self._buckets is not None and self._overlap_ready():
+            self._overlap.stepped(self._calls // self._passes - 1)
+        return out
+
+    def _step_index(self):
+        """The optimizer step the gradients being reduced belong to: calls made so far // passes
+        during backward (or a synchronize() before step()), one less inside step(), which has
+        counted its own call already."""
+        return (self._calls - (1 if self._in_step else 0)) // self._passes
+
+    def _overlap_ready(self):
+        from . import basics
+        return basics.is_initialized() and basics.size() > 1
 
 
 def _validate(op, gradient_predivide_factor, num_groups, groups):

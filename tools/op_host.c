@@ -5,9 +5,11 @@
  * thread runs ComputeAsync, which allocates the output, enqueues the host tensor under the op's
  * name with a callback (EnqueueTensorCollective, coordinator.cc:223-241) and returns; rank 0's
  * background loop (coordinator.cc:355-513) runs every name in readiness order and the callback
- * calls done(). Here each step, four executor threads issue their share of the 214 gradients in a
- * per-rank shuffled order with tips_enqueue_allreduce_shaped (the gradient's TF shape) + tips_on_done,
- * and main waits for the 214 callbacks: one step = one training step's gradient allreduce. The
+ * calls done(). Here each step, four persistent executor threads (TF's inter-op pool) issue their
+ * share of the 214 gradients in a per-rank shuffled order with tips_enqueue_allreduce_shaped (the
+ * gradient's TF shape) + tips_on_done, and main waits until the last callback has come (the callbacks
+ * count; only the last one wakes main, as TF's executor wakes the step's caller once its last op is
+ * done): one step = one training step's gradient allreduce. The
  * library fuses the host requests each negotiation cycle hands it (negotiate.cc execute: one
  * tips_fused_allreduce_host call per run of host allreduces).
  *
@@ -119,6 +121,20 @@ static void fill(float* x, int r, int i, int64_t n) {
   for (int64_t j = 0; j < n; j++) x[j] = value(r, i, j);
 }
 
+static double now(void);
+static double g_t_first_cb, g_t_enq;  /* OP_HOST_TRACE: the step's first callback, the last enqueue */
+static atomic_int g_enq_threads;
+
+static void count_done(void) {
+  const int k = atomic_fetch_add(&g_done, 1);
+  if (k == 0) g_t_first_cb = now();
+  if (k + 1 == g_n) {  /* the step's last callback wakes main */
+    pthread_mutex_lock(&g_mu);
+    pthread_cond_broadcast(&g_cv);
+    pthread_mutex_unlock(&g_mu);
+  }
+}
+
 static void on_done(void* ctx, int status, const char* message) {
   Grad* g = (Grad*)ctx;
   atomic_store(&g->status, status);
@@ -128,39 +144,43 @@ static void on_done(void* ctx, int status, const char* message) {
     pthread_mutex_unlock(&g_mu);
     atomic_fetch_add(&g_failed, 1);
   }
-  pthread_mutex_lock(&g_mu);
-  atomic_fetch_add(&g_done, 1);
-  pthread_cond_broadcast(&g_cv);
-  pthread_mutex_unlock(&g_mu);
+  count_done();
 }
+
+/* the executor threads: persistent, released once per step (a barrier), each enqueues its share */
+static pthread_barrier_t g_go;
+static atomic_int g_quit;
 
 static void* executor(void* arg) {
   const int t = (int)(intptr_t)arg;
-  for (int k = 0; k < g_n; k++) {
-    const int i = g_order[k];
-    if (i % g_threads != t) continue;
-    Grad* g = &g_g[i];
-    const int64_t h = tips_enqueue_allreduce_shaped(g->name, g->in, g->out, g->dims, g->ndim, TIPS_FLOAT32, NULL);
-    if (h < 0 || tips_on_done(h, on_done, g) != TIPS_OK) {
-      pthread_mutex_lock(&g_mu);
-      if (!g_err[0]) snprintf(g_err, sizeof g_err, "%s: %s", g->name, tips_last_error());
-      pthread_mutex_unlock(&g_mu);
-      atomic_fetch_add(&g_failed, 1);
-      pthread_mutex_lock(&g_mu);
-      atomic_fetch_add(&g_done, 1);
-      pthread_cond_broadcast(&g_cv);
-      pthread_mutex_unlock(&g_mu);
+  while (1) {
+    pthread_barrier_wait(&g_go);
+    if (atomic_load(&g_quit)) return NULL;
+    for (int k = 0; k < g_n; k++) {
+      const int i = g_order[k];
+      if (i % g_threads != t) continue;
+      Grad* g = &g_g[i];
+      const int64_t h = tips_enqueue_allreduce_shaped(g->name, g->in, g->out, g->dims, g->ndim, TIPS_FLOAT32, NULL);
+      if (h < 0 || tips_on_done(h, on_done, g) != TIPS_OK) {
+        pthread_mutex_lock(&g_mu);
+        if (!g_err[0]) snprintf(g_err, sizeof g_err, "%s: %s", g->name, tips_last_error());
+        pthread_mutex_unlock(&g_mu);
+        atomic_fetch_add(&g_failed, 1);
+        count_done();
+      }
     }
+    if (atomic_fetch_add(&g_enq_threads, 1) + 1 == g_threads) g_t_enq = now();
   }
-  return NULL;
 }
 
 /* one step: every gradient enqueued by the executor threads; returns when all 214 are done */
+static int g_trace;
+
 static int step(void) {
   atomic_store(&g_done, 0);
-  pthread_t th[MAX_THREADS];
-  for (int t = 0; t < g_threads; t++) pthread_create(&th[t], NULL, executor, (void*)(intptr_t)t);
-  for (int t = 0; t < g_threads; t++) pthread_join(th[t], NULL);
+  atomic_store(&g_enq_threads, 0);
+  const double t0 = now();
+  pthread_barrier_wait(&g_go);
   struct timespec dl;
   clock_gettime(CLOCK_REALTIME, &dl);
   dl.tv_sec += 120;
@@ -168,6 +188,9 @@ static int step(void) {
   while (atomic_load(&g_done) < g_n)
     if (pthread_cond_timedwait(&g_cv, &g_mu, &dl) != 0) break;
   pthread_mutex_unlock(&g_mu);
+  if (g_trace)
+    fprintf(stderr, "[op_host] step: enqueued %.0f us, first callback %.0f us, last %.0f us\n", (g_t_enq - t0) * 1e6,
+            (g_t_first_cb - t0) * 1e6, (now() - t0) * 1e6);
   return atomic_load(&g_done) == g_n && atomic_load(&g_failed) == 0 ? 0 : -1;
 }
 
@@ -185,6 +208,7 @@ static int env_int(const char* k, int d) {
 int main(void) {
   const int steps = env_int("OP_HOST_STEPS", 20), warmup = env_int("OP_HOST_WARMUP", 3);
   g_threads = env_int("OP_HOST_THREADS", 4);
+  g_trace = env_int("OP_HOST_TRACE", 0);
   if (g_threads < 1 || g_threads > MAX_THREADS || steps < 1) return 2;
   resnet50();
   tips_init();
@@ -211,6 +235,9 @@ int main(void) {
     g_order[i] = g_order[j];
     g_order[j] = tmp;
   }
+  pthread_barrier_init(&g_go, NULL, (unsigned)g_threads + 1);
+  pthread_t th[MAX_THREADS];
+  for (int t = 0; t < g_threads; t++) pthread_create(&th[t], NULL, executor, (void*)(intptr_t)t);
   int rc = 0;
   for (int s = 0; s < warmup && rc == 0; s++) rc = step();
   double best = 1e30, sum = 0;
@@ -229,6 +256,9 @@ int main(void) {
       per[b] = per[b - 1], per[b - 1] = t;
     }
   const double med = per[steps / 2];
+  atomic_store(&g_quit, 1);  /* (a failed step may leave requests open: the threads are only released) */
+  pthread_barrier_wait(&g_go);
+  for (int t = 0; t < g_threads; t++) pthread_join(th[t], NULL);
   const char* check = "not checked";
   int bad = 0;
   if (rc == 0 && g_size == 1) {
