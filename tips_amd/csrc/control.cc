@@ -161,7 +161,7 @@ int tips_broadcast(const void* in, void* out, int64_t count, int dtype, int root
   const size_t bytes = (size_t)count * tips::dtype_size(dtype);
   return run_staged(st, in, bytes, out, bytes, (hipStream_t)stream, [&](const void* i, void* o, hipStream_t s) {
     if (st.size == 1) {
-      if (i != o) HIP_TRY(hipMemcpyAsync(o, i, bytes, hipMemcpyDeviceToDevice, s));
+      if (i != o) HIP_TRY(tips::launch_copy_buf(o, i, (int64_t)bytes, s));
       return 0;
     }
     if (peer_selected(st))

@@ -49,6 +49,10 @@ struct CopySeg {
 hipError_t launch_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int64_t tile_bytes,
                             int pol, hipStream_t s);
 
+// One contiguous device-to-device copy of `bytes` (tips_allreduce / tips_broadcast at one rank, out
+// of place): copy_buf_kernel when both pointers are 16-B aligned, else hipMemcpyAsync.
+hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_t s);
+
 // Peer transfers of the xGMI peer schedule (peer.cc): up to kMaxXferSegs byte
 // segments {src, dst, bytes} copied by one launch, segments interleaved over
 // the workgroups so every xGMI link carries traffic at once. src/dst may be

@@ -560,6 +560,46 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __
 #endif  // TIPS_DEV
 
 // ---------------------------------------------------------------------------
+// Contiguous copy: the out-of-place allreduce at one rank (MPI_Allreduce returns the input). Shaped
+// as sum2_buf_kernel with one operand: one 8 KiB tile per 256-lane workgroup in XCD-contiguous
+// order, buffer loads nt, buffer stores sc1 (the line leaves the XCD's L2), descriptors covering
+// exactly the tile; the < 16 trailing bytes go bytewise in workgroup 0. (hipMemcpyAsync's D2D blit
+// moved config 3's 1 GiB at 0.62 of HBM, profiles/r04/n_bench_n1.jsonl.)
+template <int U>
+__global__ __launch_bounds__(kBlock) void copy_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
+                                                         int64_t nvec, int64_t tail_begin, int64_t bytes) {
+  constexpr int64_t kTile = (int64_t)kBlock * U;
+  const int64_t first = xcd_tile(blockIdx.x, gridDim.x) * kTile;
+  const int tid = threadIdx.x;
+  if (first < nvec) {
+    const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + first), (short)0, rec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, 2);
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (u * kBlock + tid) * 16, 0, 16);
+  }
+  if (blockIdx.x == 0 && tail_begin + tid < bytes)
+    reinterpret_cast<char*>(dst)[tail_begin + tid] = reinterpret_cast<const char*>(src)[tail_begin + tid];
+}
+
+hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_t s) {
+  if (bytes <= 0 || dst == src) return hipSuccess;
+  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) != 0)
+    return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
+  constexpr int U = 2;
+  const int64_t nvec = bytes / 16;
+  int64_t grid = (nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
+  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
+  if (grid > 0x7fffffff) return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
+  hipLaunchKernelGGL((copy_buf_kernel<U>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst, (const u32x4*)src,
+                     nvec, nvec * 16, bytes);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Segment copy (fusion pack / unpack / identity copy since round 3; fusion.cc)
 //
 // Tiles are cut from a virtual byte space (a fusion bucket, or the flat layout of a whole tensor

@@ -533,7 +533,7 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
     return rccl_leave(st, stream);
   }
   if (st.size == 1) {  // MPI_Allreduce on one rank returns the input
-    if (in != out) HIP_TRY(hipMemcpyAsync(out, in, (size_t)(n * es), hipMemcpyDeviceToDevice, stream));
+    if (in != out) HIP_TRY(tips::launch_copy_buf(out, in, n * es, stream));
     return 0;
   }
   if (algo == TIPS_ALGO_PEER && st.size <= tips::kMaxSrcs)

@@ -124,6 +124,7 @@ static void fill(float* x, int r, int i, int64_t n) {
 static double now(void);
 static double g_t_first_cb, g_t_enq;  /* OP_HOST_TRACE: the step's first callback, the last enqueue */
 static atomic_int g_enq_threads;
+static double g_t_start[64], g_t_in_enq[64], g_t_in_reg[64];  /* OP_HOST_TRACE, per executor thread */
 
 static void count_done(void) {
   const int k = atomic_fetch_add(&g_done, 1);
@@ -156,12 +157,19 @@ static void* executor(void* arg) {
   while (1) {
     pthread_barrier_wait(&g_go);
     if (atomic_load(&g_quit)) return NULL;
+    double t_enq = 0, t_reg = 0;
+    if (t < 64) g_t_start[t] = now();
     for (int k = 0; k < g_n; k++) {
       const int i = g_order[k];
       if (i % g_threads != t) continue;
       Grad* g = &g_g[i];
+      const double a = now();
       const int64_t h = tips_enqueue_allreduce_shaped(g->name, g->in, g->out, g->dims, g->ndim, TIPS_FLOAT32, NULL);
-      if (h < 0 || tips_on_done(h, on_done, g) != TIPS_OK) {
+      const double b = now();
+      const int rc = h < 0 ? TIPS_OK : tips_on_done(h, on_done, g);
+      t_enq += b - a;
+      t_reg += now() - b;
+      if (h < 0 || rc != TIPS_OK) {
         pthread_mutex_lock(&g_mu);
         if (!g_err[0]) snprintf(g_err, sizeof g_err, "%s: %s", g->name, tips_last_error());
         pthread_mutex_unlock(&g_mu);
@@ -169,6 +177,7 @@ static void* executor(void* arg) {
         count_done();
       }
     }
+    if (t < 64) g_t_in_enq[t] = t_enq, g_t_in_reg[t] = t_reg;
     if (atomic_fetch_add(&g_enq_threads, 1) + 1 == g_threads) g_t_enq = now();
   }
 }
@@ -188,9 +197,13 @@ static int step(void) {
   while (atomic_load(&g_done) < g_n)
     if (pthread_cond_timedwait(&g_cv, &g_mu, &dl) != 0) break;
   pthread_mutex_unlock(&g_mu);
-  if (g_trace)
+  if (g_trace) {
     fprintf(stderr, "[op_host] step: enqueued %.0f us, first callback %.0f us, last %.0f us\n", (g_t_enq - t0) * 1e6,
             (g_t_first_cb - t0) * 1e6, (now() - t0) * 1e6);
+    for (int t = 0; t < g_threads && t < 64; t++)  /* when each thread started; its time inside the two calls */
+      fprintf(stderr, "[op_host]   thread %d: start %.0f us, in enqueue %.0f us, in on_done %.0f us\n", t,
+              (g_t_start[t] - t0) * 1e6, g_t_in_enq[t] * 1e6, g_t_in_reg[t] * 1e6);
+  }
   return atomic_load(&g_done) == g_n && atomic_load(&g_failed) == 0 ? 0 : -1;
 }
 
