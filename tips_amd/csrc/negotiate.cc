@@ -453,30 +453,33 @@ class Negotiator {
     if (ndim == 0) r->shape.push_back(1);  // a scalar travels as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
     r->dtype = dtype;
     r->stream = s;
-    if (!dry_ && !r->body) {  // the real executor (the dry run touches no memory; a routed body checks its own)
-      // (no st.mu here: the executor holds it while it reduces, and nothing below needs it;
-      // st.device is fixed from init on)
-      if (!pr || !pr->device_set) TRY(set_device(S()));
-      if (pr) pr->device_set = true;
+    const bool need_ev = !dry_ && !r->body;
+    if (need_ev && r->count > 0) {  // the real executor (the dry run touches no memory; a routed body checks its own)
       // device tensors run stream-ordered on `s`; host tensors (the reference's MPIAllreduce is a
       // CPU op, ops.cc:118) run synchronously on the executor thread, staged through HBM as
       // tips_allreduce stages them. Both pointers of a request live on the same side.
-      if (r->count > 0) {
-        auto dev = [&](const void* q) { return pr ? pr->is_device(q) : is_device_ptr(q); };
-        const bool din = dev(in), dout = type == TIPS_REQ_ALLGATHER ? din : dev(out);
-        if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "named request %s: one device and one host pointer", name.c_str());
-        r->host = !din;
-      }
-      {
-        std::lock_guard<std::mutex> l(m_);
-        if (!ev_pool_.empty()) {
-          r->ev = ev_pool_.back();
-          ev_pool_.pop_back();
-        }
-      }
-      if (!r->ev) HIP_TRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+      // (hipPointerGetAttributes needs no current device, so there is no hipSetDevice per request)
+      auto dev = [&](const void* q) { return pr ? pr->is_device(q) : is_device_ptr(q); };
+      const bool din = dev(in), dout = type == TIPS_REQ_ALLGATHER ? din : dev(out);
+      if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "named request %s: one device and one host pointer", name.c_str());
+      r->host = !din;
     }
-    std::lock_guard<std::mutex> l(m_);
+    // One lock for the event and the tables (executor threads enqueue concurrently); a new event
+    // (pool empty: the first requests of a job) is created outside it, on the library's device.
+    // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
+    std::unique_lock<std::mutex> l(m_);
+    if (need_ev) {
+      if (!ev_pool_.empty()) {
+        r->ev = ev_pool_.back();
+        ev_pool_.pop_back();
+      } else {
+        l.unlock();
+        if (!pr || !pr->device_set) TRY(set_device(S()));
+        if (pr) pr->device_set = true;
+        HIP_TRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+        l.lock();
+      }
+    }
     auto refuse = [&](int code, const std::string& msg) -> int64_t {  // the event goes back to the pool
       if (r->ev) ev_pool_.push_back(r->ev);
       r->ev = nullptr;
