@@ -163,6 +163,31 @@ def test_allreduce_single_rank_device_and_host(gpu):
         gpu.allreduce(torch.zeros(3, dtype=torch.uint8, device="cuda"))
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 1023, 4099, (1 << 20) + 7, 3 << 21])
+@pytest.mark.parametrize("dtype", [F32, F16, F64])
+def test_single_rank_out_of_place_copy(gpu, n, dtype):
+    """At one rank an out-of-place tips_allreduce / tips_broadcast is a copy (MPI_Allreduce returns the
+    input): copy_buf_kernel for 16-B aligned pointers (vectors + a bytewise tail), hipMemcpyAsync
+    otherwise. Every byte of out copied, nothing past it touched, for aligned and shifted views."""
+    import torch
+    from tips_amd import _lib
+    tdt, idt = {F32: (torch.float32, torch.int32), F16: (torch.float16, torch.int16),
+                F64: (torch.float64, torch.int64)}[dtype]
+    s = torch.cuda.current_stream().cuda_stream
+    for shift in (0, 1, 2):  # elements: shift * element size bytes off the allocation's aligned base
+        src = torch.randn(n + 8, device="cuda").to(tdt)
+        sentinel = torch.full((n + 8,), 7.0, device="cuda", dtype=tdt)
+        i = src[shift:shift + n]
+        for call in ("tips_allreduce", "tips_broadcast"):
+            dst = sentinel.clone()
+            o = dst[shift:shift + n]
+            args = (_lib.OP_SUM,) if call == "tips_allreduce" else (0,)  # op / root
+            assert _lib.call(call, i.data_ptr(), o.data_ptr(), n, dtype, *args, s) == 0
+            torch.cuda.synchronize()
+            assert torch.equal(o.view(idt), i.view(idt)), (call, shift)
+            assert torch.equal(dst[:shift], sentinel[:shift]) and torch.equal(dst[shift + n:], sentinel[shift + n:])
+
+
 def test_rccl_allreduce_single_rank(gpu):
     import torch
     prev = gpu.set_algorithm("rccl")
