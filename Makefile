@@ -69,6 +69,11 @@ tools/_bin/op_body: tests/c/op_body.c $(LIB) include/tips_hip.h oracle/build/lib
 	  -Ltips_amd/lib -ltips_hip -Loracle/build -loracle -L/opt/rocm/lib -lamdhip64 -lpthread \
 	  -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -Wl,-rpath,/opt/rocm/lib
 
+# what the HIP calls of a named-request enqueue cost (diagnostic, tools/enqueue_probe.cc)
+tools/_bin/enqueue_probe: tools/enqueue_probe.cc
+	@mkdir -p tools/_bin
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -o $@ $< -lpthread
+
 # config 5 as 214 named host requests from TF-style executor threads (tools/op_host.c): bench.py's
 # leg links the product library only; the -m gpu test's build also checks against the oracle's fold
 tools/_bin/op_host: tools/op_host.c $(LIB) include/tips_hip.h

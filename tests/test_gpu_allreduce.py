@@ -724,6 +724,32 @@ def test_enqueue_n_classifies_each_pointer(gpu):
     assert np.array_equal(h_in, h_out)
 
 
+def test_single_enqueue_classified_by_the_negotiation_thread(gpu):
+    """A single named request is classified (device / host) on the negotiation thread, not in the
+    enqueue (Req::classify): device, host and mixed requests enqueued back to back; the mixed one is
+    announced as bad and fails through tips_wait with the reason, the others complete exactly."""
+    import ctypes
+    import torch
+    from tips_amd import _lib
+    L = _lib.lib()
+    d_in = torch.randn(4099, device="cuda")
+    d_out = torch.empty_like(d_in)
+    h_in = np.random.default_rng(2).random(3001).astype(np.float32)
+    h_out = np.empty_like(h_in)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    hd = L.tips_enqueue_allreduce(b"classify.dev", ctypes.c_void_p(d_in.data_ptr()), ctypes.c_void_p(d_out.data_ptr()),
+                                  d_in.numel(), _lib.FLOAT32, stream)
+    hm = L.tips_enqueue_allreduce(b"classify.mixed", ctypes.c_void_p(d_in.data_ptr()), h_out.ctypes.data_as(ctypes.c_void_p),
+                                  100, _lib.FLOAT32, stream)
+    hh = L.tips_enqueue_allreduce(b"classify.host", h_in.ctypes.data_as(ctypes.c_void_p), h_out.ctypes.data_as(ctypes.c_void_p),
+                                  h_in.size, _lib.FLOAT32, stream)
+    assert hd > 0 and hm > 0 and hh > 0, _lib.last_error()
+    assert L.tips_wait(hm) < 0 and "one device and one host pointer on rank 0" in _lib.last_error()
+    assert L.tips_wait(hd) == 0 and L.tips_wait(hh) == 0, _lib.last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(d_out, d_in) and np.array_equal(h_out, h_in)
+
+
 def test_sparse_allreduce_single_rank(gpu):
     """The reference's IndexedSlices branch (allgather of values and indices, __init__.py:59-74) through
     tips_allgatherv on one rank: device and host, IndexedSlices and torch sparse COO."""

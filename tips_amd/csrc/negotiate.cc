@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <pthread.h>
 #include <deque>
 #include <memory>
 #include <thread>
@@ -44,6 +45,31 @@ struct GroupEv {
   ~GroupEv() {
     if (ev) (void)hipEventDestroy(ev);
   }
+};
+
+// The request tables' lock (and the negotiator's): glibc's adaptive mutex, which spins briefly
+// before it sleeps. Executor threads enqueueing at once hold it for well under a microsecond; with
+// std::mutex each hand-over between them went through a futex wake, and four threads enqueueing
+// config 5's 214 requests took longer than one thread (tools/op_host.c, OP_HOST_TRACE).
+class AdaptiveMutex {
+ public:
+  AdaptiveMutex() {
+    pthread_mutexattr_t a;
+    pthread_mutexattr_init(&a);
+    // (TIPS_ADAPTIVE_LOCKS=0: a plain mutex, as std::mutex, for A/B runs of tools/op_host_sweep.sh)
+    pthread_mutexattr_settype(&a, env_i64("TIPS_ADAPTIVE_LOCKS", 1) ? PTHREAD_MUTEX_ADAPTIVE_NP : PTHREAD_MUTEX_NORMAL);
+    pthread_mutex_init(&m_, &a);
+    pthread_mutexattr_destroy(&a);
+  }
+  ~AdaptiveMutex() { pthread_mutex_destroy(&m_); }
+  AdaptiveMutex(const AdaptiveMutex&) = delete;
+  AdaptiveMutex& operator=(const AdaptiveMutex&) = delete;
+  void lock() { pthread_mutex_lock(&m_); }
+  bool try_lock() { return pthread_mutex_trylock(&m_) == 0; }
+  void unlock() { pthread_mutex_unlock(&m_); }
+
+ private:
+  pthread_mutex_t m_;
 };
 
 struct Req {
@@ -73,6 +99,13 @@ struct Req {
   tips_done_fn cb = nullptr;
   void* cb_ctx = nullptr;
   bool cb_queued = false;
+  // A single enqueue does not ask HIP where its pointers live: hipPointerGetAttributes takes a
+  // runtime-wide lock, and TF-style executor threads enqueueing at once queued on it (4 threads:
+  // 1.38 us per lookup, 0.10 alone; tools/enqueue_probe.cc). The negotiation thread classifies
+  // the cycle's requests before announcing them, one thread, no contention; a request whose two
+  // pointers disagree is announced as bad and fails on every rank once all have announced it.
+  bool classify = false;
+  std::string bad;
 };
 
 // The negotiation thread itself: a collective entry point called there runs directly (it is the
@@ -170,6 +203,7 @@ struct Reader {
 //   (sizes: an allgather's first dimension per rank, the ResponseMessage's tensor_sizes)
 struct Announce {
   int type = TIPS_REQ_ALLREDUCE, root = 0;
+  bool bad = false;  // the announcing rank found the request unusable (its pointers disagree)
   int dtype;
   int64_t count;
   std::vector<int64_t> shape;
@@ -194,6 +228,7 @@ struct Table {
     int nseen = 0;
     bool queued = false;
     std::string dup;  // set when a rank announced this name twice while unresolved
+    std::string bad;  // set when a rank announced this name as unusable (failed once all announced)
   };
   int p = 1;
   std::unordered_map<std::string, Row> rows;
@@ -216,6 +251,7 @@ struct Table {
         r.nseen = 0;
         r.queued = false;
         r.dup.clear();
+        r.bad.clear();
         it = rows.insert(std::move(nh)).position;
       } else {
         Row r;
@@ -231,6 +267,8 @@ struct Table {
     } else {
       r.seen[rank] = 1;
       r.nseen++;
+      if (a.bad && r.bad.empty())
+        r.bad = "named request " + a.name + ": one device and one host pointer on rank " + std::to_string(rank);
       int64_t* rec = &r.rec[(size_t)rank * TIPS_REQUEST_WORDS];
       rec[0] = a.type;
       rec[1] = a.dtype;
@@ -253,6 +291,8 @@ struct Table {
       Row& r = it->second;
       if (!r.dup.empty()) {
         out.push_back({false, name, r.dup});
+      } else if (!r.bad.empty()) {
+        out.push_back({false, name, r.bad});
       } else {
         const int W = TIPS_REQUEST_WORDS;
         int rc = check_records(r.rec.data(), p);
@@ -457,17 +497,24 @@ class Negotiator {
     if (need_ev && r->count > 0) {  // the real executor (the dry run touches no memory; a routed body checks its own)
       // device tensors run stream-ordered on `s`; host tensors (the reference's MPIAllreduce is a
       // CPU op, ops.cc:118) run synchronously on the executor thread, staged through HBM as
-      // tips_allreduce stages them. Both pointers of a request live on the same side.
-      // (hipPointerGetAttributes needs no current device, so there is no hipSetDevice per request)
-      auto dev = [&](const void* q) { return pr ? pr->is_device(q) : is_device_ptr(q); };
-      const bool din = dev(in), dout = type == TIPS_REQ_ALLGATHER ? din : dev(out);
-      if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "named request %s: one device and one host pointer", name.c_str());
-      r->host = !din;
+      // tips_allreduce stages them. Both pointers of a request live on the same side. A list
+      // enqueue knows its allocations (pr: one HIP lookup per segment) and checks here; a single
+      // request is classified by the negotiation thread (Req::classify).
+      static const bool at_enqueue = env_i64("TIPS_CLASSIFY_AT_ENQUEUE", 0) != 0;  // (A/B: round 3's place)
+      PtrRanges one;
+      if (!pr && at_enqueue) pr = &one;
+      if (pr) {
+        const bool din = pr->is_device(in), dout = type == TIPS_REQ_ALLGATHER ? din : pr->is_device(out);
+        if (din != dout) return fail(TIPS_ERR_INVALID_ARG, "named request %s: one device and one host pointer", name.c_str());
+        r->host = !din;
+      } else {
+        r->classify = true;
+      }
     }
     // One lock for the event and the tables (executor threads enqueue concurrently); a new event
     // (pool empty: the first requests of a job) is created outside it, on the library's device.
     // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
-    std::unique_lock<std::mutex> l(m_);
+    std::unique_lock<AdaptiveMutex> l(m_);
     if (need_ev) {
       if (!ev_pool_.empty()) {
         r->ev = ev_pool_.back();
@@ -506,7 +553,7 @@ class Negotiator {
   int poll(int64_t h, bool block, bool routed = false) {
     std::shared_ptr<Req> r;
     {
-      std::unique_lock<std::mutex> l(m_);
+      std::unique_lock<AdaptiveMutex> l(m_);
       auto it = by_handle_.find(h);
       if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
       r = it->second;
@@ -529,7 +576,7 @@ class Negotiator {
   }
 
   void release(int64_t h, const std::shared_ptr<Req>& r) {
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     if (r->ev) ev_pool_.push_back(r->ev);  // reused by the next request
     r->ev = nullptr;
     r->gev.reset();
@@ -540,7 +587,7 @@ class Negotiator {
   // request has finished (a device request: when its work on the device is done); the handle is
   // released then. A request that has already finished is queued at once.
   int on_done(int64_t h, tips_done_fn fn, void* ctx) {
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     auto it = by_handle_.find(h);
     if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
     auto& r = it->second;
@@ -555,14 +602,14 @@ class Negotiator {
   // collective: every rank's loop learns from rank 0 that all ranks asked to stop
   int stop() {
     {
-      std::lock_guard<std::mutex> l(m_);
+      std::lock_guard<AdaptiveMutex> l(m_);
       if (!running_ && !thread_.joinable() && !waiter_.joinable()) return 0;
       want_stop_ = true;
       cv_.notify_all();
     }
     if (thread_.joinable()) thread_.join();
     {  // the completion thread drains what is queued (the loop failed every unmatched request), then ends
-      std::lock_guard<std::mutex> l(m_);
+      std::lock_guard<AdaptiveMutex> l(m_);
       waiter_stop_ = true;
       done_cv_.notify_all();
     }
@@ -574,7 +621,7 @@ class Negotiator {
 
   // number of completion callbacks called so far (the selftest's log)
   int64_t callbacks_called() {
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     return cb_called_;
   }
 
@@ -587,15 +634,15 @@ class Negotiator {
   }
 
   bool running() {
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     return running_;
   }
   std::vector<std::string> log() {
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     return log_;
   }
   void note(const std::string& s) {
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     log_.push_back(s);
   }
 
@@ -615,7 +662,7 @@ class Negotiator {
       set_phase("waiting for requests");
       long long t_linger = 0;
       {
-        std::unique_lock<std::mutex> l(m_);
+        std::unique_lock<AdaptiveMutex> l(m_);
         cv_.wait_for(l, cycle, [&] { return !fresh_.empty() || want_stop_; });
         // Linger while requests keep arriving (a gradient list is enqueued in a burst), so one
         // cycle announces - and one fused batch reduces - the whole burst instead of its first
@@ -631,6 +678,13 @@ class Negotiator {
         stopping = want_stop_;
         t_linger = us_since(t0);
       }
+      for (auto& r : batch)
+        if (r->classify) {  // (see Req::classify; nothing else reads host / bad before execute)
+          const bool din = is_device_ptr(r->in), dout = r->type == TIPS_REQ_ALLGATHER ? din : is_device_ptr(r->out);
+          if (din != dout) r->bad = "one device and one host pointer";
+          r->host = !din;
+          r->classify = false;
+        }
       const auto t_x = std::chrono::steady_clock::now();
       Writer w;
       w.put<uint8_t>(stopping ? 1 : 0);
@@ -638,6 +692,7 @@ class Negotiator {
       for (auto& r : batch) {
         w.put<int32_t>(r->type);
         w.put<int32_t>(r->root);
+        w.put<uint8_t>(r->bad.empty() ? 0 : 1);
         w.put<int32_t>(r->dtype);
         w.put<int64_t>(r->count);
         w.put<uint32_t>((uint32_t)r->shape.size());
@@ -676,7 +731,7 @@ class Negotiator {
                 "execute %lld us\n", rank_, (long long)cycles_, batch.size(), ds.size(), t_linger, t_exchange, us_since(t_e));
       if (shutdown) break;
     }
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     running_ = false;
     std::vector<std::string> unmatched;
     for (auto& kv : by_name_) unmatched.push_back(kv.first);
@@ -711,7 +766,7 @@ class Negotiator {
     std::deque<std::shared_ptr<Req>> batch;
     while (true) {
       {
-        std::unique_lock<std::mutex> l(m_);
+        std::unique_lock<AdaptiveMutex> l(m_);
         done_cv_.wait(l, [&] { return !done_q_.empty() || waiter_stop_; });
         if (done_q_.empty()) return;
         batch.swap(done_q_);
@@ -737,7 +792,7 @@ class Negotiator {
         r->cb(r->cb_ctx, status, msg.c_str());
       }
       set_waiter_req(nullptr, false);
-      std::lock_guard<std::mutex> l(m_);
+      std::lock_guard<AdaptiveMutex> l(m_);
       for (auto& r : batch) {  // (release() for the whole batch)
         if (r->ev) ev_pool_.push_back(r->ev);
         r->ev = nullptr;
@@ -787,6 +842,7 @@ class Negotiator {
         a.shape.clear();
         a.type = rd.get<int32_t>();
         a.root = rd.get<int32_t>();
+        a.bad = rd.get<uint8_t>() != 0;
         a.dtype = rd.get<int32_t>();
         a.count = rd.get<int64_t>();
         const uint32_t ndim = rd.get<uint32_t>();
@@ -824,7 +880,7 @@ class Negotiator {
     const size_t n = ds.size();
     std::vector<std::shared_ptr<Req>> reqs(n);
     {
-      std::lock_guard<std::mutex> l(m_);
+      std::lock_guard<AdaptiveMutex> l(m_);
       for (size_t i = 0; i < n; i++) {
         auto it = by_name_.find(ds[i].name);
         if (it == by_name_.end()) continue;  // (cannot happen: every rank announced it)
@@ -928,7 +984,7 @@ class Negotiator {
         i = j;
       }
     }
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     for (size_t i = 0; i < n; i++)
       if (reqs[i]) {
         reqs[i]->state = state[i];
@@ -1006,7 +1062,7 @@ class Negotiator {
   }
 
   void set_loop_error(const std::string& e) {
-    std::lock_guard<std::mutex> l(m_);
+    std::lock_guard<AdaptiveMutex> l(m_);
     if (loop_err_.empty()) loop_err_ = e;
   }
 
@@ -1016,8 +1072,8 @@ class Negotiator {
   std::vector<int> peers_;
   Table table_;
   std::thread thread_;
-  std::mutex m_;
-  std::condition_variable cv_;
+  AdaptiveMutex m_;
+  std::condition_variable_any cv_;
   bool running_ = false, want_stop_ = false;
   int64_t next_handle_ = 0;
   std::deque<std::shared_ptr<Req>> fresh_;
@@ -1029,7 +1085,7 @@ class Negotiator {
   hipStream_t neg_stream_ = nullptr;  // fused batches whose requests came on several streams
   std::thread waiter_;                // completion callbacks (started by the first tips_on_done)
   std::deque<std::shared_ptr<Req>> done_q_;
-  std::condition_variable done_cv_;
+  std::condition_variable_any done_cv_;
   bool waiter_stop_ = false;
   int64_t cb_called_ = 0;
 
@@ -1076,7 +1132,7 @@ class Negotiator {
                           : waiter_syncing_ ? "hipEventSynchronize of " + waiter_req_->name + (waiter_req_->gev ? " (fused batch)" : "")
                                             : "callback of " + waiter_req_->name);
     }
-    std::unique_lock<std::mutex> l(m_, std::try_to_lock);
+    std::unique_lock<AdaptiveMutex> l(m_, std::try_to_lock);
     if (!l.owns_lock()) return out + " | (request lock held)";
     out += " | fresh " + std::to_string(fresh_.size()) + " pending " + std::to_string(by_name_.size()) + " handles " +
            std::to_string(by_handle_.size()) + " done_q " + std::to_string(done_q_.size()) + " callbacks " +
@@ -1091,7 +1147,7 @@ class Negotiator {
   }
 };
 
-std::mutex g_neg_mu;
+AdaptiveMutex g_neg_mu;
 std::shared_ptr<Negotiator> g_neg;  // (shared: a caller waiting on a request keeps it alive through a shutdown)
 std::string g_neg_failed;           // a failed start's verdict: later named requests fail with it at once
 Negotiator* g_selftest_neg = nullptr;  // a running tips_negotiation_selftest's own (tips_debug_state)
@@ -1110,7 +1166,7 @@ const char* master_addr() {
 int negotiation_stop() {
   std::shared_ptr<Negotiator> n;
   {
-    std::lock_guard<std::mutex> l(g_neg_mu);
+    std::lock_guard<AdaptiveMutex> l(g_neg_mu);
     n.swap(g_neg);
     g_neg_failed.clear();
   }
@@ -1133,7 +1189,7 @@ bool route_collective(int type, int dtype, const int64_t* shape, int ndim, int r
   if (tl_negotiation_thread) return false;
   std::shared_ptr<Negotiator> n;
   {
-    std::lock_guard<std::mutex> l(g_neg_mu);
+    std::lock_guard<AdaptiveMutex> l(g_neg_mu);
     n = g_neg;
   }
   if (!n || !n->running()) {
@@ -1162,7 +1218,7 @@ using namespace tips::rt;
 namespace {
 
 std::shared_ptr<Negotiator> negotiator(int* code) {  // started by the first named request (collective)
-  std::lock_guard<std::mutex> l(g_neg_mu);
+  std::lock_guard<AdaptiveMutex> l(g_neg_mu);
   if (!g_neg) {
     if (!g_neg_failed.empty()) {
       *code = fail(TIPS_ERR_MISMATCH, "%s", g_neg_failed.c_str());
@@ -1216,7 +1272,7 @@ int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t
 }
 
 std::shared_ptr<Negotiator> current() {
-  std::lock_guard<std::mutex> l(g_neg_mu);
+  std::lock_guard<AdaptiveMutex> l(g_neg_mu);
   return g_neg;
 }
 
@@ -1268,7 +1324,7 @@ int tips_on_done(int64_t handle, tips_done_fn fn, void* ctx) {
 int tips_debug_state(char* out, int64_t cap) {
   if (!out || cap < 1) return fail(TIPS_ERR_INVALID_ARG, "tips_debug_state: no buffer");
   std::string st = "no negotiation";
-  std::unique_lock<std::mutex> l(g_neg_mu, std::try_to_lock);
+  std::unique_lock<AdaptiveMutex> l(g_neg_mu, std::try_to_lock);
   if (!l.owns_lock()) st = "(negotiation being started or stopped)";
   else if (g_neg) st = g_neg->debug_state();
   else if (g_selftest_neg) st = g_selftest_neg->debug_state();
@@ -1392,11 +1448,11 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   TRY(neg.start(rank, size, (host && *host) ? host : "127.0.0.1", port, true, 120, 0, synccount));
   struct Registered {  // visible to tips_debug_state while it runs
     explicit Registered(Negotiator* n) {
-      std::lock_guard<std::mutex> l(g_neg_mu);
+      std::lock_guard<AdaptiveMutex> l(g_neg_mu);
       g_selftest_neg = n;
     }
     ~Registered() {
-      std::lock_guard<std::mutex> l(g_neg_mu);
+      std::lock_guard<AdaptiveMutex> l(g_neg_mu);
       g_selftest_neg = nullptr;
     }
   } registered(&neg);
