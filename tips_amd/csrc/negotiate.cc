@@ -315,6 +315,9 @@ struct Table {
   }
 };
 
+using NameMap = std::unordered_map<std::string, std::shared_ptr<Req>>;
+using HandleMap = std::unordered_map<int64_t, std::shared_ptr<Req>>;
+
 class Negotiator {
  public:
   // Rank 0 listens on the first free port of [port, port + kPortTries); every other rank connects
@@ -348,6 +351,8 @@ class Negotiator {
     dry_ = dry_run;
     timeout_ms_ = timeout_s * 1000;
     table_.p = size;
+    by_name_.reserve(4096);  // (no rehash under the lock for a few thousand requests in flight)
+    by_handle_.reserve(4096);
     std::string err;
     if (size > 1) {
       const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
@@ -511,8 +516,18 @@ class Negotiator {
         r->classify = true;
       }
     }
-    // One lock for the event and the tables (executor threads enqueue concurrently); a new event
-    // (pool empty: the first requests of a job) is created outside it, on the library's device.
+    // The two table entries are allocated here, outside the lock (executor threads enqueue at
+    // once, and the lock's hold time, not the work, bounded them: 4 threads enqueueing config 5
+    // were no faster than one); under it they are only linked in.
+    r->handle = next_handle_.fetch_add(1) + 1;
+    thread_local NameMap name_scratch;
+    thread_local HandleMap handle_scratch;
+    name_scratch.emplace(name, r);
+    NameMap::node_type name_node = name_scratch.extract(name_scratch.begin());
+    handle_scratch.emplace(r->handle, r);
+    HandleMap::node_type handle_node = handle_scratch.extract(handle_scratch.begin());
+    // One lock for the event and the tables; a new event (pool empty: the first requests of a
+    // job) is created outside it, on the library's device.
     // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
     std::unique_lock<AdaptiveMutex> l(m_);
     if (need_ev) {
@@ -533,10 +548,9 @@ class Negotiator {
       return fail(code, "%s", msg.c_str());
     };
     if (!running_) return refuse(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
-    if (by_name_.count(name)) return refuse(TIPS_ERR_INVALID_ARG, "a request named " + name + " is already pending");
-    r->handle = ++next_handle_;
-    by_name_[name] = r;
-    by_handle_[r->handle] = r;
+    if (!by_name_.insert(std::move(name_node)).inserted)
+      return refuse(TIPS_ERR_INVALID_ARG, "a request named " + name + " is already pending");
+    by_handle_.insert(std::move(handle_node));
     // Wake the background thread only for the first request of a batch: it waits for that one up
     // to a cycle; after it, it lingers in steps of TIPS_BATCH_LINGER_US and sees later arrivals at
     // the next step anyway. (A wake per request cost a futex call here and a context switch
@@ -792,14 +806,19 @@ class Negotiator {
         r->cb(r->cb_ctx, status, msg.c_str());
       }
       set_waiter_req(nullptr, false);
-      std::lock_guard<AdaptiveMutex> l(m_);
-      for (auto& r : batch) {  // (release() for the whole batch)
-        if (r->ev) ev_pool_.push_back(r->ev);
-        r->ev = nullptr;
-        r->gev.reset();
-        by_handle_.erase(r->handle);
+      std::vector<HandleMap::node_type> gone;  // (freed after the lock: enqueueing threads wait on it)
+      gone.reserve(batch.size());
+      {
+        std::lock_guard<AdaptiveMutex> l(m_);
+        for (auto& r : batch) {  // (release() for the whole batch)
+          if (r->ev) ev_pool_.push_back(r->ev);
+          r->ev = nullptr;
+          r->gev.reset();
+          gone.push_back(by_handle_.extract(r->handle));
+        }
+        cb_called_ += (int64_t)batch.size();
       }
-      cb_called_ += (int64_t)batch.size();
+      gone.clear();
       batch.clear();
     }
   }
@@ -879,13 +898,15 @@ class Negotiator {
   void execute(const std::vector<Decision>& ds) {
     const size_t n = ds.size();
     std::vector<std::shared_ptr<Req>> reqs(n);
+    std::vector<NameMap::node_type> gone;  // (freed after the lock: enqueueing threads wait on it)
+    gone.reserve(n);
     {
       std::lock_guard<AdaptiveMutex> l(m_);
       for (size_t i = 0; i < n; i++) {
         auto it = by_name_.find(ds[i].name);
         if (it == by_name_.end()) continue;  // (cannot happen: every rank announced it)
         reqs[i] = it->second;
-        by_name_.erase(it);
+        gone.push_back(by_name_.extract(it));
         if (dry_) {
           std::string sz;
           for (size_t k = 0; k < ds[i].sizes.size(); k++) sz += (k ? "," : " sizes=") + std::to_string(ds[i].sizes[k]);
@@ -893,6 +914,7 @@ class Negotiator {
         }
       }
     }
+    gone.clear();
     std::vector<int> state(n, 0), code(n, TIPS_ERR_MISMATCH);
     std::vector<std::string> msg(n);
     for (size_t i = 0; i < n; i++) {
@@ -1075,10 +1097,10 @@ class Negotiator {
   AdaptiveMutex m_;
   std::condition_variable_any cv_;
   bool running_ = false, want_stop_ = false;
-  int64_t next_handle_ = 0;
+  std::atomic<int64_t> next_handle_{0};
   std::deque<std::shared_ptr<Req>> fresh_;
-  std::unordered_map<std::string, std::shared_ptr<Req>> by_name_;
-  std::unordered_map<int64_t, std::shared_ptr<Req>> by_handle_;
+  NameMap by_name_;
+  HandleMap by_handle_;
   std::vector<std::string> log_;
   std::vector<hipEvent_t> ev_pool_;
   std::string loop_err_;
