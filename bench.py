@@ -1205,6 +1205,11 @@ class Workload(object):
                                    "reduces gradient set i %% %d, so no step finds its gradients in the 256 MiB "
                                    "Infinity Cache" % self.rot)}
             del rec["busbw_GBps"]
+            if self.workload == "bucket":  # the copy kernel's own PMC passes (tools/gpu_pmc_round.sh)
+                tr = pmc_traffic("copy_buf_kernel", "*pmc_bucket.json")
+                if tr:
+                    rec["roofline"]["traffic"] = round(tr["bytes"])
+                    rec["roofline"]["traffic_source"] = tr["source"]
             if self.measure_pack:  # the dominant kernel (fusion pack / unpack) timed per launch; the step beside it
                 rec["fusion_one_rank"] = ("TIPS_FUSION_MEASURE_PACK=1: buckets packed and unpacked as at N > 1 (the "
                                           "default one-rank path does no bucket work)")

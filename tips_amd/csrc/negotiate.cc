@@ -232,7 +232,8 @@ struct Table {
   };
   int p = 1;
   std::unordered_map<std::string, Row> rows;
-  std::vector<std::string> ready_q;
+  std::vector<std::string> ready_q;  // [0, nready): names that became ready (slots reused across cycles)
+  size_t nready = 0;
   // Rows resolved in earlier cycles, kept with their map node, key and vectors: a new name reuses
   // one instead of allocating all four (a 1000-gradient step resolves 1000 names a cycle).
   std::vector<std::unordered_map<std::string, Row>::node_type> spare;
@@ -278,40 +279,52 @@ struct Table {
     }
     if (!r.queued && (!r.dup.empty() || r.nseen == p)) {
       r.queued = true;
-      ready_q.push_back(a.name);
+      if (nready < ready_q.size()) ready_q[nready] = a.name;  // (assign into a kept string: no allocation)
+      else ready_q.push_back(a.name);
+      nready++;
     }
   }
 
-  // the names that became ready since the last call, in readiness order, with their verdicts
-  std::vector<Decision> ready() {
-    std::vector<Decision> out;
-    out.reserve(ready_q.size());
-    for (auto& name : ready_q) {
+  // The names that became ready since the last call, in readiness order, each with its verdict,
+  // written straight into rank 0's response (ok, name, error, allgather sizes): no per-name
+  // Decision objects on the way. Returns how many.
+  uint32_t write_ready(Writer& w) {
+    const int W = TIPS_REQUEST_WORDS;
+    for (size_t q = 0; q < nready; q++) {
+      const std::string& name = ready_q[q];
       auto it = rows.find(name);
       Row& r = it->second;
-      if (!r.dup.empty()) {
-        out.push_back({false, name, r.dup});
-      } else if (!r.bad.empty()) {
-        out.push_back({false, name, r.bad});
-      } else {
-        const int W = TIPS_REQUEST_WORDS;
-        int rc = check_records(r.rec.data(), p);
-        Decision d{rc == 0, name, rc == 0 ? std::string() : last_error(), {}};
-        if (d.ok && r.rec[0] == TIPS_REQ_BROADCAST)
-          for (int i = 1; i < p && d.ok; i++)
+      const std::string* err = &r.dup;
+      std::string why;
+      bool ok = false;
+      if (r.dup.empty() && !r.bad.empty()) {
+        err = &r.bad;
+      } else if (r.dup.empty()) {
+        ok = check_records(r.rec.data(), p) == 0;
+        if (!ok) why = last_error();
+        if (ok && r.rec[0] == TIPS_REQ_BROADCAST)
+          for (int i = 1; i < p && ok; i++)
             if (r.roots[i] != r.roots[0]) {
-              d.ok = false;
-              d.err = "Mismatched broadcast root ranks: " + std::to_string(r.roots[0]) + " vs " + std::to_string(r.roots[i]);
+              ok = false;
+              why = "Mismatched broadcast root ranks: " + std::to_string(r.roots[0]) + " vs " + std::to_string(r.roots[i]);
             }
-        if (d.ok && r.rec[0] == TIPS_REQ_ALLGATHER)  // GatherFirstRankSizes (coordinator.cc:40-88)
-          for (int i = 0; i < p; i++) d.sizes.push_back(r.rec[(size_t)i * W + 3]);
-        out.push_back(std::move(d));
+        err = &why;
+      }
+      w.put<uint8_t>(ok ? 1 : 0);
+      w.str(name);
+      w.str(ok ? std::string() : *err);
+      if (ok && r.rec[0] == TIPS_REQ_ALLGATHER) {  // GatherFirstRankSizes (coordinator.cc:40-88)
+        w.put<uint32_t>((uint32_t)p);
+        for (int i = 0; i < p; i++) w.put<int64_t>(r.rec[(size_t)i * W + 3]);
+      } else {
+        w.put<uint32_t>(0);
       }
       if (spare.size() < 4096) spare.push_back(rows.extract(it));
       else rows.erase(it);
     }
-    ready_q.clear();
-    return out;
+    const uint32_t n = (uint32_t)nready;
+    nready = 0;
+    return n;
   }
 };
 
@@ -670,6 +683,10 @@ class Negotiator {
     auto us_since = [](std::chrono::steady_clock::time_point t) {
       return (long long)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
     };
+    // (kept across cycles: the announce, the response and the decided list reuse their buffers)
+    Writer w;
+    std::string resp;
+    std::vector<Decision> ds;
     while (true) {
       std::vector<std::shared_ptr<Req>> batch;
       bool stopping;
@@ -700,7 +717,7 @@ class Negotiator {
           r->classify = false;
         }
       const auto t_x = std::chrono::steady_clock::now();
-      Writer w;
+      w.b.clear();
       w.put<uint8_t>(stopping ? 1 : 0);
       w.put<uint32_t>((uint32_t)batch.size());
       for (auto& r : batch) {
@@ -713,7 +730,6 @@ class Negotiator {
         for (int64_t d : r->shape) w.put<int64_t>(d);
         w.str(r->name);
       }
-      std::string resp;
       set_phase("exchange (cycle " + std::to_string((long long)cycles_) + ", announcing " + std::to_string(batch.size()) + ")");
       if (!exchange(w.b, &resp)) break;
       {
@@ -723,15 +739,16 @@ class Negotiator {
       Reader rd(resp);
       const bool shutdown = rd.get<uint8_t>() != 0;
       const uint32_t n = rd.get<uint32_t>();
-      std::vector<Decision> ds;
+      size_t nd = 0;
       for (uint32_t i = 0; i < n && rd.ok; i++) {
-        Decision d;
+        if (nd == ds.size()) ds.emplace_back();
+        Decision& d = ds[nd++];  // (a kept slot: its strings keep their capacity)
         d.ok = rd.get<uint8_t>() != 0;
-        d.name = rd.str();
-        d.err = rd.str();
+        rd.str_into(d.name);
+        rd.str_into(d.err);
+        d.sizes.clear();
         const uint32_t m = rd.get<uint32_t>();
         for (uint32_t k = 0; k < m && rd.ok && k < (1u << 20); k++) d.sizes.push_back(rd.get<int64_t>());
-        ds.push_back(std::move(d));
       }
       if (!rd.ok) {
         set_loop_error("negotiation: malformed response");
@@ -739,10 +756,10 @@ class Negotiator {
       }
       const long long t_exchange = us_since(t_x);
       const auto t_e = std::chrono::steady_clock::now();
-      execute(ds);
-      if (trace && (!batch.empty() || !ds.empty()))
+      execute(ds, nd);
+      if (trace && (!batch.empty() || nd))
         fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us, exchange %lld us, "
-                "execute %lld us\n", rank_, (long long)cycles_, batch.size(), ds.size(), t_linger, t_exchange, us_since(t_e));
+                "execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, t_exchange, us_since(t_e));
       if (shutdown) break;
     }
     std::lock_guard<AdaptiveMutex> l(m_);
@@ -875,18 +892,15 @@ class Negotiator {
         return false;
       }
     }
-    const std::vector<Decision> ready = table_.ready();
     Writer w;
+    w.b.swap(*resp);  // (the previous response's buffer, reused)
+    w.b.clear();
     w.put<uint8_t>(everyone_stops ? 1 : 0);
-    w.put<uint32_t>((uint32_t)ready.size());
-    for (auto& d : ready) {
-      w.put<uint8_t>(d.ok ? 1 : 0);
-      w.str(d.name);
-      w.str(d.err);
-      w.put<uint32_t>((uint32_t)d.sizes.size());
-      for (int64_t v : d.sizes) w.put<int64_t>(v);
-    }
-    *resp = w.b;
+    const size_t count_at = w.b.size();
+    w.put<uint32_t>(0);
+    const uint32_t n = table_.write_ready(w);
+    memcpy(&w.b[count_at], &n, sizeof n);
+    resp->swap(w.b);
     return true;
   }
 
@@ -895,8 +909,7 @@ class Negotiator {
   // threshold and together within it, is reduced as ONE fused allreduce (pack, one
   // bucket exchange, unpack; fusion.cc) instead of one exchange per tensor. Every rank
   // received the same list, so every rank forms the same batches.
-  void execute(const std::vector<Decision>& ds) {
-    const size_t n = ds.size();
+  void execute(const std::vector<Decision>& ds, size_t n) {  // ds[0, n): this cycle's decisions
     std::vector<std::shared_ptr<Req>> reqs(n);
     std::vector<NameMap::node_type> gone;  // (freed after the lock: enqueueing threads wait on it)
     gone.reserve(n);
