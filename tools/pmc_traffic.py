@@ -9,7 +9,7 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7):
 FETCH_SIZE (3 TCC slots) and WRITE_SIZE (2) cannot share a pass: collect them in
 two separate rocprofv3 runs and pass both directories.
 
-usage: pmc_traffic.py OUT.json --fetch DIR --write DIR [--kernel SUBSTR] [--algo-bytes N]
+usage: pmc_traffic.py OUT.json --fetch DIR --write DIR [--kernel SUBSTR] [--algo-bytes N] [--stat median|mean]
 """
 import argparse
 import csv
@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--kernel", default="")
     ap.add_argument("--algo-bytes", type=float, default=None)
     ap.add_argument("--note", default="")
+    ap.add_argument("--stat", choices=("median", "mean"), default="median",
+                    help="per-dispatch statistic: mean when one launch covers buckets of different sizes")
     a = ap.parse_args()
     fv, ff = read_counters(a.fetch)
     wv, wf = read_counters(a.write)
@@ -57,13 +59,17 @@ def main():
         write = wv.get(k, {}).get("WRITE_SIZE", [])
         if not fetch or not write:
             continue
-        # median dispatch (the first dispatches of a process include cold-cache effects)
-        fm = sorted(fetch)[len(fetch) // 2]
-        wm = sorted(write)[len(write) // 2]
+        # median dispatch (the first dispatches of a process include cold-cache effects); mean for
+        # launches of different sizes (a list's buckets), against the mean algorithmic bytes
+        if a.stat == "mean":
+            fm, wm = sum(fetch) / len(fetch), sum(write) / len(write)
+        else:
+            fm = sorted(fetch)[len(fetch) // 2]
+            wm = sorted(write)[len(write) // 2]
         hbm = (2 * fm + wm) * 1024
         e = {"dispatches_fetch": len(fetch), "dispatches_write": len(write), "FETCH_SIZE_KiB_median": fm,
              "WRITE_SIZE_KiB_median": wm, "read_bytes_corrected": 2 * fm * 1024, "write_bytes": wm * 1024,
-             "hbm_bytes_per_launch": hbm}
+             "hbm_bytes_per_launch": hbm, "statistic": a.stat + " over dispatches"}
         if a.algo_bytes:
             e["algorithmic_bytes_per_launch"] = a.algo_bytes
             e["traffic_over_algorithmic"] = hbm / a.algo_bytes
