@@ -1200,7 +1200,7 @@ class Workload(object):
                                "unit": "GB/s", "frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                                "traffic": None,
                                "note": "one rank: the allreduce of a bucket is the identity; %s" % (
-                                   "in -> out copy (copy_buf_kernel: 8 KiB tiles, nt loads, sc1 stores)" if self.workload == "bucket" else
+                                   "in -> out copy (copy_buf_kernel: 4 KiB tiles, nt loads, sc1 stores)" if self.workload == "bucket" else
                                    "algorithmic bytes = pack + unpack of every tensor (2 reads + 2 writes); step i "
                                    "reduces gradient set i %% %d, so no step finds its gradients in the 256 MiB "
                                    "Infinity Cache" % self.rot)}

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -561,11 +562,11 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __
 
 // ---------------------------------------------------------------------------
 // Contiguous copy: the out-of-place allreduce at one rank (MPI_Allreduce returns the input). Shaped
-// as sum2_buf_kernel with one operand: one 8 KiB tile per 256-lane workgroup in XCD-contiguous
+// as sum2_buf_kernel with one operand: one 4 KiB tile per 256-lane workgroup in XCD-contiguous
 // order, buffer loads nt, buffer stores sc1 (the line leaves the XCD's L2), descriptors covering
 // exactly the tile; the < 16 trailing bytes go bytewise in workgroup 0. (hipMemcpyAsync's D2D blit
 // moved config 3's 1 GiB at 0.62 of HBM, profiles/r04/n_bench_n1.jsonl.)
-template <int U>
+template <int U, int SAUX = 16>
 __global__ __launch_bounds__(kBlock) void copy_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
                                                          int64_t nvec, int64_t tail_begin, int64_t bytes) {
   constexpr int64_t kTile = (int64_t)kBlock * U;
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(kBlock) void copy_buf_kernel(u32x4* __restrict__ ds
 #pragma unroll
     for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, 2);
 #pragma unroll
-    for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (u * kBlock + tid) * 16, 0, 16);
+    for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (u * kBlock + tid) * 16, 0, SAUX);
   }
   if (blockIdx.x == 0 && tail_begin + tid < bytes)
     reinterpret_cast<char*>(dst)[tail_begin + tid] = reinterpret_cast<const char*>(src)[tail_begin + tid];
@@ -589,13 +590,29 @@ hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_
   if (bytes <= 0 || dst == src) return hipSuccess;
   if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) != 0)
     return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
-  constexpr int U = 2;
+  // TIPS_COPY_BUF_VARIANT (a sweep knob, read once; tools/copy_buf_sweep.sh): 0 = 4 KiB tiles, sc1
+  // stores (shipped: 0.81-0.83 of HBM on config 3's 1 GiB, profiles/r04/z_copy_buf_sweep.txt);
+  // 1 = 8 KiB tiles (0.71-0.75); 2 = 16 KiB tiles (0.73); 3 = 4 KiB tiles, nt stores;
+  // 4 = hipMemcpyAsync (0.59-0.65)
+  static const int variant = [] {
+    const char* v = getenv("TIPS_COPY_BUF_VARIANT");
+    return v && *v ? atoi(v) : 0;
+  }();
+  if (variant == 4) return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
+  const int U = variant == 1 ? 2 : variant == 2 ? 4 : 1;
   const int64_t nvec = bytes / 16;
   int64_t grid = (nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
   grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
   if (grid > 0x7fffffff) return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
-  hipLaunchKernelGGL((copy_buf_kernel<U>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst, (const u32x4*)src,
-                     nvec, nvec * 16, bytes);
+  const dim3 g((unsigned)grid), b(kBlock);
+  if (variant == 1)
+    hipLaunchKernelGGL((copy_buf_kernel<2>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
+  else if (variant == 2)
+    hipLaunchKernelGGL((copy_buf_kernel<4>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
+  else if (variant == 3)
+    hipLaunchKernelGGL((copy_buf_kernel<1, 2>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
+  else
+    hipLaunchKernelGGL((copy_buf_kernel<1>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
   return hipGetLastError();
 }
 
