@@ -451,6 +451,27 @@ def shapes_case(c, rank, size, L, _lib, sp):
             errs.append("wrong error: %s" % e)
     if float(tips_amd.synchronize(s).item()) != float(sum(3 + r for r in range(size))):
         errs.append("scalar differs")
+    # A request whose pointers disagree on ONE rank (device in, host out on the last rank): that rank's
+    # negotiation thread classifies it and announces it as bad; it fails on EVERY rank, naming the
+    # rank, once all have announced it - no rank issues its allreduce alone - and the next one runs.
+    import ctypes
+    import numpy as np
+    d_out = torch.empty(64, device="cuda")
+    h_out = np.zeros(64, dtype=np.float32)
+    xin = torch.full((64,), float(rank + 1), device="cuda")
+    mixed = rank == size - 1
+    out_ptr = h_out.ctypes.data if mixed else d_out.data_ptr()
+    h = L.tips_enqueue_allreduce(b"ptrs.mixed", ctypes.c_void_p(xin.data_ptr()), ctypes.c_void_p(out_ptr), 64,
+                                 _lib.FLOAT32, ctypes.c_void_p(sp))
+    after = tips_amd.allreduce_async(xin, "ptrs.after")
+    if h <= 0:
+        errs.append("mixed enqueue refused at once: %s" % _lib.last_error())
+    elif L.tips_wait(h) == 0:
+        errs.append("a request with one device and one host pointer (rank %d) ran" % (size - 1))
+    elif "one device and one host pointer on rank %d" % (size - 1) not in _lib.last_error():
+        errs.append("wrong mixed-pointer error: %s" % _lib.last_error())
+    if float(tips_amd.synchronize(after)[0].item()) != float(sum(r + 1 for r in range(size))):
+        errs.append("the request after the mixed one differs")
     return {"case": {"shapes": True}, "rc": 0, "ok": not errs, "error": "; ".join(errs)}
 
 
