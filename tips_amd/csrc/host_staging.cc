@@ -6,6 +6,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <cctype>
 #include <chrono>
 #include <cstdio>
@@ -448,7 +449,11 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   };
   const int lag = direct_out ? np : (int)std::max<int64_t>(1, std::min<int64_t>(R - 1, env_i64("TIPS_HOST_UNPACK_LAG", 2)));
   // TIPS_HOST_TRACE=1: where one call's time goes (stderr), for tuning the piece and thread counts
-  static const bool trace = env_i64("TIPS_HOST_TRACE", 0) != 0;
+  static const int64_t trace_level = env_i64("TIPS_HOST_TRACE", 0);
+  const bool trace = trace_level != 0;
+  // TIPS_HOST_TRACE=2: also each piece's host timeline (us from the call's start): slot free, packed,
+  // issued, unpacked - to line up with a rocprofv3 memory-copy trace (tools/copytrace_report.py)
+  std::vector<std::array<double, 4>> tl(trace_level >= 2 ? (size_t)np : 0, std::array<double, 4>{0, 0, 0, 0});
   double t_pack = 0, t_wait = 0, t_unpack = 0, t_issue = 0;
   const auto t_start = std::chrono::steady_clock::now();
   auto since = [](std::chrono::steady_clock::time_point t) {
@@ -467,6 +472,9 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
             "unpack %.0f us, issue %.0f us, total %.0f us; device: first H2D -> last H2D %.0f us "
             "(%.1f GiB/s), -> last D2H %.0f us\n", (long long)total, np, nthreads, (int)direct_out, t_pack, t_wait,
             t_unpack, t_issue, since(t_start), h2d * 1e3, total / (h2d * 1e-3) / 1073741824.0, d2h * 1e3);
+    for (size_t i = 0; i < tl.size(); i++)
+      fprintf(stderr, "[tips host]   piece %zu %lld B: slot %.0f packed %.0f issued %.0f unpacked %.0f us\n", i,
+              (long long)pieces[i].len, tl[i][0], tl[i][1], tl[i][2], tl[i][3]);
   };
   // TIPS_HOST_H2D_STREAMS=2: odd pieces' H2D on a second stream (a second DMA queue), so the link
   // does not idle between one piece's copy and the next while the runtime starts it
@@ -477,9 +485,11 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     auto t0 = std::chrono::steady_clock::now();
     if (i >= R) HIP_TRY(hipEventSynchronize(ev[3 * (i - R)]));  // slot i % R: its last H2D has read it
     t_wait += since(t0);
+    if (!tl.empty()) tl[(size_t)i][0] = since(t_start);
     t0 = std::chrono::steady_clock::now();
     host_copy(i, true);
     t_pack += since(t0);
+    if (!tl.empty()) tl[(size_t)i][1] = since(t_start);
     t0 = std::chrono::steady_clock::now();
     if (trace && i == 0) HIP_TRY(hipEventRecord(tev[0], hs));
     HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice, hs));
@@ -497,6 +507,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
       HIP_TRY(hipEventRecord(tev[2], st.d2h_stream));
     }
     t_issue += since(t0);
+    if (!tl.empty()) tl[(size_t)i][2] = since(t_start);
     if (i >= lag) {
       t0 = std::chrono::steady_clock::now();
       HIP_TRY(hipEventSynchronize(ev[3 * (i - lag) + 2]));
@@ -504,6 +515,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
       t0 = std::chrono::steady_clock::now();
       host_copy(i - lag, false);
       t_unpack += since(t0);
+      if (!tl.empty()) tl[(size_t)(i - lag)][3] = since(t_start);
     }
   }
   if (direct_out) {
@@ -520,6 +532,7 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     t0 = std::chrono::steady_clock::now();
     host_copy(j, false);
     t_unpack += since(t0);
+    if (!tl.empty()) tl[(size_t)j][3] = since(t_start);
   }
   report();
   return 0;
