@@ -431,6 +431,17 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
   char* dev = (char*)st.host_in.p;
   char* pin_in = (char*)st.hpin[0];
   char* pin_out = (char*)st.hpin[1];
+  // TIPS_HOST_H2D_KERNEL=1 (an A/B knob, off): the H2D of each piece by copy_buf_kernel reading the
+  // page-locked slot through its device mapping (zero-copy) instead of a hipMemcpyAsync on the DMA
+  // engine. The runtime does the D2H with a blit kernel, and a DMA H2D issued while such a blit runs
+  // starts only when the blit ends (profiles/r04/ze_host_copytrace.json); but a kernel H2D holds the
+  // CUs while it waits on PCIe reads and starves the D2H blits: config 5 host -> host 4.1-4.4 ms
+  // against 2.6-3.2 ms (profiles/r04/zk_host_h2d_ab.txt).
+  char* pin_in_dev = nullptr;
+  if (env_i64("TIPS_HOST_H2D_KERNEL", 0) != 0 && hipHostGetDevicePointer((void**)&pin_in_dev, pin_in, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    pin_in_dev = nullptr;
+  }
   // D2H straight into the output (TIPS_HOST_DIRECT_OUT=0: through the page-locked slots, probing only)
   const bool direct_out = flat && env_i64("TIPS_HOST_DIRECT_OUT", 1) != 0 && is_pinned_host(flat, total);
 
@@ -492,7 +503,8 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     if (!tl.empty()) tl[(size_t)i][1] = since(t_start);
     t0 = std::chrono::steady_clock::now();
     if (trace && i == 0) HIP_TRY(hipEventRecord(tev[0], hs));
-    HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice, hs));
+    if (pin_in_dev) HIP_TRY(tips::launch_copy_buf(dev + off, pin_in_dev + (int64_t)(i % R) * piece, len, hs));
+    else HIP_TRY(hipMemcpyAsync(dev + off, pin_in + (int64_t)(i % R) * piece, (size_t)len, hipMemcpyHostToDevice, hs));
     HIP_TRY(hipEventRecord(ev[3 * i], hs));
     HIP_TRY(hipStreamWaitEvent(st.io_stream, ev[3 * i], 0));
     TRY(allreduce_device(st, dev + off, dev + off, len / es, dtype, st.io_stream));
