@@ -51,6 +51,10 @@ struct GroupEv {
 // before it sleeps. Executor threads enqueueing at once hold it for well under a microsecond; with
 // std::mutex each hand-over between them went through a futex wake, and four threads enqueueing
 // config 5's 214 requests took longer than one thread (tools/op_host.c, OP_HOST_TRACE).
+inline int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 class AdaptiveMutex {
  public:
   AdaptiveMutex() {
@@ -486,10 +490,20 @@ class Negotiator {
     up_ = lfd_ = -1;
   }
 
-  int64_t enqueue(const std::string& name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
-                  hipStream_t s, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
-                  void* actx = nullptr, int64_t* out_rows = nullptr, std::function<int()> body = nullptr,
-                  PtrRanges* pr = nullptr) {
+  // A request made ready for the tables outside their lock (enqueue, enqueue_list)
+  struct Prepared {
+    std::shared_ptr<Req> r;
+    NameMap::node_type name_node;
+    HandleMap::node_type handle_node;
+    bool need_ev = false;
+  };
+
+  // Everything of an enqueue that needs no lock: the request, where its memory lives, its two
+  // table entries (allocated here: executor threads enqueue at once, and the lock's hold time, not
+  // the work, bounded them - 4 threads enqueueing config 5 were no faster than one).
+  int prepare(Prepared& p, const std::string& name, const void* in, void* out, const int64_t* shape, int ndim,
+              int dtype, hipStream_t s, int type, int root, tips_alloc_fn alloc, void* actx, int64_t* out_rows,
+              std::function<int()> body, PtrRanges* pr) {
     if (ndim < 0 || ndim > TIPS_MAX_DIMS) return fail(TIPS_ERR_INVALID_ARG, "bad ndim %d", ndim);
     if (type == TIPS_REQ_ALLGATHER && ndim < 1) return fail(TIPS_ERR_INVALID_ARG, "An empty tensor found");
     auto r = std::make_shared<Req>();
@@ -503,6 +517,7 @@ class Negotiator {
     r->in = in;
     r->out = out;
     r->count = 1;
+    r->shape.reserve((size_t)std::max(ndim, 1));
     for (int d = 0; d < ndim; d++) {
       if (shape[d] < 0) return fail(TIPS_ERR_INVALID_ARG, "negative dimension");
       r->shape.push_back(shape[d]);
@@ -511,8 +526,8 @@ class Negotiator {
     if (ndim == 0) r->shape.push_back(1);  // a scalar travels as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
     r->dtype = dtype;
     r->stream = s;
-    const bool need_ev = !dry_ && !r->body;
-    if (need_ev && r->count > 0) {  // the real executor (the dry run touches no memory; a routed body checks its own)
+    p.need_ev = !dry_ && !r->body;
+    if (p.need_ev && r->count > 0) {  // the real executor (the dry run touches no memory; a routed body checks its own)
       // device tensors run stream-ordered on `s`; host tensors (the reference's MPIAllreduce is a
       // CPU op, ops.cc:118) run synchronously on the executor thread, staged through HBM as
       // tips_allreduce stages them. Both pointers of a request live on the same side. A list
@@ -529,49 +544,92 @@ class Negotiator {
         r->classify = true;
       }
     }
-    // The two table entries are allocated here, outside the lock (executor threads enqueue at
-    // once, and the lock's hold time, not the work, bounded them: 4 threads enqueueing config 5
-    // were no faster than one); under it they are only linked in.
     r->handle = next_handle_.fetch_add(1) + 1;
     thread_local NameMap name_scratch;
     thread_local HandleMap handle_scratch;
     name_scratch.emplace(name, r);
-    NameMap::node_type name_node = name_scratch.extract(name_scratch.begin());
+    p.name_node = name_scratch.extract(name_scratch.begin());
     handle_scratch.emplace(r->handle, r);
-    HandleMap::node_type handle_node = handle_scratch.extract(handle_scratch.begin());
-    // One lock for the event and the tables; a new event (pool empty: the first requests of a
-    // job) is created outside it, on the library's device.
-    // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
-    std::unique_lock<AdaptiveMutex> l(m_);
-    if (need_ev) {
+    p.handle_node = handle_scratch.extract(handle_scratch.begin());
+    p.r = std::move(r);
+    return 0;
+  }
+
+  // Under m_ (held by l): the request's event, its table entries, the fresh queue. The handle, or
+  // < 0 (the event back in the pool). A new event (pool empty: the first requests of a job) is
+  // made with the lock released, on the library's device.
+  int64_t commit(Prepared& p, std::unique_lock<AdaptiveMutex>& l, PtrRanges* pr) {
+    Req& r = *p.r;
+    if (p.need_ev) {
       if (!ev_pool_.empty()) {
-        r->ev = ev_pool_.back();
+        r.ev = ev_pool_.back();
         ev_pool_.pop_back();
       } else {
         l.unlock();
-        if (!pr || !pr->device_set) TRY(set_device(S()));
-        if (pr) pr->device_set = true;
-        HIP_TRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+        int rc = 0;
+        if (!pr || !pr->device_set) rc = set_device(S());
+        if (pr && rc == 0) pr->device_set = true;
+        const hipError_t e = rc == 0 ? hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) : hipSuccess;
         l.lock();
+        if (rc) return rc;
+        if (e != hipSuccess) return fail(TIPS_ERR_HIP, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
       }
     }
     auto refuse = [&](int code, const std::string& msg) -> int64_t {  // the event goes back to the pool
-      if (r->ev) ev_pool_.push_back(r->ev);
-      r->ev = nullptr;
+      if (r.ev) ev_pool_.push_back(r.ev);
+      r.ev = nullptr;
       return fail(code, "%s", msg.c_str());
     };
     if (!running_) return refuse(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
-    if (!by_name_.insert(std::move(name_node)).inserted)
-      return refuse(TIPS_ERR_INVALID_ARG, "a request named " + name + " is already pending");
-    by_handle_.insert(std::move(handle_node));
+    if (!by_name_.insert(std::move(p.name_node)).inserted)
+      return refuse(TIPS_ERR_INVALID_ARG, "a request named " + r.name + " is already pending");
+    by_handle_.insert(std::move(p.handle_node));
+    fresh_.push_back(p.r);
+    return r.handle;
+  }
+
+  int64_t enqueue(const std::string& name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
+                  hipStream_t s, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
+                  void* actx = nullptr, int64_t* out_rows = nullptr, std::function<int()> body = nullptr,
+                  PtrRanges* pr = nullptr) {
+    Prepared p;
+    TRY(prepare(p, name, in, out, shape, ndim, dtype, s, type, root, alloc, actx, out_rows, std::move(body), pr));
+    // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
+    std::unique_lock<AdaptiveMutex> l(m_);
     // Wake the background thread only for the first request of a batch: it waits for that one up
-    // to a cycle; after it, it lingers in steps of TIPS_BATCH_LINGER_US and sees later arrivals at
-    // the next step anyway. (A wake per request cost a futex call here and a context switch
-    // there for each of a 1000-tensor burst.)
+    // to a cycle; after it, it lingers and sees later arrivals anyway. (A wake per request cost a
+    // futex call here and a context switch there for each of a 1000-tensor burst.)
     const bool first = fresh_.empty();
-    fresh_.push_back(r);
-    if (first) cv_.notify_all();
-    return r->handle;
+    const int64_t h = commit(p, l, pr);
+    if (h > 0) {
+      last_arrival_ns_.store(steady_ns(), std::memory_order_release);
+      if (first) cv_.notify_all();
+    }
+    return h;
+  }
+
+  // A list (tips_enqueue_*_n): every request prepared before the lock, all of them committed under
+  // one hold, one wake-up. The negotiation then sees the list arrive at once instead of lingering
+  // through it (1000 requests one lock each took ~0.9 ms on the GPU box). handles[i] < 0 entries
+  // (refused before, or here) are skipped / set; returns the first refusal or 0.
+  int enqueue_list(std::vector<Prepared>& ps, int64_t* handles, PtrRanges* pr, std::string* first_err) {
+    int rc = 0;
+    std::unique_lock<AdaptiveMutex> l(m_);
+    bool any = false;
+    for (size_t i = 0; i < ps.size(); i++) {
+      if (!ps[i].r) continue;
+      handles[i] = commit(ps[i], l, pr);
+      if (handles[i] < 0 && rc == 0) {
+        rc = (int)handles[i];
+        *first_err = last_error();
+      }
+      any |= handles[i] > 0;
+    }
+    if (any) {
+      last_arrival_ns_.store(steady_ns(), std::memory_order_release);
+      cv_.notify_all();
+    }
+    return rc;
   }
 
   // 1 = done, 0 = pending, < 0 = error; a finished handle is released by the call that reports it.
@@ -692,6 +750,7 @@ class Negotiator {
       bool stopping;
       set_phase("waiting for requests");
       long long t_linger = 0;
+      int windows = 0;
       {
         std::unique_lock<AdaptiveMutex> l(m_);
         cv_.wait_for(l, cycle, [&] { return !fresh_.empty() || want_stop_; });
@@ -699,9 +758,21 @@ class Negotiator {
         // cycle announces - and one fused batch reduces - the whole burst instead of its first
         // few tensors. Bounded by the cycle time; TIPS_BATCH_LINGER_US = 0 turns it off.
         const auto t0 = std::chrono::steady_clock::now();
-        while (!fresh_.empty() && !want_stop_ && linger.count() > 0 && std::chrono::steady_clock::now() - t0 < cycle) {
-          const size_t seen = fresh_.size();
-          if (!cv_.wait_for(l, linger, [&] { return fresh_.size() != seen || want_stop_; })) break;
+        windows = 0;
+        if (!fresh_.empty() && !want_stop_ && linger.count() > 0) {
+          // Until TIPS_BATCH_LINGER_US have passed since the latest arrival (bounded by the cycle):
+          // each wait lasts just what is left of that quiet time. (Round 3 waited in whole 30 us
+          // windows until one saw no arrival; a timed wait oversleeps by ~50 us on the GPU box, so
+          // a cycle lingered one to two 83 us windows past the burst. Spinning instead was no
+          // faster within noise and kept a core busy: profiles/r04/zs_op_linger_ab.txt.)
+          const int64_t start = steady_ns(), linger_ns = (int64_t)linger.count() * 1000,
+                        cycle_ns = (int64_t)cycle.count() * 1000;
+          while (!want_stop_) {
+            const int64_t now = steady_ns(), quiet = now - last_arrival_ns_.load(std::memory_order_acquire);
+            if (quiet >= linger_ns || now - start >= cycle_ns) break;
+            windows++;
+            cv_.wait_for(l, std::chrono::nanoseconds(std::min(linger_ns - quiet, cycle_ns - (now - start))));
+          }
         }
         batch.assign(fresh_.begin(), fresh_.end());
         fresh_.clear();
@@ -758,8 +829,9 @@ class Negotiator {
       const auto t_e = std::chrono::steady_clock::now();
       execute(ds, nd);
       if (trace && (!batch.empty() || nd))
-        fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us, exchange %lld us, "
-                "execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, t_exchange, us_since(t_e));
+        fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us (%d windows), "
+                "exchange %lld us, execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, windows,
+                t_exchange, us_since(t_e));
       if (shutdown) break;
     }
     std::lock_guard<AdaptiveMutex> l(m_);
@@ -1112,6 +1184,7 @@ class Negotiator {
   bool running_ = false, want_stop_ = false;
   std::atomic<int64_t> next_handle_{0};
   std::deque<std::shared_ptr<Req>> fresh_;
+  std::atomic<int64_t> last_arrival_ns_{0};  // (steady clock) the latest enqueue: the linger's clock
   NameMap by_name_;
   HandleMap by_handle_;
   std::vector<std::string> log_;
@@ -1285,9 +1358,9 @@ std::shared_ptr<Negotiator> negotiator(int* code) {  // started by the first nam
   return g_neg;
 }
 
-int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
-                      void* stream, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
-                      void* actx = nullptr, int64_t* out_rows = nullptr, PtrRanges* pr = nullptr) {
+// The argument checks of a named request (before any negotiation state is touched)
+int check_named(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype, int type,
+                int root, tips_alloc_fn alloc) {
   TRY(check_dtype(dtype));
   if (!name || !*name || ndim < 0 || ndim > TIPS_MAX_DIMS || (ndim > 0 && !shape))
     return fail(TIPS_ERR_INVALID_ARG, "bad named request");
@@ -1299,11 +1372,71 @@ int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t
     const int size = tips_size();
     if (root < 0 || (size > 0 && root >= size)) return fail(TIPS_ERR_INVALID_ARG, "root rank %d out of range", root);
   }
+  return 0;
+}
+
+int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
+                      void* stream, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
+                      void* actx = nullptr, int64_t* out_rows = nullptr) {
+  TRY(check_named(name, in, out, shape, ndim, dtype, type, root, alloc));
   int code = TIPS_ERR_NOT_INITIALIZED;
   std::shared_ptr<Negotiator> n = negotiator(&code);
   if (!n) return code;
-  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, type, root, alloc, actx, out_rows, nullptr,
-                    pr);
+  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, type, root, alloc, actx, out_rows, nullptr);
+}
+
+// tips_enqueue_allreduce[_shaped]_n: request i has shape dims(i) = {pointer, ndim}. Every request is
+// checked and prepared first, then all are committed at once (Negotiator::enqueue_list); handles[i]
+// < 0 for a refused one, the first refusal returned.
+template <class Dims>
+int enqueue_named_list(const char* const* names, const void* const* ins, void* const* outs, int n, int dtype,
+                       void* stream, int64_t* handles, Dims dims) {
+  int rc = 0;
+  std::string first_err;
+  auto refused = [&](int i, int code) {
+    handles[i] = code;
+    if (rc == 0) {
+      rc = code;
+      first_err = last_error();
+    }
+  };
+  int code = TIPS_ERR_NOT_INITIALIZED;
+  std::shared_ptr<Negotiator> neg;
+  std::vector<Negotiator::Prepared> ps((size_t)n);
+  PtrRanges pr;  // (the list's device allocations, one HIP lookup per segment)
+  for (int i = 0; i < n; i++) {
+    const std::pair<const int64_t*, int> d = dims(i);
+    // (ndim -1: a bad request; -2: one whose reason dims() has already set)
+    int e = d.second == -2 ? (int)TIPS_ERR_INVALID_ARG
+            : d.second < 0 ? fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request")
+                           : check_named(names[i], ins[i], outs[i], d.first, d.second, dtype, TIPS_REQ_ALLREDUCE, 0, nullptr);
+    if (e == 0 && !neg && !(neg = negotiator(&code))) e = code;
+    if (e == 0)
+      e = neg->prepare(ps[(size_t)i], names[i], ins[i], outs[i], d.first, d.second, dtype, (hipStream_t)stream,
+                       TIPS_REQ_ALLREDUCE, 0, nullptr, nullptr, nullptr, nullptr, &pr);
+    if (e) refused(i, e);
+  }
+  if (neg && env_i64("TIPS_LIST_ONE_LOCK", 1) == 0) {  // (A/B: one commit per request, as round 3)
+    std::vector<Negotiator::Prepared> one(1);
+    for (int i = 0; i < n; i++) {
+      if (!ps[(size_t)i].r) continue;
+      one[0] = std::move(ps[(size_t)i]);
+      std::string err;
+      const int e = neg->enqueue_list(one, handles + i, &pr, &err);
+      if (e && rc == 0) {
+        rc = e;
+        first_err = err;
+      }
+    }
+  } else if (neg) {
+    std::string err;
+    const int e = neg->enqueue_list(ps, handles, &pr, &err);
+    if (e && rc == 0) {
+      rc = e;
+      first_err = err;
+    }
+  }
+  return rc ? fail(rc, "%s", first_err.c_str()) : 0;
 }
 
 std::shared_ptr<Negotiator> current() {
@@ -1377,19 +1510,9 @@ int tips_enqueue_allreduce_n(const char* const* names, const void* const* ins, v
                              int n, int dtype, void* stream, int64_t* handles) {
   if (n < 0 || (n > 0 && (!names || !ins || !outs || !counts || !handles)))
     return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce list");
-  int rc = 0;
-  std::string first_err;
-  PtrRanges pr;
-  for (int i = 0; i < n; i++) {
-    handles[i] = counts[i] < 0 ? fail(TIPS_ERR_INVALID_ARG, "bad named allreduce request")
-                               : enqueue_named(names[i], ins[i], outs[i], &counts[i], 1, dtype, stream,
-                                               TIPS_REQ_ALLREDUCE, 0, nullptr, nullptr, nullptr, &pr);
-    if (handles[i] < 0 && rc == 0) {
-      rc = (int)handles[i];
-      first_err = last_error();
-    }
-  }
-  return rc ? fail(rc, "%s", first_err.c_str()) : 0;
+  return enqueue_named_list(names, ins, outs, n, dtype, stream, handles, [&](int i) {
+    return std::make_pair(&counts[i], counts[i] < 0 ? -1 : 1);  // shape [count]
+  });
 }
 
 int tips_enqueue_allreduce_shaped_n(const char* const* names, const void* const* ins, void* const* outs,
@@ -1397,24 +1520,13 @@ int tips_enqueue_allreduce_shaped_n(const char* const* names, const void* const*
                                     int64_t* handles) {
   if (n < 0 || (n > 0 && (!names || !ins || !outs || !ndims || !handles)))
     return fail(TIPS_ERR_INVALID_ARG, "bad named allreduce list");
-  int rc = 0;
-  std::string first_err;
-  int64_t off = 0;
-  PtrRanges pr;
-  for (int i = 0; i < n; i++) {
-    if (ndims[i] < 0 || ndims[i] > TIPS_MAX_DIMS || (ndims[i] > 0 && !dims)) {
-      handles[i] = fail(TIPS_ERR_INVALID_ARG, "bad ndim %d for %s", ndims[i], names[i] ? names[i] : "?");
-    } else {
-      handles[i] = enqueue_named(names[i], ins[i], outs[i], dims ? dims + off : nullptr, ndims[i], dtype, stream,
-                                 TIPS_REQ_ALLREDUCE, 0, nullptr, nullptr, nullptr, &pr);
-      off += ndims[i];
-    }
-    if (handles[i] < 0 && rc == 0) {
-      rc = (int)handles[i];
-      first_err = last_error();
-    }
-  }
-  return rc ? fail(rc, "%s", first_err.c_str()) : 0;
+  std::vector<int64_t> offs((size_t)n + 1, 0);  // where request i's dims start (bad entries take none)
+  for (int i = 0; i < n; i++) offs[(size_t)i + 1] = offs[(size_t)i] + (ndims[i] > 0 && ndims[i] <= TIPS_MAX_DIMS ? ndims[i] : 0);
+  return enqueue_named_list(names, ins, outs, n, dtype, stream, handles, [&](int i) {
+    const bool ok = ndims[i] >= 0 && ndims[i] <= TIPS_MAX_DIMS && (ndims[i] == 0 || dims);
+    if (!ok) fail(TIPS_ERR_INVALID_ARG, "bad ndim %d for %s", ndims[i], names[i] ? names[i] : "?");
+    return std::make_pair(dims ? dims + offs[(size_t)i] : (const int64_t*)nullptr, ok ? ndims[i] : -2);
+  });
 }
 
 int tips_wait_n(const int64_t* handles, int n) {
