@@ -33,7 +33,8 @@ TIPS_API int tips_host_pool_selftest(int nthreads, int runs, int njobs);
 
 /* The negotiation protocol with an executor that only logs (no GPU): each
  * rank enqueues the newline-separated "name dtype count" lines of `requests`
- * ("@sleep ms" pauses, "@wait" blocks until every earlier request is
+ * ("@batch" ... "@endbatch" commits the lines between as one list, as
+ * tips_enqueue_allreduce_n does; "@sleep ms" pauses, "@wait" blocks until every earlier request is
  * decided, "@mark" logs "# mark <microseconds since the call began>"), stops,
  * and writes its execution log ("name OK" / "name ERR message", one per line,
  * in execution order) into out. For tests and the latency tool. */

@@ -72,6 +72,42 @@ def test_same_order_everywhere_despite_different_enqueue_orders():
     assert sorted(logs[0]) == sorted(n + " OK" for n in names)
 
 
+def test_list_commits_mixed_with_single_requests():
+    """Lists committed under one lock hold (Negotiator::enqueue_list, as tips_enqueue_allreduce_n):
+    3 ranks, each a different mix of lists and single requests in its own order, one rank's list
+    carrying a shape mismatch, and executor threads enqueueing lists beside the main thread; every
+    rank runs the same names in the same order, the mismatch fails everywhere, the rest succeed."""
+    names = ["g%d" % i for i in range(60)]
+    reqs = []
+    for r in range(3):
+        order = names[r * 7:] + names[:r * 7]
+        if r == 1:
+            order = list(reversed(order))
+        body = []
+        for i, n in enumerate(order):
+            if i % 10 == 0:
+                body.append(("@endbatch\n" if i else "") + "@batch")
+            count = 200 + names.index(n)
+            if n == "g13" and r == 2:
+                count += 1  # shape mismatch on one rank only
+            body.append("%s 0 %d" % (n, count))
+        body.append("@endbatch")
+        if r == 0:  # a second thread's lists beside the main thread's
+            body += ["t1: @batch"] + ["t1: x%d 0 8" % k for k in range(20)] + ["t1: @endbatch", "t1: @wait"]
+        else:
+            body += ["@batch"] + ["x%d 0 8" % k for k in range(19, -1, -1)] + ["@endbatch"]
+        body.append("@wait")
+        reqs.append("\n".join(body))
+    res = run(reqs)
+    logs = [[l for l in lines(log) if not l.startswith("callbacks")] for _, _, log, _ in res]
+    for rank, rc, log, err in res:
+        assert rc == 0, (rank, err)
+    assert logs[0] == logs[1] == logs[2]
+    got = dict(l.split(" ", 1) for l in logs[0])
+    assert got["g13"].startswith("ERR Mismatched allreduce tensor shapes")
+    assert all(got[n] == "OK" for n in names if n != "g13") and all(got["x%d" % k] == "OK" for k in range(20))
+
+
 def test_mismatch_fails_everywhere_with_reference_text():
     reqs = ["a 0 8\nb 0 8\nc 0 8", "c 0 8\nb 1 8\na 0 9"]  # b: dtype mismatch; a: shape mismatch
     res = run(reqs)

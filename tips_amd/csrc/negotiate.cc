@@ -1564,7 +1564,8 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   if (size < 1 || rank < 0 || rank >= size || !requests || !out || cap < 1)
     return fail(TIPS_ERR_INVALID_ARG, "bad selftest args");
   // lines: "name dtype count [d0,d1,...|-] [ar|ag|bc:ROOT]" (shape: default [count]; request type:
-  // default allreduce), "@sleep ms", "@wait" (all so far resolved), "@mark" (log "# mark us"),
+  // default allreduce), "@batch" ... "@endbatch" (the requests between them committed as one list,
+  // as tips_enqueue_allreduce_n does), "@sleep ms", "@wait" (all so far resolved), "@mark" (log "# mark us"),
   // "@synccount N" (this rank claims N synchronous collectives before the join). A line "tK: ..."
   // belongs to thread K: threads 1.. issue their lines concurrently with the main thread's (thread
   // 0), as a framework's executor threads issue ops, and every request then completes through a
@@ -1608,10 +1609,41 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   std::vector<int> issued(per.size(), 0), rcs(per.size(), 0);
   auto run = [&](size_t k) {
     std::vector<int64_t> handles;
+    bool batching = false;  // between "@batch" and "@endbatch": one list commit (Negotiator::enqueue_list)
+    std::vector<Negotiator::Prepared> batch;
+    auto issued_one = [&](int64_t h) -> bool {
+      if (h < 0) {
+        rcs[k] = (int)h;
+        return false;
+      }
+      if (cbs) {
+        issued[k]++;
+        if (neg.on_done(h, selftest_done, &counts[k]) != 0) {
+          rcs[k] = TIPS_ERR_INVALID_ARG;
+          return false;
+        }
+      } else {
+        handles.push_back(h);
+      }
+      return true;
+    };
     for (const std::string& line : per[k]) {
       char nm[256], dims[256] = "", kind[64] = "ar";
       long long dt = 0, cnt = 0;
-      if (line.rfind("@sleep ", 0) == 0) {
+      if (line == "@batch") {
+        batching = true;
+        batch.clear();
+      } else if (line == "@endbatch") {
+        batching = false;
+        std::vector<int64_t> hs(batch.size(), 0);
+        std::string err;
+        if (neg.enqueue_list(batch, hs.data(), nullptr, &err) != 0) {
+          rcs[k] = TIPS_ERR_INVALID_ARG;
+          return;
+        }
+        for (int64_t h : hs)
+          if (!issued_one(h)) return;
+      } else if (line.rfind("@sleep ", 0) == 0) {
         std::this_thread::sleep_for(std::chrono::milliseconds(atoi(line.c_str() + 7)));
       } else if (line == "@wait") {
         if (cbs) {
@@ -1635,19 +1667,16 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
           q = q ? q + 1 : "";
         }
         if (shape.empty()) shape.push_back(cnt);
-        const int64_t h = neg.enqueue(nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr, type, root);
-        if (h < 0) {
-          rcs[k] = (int)h;
-          return;
-        }
-        if (cbs) {
-          issued[k]++;
-          if (neg.on_done(h, selftest_done, &counts[k]) != 0) {
+        if (batching) {
+          batch.emplace_back();
+          if (neg.prepare(batch.back(), nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr, type,
+                          root, nullptr, nullptr, nullptr, nullptr, nullptr) != 0) {
             rcs[k] = TIPS_ERR_INVALID_ARG;
             return;
           }
-        } else {
-          handles.push_back(h);
+        } else if (!issued_one(neg.enqueue(nm, nullptr, nullptr, shape.data(), (int)shape.size(), (int)dt, nullptr,
+                                           type, root))) {
+          return;
         }
       }
     }
