@@ -32,29 +32,37 @@ def _port():
     return p
 
 
-def _op_body_scripts(ranks, names, threads, seed):
+def _op_body_scripts(ranks, names, threads, seed, batch=0):
+    """batch > 0: each thread commits its requests as lists of that many (@batch ... @endbatch,
+    Negotiator::enqueue_list) instead of one at a time."""
     out = []
     for r in range(ranks):
         rnd = random.Random(seed + r)
         order = names[:]
         rnd.shuffle(order)
         body = []
+        per_thread = [0] * threads
         for k, n in enumerate(order):
             t = k % threads
+            if batch and per_thread[t] % batch == 0:
+                body.append(("t%d: @endbatch\n" % t if per_thread[t] else "") + "t%d: @batch" % t)
+            per_thread[t] += 1
             kind = "bc:1" if names.index(n) % 7 == 3 else "ar"
             body.append("t%d: %s %d %d - %s" % (t, n, names.index(n) % 4, 64 + names.index(n), kind))
-            if rnd.random() < 0.1:
+            if rnd.random() < 0.1 and not batch:
                 body.append("t%d: @sleep %d" % (t, rnd.randint(1, 3)))
+        if batch:
+            body += ["t%d: @endbatch" % t for t in range(threads) if per_thread[t]]
         body.append("t1: @wait")
         out.append("\n".join(body) + "\n")
     return out
 
 
-@pytest.mark.parametrize("ranks,seed", [(3, 100), (2, 7)])
-def test_negotiation_threads_and_callbacks_race_free(tmp_path, ranks, seed):
+@pytest.mark.parametrize("ranks,seed,batch", [(3, 100, 0), (2, 7, 0), (3, 11, 5)])
+def test_negotiation_threads_and_callbacks_race_free(tmp_path, ranks, seed, batch):
     assert os.path.exists(BIN), "tools/_bin/tsan_selftest missing: run make (builds the tsan target)"
     names = ["layer%d/grad" % i for i in range(40)]
-    scripts = _op_body_scripts(ranks, names, 4, seed)
+    scripts = _op_body_scripts(ranks, names, 4, seed, batch)
     port = _port()
     procs = []
     for r, sc in enumerate(scripts):
