@@ -600,6 +600,7 @@ def graphs_case(c, rank, size, L, _lib, sp):
         x = to_dev(rand(dtype, n, np.random.default_rng(0)))
         bufs.append((x, x if inplace else torch.empty_like(x)))
     bad = []
+    trace, trace_prev = [], [(0, 0, 0)]
     for rnd in range(c.get("rounds", 6)):
         if rnd == 3:
             dtype, n, inplace, _ = specs[0]
@@ -625,8 +626,17 @@ def graphs_case(c, rank, size, L, _lib, sp):
                 continue
             if not same_bits(from_dev(y, dtype), expected(ins, dtype, JOB_ALGO), dtype):
                 bad.append("round %d buf %d (dtype %d, n %d) differs" % (rnd, i, dtype, n))
+            if c.get("trace"):  # per call: "w" = a host wait, "r" = a replay, "c" = a capture
+                cap, rep, cached = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+                L.tips_graph_stats(ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(cached))
+                w, wn = ctypes.c_int64(), ctypes.c_int64()
+                _lib.call("tips_replay_order_stats", ctypes.byref(w), ctypes.byref(wn))
+                now = (w.value, rep.value, cap.value)
+                prev = trace_prev[0]
+                trace.append("w" * (now[0] - prev[0]) + "r" * (now[1] - prev[1]) + "c" * (now[2] - prev[2]) or "-")
+                trace_prev[0] = now
     torch.cuda.synchronize()
-    timing = {}
+    timing = {"trace": " ".join(trace)} if c.get("trace") else {}
     if c.get("time_calls"):  # host time inside tips_allreduce and wall time per call, buffer 0, back to back
         import time
         dtype, n, _, _ = specs[0]
@@ -640,6 +650,23 @@ def graphs_case(c, rank, size, L, _lib, sp):
         torch.cuda.synchronize()
         timing = {"enqueue_us": round(enq / c["time_calls"] * 1e6, 2),
                   "call_us": round((time.perf_counter() - t0) / c["time_calls"] * 1e6, 2)}
+    if c.get("time_rounds"):  # the whole mixed sequence back to back: wall per round, and the share
+        import time           # of it the replay -> eager host waits took (TIPS_REPLAY_HOST_ORDER's cost)
+        w0, n0 = ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("tips_replay_order_stats", ctypes.byref(w0), ctypes.byref(n0))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(c["time_rounds"]):
+            for i, (dtype, n, inplace, second) in enumerate(specs):
+                x, y = bufs[i]
+                L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, sp)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        w1, n1 = ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("tips_replay_order_stats", ctypes.byref(w1), ctypes.byref(n1))
+        timing.update(round_ms=round(wall / c["time_rounds"] * 1e3, 3),
+                      waits_per_round=round((w1.value - w0.value) / c["time_rounds"], 2),
+                      wait_ms_per_round=round((n1.value - n0.value) / 1e6 / c["time_rounds"], 3))
     cap, rep, cached = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     off = L.tips_graph_stats(ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(cached))
     waits, wait_ns = ctypes.c_int64(), ctypes.c_int64()

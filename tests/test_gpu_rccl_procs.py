@@ -124,9 +124,10 @@ def test_replayed_plans_in_python_processes(gpu, algo, p):
     after round from two streams, one reallocated half way, interleaved with an eager bucket
     over the replay limit: replays happen and every result is bit-exact. Every eager bucket that
     follows a replay takes order_after_replays' host wait (tips_replay_order_stats counts them;
-    tests/test_plans.py::test_eager_after_replay_takes_the_host_wait shows why it must)."""
+    tests/test_plans.py::test_eager_after_replay_takes_the_host_wait shows why it must). The
+    eager bucket stays eager here (TIPS_GRAPH_MIXED_MAX_BYTES=0), so every round takes the wait."""
     env = rccl_env(algo)
-    env.update(TIPS_GRAPHS="1", TIPS_GRAPH_MAX_BYTES=str(2 << 20))
+    env.update(TIPS_GRAPHS="1", TIPS_GRAPH_MAX_BYTES=str(2 << 20), TIPS_GRAPH_MIXED_MAX_BYTES="0")
     bufs = [[F32, 300007, False, False], [I64, 70001, True, False], [BF16, 4099, False, True],
             [F32, (3 << 20) + 17, True, False]]
     results = run_job(p, [{"bufs": bufs, "seed": 8, "rounds": 6}], timeout=600, **env)
@@ -134,8 +135,33 @@ def test_replayed_plans_in_python_processes(gpu, algo, p):
     for res in results:
         c = res["results"][0]
         assert c["graphs_off"] == 0 and c["captured"] >= 3 and c["replayed"] >= 9, c
-        # each round from the third on: replays of buffers 0-2, then the eager 3 MiB bucket
+        # rounds 2-5: replays of buffers 0-2, then the eager 12 MiB bucket (round 0 grows the staging)
         assert c["replay_host_waits"] >= 4, c
+
+
+@pytest.mark.parametrize("algo,p", [("direct", 2), ("oneshot", 3)])
+def test_mixed_buckets_become_replays(gpu, algo, p):
+    """The same rounds with the default TIPS_GRAPH_MIXED_MAX_BYTES. Per-call trace (w = a host wait,
+    r = a replay, c = a capture): round 0 grows the staging (which drops every graph key), round 1
+    sees each small key once, round 2 captures and replays them and then the 12 MiB bucket waits
+    (the first wait: plans up to 1 GiB become replayable), round 3 runs it eagerly once more (its
+    first eligible call: the second wait), round 4 captures it, and from then on every call is a
+    replay: 2 waits instead of 4, results bit-exact. (The reallocated buffer 0 of round 3 may land
+    at its old address in the same allocator segment, the same key: it replays.)"""
+    env = rccl_env(algo)
+    env.update(TIPS_GRAPHS="1", TIPS_GRAPH_MAX_BYTES=str(2 << 20))
+    bufs = [[F32, 300007, False, False], [I64, 70001, True, False], [BF16, 4099, False, True],
+            [F32, (3 << 20) + 17, True, False]]
+    results = run_job(p, [{"bufs": bufs, "seed": 9, "rounds": 7, "trace": True}], timeout=600, **env)
+    check(results)
+    for res in results:
+        c = res["results"][0]
+        calls = c["trace"].split()
+        rounds = [calls[i:i + len(bufs)] for i in range(0, len(calls), len(bufs))]
+        assert len(rounds) == 7 and c["graphs_off"] == 0, c["trace"]
+        assert c["replay_host_waits"] == 2 and "".join(calls).count("w") == 2, c["trace"]
+        assert rounds[4][3] == "rc", c["trace"]  # the large bucket captured in round 4
+        assert all(t == "r" for r in rounds[5:] for t in r), c["trace"]  # then replays only
 
 
 @pytest.mark.parametrize("p", [2, 3])

@@ -235,6 +235,8 @@ struct State {
   int64_t graphs_captured = 0, graphs_replayed = 0;
   // order_after_replays' host waits (eager RCCL work issued while a replay was pending) and their time
   int64_t replay_host_waits = 0, replay_host_wait_ns = 0;
+  // an eager plan followed a replay: larger plans become replayable too (graph_eligible)
+  bool replays_mixed = false;
 };
 
 State& S();

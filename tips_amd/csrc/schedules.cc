@@ -59,6 +59,7 @@ int order_after_replays(State& st) {
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventSynchronize(st.ev_graph[4]));
     st.replay_host_waits++;
+    st.replays_mixed = true;
     st.replay_host_wait_ns +=
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -239,6 +240,10 @@ void destroy_exec(State& st, hipGraphExec_t e) {
 // on the p = 2 rehearsal a replayed one-shot was the fastest path at every size from 16 KiB to
 // 8 MiB, 4-30 % under the eager one (profiles/r03/small_bucket_rehearsal_n2_before.json; round 2 stopped
 // at 1 MiB). TIPS_GRAPHS=0 turns them off; 2 forces them on any runtime (probing only).
+// Once an eager plan has had to wait on the host for a replay (order_after_replays: replayed and
+// eager buckets alternate, e.g. a step's buckets straddle the 8 MiB limit), plans up to
+// TIPS_GRAPH_MIXED_MAX_BYTES (1 GiB; 0 keeps the limit) are replayed as well: from their third call
+// on, the alternation is replay -> replay, which needs no host wait.
 bool graphs_supported() {
   static std::atomic<int> ok{-1};  // (set once, by whichever thread asks first)
   int v = ok.load(std::memory_order_relaxed);
@@ -255,7 +260,9 @@ bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
   if (st.graphs && st.graphs->off) return false;
   const int64_t want = env_i64("TIPS_GRAPHS", 1);
   if (want <= 0 || (want == 1 && !graphs_supported())) return false;
-  if (pl.n * tips::dtype_size(pl.dtype) > env_i64("TIPS_GRAPH_MAX_BYTES", 8 << 20)) return false;
+  int64_t cap = env_i64("TIPS_GRAPH_MAX_BYTES", 8 << 20);
+  if (st.replays_mixed) cap = std::max(cap, env_i64("TIPS_GRAPH_MIXED_MAX_BYTES", int64_t(1) << 30));
+  if (pl.n * tips::dtype_size(pl.dtype) > cap) return false;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(user, &cs) != hipSuccess) {
     (void)hipGetLastError();
@@ -592,6 +599,7 @@ void graphs_release(State& st) {
   st.graph_pending = st.eager_pending = false;
   st.graphs_captured = st.graphs_replayed = 0;
   st.replay_host_waits = st.replay_host_wait_ns = 0;
+  st.replays_mixed = false;
 }
 
 #ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
