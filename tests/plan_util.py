@@ -307,3 +307,35 @@ def proxy_order(calls, host_wait="end"):
         posted.extend((c, k) for k in range(ng))
     posted.extend(deferred)
     return posted, device
+
+
+def replay_trace(rounds, sizes, cap=2 << 20, mixed_cap=1 << 30):
+    """schedules.cc's replay bookkeeping over `rounds` rounds of calls on the same buffers, one per
+    entry of `sizes` (bytes) in order: graph_eligible (bytes <= cap, or <= mixed_cap once a host wait
+    has happened; mixed_cap = 0 keeps cap), plan_graph (a key's first eligible call only records it,
+    its next is captured and replayed), run_plan's staging growth (a larger plan than any before drops
+    every key) and order_after_replays (an eager call after a replay waits on the host). Returns
+    [(trace token, mode)] per call, tokens as tests/peer_worker.py graphs_case prints them ("w" a host
+    wait, "r" a replay, "c" a capture, "-" none) and mode "replay" | "eager" for proxy_order."""
+    keys, staging, pending, mixed, out = {}, 0, False, False, []
+    for _ in range(rounds):
+        for i, b in enumerate(sizes):
+            if b > staging:
+                staging = b
+                keys.clear()
+            limit = max(cap, mixed_cap) if mixed else cap
+            replay = captured = False
+            if b <= limit:
+                if i not in keys:
+                    keys[i] = False
+                else:
+                    captured, keys[i] = not keys[i], True
+                    replay = True
+            if replay:
+                pending = True
+                out.append(("r" + ("c" if captured else ""), "replay"))
+            else:
+                out.append(("w" if pending else "-", "eager"))
+                mixed = mixed or pending
+                pending = False
+    return out
