@@ -309,12 +309,13 @@ def proxy_order(calls, host_wait="end"):
     return posted, device
 
 
-def replay_trace(rounds, sizes, cap=2 << 20, mixed_cap=1 << 30):
+def replay_trace(rounds, sizes, cap=2 << 20, mixed_cap=1 << 30, note_on_wait=True):
     """schedules.cc's replay bookkeeping over `rounds` rounds of calls on the same buffers, one per
     entry of `sizes` (bytes) in order: graph_eligible (bytes <= cap, or <= mixed_cap once a host wait
     has happened; mixed_cap = 0 keeps cap), plan_graph (a key's first eligible call only records it,
     its next is captured and replayed), run_plan's staging growth (a larger plan than any before drops
-    every key) and order_after_replays (an eager call after a replay waits on the host). Returns
+    every key) and order_after_replays (an eager call after a replay waits on the host; a wait that
+    widens the limit records the call's key as seen). Returns
     [(trace token, mode)] per call, tokens as tests/peer_worker.py graphs_case prints them ("w" a host
     wait, "r" a replay, "c" a capture, "-" none) and mode "replay" | "eager" for proxy_order."""
     keys, staging, pending, mixed, out = {}, 0, False, False, []
@@ -338,4 +339,6 @@ def replay_trace(rounds, sizes, cap=2 << 20, mixed_cap=1 << 30):
                 out.append(("w" if pending else "-", "eager"))
                 mixed = mixed or pending
                 pending = False
+                if note_on_wait and b > limit and b <= (max(cap, mixed_cap) if mixed else cap):
+                    keys.setdefault(i, False)  # the wait widened the limit: seen (run_plan's note_only)
     return out

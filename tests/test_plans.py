@@ -238,24 +238,27 @@ def test_eager_after_replay_takes_the_host_wait(seq, algo, p, n, K):
     assert (posted == device) == (ng == 1)
 
 
-# tests/test_gpu_rccl_procs.py::test_mixed_buckets_become_replays: the per-call trace a rank printed
-# on the MI355X box (profiles/r04/zzb_mixed_replay_trace.txt), 6 rounds of 1.2 MB, 0.56 MB and 8 KB
-# buckets (limit 2 MiB) and one of 12 MiB
-GPU_MIXED_TRACE = "- - - - - - - - rc rc rc w r r r w r r r rc r r r r"
+# tests/test_gpu_rccl_procs.py::test_mixed_buckets_become_replays: the per-call traces a rank printed
+# on the MI355X box, 6 rounds of 1.2 MB, 0.56 MB and 8 KB buckets (limit 2 MiB) and one of 12 MiB:
+# before and after the widening wait recorded the waiting call's key (profiles/r04/zzb_, zzg_
+# mixed_replay_trace.txt; the latter ran 7 rounds, its first 6 are these)
+GPU_MIXED_TRACE_FIRST = "- - - - - - - - rc rc rc w r r r w r r r rc r r r r"
+GPU_MIXED_TRACE = "- - - - - - - - rc rc rc w r r r rc r r r r r r r r"
 
 
-@pytest.mark.parametrize("mixed_cap", [1 << 30, 0])
-def test_mixed_replays_model(mixed_cap):
+@pytest.mark.parametrize("mixed_cap,note", [(1 << 30, True), (1 << 30, False), (0, True)])
+def test_mixed_replays_model(mixed_cap, note):
     """plan_util.replay_trace restates schedules.cc's replay bookkeeping. With the default
-    TIPS_GRAPH_MIXED_MAX_BYTES it reproduces the trace the GPU test printed call for call (2 host
-    waits, then replays only); with 0 the 12 MiB bucket waits in every round from the third. Either
-    way proxy_order with the host wait at the replay's end posts every group in device order, and
-    once the sequence is all replays no wait is needed to keep it so."""
+    TIPS_GRAPH_MIXED_MAX_BYTES it reproduces the traces the GPU test printed call for call: one
+    host wait, then replays only (two waits before the waiting call's key was recorded); with 0 the
+    12 MiB bucket waits in every round from the third. Either way proxy_order with the host wait at
+    the replay's end posts every group in device order, and once the sequence is all replays no
+    wait is needed to keep it so."""
     sizes = [300007 * 4, 70001 * 8, 4099 * 2, ((3 << 20) + 17) * 4]
-    tr = pu.replay_trace(6, sizes, mixed_cap=mixed_cap)
+    tr = pu.replay_trace(6, sizes, mixed_cap=mixed_cap, note_on_wait=note)
     tokens = " ".join(t for t, _ in tr)
     if mixed_cap:
-        assert tokens == GPU_MIXED_TRACE
+        assert tokens == (GPU_MIXED_TRACE if note else GPU_MIXED_TRACE_FIRST)
     else:
         assert tokens.split().count("w") == 4 and tokens.endswith("r r r w")
     calls = [(m, 3) for _, m in tr]

@@ -304,7 +304,8 @@ int capture_plan(State& st, const Plan& pl, char* const* base, hipGraphExec_t* e
 }
 
 // The graph to replay for this call, or null: run eagerly (first call of a key, or graphs off).
-hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base) {
+// note_only: record a new key as seen, never capture.
+hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base, bool note_only = false) {
   if (!st.graphs) st.graphs = new PlanGraphs();
   PlanGraphs& G = *st.graphs;
   const unsigned long long in_id = allocation_id(base[kBufIn]), out_id = allocation_id(base[kBufOut]);
@@ -324,6 +325,7 @@ hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base) {
     return nullptr;
   }
   it->second.stamp = ++G.clock;
+  if (note_only) return nullptr;
   if (!it->second.exec) {
     if (capture_plan(st, pl, base, &it->second.exec) != 0) {
       if (getenv("TIPS_VERBOSE")) fprintf(stderr, "[tips] plan capture failed, eager from now on: %s\n", last_error().c_str());
@@ -386,12 +388,16 @@ int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t u
   TRY(st.recv_ev.ensure(nsteps));
   TRY(st.sum_ev.ensure(nsteps));
   char* base[3] = {(char*)in, out, (char*)st.staging.p};
-  if (L == 1 && graph_eligible(st, pl, user)) {
+  const bool eligible = L == 1 && graph_eligible(st, pl, user);
+  if (eligible) {
     hipGraphExec_t exec = plan_graph(st, pl, base);
     if (exec) return replay(st, exec, user);
   }
   if (L > 1) TRY(lanes_ensure(st, L));
   TRY(prologue(st, user, L));
+  // this call's host wait may just have widened the replay limit (replays_mixed): its key counts as
+  // seen, so its next call is captured instead of waiting once more
+  if (L == 1 && !eligible && graph_eligible(st, pl, user)) (void)plan_graph(st, pl, base, true);
   TRY(issue_steps(st, pl, base, L));
   return epilogue(st, user, L);
 }
