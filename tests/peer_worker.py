@@ -546,6 +546,41 @@ def fused_case(c, rank, size, L, _lib, sp):
         ok = d["layouts_built"] <= 1 and d["layout_hits"] >= steps - 1
         return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": ok, "stats": d,
                 "error": "" if ok else "fusion caches: %r" % d}
+    elif mode == "mixed":
+        # a small list (one <= 8 MiB bucket: replayed from its second call) and this workload's list
+        # (buckets over 8 MiB: eager until a host wait widens the replay limit, then replayed too),
+        # alternating in place round after round with new values; every round bit-exact, and the
+        # replay -> eager host waits stop after the first (schedules.cc TIPS_GRAPH_MIXED_MAX_BYTES)
+        import ctypes
+        small = [16384] * 40  # 2.5 MiB
+        rounds = c.get("rounds", 5)
+        big_t = torch.empty(sum(sizes), dtype=torch.float32, device="cuda")
+        small_t = torch.empty(sum(small), dtype=torch.float32, device="cuda")
+        lists = [(small, small_t, [x.clone() for x in torch.split(small_t, small)]),
+                 (sizes, big_t, [x.clone() for x in torch.split(big_t, sizes)])]
+        waits = []
+        for rnd in range(rounds):
+            for li, (ks, _, ts) in enumerate(lists):
+                seed = c["seed"] * 100 + 31 * rnd + 7 * li
+                def vals(r, ks=ks, seed=seed):
+                    g.manual_seed(seed * 10 + r)
+                    return torch.empty(sum(ks), device="cuda").uniform_(-1.0, 1.0, generator=g)
+                for t, v in zip(ts, torch.split(vals(rank), ks)):
+                    t.copy_(v)
+                tips_amd.fused_allreduce_(ts)
+                torch.cuda.synchronize()
+                exp = oracle_bind.fold([vals(r).cpu().numpy() for r in range(size)], code=0, wide_acc=True)
+                gotf = torch.cat([t.reshape(-1) for t in ts]).cpu().numpy()
+                if not np.array_equal(gotf.view(np.uint32), exp.view(np.uint32)):
+                    return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": False,
+                            "error": "round %d list %d: %d elements differ" % (rnd, li, int((gotf != exp).sum()))}
+                w, wn = ctypes.c_int64(), ctypes.c_int64()
+                _lib.call("tips_replay_order_stats", ctypes.byref(w), ctypes.byref(wn))
+                waits.append(w.value)
+        cap, rep, cached = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        L.tips_graph_stats(ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(cached))
+        return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": True, "error": "",
+                "waits_after_each_call": waits, "captured": cap.value, "replayed": rep.value}
     elif mode == "host_grads":
         # the reference's op is a CPU op (ops.cc:118): host gradients (numpy), fused into page-locked
         # pieces (tips_fused_allreduce_host) by allreduce_grads

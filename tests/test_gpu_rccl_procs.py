@@ -82,6 +82,24 @@ def test_fusion_workloads_over_rccl(gpu, workload, p):
     check(run_job(p, cases, timeout=600, **rccl_env("auto")))
 
 
+@pytest.mark.parametrize("p", [2, 3])
+def test_fusion_buckets_mixed_with_a_replayed_list(gpu, p):
+    """Config 4's fusion buckets (two of ~41 MB: eager) alternating with a 2.5 MiB list (one bucket,
+    replayed from its second call), in place, new values every round, over real RCCL ranks: every
+    round bit-exact against the fold, and the replay -> eager host waits stop once the first one has
+    widened the replay limit (TIPS_GRAPH_MIXED_MAX_BYTES): the fusion buckets become replays too."""
+    results = run_job(p, [{"fused": "config4", "seed": 3, "mode": "mixed", "rounds": 5}], timeout=600,
+                      **rccl_env("auto"))
+    check(results)
+    for res in results:
+        c = res["results"][0]
+        w = c["waits_after_each_call"]
+        assert w[-1] <= 2 and w[-1] == w[-5], c  # no waits in the last two rounds
+        # round 0 grows the staging (every key dropped); the small bucket replays from round 2, the
+        # fusion buckets from round 3, after round 2's one wait: 1 + 3 + 3 replays, 3 captures
+        assert c["replayed"] >= 7 and c["captured"] >= 3, c
+
+
 @pytest.mark.parametrize("workload", ["config4", "config5"])
 def test_allreduce_grads_fresh_tensors_over_rccl(gpu, workload):
     """allreduce_grads over 3 real RCCL ranks with FRESH gradient tensors every step (a training
