@@ -269,3 +269,23 @@ def test_mixed_replays_model(mixed_cap, note):
         assert all(m == "replay" for m, _ in tail)
         posted, device = pu.proxy_order(tail, "none")
         assert posted == device
+
+
+@settings(max_examples=200, deadline=None)
+@given(sizes=hs.lists(hs.integers(1 << 10, 64 << 20), min_size=1, max_size=6),
+       groups=hs.lists(hs.integers(1, 4), min_size=6, max_size=6), rounds=hs.integers(5, 8),
+       mixed=hs.booleans())
+def test_replay_bookkeeping_properties(sizes, groups, rounds, mixed):
+    """Any fixed list of bucket sizes called round after round (plan_util.replay_trace): with the
+    host wait at the replay's end, RCCL's proxy receives every group in device order (proxy_order);
+    with the mixed limit on (covering every size here), the sequence settles: from round 4 on no
+    call waits, and every call of the last round is a replay once any call has replayed."""
+    tr = pu.replay_trace(rounds, sizes, mixed_cap=(1 << 30) if mixed else 0)
+    calls = [(m, groups[i % len(sizes)]) for i, (_, m) in enumerate(tr)]
+    posted, device = pu.proxy_order(calls, "end")
+    assert posted == device
+    if mixed:
+        late = tr[4 * len(sizes):]
+        assert all(t != "w" for t, _ in late)
+        if any(m == "replay" for _, m in tr):
+            assert all(m == "replay" for _, m in tr[-len(sizes):])
