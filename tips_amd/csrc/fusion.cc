@@ -271,14 +271,16 @@ Layout* find_layout(State& st, FusionCache& fc, const int64_t* counts, int n, in
 // The resolved segment table(s) of this call's pointers: a cached one when this layout saw the
 // same pointers (and mode and base) recently, else built on the host and uploaded.
 // The order a launch's workgroups take a group's tiles in (a group: one bucket, or the region of
-// tensors reduced where they lie; launches cover whole groups). TIPS_COPY_ORDER=1: the tiles that
-// meet a tensor boundary (two or more segments, or a segment that does not cover the tile) first,
-// then the tiles inside one tensor - the slow tiles start while the queue is full instead of
-// trailing at the end of the launch; 0: tile order.
+// tensors reduced where they lie; launches cover whole groups). The tiles that meet a tensor
+// boundary (two or more segments, or a segment that does not cover the tile) are the slow ones.
+// TIPS_COPY_ORDER=2 (default): each XCD's range of slots gets an equal share of them, first; config
+// 4's pack 14.0 against 14.5-14.7 us per bucket launch (profiles/r04/zzl_pack_order_ab.txt).
+// 1: all of them first (they then land on the first XCDs); 0: tile order.
 std::vector<int> tile_order(const Layout& L) {
   std::vector<int> order(L.ntiles);
   for (int j = 0; j < L.ntiles; j++) order[j] = j;
-  if (env_i64("TIPS_COPY_ORDER", 1) == 0) return order;
+  const int64_t mode = env_i64("TIPS_COPY_ORDER", 2);
+  if (mode == 0) return order;
   const int64_t es = tips::dtype_size(L.dtype);
   auto covered = [&](int j) {
     if (L.tiles[2 * j + 1] != 1) return false;
@@ -289,9 +291,32 @@ std::vector<int> tile_order(const Layout& L) {
   for (const Bucket& b : L.buckets) bounds.push_back(b.tile0);
   bounds.push_back(L.buckets.empty() ? 0 : L.buckets.back().tile0 + L.buckets.back().ntiles);
   bounds.push_back(L.ntiles);
+  const bool spread = mode == 2;
   for (size_t g = 0; g + 1 < bounds.size(); g++) {
     const int g0 = bounds[g], g1 = std::min(bounds[g + 1], L.ntiles);
-    std::stable_partition(order.begin() + g0, order.begin() + std::max(g0, g1), [&](int j) { return !covered(j); });
+    if (g1 <= g0) continue;
+    auto mid = std::stable_partition(order.begin() + g0, order.begin() + g1, [&](int j) { return !covered(j); });
+    if (!spread) continue;
+    // TIPS_COPY_ORDER=2: the launch deals slot s to XCD s / R (R = grid / 8, xcd_tile in
+    // kernels.hip), so "boundary tiles first" puts them all on the first XCDs. Instead each XCD's
+    // range gets an equal share of them, first in the range, then interior tiles.
+    const int n = g1 - g0, R = (int)(std::max<int64_t>(8, ((int64_t)n + 7) / 8 * 8) / 8);
+    std::vector<int> slow(order.begin() + g0, mid), fast(mid, order.begin() + g1);
+    std::vector<std::vector<int>> xcd(8);
+    size_t si = 0, fi = 0;
+    for (int x = 0; x < 8; x++) {
+      const int cap = std::max(0, std::min(R, n - x * R));
+      const size_t share = std::min<size_t>((size_t)cap, (slow.size() - si + (7 - x)) / (8 - x));
+      for (size_t k = 0; k < share; k++) xcd[x].push_back(slow[si++]);
+    }
+    for (int x = 0; x < 8; x++) {  // (slow tiles a full range could not take go to later ranges)
+      const int cap = std::max(0, std::min(R, n - x * R));
+      while ((int)xcd[x].size() < cap && si < slow.size()) xcd[x].push_back(slow[si++]);
+      while ((int)xcd[x].size() < cap && fi < fast.size()) xcd[x].push_back(fast[fi++]);
+    }
+    int at = g0;
+    for (int x = 0; x < 8; x++)
+      for (int j : xcd[x]) order[at++] = j;
   }
   return order;
 }
