@@ -1394,6 +1394,100 @@ def op_host_leg(steps=20, warmup=3):
                  "fuses each cycle's host requests into one tips_fused_allreduce_host call")
     return d
 
+# ----------------------------------------------------------------------------- the north star's ring (N > 1, mandatory)
+
+def ring_depth_choice(job, w):
+    """The ring's pipeline depth for config 3's bucket: the faster ring depth the tuner timed
+    (tips_tuned_timings: the slowest rank's ms per call, the same on every rank), else the default."""
+    import ctypes
+    _lib, L = job._lib, job.L
+    cap = 16
+    al, de, la, ms = (ctypes.c_int * cap)(), (ctypes.c_int * cap)(), (ctypes.c_int * cap)(), (ctypes.c_double * cap)()
+    n = L.tips_tuned_timings(w.qbytes, al, de, la, ms, cap)
+    rings = sorted((ms[i], de[i]) for i in range(max(0, min(n, cap))) if al[i] == _lib.ALGO_RING and la[i] == 1)
+    timed = [{"algorithm": job.inv.get(al[i], str(al[i])), "pipeline_depth": de[i], "lanes": la[i],
+              "ms_per_call": round(ms[i], 3)} for i in range(max(0, min(n, cap)))]
+    if rings:
+        return rings[0][1], "the faster ring depth the tuner measured on this job", timed
+    depth, sub = ctypes.c_int(), ctypes.c_int64()
+    _lib.call("tips_schedule_shape", w.sizes[0], job.world, _lib.FLOAT32, ctypes.byref(depth), ctypes.byref(sub))
+    return depth.value, "the default depth (TIPS_PIPELINE_DEPTH / TIPS_MIN_SUBCHUNK_BYTES; no tuner timings)", timed
+
+
+def schedule_record(job, w, algo, env, steps):
+    """Config 3's bucket (the headline's buffers) through one explicitly selected schedule: warm-up,
+    `steps` timed calls (max over ranks), the parity check; the record's rate as the headline's."""
+    _lib = job._lib
+    saved = {k: os.environ.get(k) for k in env}
+    try:
+        os.environ.update(env)
+        _lib.call("tips_set_algorithm", algo)
+        for _ in range(2):
+            w.step()
+        job.torch.cuda.synchronize()
+        t = w.timed(steps)
+        good, msg = w.parity(algo)
+        ok = all_ranks_ok(job.dist, good)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        _lib.call("tips_set_algorithm", w.algo if w.fallbacks else job.algo_names[job.args.algo])
+    ms = t / steps * 1e3
+    world = job.world
+    algbw = w.total_elems * 4 / (ms / 1e3)
+    busbw = algbw * 2 * (world - 1) / world
+    return {"value": round(world * w.total_elems * 4 / (ms / 1e3) / GIB, 2), "unit": "GiB/s", "steps": steps,
+            "ms_per_step": round(ms, 4), "algbw_gib_s": round(algbw / GIB, 2), "busbw_GBps": round(busbw / 1e9, 2),
+            "check": msg if ok else "FAIL on some rank (%s here)" % msg}, ok
+
+
+def north_star_ring(job, w, line):
+    """The north star's multi-GPU target, measured right after the headline whatever schedule the
+    tuner kept: config 3's 1 GiB bucket through the ring at its best measured depth (busbw against
+    one xGMI link, target 0.70; the reference's data call is utils.h:60-65), and RCCL's own
+    ncclAllReduce on the same bucket as a reference point. Not budgeted: every N > 1 line has both."""
+    _lib = job._lib
+    kc = max(3, min(w.steps, 10))
+    subs = line.setdefault("configs", {})
+    progress(job.rank, "config3_ring")
+    try:
+        depth, why, timed = ring_depth_choice(job, w)
+        env = {"TIPS_PIPELINE_DEPTH": str(depth), "TIPS_MIN_SUBCHUNK_BYTES": str(256)}
+        rec, ok = schedule_record(job, w, _lib.ALGO_RING, env, kc)
+        rb = rec["busbw_GBps"]
+        rec.update({"algorithm": "ring", "pipeline_depth": depth, "depth_selection": why,
+                    "workload": "config 3: allreduce of one 1 GiB fp32 bucket per GPU, ring schedule (one xGMI link "
+                                "per direction per rank)",
+                    "roofline": {"bound": "xgmi", "achieved": rb, "peak": XGMI_LINK_GBPS, "unit": "GB/s",
+                                 "frac": round(rb / XGMI_LINK_GBPS, 4), "frac_of_one_link": round(rb / XGMI_LINK_GBPS, 4),
+                                 "target_frac": 0.70, "links_used": 1}})
+        if timed:
+            rec["tuner_timings"] = timed
+        subs["config3_ring"] = rec
+        line["ring_xgmi"] = {"busbw_GBps": rb, "link_peak_GBps": XGMI_LINK_GBPS,
+                             "frac_of_one_link": round(rb / XGMI_LINK_GBPS, 4), "target_frac": 0.70,
+                             "pipeline_depth": depth, "check": rec["check"], "source": "configs.config3_ring"}
+        line["sub_records_ok"] = line.get("sub_records_ok", True) and ok
+    except Exception as e:  # noqa: BLE001 - reported, never costs the headline
+        subs["config3_ring"] = {"error": "%s: %s" % (type(e).__name__, e)}
+        line["sub_records_ok"] = False
+    if os.environ.get("TIPS_NO_RCCL"):
+        return
+    progress(job.rank, "config3_rccl")
+    try:
+        rec, ok = schedule_record(job, w, _lib.ALGO_RCCL, {}, kc)
+        rec.update({"algorithm": "ncclAllReduce (RCCL's own collective)",
+                    "workload": "config 3's bucket through ncclAllReduce: the reference point for the schedules"})
+        subs["config3_rccl"] = rec
+        line["sub_records_ok"] = line.get("sub_records_ok", True) and ok
+    except Exception as e:  # noqa: BLE001
+        subs["config3_rccl"] = {"error": "%s: %s" % (type(e).__name__, e)}
+        line["sub_records_ok"] = False
+
+
 # ----------------------------------------------------------------------------- comparisons (after the sub-records)
 
 def comparisons(job, w, line, last_words):
@@ -1460,7 +1554,8 @@ def comparisons(job, w, line, last_words):
     # (oneshot targets small buckets only.) The _k entries re-run a schedule at another sub-chunk
     # pipeline depth (read per call). Order: RCCL's allreduce and the other schedules, the link probe,
     # the probes; then the opt-in legs (IPC peer schedules, transfer lanes).
-    run_variants([("rccl", "rccl", {}), ("ring", "ring", {}), ("direct", "direct", {}),
+    # (ring at its best depth and ncclAllReduce are the mandatory configs.config3_ring / _rccl records)
+    run_variants([("direct", "direct", {}),
                   ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
                   ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
                   ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
@@ -1507,11 +1602,6 @@ def comparisons(job, w, line, last_words):
             and os.environ.get("TIPS_BENCH_ENV_VARIANTS") == "1":
         note_progress("the RCCL-setting child jobs")
         line["env_variants"] = env_variant_jobs(job.args, job.dist, job.rank, job.world)
-    ring_algbw = w.total_elems * 4 / (w.ms / 1e3) if w.algo == _lib.ALGO_RING else (compare.get("ring") or 0) * GIB
-    if job.world > 1 and ring_algbw:  # the north star's ring target: >= 70 % of one xGMI link
-        rb = ring_algbw * 2 * (job.world - 1) / job.world
-        line["ring_xgmi"] = {"busbw_GBps": round(rb / 1e9, 2), "link_peak_GBps": XGMI_LINK_GBPS,
-                             "frac_of_one_link": round(rb / 1e9 / XGMI_LINK_GBPS, 4), "target_frac": 0.70}
 
 
 # ----------------------------------------------------------------------------- the run
@@ -1623,6 +1713,9 @@ def bench_job(args):
             line["gpu_topology"] = topo
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True
+    if w is not None and workload == "bucket" and world > 1:
+        north_star_ring(job, w, line)  # mandatory, before every sub-record and budgeted leg
+        _RESULT["line"] = line if rank == 0 else None
     if args.workload == "auto" and not args.no_sub:
         sub_records(job, line, args.sub_steps)
         _RESULT["line"] = line if rank == 0 else None

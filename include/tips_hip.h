@@ -204,7 +204,14 @@ TIPS_API int tips_host_unregister(void* ptr);
  * run on `stream` itself (the bucket allreduces at N > 1 on a library stream forked
  * from it and joined back). Calls from different streams are safe: the fused calls
  * form one chain (each ends with an event a call from another stream waits for),
- * since the fusion slots and pointer tables are shared. */
+ * since the fusion slots and pointer tables are shared.
+ * Graph capture: a fused call made under stream capture must find its pointer table
+ * built (the same call made once before the capture) and stays out of the chain. The
+ * table it used is then kept for the life of the job - never refilled, reused or freed
+ * - and changing TIPS_FUSION_THRESHOLD afterwards fails (the replays pack into the
+ * current slots). The replays share those slots with eager fused calls: order a replay
+ * with fused calls on other streams yourself (launch it on the same stream, or join
+ * the streams), as for any graph that uses a shared workspace. */
 TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
 /* The same, out of place: outs[i] = SUM over ranks of ins[i] (ins[i] == outs[i]
  * allowed); the inputs are left unchanged. What the reference's per-gradient
@@ -349,6 +356,11 @@ TIPS_API int tips_tuned_choice(int64_t bytes, int* algo, int* depth);
  * the job's, whose groups of consecutive plan steps are in flight together (1 = the comm stream
  * alone). TIPS_LANES sets it (the same on every rank) for an explicitly selected schedule. */
 TIPS_API int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lanes);
+/* Every candidate the tuner timed for `bytes`' size class: schedule, pipeline depth, lanes and
+ * the slowest rank's ms per call (the numbers the choice was made on; the same on every rank).
+ * Fills up to `cap` entries and returns how many candidates there were (0 before that class was
+ * tuned; cap 0 asks the count), < 0 on error. */
+TIPS_API int tips_tuned_timings(int64_t bytes, int* algos, int* depths, int* lanes, double* ms, int cap);
 /* Replayed plans (TIPS_GRAPHS, default 1): a ring / direct / one-shot call of at most
  * TIPS_GRAPH_MAX_BYTES (1 MiB: latency-bound buckets) made again on the same buffers (same
  * addresses and allocations) is captured once into a HIP graph and replayed with one launch;

@@ -79,8 +79,11 @@ TIPS_API int tips_sum_variant(void* dst, const void* a, const void* b, int64_t c
 /* Tuning entry for the multi-input sum (tools/sum_sweep.cc): f32 only,
  * nsrc 2, 4 or 8, 16-B aligned pointers. variant 0 = global non-temporal
  * loads, 1 = buffer nt loads 1 vector per lane, 2 = the same with 2 vectors,
- * 3 = buffer plain loads, 4 = buffer nt loads 4 vectors per lane.
- * Others: TIPS_ERR_HIP. tips_multi_sum uses the default chosen from that sweep. */
+ * 3 = buffer plain loads, 4 = buffer nt loads 4 vectors per lane; 8-49 = round 5's sweep of
+ * tile order, store policy, lanes, workgroups per CU and grid-stride forms (kernels.hip
+ * run_multi_x lists them; tools/multi_sum_sweep.py); 36 = round 4's shipped fold; 50 = what
+ * tips_multi_sum launches now. Others: TIPS_ERR_HIP. tips_multi_sum uses the default chosen from
+ * those sweeps. */
 TIPS_API int tips_multi_sum_variant(void* dst, const void* const* srcs, int nsrc, int64_t count, int dtype, int variant,
                                     void* stream);
 
@@ -108,6 +111,12 @@ TIPS_API int tips_xfer(void* const* dsts, const void* const* srcs, const int64_t
  *   nsrc, nsrc x {buf, byte_off}}; buf 0 = in, 1 = out, 2 = staging. */
 TIPS_API int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, int depth, int64_t* out,
                                     int64_t cap);
+
+/* The candidates TIPS_ALGO_TUNE would time for a bucket of `count` elements on p ranks, in the order
+ * it runs them (schedule, pipeline depth, lanes; TIPS_TUNE_LANES / TIPS_TUNE_PEER read as at a call).
+ * Pure host function: fills up to cap entries and returns the number of candidates (< 0 = error).
+ * tests/test_plans.py checks that a chunk of 16 MiB or more is never offered unpipelined. */
+TIPS_API int tips_tune_candidates(int p, int64_t count, int dtype, int* algos, int* depths, int* lanes, int cap);
 
 #ifdef __cplusplus
 }

@@ -235,6 +235,30 @@ def hazards(plan, es, nbytes, inplace=False, modes=("eager", "eager"), replay_jo
     return races
 
 
+def sums_under_transfers(plan):
+    """One eager call's happens-before graph (schedules.cc issue_steps: step i's group on the comm
+    stream behind its wait on an earlier step's sums, step i's sums on the compute stream behind
+    step i's receive event). Returns {i: [j, ...]}: the steps j > i whose transfer group is NOT
+    ordered after step i's sums, i.e. may run on the links while those sums run on the CUs."""
+    steps = plan["steps"]
+    group_after_sum = {}  # j -> set of sum steps the group of j is ordered after (transitively)
+    sum_after = {}        # i -> set of sum steps the sums of i follow (stream order + their group)
+    prev_group = set()
+    prev_sums = set()
+    for j, s in enumerate(steps):
+        g = set(prev_group)  # the comm stream's order: everything the previous group followed
+        if s["wait_sum"] >= 0:
+            g |= {s["wait_sum"]} | sum_after.get(s["wait_sum"], set())
+        group_after_sum[j] = g
+        prev_group = g
+        if s["sums"]:
+            sa = prev_sums | g  # compute stream's order + this step's receive event
+            sum_after[j] = sa
+            prev_sums = sa | {j}
+    return {i: [j for j in range(i + 1, len(steps)) if steps[j]["xfers"] and i not in group_after_sum[j]]
+            for i in sum_after}
+
+
 def interpret(plans, ins, dtype, inplace=False):
     """Execute p ranks' plans on host buffers: step by step, transfers first (paired as
     pairing() checks), then the step's sums with the oracle's arithmetic. Returns p outputs."""

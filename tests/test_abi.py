@@ -65,7 +65,8 @@ def test_product_and_development_exports():
     assert prod == set(header_functions())
     assert not prod & dev_only
     assert dev == prod | dev_only
-    assert len(dev_only) == 12  # simulators (4), self-tests (2), sweeps (4), tips_schedule_plan, tile table
+    assert len(dev_only) == 13  # simulators (4), self-tests (2), sweeps (4), tips_schedule_plan, tile table,
+    #                             tips_tune_candidates
     from tips_amd import _lib
     D, L = _lib.dev(), _lib.lib()
     assert D is not L and not hasattr_c(L, "tips_ring_simulate") and hasattr_c(D, "tips_ring_simulate")

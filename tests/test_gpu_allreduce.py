@@ -261,6 +261,78 @@ def test_fused_call_captures_into_a_graph(gpu, monkeypatch):
                 assert torch.equal(o, t)
 
 
+def test_captured_fused_call_keeps_its_table():
+    """a captured fused call's replays read its pointer table long after the capture.
+    Capture, then 20 eager calls on other pointer sets of the same layout (more than the 16 tables
+    a layout keeps, so the LRU reuses buffers) plus one from a second stream; then replay: the
+    replay must still move its own tensors, bit-exact, and leave the others alone. A threshold
+    change while the graph lives fails clearly instead of moving the slots under it. (Its own
+    process: the captured table stays pinned for the life of the job.)"""
+    import subprocess
+    import sys
+    from conftest import REPO
+    code = r'''
+import os, numpy as np, torch
+os.environ.update(TIPS_FUSION_MEASURE_PACK="1", TIPS_FUSION_THRESHOLD=str(1 << 20))
+import tips_amd
+from tips_amd import _lib
+tips_amd.init()
+rng = np.random.default_rng(78)
+sizes = [int(round(2 ** rng.uniform(0, 16))) for _ in range(40)]
+ins = [torch.randn(n, device="cuda") for n in sizes]
+outs = [torch.empty_like(t) for t in ins]
+side, other = torch.cuda.Stream(), torch.cuda.Stream()
+side.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(side):
+    tips_amd.fused_allreduce(ins, out_list=outs)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        tips_amd.fused_allreduce(ins, out_list=outs)
+torch.cuda.synchronize()
+sets = []
+for k in range(20):
+    xi = [torch.randn(n, device="cuda") for n in sizes]
+    xo = [torch.empty_like(t) for t in xi]
+    with torch.cuda.stream(other if k == 19 else side):
+        tips_amd.fused_allreduce(xi, out_list=xo)
+    sets.append((xi, xo))
+torch.cuda.synchronize()
+for xi, xo in sets:
+    assert all(torch.equal(a, b) for a, b in zip(xi, xo))
+snap = [[o.clone() for o in xo] for _, xo in sets]
+for t in ins:
+    t.add_(2.0)
+for o in outs:
+    o.zero_()
+with torch.cuda.stream(side):
+    g.replay()
+torch.cuda.synchronize()
+assert all(torch.equal(o, t) for t, o in zip(ins, outs))
+for (_, xo), sn in zip(sets, snap):
+    assert all(torch.equal(a, b) for a, b in zip(xo, sn))
+os.environ["TIPS_FUSION_THRESHOLD"] = str(2 << 20)
+try:
+    tips_amd.fused_allreduce(ins, out_list=outs)
+    raise SystemExit("a threshold change under a live capture must fail")
+except _lib.TipsError as e:
+    assert "threshold changed" in str(e), e
+os.environ["TIPS_FUSION_THRESHOLD"] = str(1 << 20)
+for t in ins:
+    t.add_(1.0)
+with torch.cuda.stream(side):
+    g.replay()
+torch.cuda.synchronize()
+assert all(torch.equal(o, t) for t, o in zip(ins, outs))
+del g
+torch.cuda.synchronize()
+tips_amd.shutdown()
+print("CAPTURE_TABLE_OK")
+'''
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, timeout=300)
+    assert "CAPTURE_TABLE_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
 def test_fused_views_of_one_buffer(gpu, monkeypatch):
     """Views of one flat buffer mixed with separate tensors (measure-pack mode: every byte through
     pack -> bucket -> unpack at one rank): the layout ignores where tensors lie, so the views are

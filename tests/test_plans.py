@@ -127,6 +127,60 @@ def test_hazard_checker_catches_a_missing_wait():
     assert pu.hazards(pl, 4, 400000)
 
 
+def _tune_candidates(p, n, dtype=F32):
+    import ctypes
+    from tips_amd import _lib
+    L = _lib.dev()
+    cap = 16
+    a, d, la = (ctypes.c_int * cap)(), (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+    k = L.tips_tune_candidates(p, n, dtype, a, d, la, cap)
+    assert k > 0, _lib.last_error()
+    return [(a[i], d[i], la[i]) for i in range(k)]
+
+
+@pytest.mark.parametrize("p", [2, 4, 8])
+def test_config3_direct_fold_runs_under_the_next_transfer(p):
+    """Config 3 (1 GiB f32, the chunk >= 16 MiB): every direct / ring depth the tuner may keep is
+    pipelined (K >= 2), and in the executor's stream model the fold of sub-chunk k is unordered
+    against the transfer group of sub-chunk k + 1, so it runs on the CUs while k + 1 is on the links
+    (the N = 8 rehearsal's tuner had kept depth 1 for config 3)."""
+    n = (1 << 30) // 4
+    cands = _tune_candidates(p, n)
+    assert {a for a, _, _ in cands} >= {pu.DIRECT, pu.RING}
+    for algo, K, _ in cands:
+        assert K >= 2, (algo, K, cands)
+        pl = pu.dump(algo, p, p - 1, n, F32, K)
+        under = pu.sums_under_transfers(pl)
+        if algo == pu.DIRECT:
+            for k in range(K - 1):  # reduce-scatter steps 0..K-1: fold k, then transfer k + 1
+                assert k + 1 in under[k], (algo, K, k, under[k])
+        else:  # ring: every step's sum overlaps the next sub-chunk's transfer of the same step
+            for i, js in under.items():
+                if (i + 1) % K:
+                    assert i + 1 in js, (algo, K, i, js)
+
+
+def test_depth_one_stays_a_candidate_below_16_mib_chunks():
+    """Below the 16 MiB chunk the tuner still times depth 1 against the default (one launch per
+    chunk can win there), and above it never."""
+    small = _tune_candidates(8, 8 * (12 << 20) // 4)  # 12 MiB chunks: K = 2 by default
+    assert (pu.DIRECT, 1, 1) in small
+    for mib in (16, 32, 128):
+        big = _tune_candidates(8, 8 * (mib << 20) // 4)
+        assert all(K >= 2 for _, K, _ in big), (mib, big)
+
+
+def test_overlap_model_sees_a_serialising_wait():
+    """The model itself: make every direct transfer group wait for the previous step's fold and
+    nothing runs under a transfer any more."""
+    pl = pu.dump(pu.DIRECT, 8, 0, (1 << 30) // 4, F32, 4)
+    assert pu.sums_under_transfers(pl)[0]
+    for i, s in enumerate(pl["steps"]):
+        if i > 0:
+            s["wait_sum"] = i - 1
+    assert not any(pu.sums_under_transfers(pl)[k] for k in range(3))
+
+
 @pytest.mark.parametrize("algo", [pu.RING, pu.DIRECT, pu.ONESHOT])
 @pytest.mark.parametrize("dtype", [F32, I32, F64, BF16])
 @pytest.mark.parametrize("p,n,K", [(2, 4099, 1), (3, 1000, 3), (4, 65539, 4), (5, 7, 2), (8, 100003, 3),

@@ -126,6 +126,9 @@ _SIGNATURES = [
     ("tips_tuned_choice", ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     ("tips_tuned_schedule", ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                            ctypes.POINTER(ctypes.c_int)]),
+    ("tips_tuned_timings", ctypes.c_int,
+     [ctypes.c_int64, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+      ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ("tips_graph_stats", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     ("tips_replay_order_stats", ctypes.c_int, [_c_i64_p, _c_i64_p]),
@@ -161,6 +164,9 @@ _DEV_SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]),
     ("tips_schedule_plan", ctypes.c_int64,
      [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _c_i64_p, ctypes.c_int64]),
+    ("tips_tune_candidates", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+      ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
 ]
 
 

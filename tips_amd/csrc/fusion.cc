@@ -72,6 +72,9 @@ struct Table {  // resolved segment records of one pointer set
   const void* base = nullptr;  // the flat output (kFlat) or the slot base (kSlot)
   CopySeg* dev = nullptr;      // kSlot: [pack | unpack], else one table; nseg records each
   uint64_t stamp = 0;
+  // a call captured into a graph read this table: a replay may read it at any later time, so it is
+  // never refilled, reused or freed (until tips_shutdown), and its layout is never evicted
+  bool pinned = false;
 };
 
 }  // namespace
@@ -92,6 +95,11 @@ struct Layout {
   int ntiles = 0;
   std::vector<Table*> tables;
   uint64_t stamp = 0;
+  bool pinned() const {
+    for (const Table* t : tables)
+      if (t->pinned) return true;
+    return false;
+  }
 };
 
 // Bucket cut and offsets: a pure function of (dtype, counts, threshold, tile, balance).
@@ -249,11 +257,14 @@ Layout* find_layout(State& st, FusionCache& fc, const int64_t* counts, int n, in
       fc.layout_hits++;
       return L;
     }
-  if (fc.layouts.size() >= kMaxLayouts) {  // evict the least recently used layout
-    auto lru = std::min_element(fc.layouts.begin(), fc.layouts.end(),
-                                [](const Layout* a, const Layout* b) { return a->stamp < b->stamp; });
-    free_layout(st, *lru);
-    fc.layouts.erase(lru);
+  if (fc.layouts.size() >= kMaxLayouts) {  // evict the least recently used layout no captured graph uses
+    auto lru = fc.layouts.end();
+    for (auto it = fc.layouts.begin(); it != fc.layouts.end(); ++it)
+      if (!(*it)->pinned() && (lru == fc.layouts.end() || (*it)->stamp < (*lru)->stamp)) lru = it;
+    if (lru != fc.layouts.end()) {
+      free_layout(st, *lru);
+      fc.layouts.erase(lru);
+    }
   }
   Layout* L = new Layout();
   L->key = h;
@@ -377,24 +388,28 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
     if (same) {
       t->stamp = ++fc.clock;
       fc.table_hits++;
+      if (st.fuse_capturing) t->pinned = true;  // the graph's replays read it from now on
       return t;
     }
   }
+  if (st.fuse_capturing) {  // (before any table is touched: nothing may be refilled under capture)
+    fail(TIPS_ERR_INVALID_ARG, "fusion: a fused call under stream capture must find its pointer table built: make "
+                               "the same call once before the capture");
+    return nullptr;
+  }
   Table* t = nullptr;
-  if (L.tables.size() >= kMaxTables) {  // reuse the least recently used table's device buffer (stream order
-    auto lru = std::min_element(L.tables.begin(), L.tables.end(),   // keeps its earlier readers first)
-                                [](const Table* a, const Table* b) { return a->stamp < b->stamp; });
+  size_t unpinned = 0;
+  for (const Table* u : L.tables) unpinned += !u->pinned;
+  if (unpinned >= kMaxTables) {  // reuse the least recently used unpinned table's device buffer (stream
+    auto lru = L.tables.end();    // order keeps its earlier readers first); pinned ones are never touched
+    for (auto it = L.tables.begin(); it != L.tables.end(); ++it)
+      if (!(*it)->pinned && (lru == L.tables.end() || (*it)->stamp < (*lru)->stamp)) lru = it;
     if ((*lru)->mode == mode) {
       t = *lru;
     } else {
       free_table(st, *lru);
       L.tables.erase(lru);
     }
-  }
-  if (st.fuse_capturing) {
-    fail(TIPS_ERR_INVALID_ARG, "fusion: a fused call under stream capture must find its pointer table built: make "
-                               "the same call once before the capture");
-    return nullptr;
   }
   const int nseg = (int)L.seg_tensor.size();
   const int ntab = mode == kSlot ? 2 : 1;
@@ -435,6 +450,11 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
 // after the fusion streams have finished with them.
 int ensure_slots(State& st, FusionCache& fc, int64_t threshold) {
   if (threshold == st.fusion_threshold && st.fusion.p) return 0;
+  for (const Layout* L : fc.layouts)  // a captured graph's replays pack into the current slots
+    if (L->pinned() && st.fusion.p)
+      return fail(TIPS_ERR_INVALID_ARG, "fusion: the fusion threshold changed (%lld -> %lld bytes) while a graph "
+                  "captured around a fused call may still replay into the fusion slots",
+                  (long long)st.fusion_threshold, (long long)threshold);
   if (st.fuse_chain_valid) {
     TRY(chain_event(st));
     HIP_TRY(hipEventSynchronize(st.ev_fuse_chain));

@@ -448,11 +448,11 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
 // Buffer-op form of the multi-input sum: one descriptor per source covering
 // this workgroup's tile, cache-policy bits on the loads (LAUX) and sc1 stores,
 // every source's vectors in flight before the fold (as sum2_buf_kernel).
-template <int DT, int NSRC, int U, int LAUX>
-__global__ __launch_bounds__(kBlock) void multi_sum_buf_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
-                                                              int64_t tail_begin, int64_t n) {
+template <int DT, int NSRC, int U, int LAUX, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void multi_sum_buf_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
+                                                             int64_t tail_begin, int64_t n) {
   using W = Wide<DT>;
-  constexpr int64_t kTile = (int64_t)kBlock * U;
+  constexpr int64_t kTile = (int64_t)BLOCK * U;
   const int tid = threadIdx.x;
   const int64_t first = xcd_tile(blockIdx.x, gridDim.x) * kTile;
   if (first < nvec) {
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kBlock) void multi_sum_buf_kernel(u32x4* __restrict
     for (int j = 0; j < NSRC; j++) {
       __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(srcs.p[j] + first), (short)0, rec, 0x00020000);
 #pragma unroll
-      for (int u = 0; u < U; u++) v[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, LAUX);
+      for (int u = 0; u < U; u++) v[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * BLOCK + tid) * 16, 0, LAUX);
     }
     __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
 #pragma unroll
@@ -470,7 +470,7 @@ __global__ __launch_bounds__(kBlock) void multi_sum_buf_kernel(u32x4* __restrict
       typename W::A acc = W::load(v[u][0]);
 #pragma unroll
       for (int j = 1; j < NSRC; j++) acc = acc + W::load(v[u][j]);
-      __builtin_amdgcn_raw_buffer_store_b128(W::store(acc), rd, (u * kBlock + tid) * 16, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(W::store(acc), rd, (u * BLOCK + tid) * 16, 0, 16);
     }
   }
   if (blockIdx.x == 0 && NSRC > 1 && tail_begin + tid < n) {
@@ -480,6 +480,124 @@ __global__ __launch_bounds__(kBlock) void multi_sum_buf_kernel(u32x4* __restrict
     fold_elem<DT>(dst, s, NSRC, tail_begin + tid);
   }
 }
+
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
+// Round-5 sweep form of the fold (f32): ORDER 0 = XCD-contiguous tiles, 1 = address order (the
+// 8 XCDs on neighbouring tiles, so the chip reads NSRC + 1 moving windows instead of 8 x that),
+// 2 = XCD-contiguous with each XCD's stretch cut into 8 interleaved runs; ITER consecutive tiles
+// per workgroup, one after the other (longer-lived workgroups, fewer ramps); ROT: the sources'
+// load order rotated by workgroup (the fold order is unchanged); SAUX store policy; BLOCK lanes.
+template <int NSRC, int U, int SAUX, int ORDER, int ITER, int ROT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void multi_sum_x_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
+                                                            int64_t tail_begin, int64_t n) {
+  constexpr int64_t kTile = (int64_t)BLOCK * U;
+  const int tid = threadIdx.x;
+  int64_t g;
+  if constexpr (ORDER == 0) {
+    g = xcd_tile(blockIdx.x, gridDim.x);
+  } else if constexpr (ORDER == 1) {
+    g = blockIdx.x;
+  } else {  // XCD x owns stretch x; inside it, its workgroups walk 8 sub-runs round-robin
+    const int64_t per = gridDim.x >> 3, k = blockIdx.x >> 3, runs = per >= 64 ? 8 : 1;
+    g = (int64_t)(blockIdx.x & 7u) * per + (k % runs) * (per / runs) + k / runs;
+  }
+  for (int it = 0; it < ITER; it++) {
+    const int64_t first = (g * ITER + it) * kTile;
+    if (first >= nvec) break;
+    const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
+    u32x4 v[U][NSRC];
+#pragma unroll
+    for (int jj = 0; jj < NSRC; jj++) {
+      const int j = ROT ? (int)((jj + blockIdx.x) % NSRC) : jj;
+      __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(srcs.p[j] + first), (short)0, rec, 0x00020000);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * BLOCK + tid) * 16, 0, 2);
+        if constexpr (ROT) {
+#pragma unroll
+          for (int q = 0; q < NSRC; q++)
+            if (q == j) v[u][q] = x;
+        } else {
+          v[u][jj] = x;
+        }
+      }
+    }
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      f32x4 acc = __builtin_bit_cast(f32x4, v[u][0]);
+#pragma unroll
+      for (int j = 1; j < NSRC; j++) acc = acc + __builtin_bit_cast(f32x4, v[u][j]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rd, (u * BLOCK + tid) * 16, 0, SAUX);
+    }
+  }
+  if (blockIdx.x == 0 && NSRC > 1 && tail_begin + tid < n) {
+    const void* s[NSRC];
+#pragma unroll
+    for (int j = 0; j < NSRC; j++) s[j] = srcs.p[j];
+    fold_elem<kF32>(dst, s, NSRC, tail_begin + tid);
+  }
+}
+
+// Grid-stride form (round-5 sweep, f32): gridDim = 256 CUs x W workgroups, XCD x walking its
+// stretch with its grid / 8 workgroups side by side (tile = stretch start + k x grid / 8 + slot).
+// The chip's loads in flight are capped by the grid, not by reserved LDS or registers, so a
+// transfer kernel beside the fold still finds room on every CU. PIPE: the next tile's loads are
+// issued before this tile's add and store.
+template <int NSRC, int BLOCK, int PIPE>
+__global__ __launch_bounds__(BLOCK) void multi_sum_gs_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
+                                                             int64_t tail_begin, int64_t n) {
+  constexpr int64_t kTile = BLOCK;
+  const int tid = threadIdx.x;
+  const int64_t ntiles = (nvec + kTile - 1) / kTile;
+  const int64_t per_xcd = (ntiles + 7) / 8, wg_xcd = gridDim.x >> 3;
+  const int64_t x = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+  const int64_t beg = x * per_xcd, end = beg + per_xcd < ntiles ? beg + per_xcd : ntiles;
+  auto load = [&](int64_t t, u32x4 (&v)[NSRC]) {
+    const int64_t first = t * kTile;
+    const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
+#pragma unroll
+    for (int j = 0; j < NSRC; j++) {
+      __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(srcs.p[j] + first), (short)0, rec, 0x00020000);
+      v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, 0, 2);
+    }
+  };
+  auto fold_store = [&](int64_t t, const u32x4 (&v)[NSRC]) {
+    const int64_t first = t * kTile;
+    const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
+    f32x4 acc = __builtin_bit_cast(f32x4, v[0]);
+#pragma unroll
+    for (int j = 1; j < NSRC; j++) acc = acc + __builtin_bit_cast(f32x4, v[j]);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rd, tid * 16, 0, 16);
+  };
+  int64_t t = beg + slot;
+  if constexpr (PIPE) {
+    u32x4 a[NSRC], b[NSRC];
+    if (t < end) load(t, a);
+    while (t < end) {
+      const int64_t t2 = t + wg_xcd;
+      if (t2 < end) load(t2, b);
+      fold_store(t, a);
+#pragma unroll
+      for (int j = 0; j < NSRC; j++) a[j] = b[j];
+      t = t2;
+    }
+  } else {
+    for (; t < end; t += wg_xcd) {
+      u32x4 v[NSRC];
+      load(t, v);
+      fold_store(t, v);
+    }
+  }
+  if (blockIdx.x == 0 && NSRC > 1 && tail_begin + tid < n) {
+    const void* s[NSRC];
+#pragma unroll
+    for (int j = 0; j < NSRC; j++) s[j] = srcs.p[j];
+    fold_elem<kF32>(dst, s, NSRC, tail_begin + tid);
+  }
+}
+#endif  // TIPS_DEV
 
 template <int DT>
 __global__ __launch_bounds__(kBlock) void multi_sum_scalar_kernel(void* dst, SrcList srcs, int nsrc, int64_t n) {
@@ -985,24 +1103,41 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
 // profiles/ + DESIGN.md §Kernels).
 constexpr int kDefMode = 3, kDefUnroll = 1, kDefNT = 1, kDefThreads = 256;
 
+// Bytes the fold keeps in flight per CU (round 5, profiles/r05/): every wave-source pair has one
+// 1 KiB wave-load outstanding, and with 9 streams the DRAM efficiency falls once a CU holds much more
+// than the ~64 KiB the 2-input sum keeps in flight. Unused LDS reserved per workgroup caps the
+// workgroups per CU (160 KiB / reservation): NSRC >= 6, 128 lanes x 5 workgroups = 10 waves
+// (80 KiB for 8 sources: 8 x 32 MiB 48.1-49.2 -> 46.9-47.5 us on the sweep's boxes); NSRC 4-5,
+// 128 lanes x 8 = 16 waves. 2-3 sources run uncapped (256 lanes x 8 = 32 waves: capping slowed
+// 2 x 128 MiB). The reservation leaves the CU at least one RCCL transfer workgroup's worth (19.5
+// KiB) at 5 workgroups; uncapped, the fold's 32 waves fill every wave slot anyway.
+constexpr int kFoldLdsCap5 = 27648;  // floor(160 KiB / 27648) = 5, 25 KiB left
+constexpr int kFoldLdsCap8 = 20480;  // 8
+
 template <int DT, int NSRC>
 hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
-  // buffer loads, 1 vector per lane, non-temporal for every source count. Round 1 kept plain
-  // loads beyond 4 sources from a sweep that re-read one buffer set (plain 44.7 vs nt 47.3 us,
-  // 8 x 32 MiB, Infinity Cache assisted); with operands from HBM, as the direct schedule's fold
-  // mostly reads them, nt wins 48.6 vs 57.8 us (profiles/r02/multi_sum_variants.jsonl).
+  // buffer loads, non-temporal for every source count. Round 1 kept plain loads beyond 4 sources
+  // from a sweep that re-read one buffer set (plain 44.7 vs nt 47.3 us, 8 x 32 MiB, Infinity Cache
+  // assisted); with operands from HBM, as the direct schedule's fold mostly reads them, nt wins
+  // 48.6 vs 57.8 us (profiles/r02/multi_sum_variants.jsonl).
   constexpr int LAUX = 2;
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
-  // 4 vectors per lane for many sources of 3-24 MiB each (8 x 4 MiB: 7.0 vs 8.3 us, 8 x 8 MiB:
-  // 12.6 vs 14.3 us; larger or smaller, or up to 4 sources, 1 vector wins or ties:
-  // profiles/r02/multi_sum_small.jsonl)
-  const bool u4 = NSRC > 4 && nvec * 16 >= (3 << 20) && nvec * 16 <= (24 << 20);
-  const int64_t per = (int64_t)kBlock * (u4 ? 4 : 1);
+  const int64_t bytes = nvec * 16;
+  // 4 vectors per lane for many sources of 3-12 MiB each (8 x 4 MiB: 7.0 vs 8.3 us, 8 x 8 MiB:
+  // 12.6 vs 14.3 us; up to 4 sources, 1 vector wins or ties: profiles/r02/multi_sum_small.jsonl)
+  const bool u4 = NSRC > 4 && bytes >= (3 << 20) && bytes <= (12 << 20);
+  const bool capped = NSRC >= 4 && !u4 && bytes > (12 << 20);
+  constexpr int kCapBlock = 128;
+  const int block = capped ? kCapBlock : kBlock;
+  const int64_t per = (int64_t)block * (u4 ? 4 : 1);
   int64_t grid = (nvec + per - 1) / per;
   grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  if (u4)
+  if (capped)
+    hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX, kCapBlock>), dim3((unsigned)grid), dim3(kCapBlock),
+                       NSRC >= 6 ? kFoldLdsCap5 : kFoldLdsCap8, s, (u32x4*)dst, sl, nvec, nvec * ve, n);
+  else if (u4)
     hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 4, LAUX>), dim3((unsigned)grid), dim3(kBlock), 0, s,
                        (u32x4*)dst, sl, nvec, nvec * ve, n);
   else
@@ -1012,6 +1147,94 @@ hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
 }
 
 #ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
+template <int NSRC, int U, int SAUX, int ORDER, int ITER, int ROT, int BLOCK>
+hipError_t launch_multi_x(void* dst, const SrcList& sl, int64_t nvec, int64_t n, unsigned shmem, hipStream_t s) {
+  const int64_t per = (int64_t)BLOCK * U * ITER;
+  int64_t grid = (nvec + per - 1) / per;
+  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);
+  if (ORDER == 2 && (grid >> 3) >= 64) grid = (grid + 63) / 64 * 64;  // every XCD's stretch splits into 8 runs
+  hipLaunchKernelGGL((multi_sum_x_kernel<NSRC, U, SAUX, ORDER, ITER, ROT, BLOCK>), dim3((unsigned)grid), dim3(BLOCK),
+                     shmem, s, (u32x4*)dst, sl, nvec, nvec * 4, n);
+  return hipGetLastError();
+}
+
+template <int NSRC, int BLOCK, int PIPE>
+hipError_t launch_multi_gs(void* dst, const SrcList& sl, int64_t nvec, int64_t n, int wpc, hipStream_t s) {
+  const int64_t tiles = (nvec + BLOCK - 1) / BLOCK;
+  const int64_t grid = std::max<int64_t>(8, std::min<int64_t>((int64_t)kNumCUs * wpc, (tiles + 7) / 8 * 8));
+  hipLaunchKernelGGL((multi_sum_gs_kernel<NSRC, BLOCK, PIPE>), dim3((unsigned)grid), dim3(BLOCK), 0, s, (u32x4*)dst, sl,
+                     nvec, nvec * 4, n);
+  return hipGetLastError();
+}
+
+// Round-5 variants (f32), all nt loads: 8 = address-order tiles; 9 = nt stores; 10 = plain stores;
+// 11 / 12 = 2 / 4 consecutive tiles per workgroup in turn; 13 / 14 = 512 / 128 lanes; 15 = load
+// order rotated per workgroup; 16 = XCD stretches cut into 8 interleaved runs; 17 / 18 / 19 =
+// 20 / 40 / 27 KiB of unused LDS per workgroup (8 / 4 / 5 workgroups per CU); 20 = address order,
+// 4 tiles per workgroup; 21 = the shipped shape through this kernel (control); 22 = address order,
+// 2 vectors per lane; 23 / 24 / 25 = 80 / 53 / 32 KiB of LDS (2 / 3 / 5 workgroups per CU);
+// 26 / 27 / 30 / 34 = 128 lanes with 40 / 20 / 27 / 13 KiB (4 / 8 / 5 / 12 workgroups per CU);
+// 28 / 29 = 2 vectors per lane with 40 / 80 KiB; 31 = address order with 40 KiB; 32 / 33 = 64
+// lanes, uncapped / 10 KiB (16 per CU); 35 = 128 lanes, 2 vectors, 20 KiB; 40-49 = the grid-stride
+// form (multi_sum_gs_kernel): 128 lanes x 4 / 5 / 6 / 8 / 12 workgroups per CU (40-43, 48), the
+// same pipelined x 4 / 5 / 3 (44, 45, 49); 256 lanes x 3 (46), pipelined x 2 (47).
+template <int NSRC>
+hipError_t run_multi_x(void* dst, const SrcList& sl, int64_t n, int variant, hipStream_t s) {
+  const int64_t nvec = n / 4;
+  switch (variant) {
+    case 8: return launch_multi_x<NSRC, 1, 16, 1, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 9: return launch_multi_x<NSRC, 1, 2, 0, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 10: return launch_multi_x<NSRC, 1, 0, 0, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 11: return launch_multi_x<NSRC, 1, 16, 0, 2, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 12: return launch_multi_x<NSRC, 1, 16, 0, 4, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 13: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 512>(dst, sl, nvec, n, 0, s);
+    case 14: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 0, s);
+    case 15: return launch_multi_x<NSRC, 1, 16, 0, 1, 1, 256>(dst, sl, nvec, n, 0, s);
+    case 16: return launch_multi_x<NSRC, 1, 16, 2, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 17: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 20 << 10, s);
+    case 18: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 40 << 10, s);
+    case 19: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 27 << 10, s);
+    case 20: return launch_multi_x<NSRC, 1, 16, 1, 4, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 21: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 22: return launch_multi_x<NSRC, 2, 16, 1, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 23: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 80 << 10, s);
+    case 24: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 53 << 10, s);
+    case 25: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 32 << 10, s);
+    case 26: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 40 << 10, s);
+    case 27: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 20 << 10, s);
+    case 28: return launch_multi_x<NSRC, 2, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 40 << 10, s);
+    case 29: return launch_multi_x<NSRC, 2, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 80 << 10, s);
+    case 30: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 27 << 10, s);
+    case 31: return launch_multi_x<NSRC, 1, 16, 1, 1, 0, 256>(dst, sl, nvec, n, 40 << 10, s);
+    case 32: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 64>(dst, sl, nvec, n, 0, s);
+    case 33: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 64>(dst, sl, nvec, n, 10 << 10, s);
+    case 34: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 13 << 10, s);
+    case 35: return launch_multi_x<NSRC, 2, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 20 << 10, s);
+    case 50: return run_multi<kF32, NSRC>(dst, sl, n, s);  // what tips_multi_sum launches
+    case 51: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 64>(dst, sl, nvec, n, 16384, s);   // 64 x 10
+    case 52: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 64>(dst, sl, nvec, n, 13312, s);   // 64 x 12
+    case 53: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 64>(dst, sl, nvec, n, 20480, s);   // 64 x 8
+    case 54: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 26624, s);  // 128 x 6
+    case 55: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 128>(dst, sl, nvec, n, 32768, s);  // 128 x 5 (no room)
+    case 56: return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 192>(dst, sl, nvec, n, 32768, s);  // 192 x 5
+    case 36:  // the round-4 shipped fold (no cap; 4 vectors per lane for > 4 sources of 3-24 MiB)
+      if (NSRC > 4 && nvec * 16 >= (3 << 20) && nvec * 16 <= (24 << 20))
+        return launch_multi_x<NSRC, 4, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+      return launch_multi_x<NSRC, 1, 16, 0, 1, 0, 256>(dst, sl, nvec, n, 0, s);
+    case 40: return launch_multi_gs<NSRC, 128, 0>(dst, sl, nvec, n, 4, s);
+    case 41: return launch_multi_gs<NSRC, 128, 0>(dst, sl, nvec, n, 5, s);
+    case 42: return launch_multi_gs<NSRC, 128, 0>(dst, sl, nvec, n, 6, s);
+    case 43: return launch_multi_gs<NSRC, 128, 0>(dst, sl, nvec, n, 8, s);
+    case 44: return launch_multi_gs<NSRC, 128, 1>(dst, sl, nvec, n, 4, s);
+    case 45: return launch_multi_gs<NSRC, 128, 1>(dst, sl, nvec, n, 5, s);
+    case 46: return launch_multi_gs<NSRC, 256, 0>(dst, sl, nvec, n, 3, s);
+    case 47: return launch_multi_gs<NSRC, 256, 1>(dst, sl, nvec, n, 2, s);
+    case 48: return launch_multi_gs<NSRC, 128, 0>(dst, sl, nvec, n, 12, s);
+    case 49: return launch_multi_gs<NSRC, 128, 1>(dst, sl, nvec, n, 3, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // Sweep entry (f32; nsrc 2, 4, 8): 0 = global nt loads (U 2 for nsrc <= 4, else 1),
 // 1 = buffer nt loads U 1, 2 = buffer nt loads U 2, 3 = buffer plain loads U 1, 4 = buffer nt loads U 4.
 template <int NSRC>
@@ -1057,7 +1280,7 @@ hipError_t run_multi_variant(void* dst, const SrcList& sl, int64_t n, int varian
                          (u32x4*)dst, sl, nvec, nvec * 4, n);
       break;
     default:
-      return hipErrorInvalidValue;
+      return run_multi_x<NSRC>(dst, sl, n, variant, s);
   }
   return hipGetLastError();
 }

@@ -32,6 +32,8 @@ namespace rt {
 using tips::CopyTile;
 
 constexpr int64_t kAlignBytes = 256;  // chunk / bucket-slot alignment (dwordx4 + 128-B lines)
+// chunks of at least this many bytes always run pipelined under TIPS_ALGO_TUNE (K >= 2 sub-chunks)
+constexpr int64_t kPipelineMinChunk = (int64_t)16 << 20;
 // host-staging piece: 16 MiB sits at the top of the measured pipeline curve (profiles/r01_pcie_probe.jsonl)
 constexpr int64_t kHostPieceBytes = 16 << 20;
 
@@ -218,6 +220,8 @@ struct State {
   FusionCache* fusion_cache = nullptr;  // created on first use
   // TIPS_ALGO_TUNE: (ranks, dtype, size class) -> schedule, the same on every rank
   std::map<std::tuple<int, int, int>, Choice> tuned;
+  // ... and every candidate the tuner timed for it, with the slowest rank's ms per call
+  std::map<std::tuple<int, int, int>, std::vector<std::pair<Choice, double>>> tuned_ms;
   // transfer lanes beyond the comm stream (TIPS_LANES, or tuned): RCCL communicators split from
   // `comm`, each with its own stream at the comm stream's priority; a plan's step i moves its
   // bytes on lane i % L, so the groups of consecutive steps can be in flight together
@@ -260,6 +264,8 @@ void rccl_env_defaults();  // before any ncclCommInitRank of ours
 
 // schedules.cc: device-resident allreduce, caller holds st.mu
 int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype, hipStream_t stream);
+// the candidates TIPS_ALGO_TUNE times for a bucket of n elements on p ranks, in its order (schedules.cc)
+std::vector<Choice> tune_candidates(int p, int64_t n, int dtype);
 void graphs_release(State& st);  // schedules.cc (shutdown, before the communicator goes)
 // schedules.cc: an RCCL operation on `comm` issued outside a plan (a control-plane collective, the
 // TIPS_ALGO_RCCL comparison) goes on stream `s` between these two calls: after everything queued

@@ -422,16 +422,19 @@ int run_choice(State& st, const Choice& c, const char* in, char* out, int64_t n,
   return plan_allreduce(st, c, in, out, n, dtype, s);
 }
 
-// Every rank runs the same candidates in the same order (collectives), on scratch copies of the
-// call's input (the caller's buffers are not touched: in-place calls stay correct), times each with
-// events on `user` (best of 2 runs of 2 back-to-back calls, after a warm-up), and the ranks agree
-// on the slowest rank's time per candidate with one small ncclAllReduce(MAX): every rank then keeps
-// the same fastest candidate.
-int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choice* best) {
-  const int p = st.size;
-  const int64_t bytes = n * tips::dtype_size(dtype);
+}  // namespace
+
+// The candidates TIPS_ALGO_TUNE times for a bucket of n elements on p ranks, in the order it runs
+// them (every rank the same): direct at the default depth K, at 1 and at 2K, ring at K and 2K.
+// A chunk of 16 MiB or more is always pipelined (K >= 2): the fold of sub-chunk k then runs under
+// the transfer of k + 1 (tests/test_plans.py), so depth 1 is a candidate only below that, where one
+// launch per chunk can beat the per-launch cost of two.
+std::vector<Choice> tune_candidates(int p, int64_t n, int dtype) {
+  const int64_t es = tips::dtype_size(dtype);
   const int K = plan_depth(p, n, dtype);
   const int K2 = std::min(16, 2 * K);
+  const int64_t chunk_bytes = chunk_of(n, p, kAlignBytes / es, 0).len() * es;
+  const bool depth1 = K > 1 && chunk_bytes < kPipelineMinChunk;
   // TIPS_TUNE_LANES=1 adds two-lane candidates (consecutive steps' groups in flight together, for
   // when one communicator's point-to-point work does not fill the links). Off by default: on the
   // socket rehearsal the split communicator slowed every later call, chosen or not
@@ -440,7 +443,7 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choi
   std::vector<Choice> cand;
   if (p <= tips::kMaxSrcs) {
     cand.push_back({TIPS_ALGO_DIRECT, K, 1});
-    cand.push_back({TIPS_ALGO_DIRECT, 1, 1});
+    if (depth1) cand.push_back({TIPS_ALGO_DIRECT, 1, 1});
     if (K < 16) cand.push_back({TIPS_ALGO_DIRECT, K2, 1});
     if (lanes && K > 1) cand.push_back({TIPS_ALGO_DIRECT, K, 2});
   }
@@ -448,6 +451,21 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choi
   if (K < 16) cand.push_back({TIPS_ALGO_RING, K2, 1});
   if (lanes) cand.push_back({TIPS_ALGO_RING, K, 2});
   if (p <= tips::kMaxSrcs && env_i64("TIPS_TUNE_PEER", 0)) cand.push_back({TIPS_ALGO_PEER, 0, 1});
+  return cand;
+}
+
+namespace {
+
+// Every rank runs the same candidates in the same order (collectives), on scratch copies of the
+// call's input (the caller's buffers are not touched: in-place calls stay correct), times each with
+// events on `user` (best of 2 runs of 2 back-to-back calls, after a warm-up), and the ranks agree
+// on the slowest rank's time per candidate with one small ncclAllReduce(MAX): every rank then keeps
+// the same fastest candidate.
+int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choice* best,
+         std::vector<std::pair<Choice, double>>* timed) {
+  const int p = st.size;
+  const int64_t bytes = n * tips::dtype_size(dtype);
+  std::vector<Choice> cand = tune_candidates(p, n, dtype);
   HIP_TRY(hipStreamSynchronize(user));
   void *sin = nullptr, *sout = nullptr;
   int rc = 0;
@@ -523,6 +541,8 @@ int tune(State& st, const char* in, int64_t n, int dtype, hipStream_t user, Choi
   for (size_t c = 1; c < cand.size(); c++)
     if (ms[c] < ms[b]) b = c;
   *best = cand[b];
+  timed->clear();
+  for (size_t c = 0; c < cand.size(); c++) timed->emplace_back(cand[c], ms[c]);
   if (getenv("TIPS_VERBOSE") && st.rank == 0) {
     fprintf(stderr, "[tips] tune p=%d bytes=%lld:", p, (long long)bytes);
     for (size_t c = 0; c < cand.size(); c++)
@@ -557,8 +577,10 @@ int allreduce_device(State& st, const void* in, void* out, int64_t n, int dtype,
     auto it = st.tuned.find(key);
     if (it == st.tuned.end()) {
       Choice best;
-      TRY(tune(st, (const char*)in, n, dtype, stream, &best));
+      std::vector<std::pair<Choice, double>> timed;
+      TRY(tune(st, (const char*)in, n, dtype, stream, &best, &timed));
       it = st.tuned.emplace(key, best).first;
+      st.tuned_ms[key] = std::move(timed);
     }
     return run_choice(st, it->second, (const char*)in, (char*)out, n, dtype, stream);
   }
@@ -800,6 +822,25 @@ int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lanes) {
   return 1;
 }
 
+int tips_tuned_timings(int64_t bytes, int* algos, int* depths, int* lanes, double* ms, int cap) {
+  if (bytes < 0 || cap < 0 || (cap > 0 && (!algos || !depths || !lanes || !ms)))
+    return fail(TIPS_ERR_INVALID_ARG, "bad tuned-timings query");
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  for (const auto& kv : st.tuned_ms)  // any dtype of this job's size class, as tips_tuned_choice
+    if (std::get<0>(kv.first) == st.size && std::get<2>(kv.first) == size_class(bytes)) {
+      const int n = (int)kv.second.size();
+      for (int i = 0; i < n && i < cap; i++) {
+        algos[i] = kv.second[i].first.algo;
+        depths[i] = kv.second[i].first.depth;
+        lanes[i] = kv.second[i].first.lanes;
+        ms[i] = kv.second[i].second;
+      }
+      return n;
+    }
+  return 0;
+}
+
 int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached) {
   if (!captured || !replayed || !cached) return fail(TIPS_ERR_INVALID_ARG, "bad graph-stats query");
   State& st = S();
@@ -824,6 +865,19 @@ int tips_replay_order_stats(int64_t* host_waits, int64_t* host_wait_ns) {
 }
 
 #ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
+int tips_tune_candidates(int p, int64_t count, int dtype, int* algos, int* depths, int* lanes, int cap) {
+  TRY(check_dtype(dtype));
+  if (p < 2 || count < 0 || cap < 0 || (cap > 0 && (!algos || !depths || !lanes)))
+    return fail(TIPS_ERR_INVALID_ARG, "bad tune-candidates query");
+  const std::vector<Choice> c = tune_candidates(p, count, dtype);
+  for (int i = 0; i < (int)c.size() && i < cap; i++) {
+    algos[i] = c[i].algo;
+    depths[i] = c[i].depth;
+    lanes[i] = c[i].lanes;
+  }
+  return (int)c.size();
+}
+
 int64_t tips_schedule_plan(int algo, int p, int rank, int64_t count, int dtype, int depth, int64_t* out, int64_t cap) {
   TRY(check_dtype(dtype));
   if (cap < 0 || (cap > 0 && !out)) return fail(TIPS_ERR_INVALID_ARG, "bad plan buffer");
