@@ -1450,7 +1450,9 @@ def north_star_ring(job, w, line):
     one xGMI link, target 0.70; the reference's data call is utils.h:60-65), and RCCL's own
     ncclAllReduce on the same bucket as a reference point. Not budgeted: every N > 1 line has both."""
     _lib = job._lib
-    kc = max(3, min(w.steps, 10))
+    # 10 timed calls (the headline's steps if fewer), down to 3 when a call takes seconds (the
+    # socket rehearsal): on xGMI a config-3 call is milliseconds and this costs well under a second
+    kc = max(3, min(w.steps, 10, int(10.0 / max(w.ms / 1e3, 1e-3))))
     subs = line.setdefault("configs", {})
     progress(job.rank, "config3_ring")
     try:
