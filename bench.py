@@ -507,7 +507,10 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
     out = {"calls": what, "bytes_per_rank": sum(sizes) * 4, "fixed_view_ms": round(fixed_ms, 4)}
     ref = [torch.cat([g.reshape(-1) for g in gs]) for gs in grads] if world == 1 else None
     for name, fn in calls.items():
-        for i in range(3):
+        # warm every rotating set: a set's first call validates the list and builds its pointer table
+        # (~1 ms for 1000 tensors); r04 warmed 3 of the 4 and the 10-step loop paid the fourth's
+        # (packed_separate_grads "2.5 x the fixed view": tools/separate_grads_probe.py, 57 vs 58 us)
+        for i in range(max(3, 2 * rot)):
             fn(i % rot)
         torch.cuda.synchronize()
         dist.barrier()
@@ -1584,7 +1587,10 @@ def comparisons(job, w, line, last_words):
     # Opt-in (TIPS_BENCH_PEER=1): the IPC peer schedules have not crossed real GPUs yet, so the
     # driver's scaling runs do not start them (a fault there would cost the whole record).
     if os.environ.get("TIPS_BENCH_PEER") == "1":
-        run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"})])
+        run_variants([("peer", "peer", {}), ("peer_push", "peer", {"TIPS_PEER_AG": "push"}),
+                      # the fused pull-fold reduce-scatter: one kernel per rank reads its chunk's slices
+                      # from every peer's workspace over xGMI and folds them (peer.cc peer_piece_pullfold)
+                      ("peer_pullfold", "peer", {"TIPS_PEER_RS": "pullfold"})])
     elif job.world > 1:
         compare_check["peer"] = "opt-in: TIPS_BENCH_PEER=1 (not yet run across real GPUs)"
     # Opt-in (TIPS_BENCH_LANES=1): transfer lanes split communicators that live to the end of

@@ -88,6 +88,37 @@ def test_peer_schedule_all_dtypes(gpu, p, ag):
     check(run_job(p, cases, TIPS_PEER_AG=ag))
 
 
+@pytest.mark.parametrize("p", [2, 3, 4])
+def test_peer_pullfold_all_dtypes(gpu, p):
+    """TIPS_PEER_RS=pullfold: every rank stages its peers' chunks in its own workspace, then folds
+    its chunk in one kernel reading every peer's slice through the IPC mapping (peer.cc
+    peer_piece_pullfold). Same rank-order fold, so the same bits as the direct schedule."""
+    cases = []
+    for dtype in ALL_DTYPES:
+        for n in (1, 7, 4099, 1000003):
+            cases.append({"dtype": dtype, "n": n, "seed": 300 * dtype + n % 83})
+    cases.append({"dtype": F32, "n": 262147, "seed": 15, "inplace": True})
+    cases.append({"dtype": I64, "n": 4099, "seed": 16, "inplace": True})
+    check(run_job(p, cases, TIPS_PEER_RS="pullfold"))
+
+
+def test_peer_pullfold_pieces_goldens_and_mode_switch(gpu):
+    """The pull-fold through a 4 MiB workspace (64 MiB buckets in many pieces, in place too), a
+    count mismatch refused on every rank, every p = 4 golden vector (MPICH's outputs), and calls
+    alternating with the push schedule in the same job (TIPS_PEER_RS read per call)."""
+    p = 4
+    names = sorted(n for n, c in golden_cases().items() if c["p"] == p)
+    cases = [
+        {"dtype": F32, "n": 1 << 24, "seed": 2},
+        {"dtype": F32, "n": 5000, "seed": 3, "count_per_rank": [5000, 5000, 5000, 5001], "expect_error": ERR_MISMATCH},
+        {"dtype": I64, "n": 3 << 20, "seed": 4},
+        {"dtype": F32, "n": (1 << 24) + 3, "seed": 7, "inplace": True},
+        {"dtype": F32, "n": 1 << 20, "seed": 8, "env": {"TIPS_PEER_RS": "push"}},
+        {"dtype": F32, "n": 1 << 20, "seed": 9},
+    ] + [{"golden": n} for n in names]
+    check(run_job(p, cases, TIPS_PEER_WS_MIB="4", TIPS_PEER_RS="pullfold"))
+
+
 @pytest.mark.parametrize("ag", ["pull", "push"])
 def test_peer_schedule_pieces_and_mismatch(gpu, ag):
     """A 4 MiB workspace: the 64 MiB buckets go through in many pieces."""

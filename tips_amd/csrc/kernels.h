@@ -15,6 +15,10 @@ hipError_t launch_sum2(void* dst, const void* a, const void* b, int64_t n, int d
 // dst = rank-order fold of srcs[0..nsrc), nsrc <= kMaxSrcs.
 constexpr int kMaxSrcs = 16;
 hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t s);
+// The same fold when most sources are peers' memory read over xGMI (the peer schedule's pull-fold,
+// peer.cc): remote loads take microseconds, so every lane keeps 4 x 16 B per source in flight
+// (256 lanes, 16 KiB per source per workgroup, no occupancy cap). Same bits as launch_multi_sum.
+hipError_t launch_multi_sum_remote(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t s);
 
 // Batched byte copy for fusion pack/unpack: one workgroup per tile.
 struct CopyTile {

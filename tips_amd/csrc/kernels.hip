@@ -1286,8 +1286,21 @@ hipError_t run_multi_variant(void* dst, const SrcList& sl, int64_t n, int varian
 }
 #endif  // TIPS_DEV
 
+// the pull-fold's launch (launch_multi_sum_remote): 4 vectors per lane, 256 lanes, uncapped
+template <int DT, int NSRC>
+hipError_t run_multi_remote(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
+  const int64_t ve = 16 / (int64_t)dtype_size(DT);
+  const int64_t nvec = n / ve;
+  int64_t grid = (nvec + 4 * kBlock - 1) / (4 * kBlock);
+  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 4, 2>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst, sl,
+                     nvec, nvec * ve, n);
+  return hipGetLastError();
+}
+
 template <int DT>
-hipError_t multi_dispatch(void* dst, const void* const* srcs, int nsrc, int64_t n, hipStream_t s) {
+hipError_t multi_dispatch(void* dst, const void* const* srcs, int nsrc, int64_t n, hipStream_t s, bool remote = false) {
   SrcList sl{};
   bool al = aligned16(dst);
   for (int j = 0; j < nsrc; j++) {
@@ -1300,6 +1313,17 @@ hipError_t multi_dispatch(void* dst, const void* const* srcs, int nsrc, int64_t 
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((multi_sum_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, sl, nsrc, n);
     return hipGetLastError();
+  }
+  if (remote) {
+    switch (nsrc) {
+#define TIPS_REMOTE_CASE(K) \
+  case K: return run_multi_remote<DT, K>(dst, sl, n, s);
+      TIPS_REMOTE_CASE(2) TIPS_REMOTE_CASE(3) TIPS_REMOTE_CASE(4) TIPS_REMOTE_CASE(5) TIPS_REMOTE_CASE(6)
+      TIPS_REMOTE_CASE(7) TIPS_REMOTE_CASE(8) TIPS_REMOTE_CASE(9) TIPS_REMOTE_CASE(10) TIPS_REMOTE_CASE(11)
+      TIPS_REMOTE_CASE(12) TIPS_REMOTE_CASE(13) TIPS_REMOTE_CASE(14) TIPS_REMOTE_CASE(15) TIPS_REMOTE_CASE(16)
+#undef TIPS_REMOTE_CASE
+      default: return hipErrorInvalidValue;
+    }
   }
   switch (nsrc) {
     case 1: return run_multi<DT, 1>(dst, sl, n, s);
@@ -1356,6 +1380,21 @@ hipError_t launch_multi_sum(void* dst, const void* const* srcs, int nsrc, int64_
     case kI64: return multi_dispatch<kI64>(dst, srcs, nsrc, n, s);
     case kF16: return multi_dispatch<kF16>(dst, srcs, nsrc, n, s);
     case kBF16: return multi_dispatch<kBF16>(dst, srcs, nsrc, n, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_multi_sum_remote(void* dst, const void* const* srcs, int nsrc, int64_t n, int dtype, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (nsrc < 1 || nsrc > kMaxSrcs) return hipErrorInvalidValue;
+  if (nsrc == 1) return launch_multi_sum(dst, srcs, nsrc, n, dtype, s);
+  switch (dtype) {
+    case kF32: return multi_dispatch<kF32>(dst, srcs, nsrc, n, s, true);
+    case kF64: return multi_dispatch<kF64>(dst, srcs, nsrc, n, s, true);
+    case kI32: return multi_dispatch<kI32>(dst, srcs, nsrc, n, s, true);
+    case kI64: return multi_dispatch<kI64>(dst, srcs, nsrc, n, s, true);
+    case kF16: return multi_dispatch<kF16>(dst, srcs, nsrc, n, s, true);
+    case kBF16: return multi_dispatch<kBF16>(dst, srcs, nsrc, n, s, true);
     default: return hipErrorInvalidValue;
   }
 }

@@ -10,6 +10,9 @@
 //           all 7 xGMI links of an MI355X carry traffic together);
 //   reduce  multi_sum over in[chunk r] and the p-1 local slots -> red;
 //   pull    one xfer_kernel reads every peer's red (its reduced chunk) into out.
+// TIPS_PEER_RS=pullfold (opt-in) replaces push + reduce with a local stage of the peers' chunks and
+// one fold kernel per rank that reads its chunk's slices from every peer's workspace over xGMI
+// (peer_piece_pullfold).
 // Each rank's workspace {p-1 slots, red} is one uncached device allocation,
 // exported once with hipIpcGetMemHandle and opened by every peer. Uncached
 // memory keeps no line of it in any L2, so a peer's write is what the next
@@ -415,6 +418,53 @@ int peer_piece(State& st, PeerState& ps, const char* in, char* out, int64_t n, i
   return 0;
 }
 
+// One piece with the fused pull-fold reduce-scatter (TIPS_PEER_RS=pullfold, opt-in): every rank
+// stages the chunks its peers own in its own workspace (a local copy), barrier; then rank r folds
+// chunk r in ONE kernel that reads every peer's staged slice over its xGMI link plus its own input
+// slice, in rank order (launch_multi_sum_remote: the same bits as the direct schedule), and writes
+// red once; barrier; pull as above. The received slices are never written to this GPU's HBM and
+// re-read by a separate fold: the reduction consumes them as they arrive, with every link busy.
+// Workspace: chunk c of the staged piece at c x cap (cap = padded chunk), red after the p chunks.
+int peer_piece_pullfold(State& st, PeerState& ps, const char* in, char* out, int64_t n, int dtype, hipStream_t user) {
+  const int p = st.size, r = st.rank;
+  const int64_t es = tips::dtype_size(dtype), align = kAlignBytes / es;
+  const int64_t cap = round_up(chunk_of(n, p, align, 0).len() * es, kAlignBytes) + kPeerSlotPad;
+  const int64_t red_off = (int64_t)p * cap;
+  if (red_off + cap > ps.ws_bytes) return fail(TIPS_ERR_INVALID_ARG, "peer schedule: piece exceeds the workspace");
+  // stage: in[chunk c] -> my workspace at c x cap for every c != r (peers read it after the barrier;
+  // their reads of the previous piece ended before its kReduced barrier)
+  for (int c = 0; c < p; c++) {
+    if (c == r) continue;
+    const Range rc = chunk_of(n, p, align, c);
+    if (rc.len() > 0) HIP_TRY(tips::launch_copy_buf(ps.rdata[r] + (int64_t)c * cap, in + rc.b * es, rc.len() * es, user));
+  }
+  HIP_TRY(hipStreamSynchronize(user));  // also: our previous pull has read the peers' red
+  Post q{};
+  q.count = n;
+  q.dtype = dtype;
+  q.phase = kStaged;
+  TRY(barrier(st, ps, q, nullptr, peer_timeout()));
+  // pull-fold: chunk r from every rank, rank order, straight from the peers' workspaces
+  const Range mine = chunk_of(n, p, align, r);
+  const void* srcs[tips::kMaxSrcs];
+  for (int j = 0; j < p; j++) srcs[j] = (j == r) ? (const void*)(in + mine.b * es) : ps.rdata[j] + (int64_t)r * cap;
+  char* red = ps.rdata[r] + red_off;
+  HIP_TRY(tips::launch_multi_sum_remote(red, srcs, p, mine.len(), dtype, user));
+  HIP_TRY(hipStreamSynchronize(user));
+  q.phase = kReduced;
+  TRY(barrier(st, ps, q, nullptr, peer_timeout()));
+  // pull: every rank's reduced chunk -> out (as peer_piece)
+  tips::XferSeg segs[tips::kMaxXferSegs];
+  int m = 0;
+  for (int d = 0; d < p; d++) {
+    const int from = mod(r + d, p);
+    const Range c = chunk_of(n, p, align, from);
+    segs[m++] = {ps.rdata[from] + red_off, out + c.b * es, c.len() * es};
+  }
+  HIP_TRY(tips::launch_xfer(segs, m, user));
+  return 0;
+}
+
 int peer_allreduce_impl(State& st, PeerState& ps, const char* in, char* out, int64_t n, int dtype, hipStream_t user,
                         bool* clean) {
   TRY(attach(st, ps));
@@ -436,11 +486,15 @@ int peer_allreduce_impl(State& st, PeerState& ps, const char* in, char* out, int
                   j, (long long)all[j].count, all[j].dtype, r, (long long)n, dtype);  // every rank, same barrier
   *clean = false;  // from here on a failure leaves the ranks out of step
   TRY(setup_ws(st, ps));
-  // piece: the largest multiple of p 256-B-aligned chunks whose p slots fit the workspace
-  const int64_t per_chunk = (ps.ws_bytes / p - kPeerSlotPad) / kAlignBytes * kAlignBytes;
+  // TIPS_PEER_RS=pullfold: the fused pull-fold reduce-scatter (its pull allgather), else push + fold
+  const char* rsv = getenv("TIPS_PEER_RS");
+  const bool pullfold = rsv && !strcmp(rsv, "pullfold");
+  // piece: the largest multiple of p 256-B-aligned chunks whose slots fit the workspace (p slots;
+  // pull-fold: p staged chunks and red)
+  const int64_t per_chunk = (ps.ws_bytes / (pullfold ? p + 1 : p) - kPeerSlotPad) / kAlignBytes * kAlignBytes;
   const int64_t piece = per_chunk / es * p;
   const char* agv = getenv("TIPS_PEER_AG");
-  const bool ag_push = agv && !strcmp(agv, "push");
+  const bool ag_push = !pullfold && agv && !strcmp(agv, "push");
   for (int64_t b = 0; b < n; b += piece) {
     if (b > 0 && ag_push) {  // every rank's local copy out of its slots is done before new pushes land
       HIP_TRY(hipStreamSynchronize(user));
@@ -448,7 +502,10 @@ int peer_allreduce_impl(State& st, PeerState& ps, const char* in, char* out, int
       u.phase = kUnpacked;
       TRY(barrier(st, ps, u, nullptr, peer_timeout()));
     }
-    TRY(peer_piece(st, ps, in + b * es, out + b * es, std::min(piece, n - b), dtype, user, ag_push));
+    if (pullfold)
+      TRY(peer_piece_pullfold(st, ps, in + b * es, out + b * es, std::min(piece, n - b), dtype, user));
+    else
+      TRY(peer_piece(st, ps, in + b * es, out + b * es, std::min(piece, n - b), dtype, user, ag_push));
   }
   if (!ps.pulled) HIP_TRY(hipEventCreateWithFlags(&ps.pulled, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(ps.pulled, user));
