@@ -368,7 +368,8 @@ TIPS_API int tips_tuned_timings(int64_t bytes, int* algos, int* depths, int* lan
  * RCCL are ROCm >= 7.0 / RCCL >= 2.26 (torch's bundled runtime and /opt/rocm's 7.2 are both
  * tested); TIPS_GRAPHS=0 turns it off.
  * Reports this process's captures, replays and cached graphs.
- * Returns 0 (graphs on), 1 (a failed capture turned them off for the job), 2 (off: not asked
+ * A plan whose capture fails runs eagerly from then on; the others keep replaying.
+ * Returns 0 (graphs on), 1 (3 failed captures turned them off for the job), 2 (off: not asked
  * for, or an older runtime), < 0 on error. */
 TIPS_API int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached);
 /* The cost of keeping RCCL's order after replays: how many times an eager RCCL call (a larger

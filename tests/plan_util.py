@@ -333,26 +333,30 @@ def proxy_order(calls, host_wait="end"):
     return posted, device
 
 
-def replay_trace(rounds, sizes, cap=2 << 20, mixed_cap=1 << 30, note_on_wait=True):
+def replay_trace(rounds, sizes, cap=2 << 20, mixed_cap=1 << 30, note_on_wait=True, fail_bytes=0):
     """schedules.cc's replay bookkeeping over `rounds` rounds of calls on the same buffers, one per
     entry of `sizes` (bytes) in order: graph_eligible (bytes <= cap, or <= mixed_cap once a host wait
     has happened; mixed_cap = 0 keeps cap), plan_graph (a key's first eligible call only records it,
     its next is captured and replayed), run_plan's staging growth (a larger plan than any before drops
     every key) and order_after_replays (an eager call after a replay waits on the host; a wait that
-    widens the limit records the call's key as seen). Returns
+    widens the limit records the call's key as seen; fail_bytes > 0: the capture of a plan of at
+    least that many bytes fails, and that key alone runs eagerly from then on). Returns
     [(trace token, mode)] per call, tokens as tests/peer_worker.py graphs_case prints them ("w" a host
     wait, "r" a replay, "c" a capture, "-" none) and mode "replay" | "eager" for proxy_order."""
-    keys, staging, pending, mixed, out = {}, 0, False, False, []
+    keys, staging, pending, mixed, out, failed = {}, 0, False, False, [], set()
     for _ in range(rounds):
         for i, b in enumerate(sizes):
             if b > staging:
                 staging = b
                 keys.clear()
+                failed.clear()
             limit = max(cap, mixed_cap) if mixed else cap
             replay = captured = False
-            if b <= limit:
+            if b <= limit and i not in failed:
                 if i not in keys:
                     keys[i] = False
+                elif not keys[i] and fail_bytes and b >= fail_bytes:
+                    failed.add(i)  # the capture failed: eager now and from now on
                 else:
                     captured, keys[i] = not keys[i], True
                     replay = True

@@ -185,6 +185,28 @@ def test_mixed_buckets_become_replays(gpu, algo, p):
 
 
 @pytest.mark.parametrize("p", [2, 3])
+def test_capture_failure_after_mixing_drops_only_that_plan(gpu, p):
+    """once replayed and eager buckets mixed, the 12 MiB bucket's capture fails
+    (TIPS_GRAPH_TEST_FAIL_BYTES). Only that plan stays eager - it keeps paying its host wait after
+    the replays before it - while the small buckets keep replaying; graphs stay on and every
+    result is bit-exact."""
+    env = rccl_env("direct")
+    env.update(TIPS_GRAPHS="1", TIPS_GRAPH_MAX_BYTES=str(2 << 20), TIPS_GRAPH_TEST_FAIL_BYTES=str(4 << 20))
+    bufs = [[F32, 300007, False, False], [I64, 70001, True, False], [BF16, 4099, False, True],
+            [F32, (3 << 20) + 17, True, False]]
+    results = run_job(p, [{"bufs": bufs, "seed": 19, "rounds": 7, "trace": True}], timeout=600, **env)
+    check(results)
+    for res in results:
+        c = res["results"][0]
+        calls = c["trace"].split()
+        rounds = [calls[i:i + len(bufs)] for i in range(0, len(calls), len(bufs))]
+        assert len(rounds) == 7 and c["graphs_off"] == 0, c["trace"]
+        assert all(r[3] == "w" for r in rounds[2:]), c["trace"]  # the failed plan: eager after a replay
+        assert all(t == "r" for r in rounds[5:] for t in r[:3]), c["trace"]  # the others replay
+        assert c["replay_host_waits"] == 5, c["trace"]
+
+
+@pytest.mark.parametrize("p", [2, 3])
 def test_tuned_schedule_across_processes(gpu, p):
     """TIPS_ALGO=tune over real RCCL ranks: the first call of each size class times ring and
     direct at several pipeline depths on scratch copies, the ranks agree on one choice, and every

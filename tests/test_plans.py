@@ -325,6 +325,21 @@ def test_mixed_replays_model(mixed_cap, note):
         assert posted == device
 
 
+def test_capture_failure_model():
+    """A capture that fails (TIPS_GRAPH_TEST_FAIL_BYTES on the GPU, test_gpu_rccl_procs.py::
+    test_capture_failure_after_mixing_drops_only_that_plan) leaves that key eager - a host wait
+    after the replays before it, every round - and every other key replaying; RCCL's proxy still
+    sees device order."""
+    sizes = [300007 * 4, 70001 * 8, 4099 * 2, ((3 << 20) + 17) * 4]
+    tr = pu.replay_trace(7, sizes, fail_bytes=4 << 20)
+    tokens = [t for t, _ in tr]
+    rounds = [tokens[i:i + 4] for i in range(0, len(tokens), 4)]
+    assert all(r[3] == "w" for r in rounds[2:]) and tokens.count("w") == 5
+    assert all(t == "r" for r in rounds[3:] for t in r[:3])
+    posted, device = pu.proxy_order([(m, 3) for _, m in tr], "end")
+    assert posted == device
+
+
 @settings(max_examples=200, deadline=None)
 @given(sizes=hs.lists(hs.integers(1 << 10, 64 << 20), min_size=1, max_size=6),
        groups=hs.lists(hs.integers(1, 4), min_size=6, max_size=6), rounds=hs.integers(5, 8),

@@ -531,3 +531,42 @@ def test_flat_output_take_is_exclusive_across_threads():
     for t in th:
         t.join()
     assert not bad
+
+
+@pytest.mark.parametrize("warm", ["0", "1", "2"])
+def test_overlap_trial_with_any_warmup(monkeypatch, warm):
+    """TIPS_OVERLAP_TRIAL_WARMUP=0 made the last trial step read the end event of a step
+    that was never recorded (KeyError inside step() on every rank). The warm-up is clamped to 1;
+    the trial then runs to its choice. Events are faked on the CPU: 'during' steps take 5 ms,
+    'after' steps 7 ms, so the choice is 'during'."""
+    import torch
+    import tips_amd.ops
+    from tips_amd import basics
+    from tips_amd.optim import _OverlapChoice
+    monkeypatch.setenv("TIPS_OVERLAP_TRIAL_WARMUP", warm)
+    monkeypatch.setenv("TIPS_OVERLAP_TRIAL_STEPS", "2")
+    clock = [0.0]
+
+    class Ev(object):
+        def record(self, *a):
+            self.t = clock[0]
+
+        def synchronize(self):
+            pass
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+    monkeypatch.setattr(torch.cuda, "Event", lambda enable_timing=True: Ev())
+    monkeypatch.setattr(tips_amd.ops, "_allgather_i64", lambda v: list(v))
+    monkeypatch.setattr(basics, "size", lambda: 1)
+    oc = _OverlapChoice("auto")
+    assert oc.warm >= 1
+    s = 0
+    while oc.chosen is None:
+        clock[0] += 5.0 if oc.on(s) else 7.0
+        oc.stepped(s)
+        s += 1
+        assert s < 20
+    assert oc.chosen is True and oc.report["chosen"] == "during"
+    assert s == oc.warm + 4

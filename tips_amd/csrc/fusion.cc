@@ -549,6 +549,13 @@ int64_t fusion_threshold_bytes() {
 void fusion_release(State& st) {
   FusionCache* fc = st.fusion_cache;
   if (st.ev_fuse_chain) {
+    // a lazy chain end (tips_fused_pack_bucket) is not recorded here: its stream may be gone by
+    // shutdown; the device synchronize covers what it would have waited for
+    if (st.fuse_chain_valid && st.fuse_chain_lazy) {
+      (void)hipDeviceSynchronize();
+      st.fuse_chain_lazy = false;
+      st.fuse_chain_valid = false;
+    }
     if (st.fuse_chain_valid && chain_event(st) == 0) (void)hipEventSynchronize(st.ev_fuse_chain);
     (void)hipEventDestroy(st.ev_fuse_chain);
     st.ev_fuse_chain = nullptr;

@@ -598,12 +598,13 @@ class Negotiator {
     std::unique_lock<AdaptiveMutex> l(m_);
     // Wake the background thread only for the first request of a batch: it waits for that one up
     // to a cycle; after it, it lingers and sees later arrivals anyway. (A wake per request cost a
-    // futex call here and a context switch there for each of a 1000-tensor burst.)
-    const bool first = fresh_.empty();
+    // futex call here and a context switch there for each of a 1000-tensor burst.) "First" is read
+    // after commit(): commit() may drop the lock to create an event, and the thread may drain the
+    // queue meanwhile - a request that lands in an empty queue always wakes it.
     const int64_t h = commit(p, l, pr);
     if (h > 0) {
       last_arrival_ns_.store(steady_ns(), std::memory_order_release);
-      if (first) cv_.notify_all();
+      if (fresh_.size() == 1) cv_.notify_all();
     }
     return h;
   }

@@ -208,10 +208,12 @@ struct PlanGraphs {
   struct Ent {
     hipGraphExec_t exec = nullptr;  // null: seen once, runs eagerly
     uint64_t stamp = 0;
+    bool failed = false;  // its capture failed: this key runs eagerly from now on
   };
   std::map<Key, Ent> m;
   uint64_t clock = 0;
-  bool off = false;  // a capture failed: eager for the rest of the job
+  int failures = 0;  // captures that failed, on distinct keys
+  bool off = false;  // kMaxCaptureFailures captures failed: eager for the rest of the job
 };
 
 namespace {
@@ -303,7 +305,10 @@ int capture_plan(State& st, const Plan& pl, char* const* base, hipGraphExec_t* e
   return rc;
 }
 
-// The graph to replay for this call, or null: run eagerly (first call of a key, or graphs off).
+constexpr int kMaxCaptureFailures = 3;
+
+// The graph to replay for this call, or null: run eagerly (first call of a key, its capture
+// failed, or graphs off).
 // note_only: record a new key as seen, never capture.
 hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base, bool note_only = false) {
   if (!st.graphs) st.graphs = new PlanGraphs();
@@ -325,11 +330,22 @@ hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base, bool not
     return nullptr;
   }
   it->second.stamp = ++G.clock;
-  if (note_only) return nullptr;
+  if (note_only || it->second.failed) return nullptr;
   if (!it->second.exec) {
-    if (capture_plan(st, pl, base, &it->second.exec) != 0) {
-      if (getenv("TIPS_VERBOSE")) fprintf(stderr, "[tips] plan capture failed, eager from now on: %s\n", last_error().c_str());
-      G.off = true;
+    // (test hook: TIPS_GRAPH_TEST_FAIL_BYTES = a capture of a plan of at least that many bytes fails)
+    const int64_t fail_bytes = env_i64("TIPS_GRAPH_TEST_FAIL_BYTES", 0);
+    const int rc = fail_bytes > 0 && pl.n * tips::dtype_size(pl.dtype) >= fail_bytes
+                       ? fail(TIPS_ERR_HIP, "capture refused by TIPS_GRAPH_TEST_FAIL_BYTES")
+                       : capture_plan(st, pl, base, &it->second.exec);
+    if (rc != 0) {
+      // only this key runs eagerly from now on (one large plan's failure used to turn
+      // replays off for every plan of the job); repeated failures mean the runtime cannot capture
+      it->second.failed = true;
+      it->second.exec = nullptr;
+      if (++G.failures >= kMaxCaptureFailures) G.off = true;
+      if (getenv("TIPS_VERBOSE"))
+        fprintf(stderr, "[tips] plan capture failed (%d so far%s): %s\n", G.failures, G.off ? ", replays off" : "",
+                last_error().c_str());
       return nullptr;
     }
     st.graphs_captured++;

@@ -273,7 +273,8 @@ class _OverlapChoice(object):
     def __init__(self, mode):
         import os
         self.mode = mode if mode in ("0", "1", "auto") else "auto"
-        self.warm = max(0, int(os.environ.get("TIPS_OVERLAP_TRIAL_WARMUP", "2")))
+        # at least 1: a trial step is timed from the end event of the step before it
+        self.warm = max(1, int(os.environ.get("TIPS_OVERLAP_TRIAL_WARMUP", "2")))
         self.trials = max(1, int(os.environ.get("TIPS_OVERLAP_TRIAL_STEPS", "3")))
         self.chosen = {"0": False, "1": True}.get(self.mode)
         self.events = {}   # optimizer step -> event recorded at its end (trial window only)
