@@ -370,7 +370,9 @@ TIPS_API int tips_tuned_timings(int64_t bytes, int* algos, int* depths, int* lan
  * Reports this process's captures, replays and cached graphs.
  * A plan whose capture fails runs eagerly from then on; the others keep replaying.
  * Returns 0 (graphs on), 1 (3 failed captures turned them off for the job), 2 (off: not asked
- * for, or an older runtime), < 0 on error. */
+ * for, or an older runtime), 3 (replays yielded: one bucket shape kept arriving at new addresses
+ * after replays - TIPS_FRESH_WAIT_LIMIT host waits, 4 - so every plan now runs eagerly and no call
+ * waits on the host), < 0 on error. */
 TIPS_API int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached);
 /* The cost of keeping RCCL's order after replays: how many times an eager RCCL call (a larger
  * bucket, a fused call, a synchronous collective) found a replay still pending and blocked the

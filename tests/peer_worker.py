@@ -636,8 +636,19 @@ def graphs_case(c, rank, size, L, _lib, sp):
         bufs.append((x, x if inplace else torch.empty_like(x)))
     bad = []
     trace, trace_prev = [], [(0, 0, 0)]
+    fresh = set(c.get("fresh", []))  # buffers reallocated at a new address every round (old ones kept)
+    kept = []
+
+    def renew(i, fill=True):
+        dtype_, n_, inplace_, _ = specs[i]
+        kept.append(bufs[i])
+        x_ = to_dev(rand(dtype_, n_, np.random.default_rng(len(kept)))) if fill else torch.empty_like(bufs[i][0])
+        bufs[i] = (x_, x_ if inplace_ else torch.empty_like(x_))
+
     for rnd in range(c.get("rounds", 6)):
-        if rnd == 3:
+        for i in sorted(fresh):
+            renew(i)
+        if rnd == 3 and 0 not in fresh:
             dtype, n, inplace, _ = specs[0]
             del bufs[0]
             torch.cuda.synchronize()
@@ -692,6 +703,8 @@ def graphs_case(c, rank, size, L, _lib, sp):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(c["time_rounds"]):
+            for i in sorted(fresh):
+                renew(i, fill=False)
             for i, (dtype, n, inplace, second) in enumerate(specs):
                 x, y = bufs[i]
                 L.tips_allreduce(x.data_ptr(), y.data_ptr(), n, dtype, _lib.OP_SUM, sp)

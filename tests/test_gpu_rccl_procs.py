@@ -207,6 +207,26 @@ def test_capture_failure_after_mixing_drops_only_that_plan(gpu, p):
 
 
 @pytest.mark.parametrize("p", [2, 3])
+def test_fresh_address_bucket_makes_replays_yield(gpu, p):
+    """a replayed small bucket alternating with a large bucket at a NEW address
+    every round (the old ones kept alive, so no address repeats) can never become a replay: each of
+    its calls waits on the host for the replay before it. After TIPS_FRESH_WAIT_LIMIT (4) such waits
+    replays yield (tips_graph_stats 3): no further wait, every result bit-exact."""
+    env = rccl_env("direct")
+    env.update(TIPS_GRAPHS="1", TIPS_GRAPH_MAX_BYTES=str(2 << 20))
+    bufs = [[F32, 262147, False, False], [F32, (3 << 20) + 17, True, False]]
+    results = run_job(p, [{"bufs": bufs, "seed": 23, "rounds": 10, "trace": True, "fresh": [1]}], timeout=600, **env)
+    check(results)
+    for res in results:
+        c = res["results"][0]
+        calls = c["trace"].split()
+        rounds = [calls[i:i + len(bufs)] for i in range(0, len(calls), len(bufs))]
+        assert c["graphs_off"] == 3, c["trace"]
+        assert c["replay_host_waits"] == 4, c["trace"]
+        assert all(r == ["-", "-"] for r in rounds[-3:]), c["trace"]  # eager, no wait
+
+
+@pytest.mark.parametrize("p", [2, 3])
 def test_tuned_schedule_across_processes(gpu, p):
     """TIPS_ALGO=tune over real RCCL ranks: the first call of each size class times ring and
     direct at several pipeline depths on scratch copies, the ranks agree on one choice, and every

@@ -241,6 +241,11 @@ struct State {
   int64_t replay_host_waits = 0, replay_host_wait_ns = 0;
   // an eager plan followed a replay: larger plans become replayable too (graph_eligible)
   bool replays_mixed = false;
+  // host waits of eager plans whose graph key was new (a bucket at an address never seen before),
+  // per plan shape (algo, K, dtype, count); at kFreshWaitLimit for one shape, replays yield: every
+  // plan runs eagerly, so no eager call waits on the host again (schedules.cc run_plan)
+  std::map<std::tuple<int, int, int, int64_t>, int> fresh_waits;
+  bool replays_yield = false;
 };
 
 State& S();

@@ -259,7 +259,7 @@ bool graphs_supported() {
 }
 
 bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
-  if (st.graphs && st.graphs->off) return false;
+  if ((st.graphs && st.graphs->off) || st.replays_yield) return false;
   const int64_t want = env_i64("TIPS_GRAPHS", 1);
   if (want <= 0 || (want == 1 && !graphs_supported())) return false;
   int64_t cap = env_i64("TIPS_GRAPH_MAX_BYTES", 8 << 20);
@@ -306,17 +306,21 @@ int capture_plan(State& st, const Plan& pl, char* const* base, hipGraphExec_t* e
 }
 
 constexpr int kMaxCaptureFailures = 3;
+// host waits of one plan shape at new addresses before replays yield (TIPS_FRESH_WAIT_LIMIT, 4)
+int fresh_wait_limit() { return (int)std::max<int64_t>(1, env_i64("TIPS_FRESH_WAIT_LIMIT", 4)); }
 
 // The graph to replay for this call, or null: run eagerly (first call of a key, its capture
 // failed, or graphs off).
 // note_only: record a new key as seen, never capture.
-hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base, bool note_only = false) {
+hipGraphExec_t plan_graph(State& st, const Plan& pl, char* const* base, bool note_only = false,
+                          bool* key_new = nullptr) {
   if (!st.graphs) st.graphs = new PlanGraphs();
   PlanGraphs& G = *st.graphs;
   const unsigned long long in_id = allocation_id(base[kBufIn]), out_id = allocation_id(base[kBufOut]);
   if (!in_id || !out_id) return nullptr;
   const PlanGraphs::Key k{pl.algo, pl.K, pl.dtype, pl.n, base[kBufIn], base[kBufOut], base[kBufStaging], in_id, out_id};
   auto it = G.m.find(k);
+  if (key_new) *key_new = it == G.m.end();
   if (it == G.m.end()) {
     const size_t cap = (size_t)std::max<int64_t>(1, env_i64("TIPS_GRAPH_CACHE", 64));
     while (G.m.size() >= cap) {  // least recently used out
@@ -405,15 +409,29 @@ int run_plan(State& st, const Plan& pl, const char* in, char* out, hipStream_t u
   TRY(st.sum_ev.ensure(nsteps));
   char* base[3] = {(char*)in, out, (char*)st.staging.p};
   const bool eligible = L == 1 && graph_eligible(st, pl, user);
+  bool key_new = false;
   if (eligible) {
-    hipGraphExec_t exec = plan_graph(st, pl, base);
+    hipGraphExec_t exec = plan_graph(st, pl, base, false, &key_new);
     if (exec) return replay(st, exec, user);
   }
   if (L > 1) TRY(lanes_ensure(st, L));
+  const int64_t waits_before = st.replay_host_waits;
   TRY(prologue(st, user, L));
   // this call's host wait may just have widened the replay limit (replays_mixed): its key counts as
   // seen, so its next call is captured instead of waiting once more
-  if (L == 1 && !eligible && graph_eligible(st, pl, user)) (void)plan_graph(st, pl, base, true);
+  if (L == 1 && !eligible && graph_eligible(st, pl, user)) (void)plan_graph(st, pl, base, true, &key_new);
+  // A bucket that waits for a replay at an address never seen before cannot become a replay by
+  // its next call. One shape doing that again and again (a buffer reallocated at a new address every
+  // step) would wait on every call, and each wait stalls the host until the device has run the
+  // replay: the host can no longer queue ahead. Then replays yield - every plan eager, no waits
+  // (tips_graph_stats returns 3).
+  if (st.replay_host_waits > waits_before && key_new &&
+      ++st.fresh_waits[std::make_tuple(pl.algo, pl.K, pl.dtype, pl.n)] >= fresh_wait_limit()) {
+    if (!st.replays_yield && getenv("TIPS_VERBOSE"))
+      fprintf(stderr, "[tips] replays yield: a %lld-element bucket waited %d times at new addresses\n",
+              (long long)pl.n, fresh_wait_limit());
+    st.replays_yield = true;
+  }
   TRY(issue_steps(st, pl, base, L));
   return epilogue(st, user, L);
 }
@@ -644,6 +662,8 @@ void graphs_release(State& st) {
   st.graphs_captured = st.graphs_replayed = 0;
   st.replay_host_waits = st.replay_host_wait_ns = 0;
   st.replays_mixed = false;
+  st.fresh_waits.clear();
+  st.replays_yield = false;
 }
 
 #ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)
@@ -868,7 +888,8 @@ int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached) {
     for (const auto& kv : st.graphs->m) *cached += kv.second.exec != nullptr;
   if (st.graphs && st.graphs->off) return 1;
   const int64_t want = env_i64("TIPS_GRAPHS", 1);
-  return (want <= 0 || (want == 1 && !graphs_supported())) ? 2 : 0;
+  if (want <= 0 || (want == 1 && !graphs_supported())) return 2;
+  return st.replays_yield ? 3 : 0;
 }
 
 int tips_replay_order_stats(int64_t* host_waits, int64_t* host_wait_ns) {

@@ -19,7 +19,29 @@ from test_gpu_peer import run_job  # noqa: E402
 from test_gpu_rccl_procs import rccl_env  # noqa: E402
 
 
+def fresh_main():
+    """a 1 MiB bucket (replayed) alternating with a 32 MiB bucket at a new address
+    every round. Modes: "yield" (default: replays yield after 4 waits at new addresses), "wait"
+    (TIPS_FRESH_WAIT_LIMIT huge: round 4's behaviour, a host wait every round) and "off"."""
+    f32 = 0
+    bufs = [[f32, 1 << 18, True, False], [f32, 1 << 23, True, False]]
+    modes = {"yield": {}, "wait": {"TIPS_FRESH_WAIT_LIMIT": "1000000000"}, "off": {"TIPS_GRAPHS": "0"}}
+    for p in (2, 3):
+        for mode, extra in modes.items():
+            env = dict(rccl_env("direct"), TIPS_GRAPH_MAX_BYTES=str(8 << 20), **extra)
+            res = run_job(p, [{"bufs": bufs, "seed": 5, "rounds": 6, "time_rounds": 30, "fresh": [1]}], timeout=240,
+                          **env)
+            r = [x["results"][0] for x in res]
+            print(json.dumps({"case": "fresh_32MiB", "ranks": p, "mode": mode, "ok": all(x["ok"] for x in r),
+                              "round_ms": max(x["round_ms"] for x in r),
+                              "waits_per_round": max(x["waits_per_round"] for x in r),
+                              "wait_ms_per_round": max(x["wait_ms_per_round"] for x in r),
+                              "graphs_state": [x["graphs_off"] for x in r]}), flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "fresh":
+        return fresh_main()
     f32 = 0
     bufs = [[f32, 1 << 18, True, False], [f32, 1 << 22, True, False], [f32, 1 << 18, False, False],
             [f32, 1 << 23, False, False]]
