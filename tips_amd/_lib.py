@@ -111,6 +111,9 @@ _SIGNATURES = [
       _c_i64_p]),
     ("tips_wait_n", ctypes.c_int, [_c_i64_p, ctypes.c_int]),
     ("tips_on_done", ctypes.c_int, [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tips_enqueue_allreduce_cb", ctypes.c_int64,
+     [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_void_p]),
     ("tips_net_stats", ctypes.c_int, [_c_i64_p, _c_i64_p]),
     ("tips_debug_state", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
     ("tips_wait", ctypes.c_int, [ctypes.c_int64]),

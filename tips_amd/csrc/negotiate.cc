@@ -591,11 +591,16 @@ class Negotiator {
   int64_t enqueue(const std::string& name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
                   hipStream_t s, int type = TIPS_REQ_ALLREDUCE, int root = 0, tips_alloc_fn alloc = nullptr,
                   void* actx = nullptr, int64_t* out_rows = nullptr, std::function<int()> body = nullptr,
-                  PtrRanges* pr = nullptr) {
+                  PtrRanges* pr = nullptr, tips_done_fn cb = nullptr, void* cb_ctx = nullptr) {
     Prepared p;
     TRY(prepare(p, name, in, out, shape, ndim, dtype, s, type, root, alloc, actx, out_rows, std::move(body), pr));
+    if (cb) {  // tips_enqueue_allreduce_cb: the callback travels with the request (one lock, as OpRecord)
+      p.r->cb = cb;
+      p.r->cb_ctx = cb_ctx;
+    }
     // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
     std::unique_lock<AdaptiveMutex> l(m_);
+    if (cb && !waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
     // Wake the background thread only for the first request of a batch: it waits for that one up
     // to a cycle; after it, it lingers and sees later arrivals anyway. (A wake per request cost a
     // futex call here and a context switch there for each of a 1000-tensor burst.) "First" is read
@@ -1481,6 +1486,17 @@ int tips_wait(int64_t handle) {
   if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
   const int rc = n->poll(handle, true);
   return rc == 1 ? 0 : rc;
+}
+
+int64_t tips_enqueue_allreduce_cb(const char* name, const void* in, void* out, const int64_t* shape, int ndim, int dtype,
+                                  void* stream, tips_done_fn fn, void* ctx) {
+  if (!fn) return fail(TIPS_ERR_INVALID_ARG, "null completion callback");
+  TRY(check_named(name, in, out, shape, ndim, dtype, TIPS_REQ_ALLREDUCE, 0, nullptr));
+  int code = TIPS_ERR_NOT_INITIALIZED;
+  std::shared_ptr<Negotiator> n = negotiator(&code);
+  if (!n) return code;
+  return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, TIPS_REQ_ALLREDUCE, 0, nullptr, nullptr,
+                    nullptr, nullptr, nullptr, fn, ctx);
 }
 
 int tips_on_done(int64_t handle, tips_done_fn fn, void* ctx) {

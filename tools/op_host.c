@@ -150,6 +150,7 @@ static void on_done(void* ctx, int status, const char* message) {
 
 /* the executor threads: persistent, released once per step (a barrier), each enqueues its share */
 static pthread_barrier_t g_go;
+static int g_one_call = 1; /* OP_HOST_ONE_CALL */
 static atomic_int g_quit;
 
 static void* executor(void* arg) {
@@ -164,9 +165,17 @@ static void* executor(void* arg) {
       if (i % g_threads != t) continue;
       Grad* g = &g_g[i];
       const double a = now();
-      const int64_t h = tips_enqueue_allreduce_shaped(g->name, g->in, g->out, g->dims, g->ndim, TIPS_FLOAT32, NULL);
-      const double b = now();
-      const int rc = h < 0 ? TIPS_OK : tips_on_done(h, on_done, g);
+      int64_t h;
+      double b;
+      int rc = TIPS_OK;
+      if (g_one_call) { /* the request and its callback in one call (tips_enqueue_allreduce_cb) */
+        h = tips_enqueue_allreduce_cb(g->name, g->in, g->out, g->dims, g->ndim, TIPS_FLOAT32, NULL, on_done, g);
+        b = now();
+      } else { /* OP_HOST_ONE_CALL=0: enqueue, then register the callback (round 4's op body) */
+        h = tips_enqueue_allreduce_shaped(g->name, g->in, g->out, g->dims, g->ndim, TIPS_FLOAT32, NULL);
+        b = now();
+        rc = h < 0 ? TIPS_OK : tips_on_done(h, on_done, g);
+      }
       t_enq += b - a;
       t_reg += now() - b;
       if (h < 0 || rc != TIPS_OK) {
@@ -222,6 +231,7 @@ int main(void) {
   const int steps = env_int("OP_HOST_STEPS", 20), warmup = env_int("OP_HOST_WARMUP", 3);
   g_threads = env_int("OP_HOST_THREADS", 4);
   g_trace = env_int("OP_HOST_TRACE", 0);
+  g_one_call = env_int("OP_HOST_ONE_CALL", 1);
   if (g_threads < 1 || g_threads > MAX_THREADS || steps < 1) return 2;
   resnet50();
   tips_init();

@@ -1,24 +1,29 @@
 #!/bin/bash
-# A/B of the named-request enqueue on one box (tools/op_host.c: config 5 as 214 named host requests):
-# variants interleaved over 3 rounds, at 1 and 4 executor threads -
-#   enqueue:  pointers classified in the enqueue, plain mutexes (round 3)
-#   deferred: classified by the negotiation thread, plain mutexes
-#   adaptive: classified by the negotiation thread, adaptive mutexes (shipped)
-# then one traced run of the shipped variant. Results in gpurun_out/$TAG/.
+# A/B of the TF-op-shaped host path on one box (tools/op_host.c: config 5 as 214 named host requests
+# from 4 executor threads), variants interleaved over 3 rounds:
+#   one_call: tips_enqueue_allreduce_cb (request + callback in one call; shipped op body, round 5)
+#   two_call: tips_enqueue_allreduce_shaped + tips_on_done (round 4's op body)
+# beside the single fused host call the ratio is taken against (tools/host_fused_once.py, the
+# body of bench.py's host_to_host_fused), then one traced run of each. Results in gpurun_out/$TAG/.
 set -e
 OUT=gpurun_out/${TAG:-opsweep}
 mkdir -p "$OUT"
-run() {  # label threads env...
-  local label=$1 t=$2
-  shift 2
-  printf '%s threads %s ' "$label" "$t" >> "$OUT/sweep.txt"
-  env "$@" OP_HOST_THREADS=$t OP_HOST_STEPS=15 timeout -k 5 60 tools/_bin/op_host >> "$OUT/sweep.txt" 2>&1
+export MASTER_ADDR=127.0.0.1
+run() {  # label env...
+  local label=$1
+  shift 1
+  printf '%s ' "$label" >> "$OUT/sweep.txt"
+  env "$@" MASTER_PORT=$((29600 + RANDOM % 200)) OP_HOST_THREADS=4 OP_HOST_STEPS=20 timeout -k 5 60 tools/_bin/op_host \
+    >> "$OUT/sweep.txt" 2>&1
 }
 for round in 1 2 3; do
-  for t in 1 4; do
-    run enqueue $t TIPS_CLASSIFY_AT_ENQUEUE=1 TIPS_ADAPTIVE_LOCKS=0
-    run deferred $t TIPS_CLASSIFY_AT_ENQUEUE=0 TIPS_ADAPTIVE_LOCKS=0
-    run adaptive $t TIPS_CLASSIFY_AT_ENQUEUE=0 TIPS_ADAPTIVE_LOCKS=1
-  done
+  run one_call OP_HOST_ONE_CALL=1
+  run two_call OP_HOST_ONE_CALL=0
+  printf 'host_fused ' >> "$OUT/sweep.txt"
+  timeout -k 5 120 python3 tools/host_fused_once.py 15 2>/dev/null | tail -15 | tr '\n' ' ' >> "$OUT/sweep.txt"
+  echo >> "$OUT/sweep.txt"
 done
-OP_HOST_TRACE=1 OP_HOST_THREADS=4 OP_HOST_STEPS=4 timeout -k 5 60 tools/_bin/op_host > "$OUT/trace_4.txt" 2>&1
+for v in 1 0; do
+  OP_HOST_ONE_CALL=$v OP_HOST_TRACE=1 TIPS_NEG_TRACE=1 MASTER_PORT=$((29800 + v)) OP_HOST_THREADS=4 OP_HOST_STEPS=6 \
+    timeout -k 5 60 tools/_bin/op_host > "$OUT/trace_one_call_$v.txt" 2>&1
+done
