@@ -1369,7 +1369,7 @@ def host_legs(job, w, line):
 def op_host_leg(steps=20, warmup=3):
     """Config 5 as the reference's TF op sees it, at one rank: tools/_bin/op_host (a plain-C host on
     the product library alone) issues the 214 gradients as named HOST requests,
-    tips_enqueue_allreduce_shaped + tips_on_done, from four executor threads per step, as TF's
+    tips_enqueue_allreduce_cb (request + callback), from four executor threads per step, as TF's
     executor runs MPIAllreduce's ComputeAsync (ops.cc:86-118, coordinator.cc:223-241). A child
     process (its own tips_init at one rank); median step of `steps`."""
     import socket
@@ -1393,8 +1393,9 @@ def op_host_leg(steps=20, warmup=3):
     d["statistic"] = "median step of %d (each step: 214 enqueues from %d threads, then every callback)" % (
         steps, d.get("threads", 4))
     d["note"] = ("tools/op_host.c: 214 named host requests per step (pageable TF-style host tensors, outputs "
-                 "reused), tips_enqueue_allreduce_shaped + tips_on_done from executor threads; the negotiation "
-                 "fuses each cycle's host requests into one tips_fused_allreduce_host call")
+                 "reused), each one tips_enqueue_allreduce_cb (the request with its completion callback, as the "
+                 "reference's OpRecord) from executor threads; the negotiation fuses each cycle's host requests "
+                 "into one tips_fused_allreduce_host call")
     return d
 
 # ----------------------------------------------------------------------------- the north star's ring (N > 1, mandatory)

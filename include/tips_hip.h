@@ -208,10 +208,11 @@ TIPS_API int tips_host_unregister(void* ptr);
  * Graph capture: a fused call made under stream capture must find its pointer table
  * built (the same call made once before the capture) and stays out of the chain. The
  * table it used is then kept for the life of the job - never refilled, reused or freed
- * - and changing TIPS_FUSION_THRESHOLD afterwards fails (the replays pack into the
- * current slots). The replays share those slots with eager fused calls: order a replay
- * with fused calls on other streams yourself (launch it on the same stream, or join
- * the streams), as for any graph that uses a shared workspace. */
+ * - and so are the fusion slots it packs into, past a change of TIPS_FUSION_THRESHOLD
+ * (new slots are allocated beside them; all are freed at tips_shutdown). The replays
+ * share those slots with eager fused calls: order a replay with fused calls on other
+ * streams yourself (launch it on the same stream, or join the streams), as for any
+ * graph that uses a shared workspace. */
 TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dtype, void* stream);
 /* The same, out of place: outs[i] = SUM over ranks of ins[i] (ins[i] == outs[i]
  * allowed); the inputs are left unchanged. What the reference's per-gradient

@@ -73,7 +73,8 @@ struct Table {  // resolved segment records of one pointer set
   CopySeg* dev = nullptr;      // kSlot: [pack | unpack], else one table; nseg records each
   uint64_t stamp = 0;
   // a call captured into a graph read this table: a replay may read it at any later time, so it is
-  // never refilled, reused or freed (until tips_shutdown), and its layout is never evicted
+  // never refilled, reused or freed (until tips_shutdown), its layout is never evicted, and the
+  // slots it packs into outlive a threshold change (State::fusion_retired)
   bool pinned = false;
 };
 
@@ -450,22 +451,28 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
 // after the fusion streams have finished with them.
 int ensure_slots(State& st, FusionCache& fc, int64_t threshold) {
   if (threshold == st.fusion_threshold && st.fusion.p) return 0;
-  for (const Layout* L : fc.layouts)  // a captured graph's replays pack into the current slots
-    if (L->pinned() && st.fusion.p)
-      return fail(TIPS_ERR_INVALID_ARG, "fusion: the fusion threshold changed (%lld -> %lld bytes) while a graph "
-                  "captured around a fused call may still replay into the fusion slots",
-                  (long long)st.fusion_threshold, (long long)threshold);
+  bool pinned = false;  // a captured graph's replays pack into the current slots: they must stay
+  for (const Layout* L : fc.layouts) pinned = pinned || L->pinned();
   if (st.fuse_chain_valid) {
     TRY(chain_event(st));
     HIP_TRY(hipEventSynchronize(st.ev_fuse_chain));
   }
   HIP_TRY(hipStreamSynchronize(st.fuse_stream));
   HIP_TRY(hipStreamSynchronize(st.bucket_stream));
-  for (Layout* L : fc.layouts) {
-    for (Table* t : L->tables) free_table(st, t);
-    L->tables.clear();
+  for (Layout* L : fc.layouts) {  // pinned tables keep the old slots' addresses and stay valid
+    std::vector<Table*> keep;
+    for (Table* t : L->tables) {
+      if (t->pinned) keep.push_back(t);
+      else free_table(st, t);
+    }
+    L->tables.swap(keep);
   }
   HIP_TRY(hipStreamSynchronize(st.fuse_stream));
+  if (pinned && st.fusion.p) {  // retired, not freed: freed at tips_shutdown (fusion_release)
+    st.fusion_retired.push_back(st.fusion.p);
+    st.fusion.p = nullptr;
+    st.fusion.bytes = 0;
+  }
   st.fusion.release();
   TRY(st.fusion.ensure((size_t)(2 * threshold), /*zero=*/true));
   st.fusion_threshold = threshold;
@@ -564,6 +571,8 @@ void fusion_release(State& st) {
   if (!fc) return;
   for (Layout* L : fc->layouts) free_layout(st, L);
   if (st.fuse_stream) (void)hipStreamSynchronize(st.fuse_stream);
+  for (void* q : st.fusion_retired) (void)hipFree(q);
+  st.fusion_retired.clear();
   for (auto& u : fc->up) {
     if (u.done) (void)hipEventSynchronize(u.done), (void)hipEventDestroy(u.done);
     if (u.host) (void)hipHostFree(u.host);

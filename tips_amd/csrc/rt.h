@@ -205,6 +205,7 @@ struct State {
   bool fuse_capturing = false;   // the call in progress is being captured into a graph (no chain)
   bool fuse_in_call = false;     // fuse_ws is set (it may be the legacy null stream, i.e. nullptr)
   int64_t fusion_threshold = 0;  // the fusion slots' size (2 slots of it in `fusion`)
+  std::vector<void*> fusion_retired;  // earlier slots a captured graph may still pack into (freed at shutdown)
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr, ev_comp_prev = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
