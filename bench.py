@@ -1281,10 +1281,10 @@ class Workload(object):
                         "(Infinity Cache assisted: in the schedule a freshly received slot may be on-die too)"}
         if nsrc > 2:  # HBM bytes from the committed PMC passes over the fold (8 x 32 MiB, rotating sets)
             try:
-                with open(os.path.join(REPO, "profiles", "r02", "pmc_multi_sum.json")) as f:
+                with open(os.path.join(REPO, "profiles", "r05", "pmc_multi_sum.json")) as f:
                     k = next(iter(json.load(f)["kernels"].values()))
                 roof["traffic_over_algorithmic_pmc"] = round(k["traffic_over_algorithmic"], 5)
-                roof["traffic_source"] = "profiles/r02/pmc_multi_sum.json (8 x 32 MiB sources)"
+                roof["traffic_source"] = "profiles/r05/pmc_multi_sum.json (8 x 32 MiB sources, the round-5 fold)"
             except Exception:  # noqa: BLE001
                 pass
         del bufs, srcs, dst
