@@ -23,6 +23,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <pthread.h>
+#include <sys/prctl.h>
 #include <deque>
 #include <memory>
 #include <thread>
@@ -111,6 +112,9 @@ struct Req {
   bool classify = false;
   std::string bad;
 };
+
+// Request handles, process-wide (per-thread blocks of 256: Negotiator::prepare)
+std::atomic<int64_t> g_next_handle{0};
 
 // The negotiation thread itself: a collective entry point called there runs directly (it is the
 // body of a routed request, or the executor's own call), never routed again.
@@ -474,7 +478,9 @@ class Negotiator {
         }
       }
     }
+    lockfree_ = env_i64("TIPS_ENQUEUE_LOCKFREE", 1) != 0;
     running_ = true;
+    accepting_.store(true, std::memory_order_release);
     thread_ = std::thread([this] {
       tl_negotiation_thread = true;
       loop();
@@ -544,7 +550,15 @@ class Negotiator {
         r->classify = true;
       }
     }
-    r->handle = next_handle_.fetch_add(1) + 1;
+    {  // handles in per-thread blocks of a process-wide counter: unique across negotiators, and one
+       // contended increment per 256 requests instead of one per request
+      thread_local int64_t tl_next = 0, tl_end = 0;
+      if (tl_next == tl_end) {
+        tl_next = g_next_handle.fetch_add(256) + 1;
+        tl_end = tl_next + 256;
+      }
+      r->handle = tl_next++;
+    }
     thread_local NameMap name_scratch;
     thread_local HandleMap handle_scratch;
     name_scratch.emplace(name, r);
@@ -599,19 +613,91 @@ class Negotiator {
       p.r->cb_ctx = cb_ctx;
     }
     // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
-    std::unique_lock<AdaptiveMutex> l(m_);
-    if (cb && !waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
-    // Wake the background thread only for the first request of a batch: it waits for that one up
-    // to a cycle; after it, it lingers and sees later arrivals anyway. (A wake per request cost a
-    // futex call here and a context switch there for each of a 1000-tensor burst.) "First" is read
-    // after commit(): commit() may drop the lock to create an event, and the thread may drain the
-    // queue meanwhile - a request that lands in an empty queue always wakes it.
-    const int64_t h = commit(p, l, pr);
-    if (h > 0) {
-      last_arrival_ns_.store(steady_ns(), std::memory_order_release);
-      if (fresh_.size() == 1) cv_.notify_all();
+    if (cb && !waiter_started_.load(std::memory_order_acquire)) {
+      std::lock_guard<AdaptiveMutex> l(m_);
+      if (!waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
+      waiter_started_.store(true, std::memory_order_release);
+    }
+    if (!lockfree_) {  // (TIPS_ENQUEUE_LOCKFREE=0: round 4's locked commit, for A/B runs only)
+      std::unique_lock<AdaptiveMutex> l(m_);
+      drain_locked();
+      const int64_t h = commit(p, l, pr);
+      if (h > 0) {
+        last_arrival_ns_.store(steady_ns(), std::memory_order_release);
+        if (fresh_.size() == 1) cv_.notify_all();
+      }
+      return h;
+    }
+    if (!accepting_.load(std::memory_order_acquire))
+      return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
+    const int64_t h = p.r->handle;
+    Pending* node = new Pending{std::move(p), nullptr};
+    Pending* old = pending_.load(std::memory_order_relaxed);
+    do {
+      node->next = old;
+    } while (!pending_.compare_exchange_weak(old, node, std::memory_order_seq_cst, std::memory_order_relaxed));
+    // the linger's quiet time, to a few microseconds (a store per request would bounce the line)
+    const int64_t now = steady_ns();
+    if (now - last_arrival_ns_.load(std::memory_order_relaxed) > 2000)
+      last_arrival_ns_.store(now, std::memory_order_release);
+    // Wake the background thread only while it waits idle for a cycle's first request (idle_):
+    // lingering, it sees later arrivals anyway, and a wake there would cut its linger window short
+    // and make this thread wait for m_. The push and the flag are sequentially consistent and the
+    // thread sets the flag before it checks the stack, so a wake cannot be lost; under m_, so it
+    // cannot fall between that check and the wait.
+    if (!old && idle_.load(std::memory_order_seq_cst)) {
+      std::lock_guard<AdaptiveMutex> l(m_);
+      cv_.notify_all();
     }
     return h;
+  }
+
+  // (m_ held) Admit the lock-free stack's requests to the tables, oldest first, as commit() does
+  // for a list; a request that cannot be admitted (a duplicate name, the thread stopped) fails
+  // through its handle or callback instead of at its enqueue.
+  void drain_locked() {
+    Pending* h = pending_.exchange(nullptr, std::memory_order_acquire);
+    if (!h) return;
+    Pending* fifo = nullptr;
+    while (h) {
+      Pending* n = h->next;
+      h->next = fifo;
+      fifo = h;
+      h = n;
+    }
+    while (fifo) {
+      Pending* n = fifo->next;
+      Prepared& p = fifo->p;
+      Req& r = *p.r;
+      std::string why;
+      if (p.need_ev && !ev_pool_.empty()) {
+        r.ev = ev_pool_.back();
+        ev_pool_.pop_back();
+      } else if (p.need_ev) {
+        const int rc = set_device(S());
+        if (rc != 0 || hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
+          r.ev = nullptr;
+          why = "hipEventCreateWithFlags failed";
+        }
+      }
+      if (why.empty() && !running_) why = "negotiation thread is not running";
+      if (why.empty() && !by_name_.insert(std::move(p.name_node)).inserted)
+        why = "a request named " + r.name + " is already pending";
+      by_handle_.insert(std::move(p.handle_node));
+      if (why.empty()) {
+        fresh_.push_back(p.r);
+      } else {
+        if (r.ev) ev_pool_.push_back(r.ev);
+        r.ev = nullptr;
+        r.state = -1;
+        r.code = running_ ? TIPS_ERR_INVALID_ARG : TIPS_ERR_NOT_INITIALIZED;
+        r.err = why;
+        if (r.cb) queue_done(p.r);
+        cv_.notify_all();
+      }
+      delete fifo;
+      fifo = n;
+    }
   }
 
   // A list (tips_enqueue_*_n): every request prepared before the lock, all of them committed under
@@ -621,6 +707,7 @@ class Negotiator {
   int enqueue_list(std::vector<Prepared>& ps, int64_t* handles, PtrRanges* pr, std::string* first_err) {
     int rc = 0;
     std::unique_lock<AdaptiveMutex> l(m_);
+    drain_locked();  // (earlier single enqueues first)
     bool any = false;
     for (size_t i = 0; i < ps.size(); i++) {
       if (!ps[i].r) continue;
@@ -645,6 +732,7 @@ class Negotiator {
     std::shared_ptr<Req> r;
     {
       std::unique_lock<AdaptiveMutex> l(m_);
+      drain_locked();
       auto it = by_handle_.find(h);
       if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
       r = it->second;
@@ -679,6 +767,7 @@ class Negotiator {
   // released then. A request that has already finished is queued at once.
   int on_done(int64_t h, tips_done_fn fn, void* ctx) {
     std::lock_guard<AdaptiveMutex> l(m_);
+    drain_locked();
     auto it = by_handle_.find(h);
     if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
     auto& r = it->second;
@@ -686,6 +775,7 @@ class Negotiator {
     r->cb = fn;
     r->cb_ctx = ctx;
     if (!waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
+    waiter_started_.store(true, std::memory_order_release);
     if (r->state >= 2 || r->state < 0) queue_done(r);
     return 0;
   }
@@ -701,6 +791,8 @@ class Negotiator {
     if (thread_.joinable()) thread_.join();
     {  // the completion thread drains what is queued (the loop failed every unmatched request), then ends
       std::lock_guard<AdaptiveMutex> l(m_);
+      accepting_.store(false, std::memory_order_release);
+      drain_locked();  // enqueued during the stop: failed (not running)
       waiter_stop_ = true;
       done_cv_.notify_all();
     }
@@ -717,6 +809,11 @@ class Negotiator {
   }
 
   ~Negotiator() {
+    for (Pending* q = pending_.exchange(nullptr); q;) {  // (never admitted)
+      Pending* n = q->next;
+      delete q;
+      q = n;
+    }
     for (auto& kv : by_handle_)  // never polled to completion
       if (kv.second->ev) ev_pool_.push_back(kv.second->ev);
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
@@ -739,8 +836,16 @@ class Negotiator {
 
  private:
   void loop() {
+    // The linger's timed waits end within a microsecond or two of their deadline, not Linux's
+    // default 50 us timer slack later: the slack alone had each 30 us linger window last ~80 us,
+    // three windows past a burst of 214 requests (TIPS_NEG_TIMER_SLACK_NS).
+    (void)prctl(PR_SET_TIMERSLACK, (unsigned long)std::max<int64_t>(1, env_i64("TIPS_NEG_TIMER_SLACK_NS", 1000)), 0, 0, 0);
     const auto cycle = std::chrono::microseconds(std::max<int64_t>(50, env_i64("TIPS_CYCLE_TIME_US", 1000)));
     const auto linger = std::chrono::microseconds(std::max<int64_t>(0, env_i64("TIPS_BATCH_LINGER_US", 30)));
+    // TIPS_LINGER_SPIN=1: spin through the linger instead of timed waits. With the 1 us timer slack
+    // below it ended cycles no sooner (38-112 us after the latest arrival against 55-80 us waiting,
+    // profiles/r05/aa_op_host_ab.txt) and keeps a core busy, so it is off.
+    const bool spin_linger = env_i64("TIPS_LINGER_SPIN", 0) != 0;
     // TIPS_NEG_TRACE=1: per cycle with requests, on stderr: the batch, and how long the linger, the
     // exchange with rank 0 and the execution took (microseconds)
     const bool trace = env_i64("TIPS_NEG_TRACE", 0) != 0;
@@ -755,11 +860,16 @@ class Negotiator {
       std::vector<std::shared_ptr<Req>> batch;
       bool stopping;
       set_phase("waiting for requests");
-      long long t_linger = 0;
+      long long t_linger = 0, t_tail = 0;
       int windows = 0;
       {
         std::unique_lock<AdaptiveMutex> l(m_);
-        cv_.wait_for(l, cycle, [&] { return !fresh_.empty() || want_stop_; });
+        idle_.store(true, std::memory_order_seq_cst);
+        cv_.wait_for(l, cycle, [&] {
+          return !fresh_.empty() || pending_.load(std::memory_order_seq_cst) != nullptr || want_stop_;
+        });
+        idle_.store(false, std::memory_order_relaxed);
+        drain_locked();
         // Linger while requests keep arriving (a gradient list is enqueued in a burst), so one
         // cycle announces - and one fused batch reduces - the whole burst instead of its first
         // few tensors. Bounded by the cycle time; TIPS_BATCH_LINGER_US = 0 turns it off.
@@ -774,17 +884,32 @@ class Negotiator {
           const int64_t start = steady_ns(), linger_ns = (int64_t)linger.count() * 1000,
                         cycle_ns = (int64_t)cycle.count() * 1000;
           while (!want_stop_) {
+            drain_locked();  // admit what arrived so far while the burst goes on, not all of it after
             const int64_t now = steady_ns(), quiet = now - last_arrival_ns_.load(std::memory_order_acquire);
             if (quiet >= linger_ns || now - start >= cycle_ns) break;
             windows++;
-            cv_.wait_for(l, std::chrono::nanoseconds(std::min(linger_ns - quiet, cycle_ns - (now - start))));
+            if (spin_linger) {
+              // Spin (without m_) until the quiet time is reached, bounded by one linger window; the
+              // loop re-checks.
+              l.unlock();
+              const int64_t stop_at = std::min(now + linger_ns, start + cycle_ns);
+              for (int64_t t = steady_ns(); t < stop_at; t = steady_ns()) {
+                if (t - last_arrival_ns_.load(std::memory_order_acquire) >= linger_ns) break;
+                __builtin_ia32_pause();
+              }
+              l.lock();
+            } else {
+              cv_.wait_for(l, std::chrono::nanoseconds(std::min(linger_ns - quiet, cycle_ns - (now - start))));
+            }
           }
         }
+        drain_locked();
         batch.assign(fresh_.begin(), fresh_.end());
         fresh_.clear();
         for (auto& r : batch) r->state = 1;
         stopping = want_stop_;
         t_linger = us_since(t0);
+        t_tail = (steady_ns() - last_arrival_ns_.load(std::memory_order_acquire)) / 1000;
       }
       for (auto& r : batch)
         if (r->classify) {  // (see Req::classify; nothing else reads host / bad before execute)
@@ -835,12 +960,14 @@ class Negotiator {
       const auto t_e = std::chrono::steady_clock::now();
       execute(ds, nd);
       if (trace && (!batch.empty() || nd))
-        fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us (%d windows), "
-                "exchange %lld us, execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, windows,
-                t_exchange, us_since(t_e));
+        fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us (%d windows, "
+                "ended %lld us after the latest arrival), exchange %lld us, execute %lld us\n", rank_,
+                (long long)cycles_, batch.size(), nd, t_linger, windows, t_tail, t_exchange, us_since(t_e));
       if (shutdown) break;
     }
     std::lock_guard<AdaptiveMutex> l(m_);
+    accepting_.store(false, std::memory_order_release);
+    drain_locked();  // (admitted while still running: they join the unmatched below)
     running_ = false;
     std::vector<std::string> unmatched;
     for (auto& kv : by_name_) unmatched.push_back(kv.first);
@@ -1188,7 +1315,20 @@ class Negotiator {
   AdaptiveMutex m_;
   std::condition_variable_any cv_;
   bool running_ = false, want_stop_ = false;
-  std::atomic<int64_t> next_handle_{0};
+  std::atomic<bool> accepting_{false};  // running_, readable without m_ (the lock-free enqueue's check)
+  // Single enqueues (TF-style executor threads, many at once) are pushed onto this lock-free stack
+  // and admitted to the tables by whoever next holds m_ (drain_locked): the negotiation thread
+  // before each announce, poll / wait / on_done before a lookup. An enqueue then touches one
+  // contended cache line (this head) instead of two locks and a reference count (round 5: 4
+  // threads enqueueing 214 requests took 250 us against 180 us from one thread).
+  struct Pending {
+    Prepared p;
+    Pending* next = nullptr;
+  };
+  std::atomic<Pending*> pending_{nullptr};
+  std::atomic<bool> idle_{false};  // the background thread waits for a cycle's first request
+  bool lockfree_ = true;           // (set in start(), before any enqueue)
+  std::atomic<bool> waiter_started_{false};
   std::deque<std::shared_ptr<Req>> fresh_;
   std::atomic<int64_t> last_arrival_ns_{0};  // (steady clock) the latest enqueue: the linger's clock
   NameMap by_name_;
