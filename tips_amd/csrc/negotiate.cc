@@ -670,6 +670,7 @@ class Negotiator {
       Prepared& p = fifo->p;
       Req& r = *p.r;
       std::string why;
+      int code = TIPS_ERR_INVALID_ARG;
       if (p.need_ev && !ev_pool_.empty()) {
         r.ev = ev_pool_.back();
         ev_pool_.pop_back();
@@ -678,9 +679,13 @@ class Negotiator {
         if (rc != 0 || hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
           r.ev = nullptr;
           why = "hipEventCreateWithFlags failed";
+          code = TIPS_ERR_HIP;
         }
       }
-      if (why.empty() && !running_) why = "negotiation thread is not running";
+      if (why.empty() && !running_) {
+        why = "negotiation thread is not running";
+        code = TIPS_ERR_NOT_INITIALIZED;
+      }
       if (why.empty() && !by_name_.insert(std::move(p.name_node)).inserted)
         why = "a request named " + r.name + " is already pending";
       by_handle_.insert(std::move(p.handle_node));
@@ -690,7 +695,7 @@ class Negotiator {
         if (r.ev) ev_pool_.push_back(r.ev);
         r.ev = nullptr;
         r.state = -1;
-        r.code = running_ ? TIPS_ERR_INVALID_ARG : TIPS_ERR_NOT_INITIALIZED;
+        r.code = code;
         r.err = why;
         if (r.cb) queue_done(p.r);
         cv_.notify_all();
