@@ -698,7 +698,8 @@ def env_variant_jobs(args, dist, rank, world, timeout_s=240):
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
                    "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
                    "--gpus", str(world), "--steps", "10", "--warmup", "2", "--algo", "direct", "--no-compare",
-                   "--no-env-variants"] + (["--bucket-mib", str(args.bucket_mib)] if args.bucket_mib else [])
+                   "--no-sub", "--no-cpu-baseline", "--no-env-variants"] + \
+                (["--bucket-mib", str(args.bucket_mib)] if args.bucket_mib else [])
             cenv = {k: v for k, v in os.environ.items()
                     if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                                  "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TIPS_BOOTSTRAP_PORT")}
@@ -727,6 +728,11 @@ def env_variant_jobs(args, dist, rank, world, timeout_s=240):
                     d = json.loads(lines[-1])
                     res.update({k: d.get(k) for k in ("value", "ms_per_step", "check", "error")})
                     res["algbw_gib_s"] = d.get("algbw_gib_s")
+                    ring = (d.get("configs") or {}).get("config3_ring") or {}
+                    if ring:  # the north star's ring under this setting (more channels per xGMI link)
+                        res["config3_ring"] = {k: ring.get(k) for k in ("ms_per_step", "busbw_GBps", "pipeline_depth",
+                                                                        "check")}
+                        res["config3_ring"]["frac_of_one_link"] = (ring.get("roofline") or {}).get("frac_of_one_link")
                 elif "error" not in res:
                     res["error"] = "no result line (exit %s): %s" % (p.returncode, (e or "")[-400:])
             except Exception as ex:  # noqa: BLE001 - a variant never costs the main line
@@ -1605,10 +1611,16 @@ def comparisons(job, w, line, last_words):
         compare_check["lanes"] = "opt-in: TIPS_BENCH_LANES=1"
     line["compare_check"] = compare_check
     line["compare_algbw_gib_s"] = compare
-    # Opt-in (TIPS_BENCH_ENV_VARIANTS=1): child jobs with other RCCL settings (one of them delivered
-    # wrong bytes in a probe, profiles/r02/rccl_nchannels_probe.txt)
-    if job.world > 1 and not job.args.no_env_variants and not os.environ.get("TIPS_NO_RCCL") \
-            and os.environ.get("TIPS_BENCH_ENV_VARIANTS") == "1":
+    # Child jobs with other RCCL settings: 4 point-to-point channels per peer (8 delivered wrong bytes
+    # over the socket transport, profiles/r02/rccl_nchannels_probe.txt). Each child also measures the
+    # north star's ring (config3_ring) under its setting: with RCCL's default channels per peer one
+    # ring link may stay under 70 % of its bandwidth. On by default where a config-3 ring call is
+    # fast (the xGMI node; the socket rehearsal's take seconds), within the budget;
+    # TIPS_BENCH_ENV_VARIANTS=1 forces it, 0 turns it off.
+    ev = os.environ.get("TIPS_BENCH_ENV_VARIANTS", "")
+    ring_ms = ((line.get("configs") or {}).get("config3_ring") or {}).get("ms_per_step")
+    if job.world > 1 and not job.args.no_env_variants and not os.environ.get("TIPS_NO_RCCL") and ev != "0" and \
+            (ev == "1" or (ring_ms is not None and ring_ms < 500)) and job.afford("the RCCL-setting child jobs", 150):
         note_progress("the RCCL-setting child jobs")
         line["env_variants"] = env_variant_jobs(job.args, job.dist, job.rank, job.world)
 
