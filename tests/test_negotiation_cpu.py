@@ -72,6 +72,36 @@ def test_same_order_everywhere_despite_different_enqueue_orders():
     assert sorted(logs[0]) == sorted(n + " OK" for n in names)
 
 
+@pytest.mark.parametrize("expect", ["1", "0"])
+def test_repeated_steps_with_growing_and_shrinking_sets(expect):
+    """Training-shaped steps: the same 30 names every step (the linger ends early once the previous
+    batch's names are all in again, TIPS_LINGER_EXPECT), then a step that adds 10 names after them
+    on one rank and before them on the other, then a step with a subset, then the full set again.
+    Every request of every step runs, in the same order on both ranks."""
+    names = ["w%d" % i for i in range(30)]
+    extra = ["e%d" % i for i in range(10)]
+    reqs = []
+    for r in range(2):
+        body = []
+        for step in range(3):
+            order = names if (step + r) % 2 == 0 else list(reversed(names))
+            body += ["%s 0 %d" % (n, 64 + names.index(n)) for n in order] + ["@wait"]
+        grown = names + extra if r == 0 else extra + names
+        body += ["%s 0 %d" % (n, 64 + names.index(n) if n in names else 16 + extra.index(n)) for n in grown]
+        body += ["@sleep 2"] if r == 1 else []
+        body += ["@wait"]
+        body += ["%s 0 %d" % (n, 64 + names.index(n)) for n in names[::3]] + ["@wait"]
+        body += ["%s 0 %d" % (n, 64 + names.index(n)) for n in names] + ["@wait"]
+        reqs.append("\n".join(body))
+    res = run(reqs, env={0: {"TIPS_LINGER_EXPECT": expect}, 1: {"TIPS_LINGER_EXPECT": expect}})
+    logs = [lines(log) for _, rc, log, _ in res]
+    for rank, rc, log, err in res:
+        assert rc == 0, (rank, err)
+    assert logs[0] == logs[1]
+    want = 3 * len(names) + len(names) + len(extra) + len(names[::3]) + len(names)
+    assert len(logs[0]) == want and all(l.endswith(" OK") for l in logs[0])
+
+
 def test_list_commits_mixed_with_single_requests():
     """Lists committed under one lock hold (Negotiator::enqueue_list, as tips_enqueue_allreduce_n):
     3 ranks, each a different mix of lists and single requests in its own order, one rank's list

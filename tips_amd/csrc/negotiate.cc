@@ -27,6 +27,7 @@
 #include <deque>
 #include <memory>
 #include <thread>
+#include <unordered_set>
 
 #include "net.h"
 #include "rt.h"
@@ -598,7 +599,7 @@ class Negotiator {
     if (!by_name_.insert(std::move(p.name_node)).inserted)
       return refuse(TIPS_ERR_INVALID_ARG, "a request named " + r.name + " is already pending");
     by_handle_.insert(std::move(p.handle_node));
-    fresh_.push_back(p.r);
+    admit(p.r);
     return r.handle;
   }
 
@@ -655,9 +656,10 @@ class Negotiator {
   // (m_ held) Admit the lock-free stack's requests to the tables, oldest first, as commit() does
   // for a list; a request that cannot be admitted (a duplicate name, the thread stopped) fails
   // through its handle or callback instead of at its enqueue.
-  void drain_locked() {
+  int drain_locked() {
     Pending* h = pending_.exchange(nullptr, std::memory_order_acquire);
-    if (!h) return;
+    if (!h) return 0;
+    int count = 0;
     Pending* fifo = nullptr;
     while (h) {
       Pending* n = h->next;
@@ -690,7 +692,7 @@ class Negotiator {
         why = "a request named " + r.name + " is already pending";
       by_handle_.insert(std::move(p.handle_node));
       if (why.empty()) {
-        fresh_.push_back(p.r);
+        admit(p.r);
       } else {
         if (r.ev) ev_pool_.push_back(r.ev);
         r.ev = nullptr;
@@ -702,7 +704,15 @@ class Negotiator {
       }
       delete fifo;
       fifo = n;
+      count++;
     }
+    return count;
+  }
+
+  // (m_ held) A request joins the next announce; counted when the previous batch named it
+  void admit(const std::shared_ptr<Req>& r) {
+    fresh_.push_back(r);
+    if (!expect_.empty() && expect_.count(r->name)) expect_hits_++;
   }
 
   // A list (tips_enqueue_*_n): every request prepared before the lock, all of them committed under
@@ -851,6 +861,15 @@ class Negotiator {
     // below it ended cycles no sooner (38-112 us after the latest arrival against 55-80 us waiting,
     // profiles/r05/aa_op_host_ab.txt) and keeps a core busy, so it is off.
     const bool spin_linger = env_i64("TIPS_LINGER_SPIN", 0) != 0;
+    // Once every request of the previous batch is in again (a step's gradients, same names), the
+    // linger ends after TIPS_LINGER_EXPECT_US of quiet instead of TIPS_BATCH_LINGER_US: the 30 us
+    // quiet time exists to catch the rest of a burst, and the burst is known to be complete. A step
+    // that adds requests after them goes on in the next cycle. TIPS_LINGER_EXPECT=0 turns it off.
+    const bool expect_on = env_i64("TIPS_LINGER_EXPECT", 1) != 0;
+    const int64_t expect_quiet_ns = 1000 * std::max<int64_t>(0, env_i64("TIPS_LINGER_EXPECT_US", 4));
+    // (the waits while the batch is not complete are stepped, so its completion is seen within this)
+    const int64_t expect_step_ns = 8000;
+    auto complete = [&] { return expect_on && !expect_.empty() && expect_hits_ == expect_.size(); };
     // TIPS_NEG_TRACE=1: per cycle with requests, on stderr: the batch, and how long the linger, the
     // exchange with rank 0 and the execution took (microseconds)
     const bool trace = env_i64("TIPS_NEG_TRACE", 0) != 0;
@@ -866,7 +885,14 @@ class Negotiator {
       bool stopping;
       set_phase("waiting for requests");
       long long t_linger = 0, t_tail = 0;
-      int windows = 0;
+      int windows = 0, last_drained = 0;
+      int64_t drain_ns = 0, last_drain_ns = 0, wait_ns = 0;
+      auto timed_drain = [&] {  // (the trace's account of the admissions)
+        const int64_t a = steady_ns();
+        last_drained = drain_locked();
+        last_drain_ns = steady_ns() - a;
+        drain_ns += last_drain_ns;
+      };
       {
         std::unique_lock<AdaptiveMutex> l(m_);
         idle_.store(true, std::memory_order_seq_cst);
@@ -889,9 +915,11 @@ class Negotiator {
           const int64_t start = steady_ns(), linger_ns = (int64_t)linger.count() * 1000,
                         cycle_ns = (int64_t)cycle.count() * 1000;
           while (!want_stop_) {
-            drain_locked();  // admit what arrived so far while the burst goes on, not all of it after
+            timed_drain();  // admit what arrived so far while the burst goes on, not all of it after
             const int64_t now = steady_ns(), quiet = now - last_arrival_ns_.load(std::memory_order_acquire);
-            if (quiet >= linger_ns || now - start >= cycle_ns) break;
+            const bool done = complete();
+            const int64_t need = done ? std::min(expect_quiet_ns, linger_ns) : linger_ns;
+            if (quiet >= need || now - start >= cycle_ns) break;
             windows++;
             if (spin_linger) {
               // Spin (without m_) until the quiet time is reached, bounded by one linger window; the
@@ -904,13 +932,27 @@ class Negotiator {
               }
               l.lock();
             } else {
-              cv_.wait_for(l, std::chrono::nanoseconds(std::min(linger_ns - quiet, cycle_ns - (now - start))));
+              int64_t wait = std::min(need - quiet, cycle_ns - (now - start));
+              if (expect_on && !expect_.empty() && !done) wait = std::min(wait, expect_step_ns);
+              const int64_t a = steady_ns();
+              cv_.wait_for(l, std::chrono::nanoseconds(wait));
+              wait_ns += steady_ns() - a;
             }
           }
         }
-        drain_locked();
+        timed_drain();
         batch.assign(fresh_.begin(), fresh_.end());
         fresh_.clear();
+        if (expect_on) {  // the next cycle expects this batch's names (kept when they are the same)
+          size_t named = 0;
+          for (auto& r : batch) named += r->name.compare(0, 6, "~sync.") != 0;
+          if (named && !(expect_hits_ == expect_.size() && named == expect_.size())) {
+            expect_.clear();
+            for (auto& r : batch)
+              if (r->name.compare(0, 6, "~sync.") != 0) expect_.insert(r->name);
+          }
+          expect_hits_ = 0;
+        }
         for (auto& r : batch) r->state = 1;
         stopping = want_stop_;
         t_linger = us_since(t0);
@@ -966,8 +1008,9 @@ class Negotiator {
       execute(ds, nd);
       if (trace && (!batch.empty() || nd))
         fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us (%d windows, "
-                "ended %lld us after the latest arrival), exchange %lld us, execute %lld us\n", rank_,
-                (long long)cycles_, batch.size(), nd, t_linger, windows, t_tail, t_exchange, us_since(t_e));
+                "ended %lld us after the latest arrival; waits %lld us, admissions %lld us, the last %d in %lld us), exchange %lld us, "
+                "execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, windows, t_tail,
+                (long long)(wait_ns / 1000), (long long)(drain_ns / 1000), last_drained, (long long)(last_drain_ns / 1000), t_exchange, us_since(t_e));
       if (shutdown) break;
     }
     std::lock_guard<AdaptiveMutex> l(m_);
@@ -1325,7 +1368,8 @@ class Negotiator {
   // and admitted to the tables by whoever next holds m_ (drain_locked): the negotiation thread
   // before each announce, poll / wait / on_done before a lookup. An enqueue then touches one
   // contended cache line (this head) instead of two locks and a reference count (round 5: 4
-  // threads enqueueing 214 requests took 250 us against 180 us from one thread).
+  // threads enqueueing 214 requests took 250 us against 180 us from one thread; the C entry
+  // points' own lock and count went too, cached()).
   struct Pending {
     Prepared p;
     Pending* next = nullptr;
@@ -1335,6 +1379,11 @@ class Negotiator {
   bool lockfree_ = true;           // (set in start(), before any enqueue)
   std::atomic<bool> waiter_started_{false};
   std::deque<std::shared_ptr<Req>> fresh_;
+  // (m_) The names the previous batch announced (routed ~sync requests aside) and how many of them
+  // fresh_ holds: a training step enqueues the same gradients every step, and once all of them are
+  // in the linger need not wait out its quiet time (loop()).
+  std::unordered_set<std::string> expect_;
+  size_t expect_hits_ = 0;
   std::atomic<int64_t> last_arrival_ns_{0};  // (steady clock) the latest enqueue: the linger's clock
   NameMap by_name_;
   HandleMap by_handle_;
@@ -1408,6 +1457,7 @@ class Negotiator {
 
 AdaptiveMutex g_neg_mu;
 std::shared_ptr<Negotiator> g_neg;  // (shared: a caller waiting on a request keeps it alive through a shutdown)
+std::atomic<uint64_t> g_neg_gen{0};  // bumped whenever g_neg changes (cached(): per-thread copies)
 std::string g_neg_failed;           // a failed start's verdict: later named requests fail with it at once
 Negotiator* g_selftest_neg = nullptr;  // a running tips_negotiation_selftest's own (tips_debug_state)
 
@@ -1427,6 +1477,7 @@ int negotiation_stop() {
   {
     std::lock_guard<AdaptiveMutex> l(g_neg_mu);
     n.swap(g_neg);
+    g_neg_gen.fetch_add(1, std::memory_order_release);
     g_neg_failed.clear();
   }
   g_sync_direct = 0;
@@ -1505,8 +1556,29 @@ std::shared_ptr<Negotiator> negotiator(int* code) {  // started by the first nam
       return nullptr;
     }
     g_neg = std::move(neg);
+    g_neg_gen.fetch_add(1, std::memory_order_release);
   }
   return g_neg;
+}
+
+std::shared_ptr<Negotiator> current() {
+  std::lock_guard<AdaptiveMutex> l(g_neg_mu);
+  return g_neg;
+}
+
+// The single-request entry points' view of g_neg: a per-thread copy, refreshed when g_neg_gen
+// moves (a start or a stop). Executor threads enqueueing at once each took g_neg_mu and bumped the
+// negotiator's shared count per request, two cache lines bounced between them on every enqueue.
+// The thread's copy keeps the negotiator alive while the pointer is used; one that was stopped
+// refuses (not accepting) until the thread's next call sees the new generation.
+Negotiator* cached(bool create, int* code) {
+  thread_local std::shared_ptr<Negotiator> tl;
+  thread_local uint64_t tl_gen = ~0ull;
+  const uint64_t g = g_neg_gen.load(std::memory_order_acquire);
+  if (g == tl_gen && tl) return tl.get();
+  tl = create ? negotiator(code) : current();
+  tl_gen = g;  // (read before the lookup: a start or stop in between only makes the next call look again)
+  return tl.get();
 }
 
 // The argument checks of a named request (before any negotiation state is touched)
@@ -1531,7 +1603,7 @@ int64_t enqueue_named(const char* name, const void* in, void* out, const int64_t
                       void* actx = nullptr, int64_t* out_rows = nullptr) {
   TRY(check_named(name, in, out, shape, ndim, dtype, type, root, alloc));
   int code = TIPS_ERR_NOT_INITIALIZED;
-  std::shared_ptr<Negotiator> n = negotiator(&code);
+  Negotiator* n = cached(true, &code);
   if (!n) return code;
   return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, type, root, alloc, actx, out_rows, nullptr);
 }
@@ -1590,10 +1662,6 @@ int enqueue_named_list(const char* const* names, const void* const* ins, void* c
   return rc ? fail(rc, "%s", first_err.c_str()) : 0;
 }
 
-std::shared_ptr<Negotiator> current() {
-  std::lock_guard<AdaptiveMutex> l(g_neg_mu);
-  return g_neg;
-}
 
 }  // namespace
 
@@ -1621,13 +1689,15 @@ int64_t tips_enqueue_allgather(const char* name, const void* in, const int64_t* 
 
 
 int tips_poll(int64_t handle) {
-  auto n = current();
+  int code = 0;
+  Negotiator* n = cached(false, &code);
   if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
   return n->poll(handle, false);
 }
 
 int tips_wait(int64_t handle) {
-  auto n = current();
+  int code = 0;
+  Negotiator* n = cached(false, &code);
   if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
   const int rc = n->poll(handle, true);
   return rc == 1 ? 0 : rc;
@@ -1638,7 +1708,7 @@ int64_t tips_enqueue_allreduce_cb(const char* name, const void* in, void* out, c
   if (!fn) return fail(TIPS_ERR_INVALID_ARG, "null completion callback");
   TRY(check_named(name, in, out, shape, ndim, dtype, TIPS_REQ_ALLREDUCE, 0, nullptr));
   int code = TIPS_ERR_NOT_INITIALIZED;
-  std::shared_ptr<Negotiator> n = negotiator(&code);
+  Negotiator* n = cached(true, &code);
   if (!n) return code;
   return n->enqueue(name, in, out, shape, ndim, dtype, (hipStream_t)stream, TIPS_REQ_ALLREDUCE, 0, nullptr, nullptr,
                     nullptr, nullptr, nullptr, fn, ctx);
@@ -1646,7 +1716,8 @@ int64_t tips_enqueue_allreduce_cb(const char* name, const void* in, void* out, c
 
 int tips_on_done(int64_t handle, tips_done_fn fn, void* ctx) {
   if (!fn) return fail(TIPS_ERR_INVALID_ARG, "null completion callback");
-  auto n = current();
+  int code = 0;
+  Negotiator* n = cached(false, &code);
   if (!n) return fail(TIPS_ERR_NOT_INITIALIZED, "no named request was ever enqueued");
   return n->on_done(handle, fn, ctx);
 }
