@@ -323,7 +323,8 @@ TIPS_API int tips_on_done(int64_t handle, tips_done_fn fn, void* ctx);
 /* tips_enqueue_allreduce_shaped and tips_on_done in one call, as the reference enqueues one
  * OpRecord that carries its callback (EnqueueTensorCollective, coordinator.cc:223-241; CHECK(record.
  * callback)): one lock instead of two per request for an op body on many executor threads. Returns
- * the handle (> 0; it completes only through fn) or < 0, in which case fn is never called. */
+ * the handle (> 0; it completes only through fn, and tips_wait / tips_poll / tips_on_done do not
+ * know it) or < 0, in which case fn is never called. */
 TIPS_API int64_t tips_enqueue_allreduce_cb(const char* name, const void* in, void* out, const int64_t* shape, int ndim,
                                            int dtype, void* stream, tips_done_fn fn, void* ctx);
 /* Named broadcast through the same negotiation (the reference's MPIBroadcast op,

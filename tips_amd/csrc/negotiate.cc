@@ -27,7 +27,6 @@
 #include <deque>
 #include <memory>
 #include <thread>
-#include <unordered_set>
 
 #include "net.h"
 #include "rt.h"
@@ -81,6 +80,7 @@ class AdaptiveMutex {
 struct Req {
   int64_t handle = 0;
   std::string name;
+  uint64_t name_hash = 0;  // (of name, made by the enqueuing thread: the linger's expected set)
   const void* in = nullptr;
   void* out = nullptr;
   int64_t count = 0;
@@ -105,6 +105,7 @@ struct Req {
   tips_done_fn cb = nullptr;
   void* cb_ctx = nullptr;
   bool cb_queued = false;
+  bool cb_only = false;  // enqueued with its callback (tips_enqueue_allreduce_cb): not in the handle table
   // A single enqueue does not ask HIP where its pointers live: hipPointerGetAttributes takes a
   // runtime-wide lock, and TF-style executor threads enqueueing at once queued on it (4 threads:
   // 1.38 us per lookup, 0.10 alone; tools/enqueue_probe.cc). The negotiation thread classifies
@@ -114,6 +115,9 @@ struct Req {
   std::string bad;
 };
 
+// Request handles, process-wide (per-thread blocks of 256: Negotiator::prepare); the submission
+// stack shard of each enqueuing thread (Negotiator::enqueue)
+std::atomic<uint64_t> g_next_shard{0};
 // Request handles, process-wide (per-thread blocks of 256: Negotiator::prepare)
 std::atomic<int64_t> g_next_handle{0};
 
@@ -136,7 +140,6 @@ struct PtrRanges {
   };
   std::vector<Range> r;
   size_t last = 0;
-  bool device_set = false;  // set_device done for this list (one thread, one device)
   bool is_device(const void* p) {
     const uintptr_t a = (uintptr_t)p;
     if (last < r.size() && a - r[last].lo < r[last].len) return true;
@@ -337,7 +340,18 @@ struct Table {
   }
 };
 
-using NameMap = std::unordered_map<std::string, std::shared_ptr<Req>>;
+// The name table's key carries the name's hash, made by the enqueuing thread (Req::name_hash): the
+// negotiation thread admits a request without reading the name's bytes, which another core wrote
+// (an insertion compares the cached hash first, the strings only when the hashes are equal).
+struct NameKey {
+  uint64_t h;
+  std::string s;
+  bool operator==(const NameKey& o) const { return h == o.h && s == o.s; }
+};
+struct NameKeyHash {
+  size_t operator()(const NameKey& k) const { return (size_t)k.h; }
+};
+using NameMap = std::unordered_map<NameKey, std::shared_ptr<Req>, NameKeyHash>;
 using HandleMap = std::unordered_map<int64_t, std::shared_ptr<Req>>;
 
 class Negotiator {
@@ -502,7 +516,6 @@ class Negotiator {
     std::shared_ptr<Req> r;
     NameMap::node_type name_node;
     HandleMap::node_type handle_node;
-    bool need_ev = false;
   };
 
   // Everything of an enqueue that needs no lock: the request, where its memory lives, its two
@@ -510,12 +523,13 @@ class Negotiator {
   // the work, bounded them - 4 threads enqueueing config 5 were no faster than one).
   int prepare(Prepared& p, const std::string& name, const void* in, void* out, const int64_t* shape, int ndim,
               int dtype, hipStream_t s, int type, int root, tips_alloc_fn alloc, void* actx, int64_t* out_rows,
-              std::function<int()> body, PtrRanges* pr) {
+              std::function<int()> body, PtrRanges* pr, bool handle_entry = true) {
     if (ndim < 0 || ndim > TIPS_MAX_DIMS) return fail(TIPS_ERR_INVALID_ARG, "bad ndim %d", ndim);
     if (type == TIPS_REQ_ALLGATHER && ndim < 1) return fail(TIPS_ERR_INVALID_ARG, "An empty tensor found");
     auto r = std::make_shared<Req>();
     r->body = std::move(body);
     r->name = name;
+    r->name_hash = std::hash<std::string>()(name);
     r->type = type;
     r->root = root;
     r->alloc = alloc;
@@ -533,8 +547,7 @@ class Negotiator {
     if (ndim == 0) r->shape.push_back(1);  // a scalar travels as shape [1] (CreateNoEmptyTfShape, coordinator.cc:212-221)
     r->dtype = dtype;
     r->stream = s;
-    p.need_ev = !dry_ && !r->body;
-    if (p.need_ev && r->count > 0) {  // the real executor (the dry run touches no memory; a routed body checks its own)
+    if (!dry_ && !r->body && r->count > 0) {  // the real executor (the dry run touches no memory; a routed body checks its own)
       // device tensors run stream-ordered on `s`; host tensors (the reference's MPIAllreduce is a
       // CPU op, ops.cc:118) run synchronously on the executor thread, staged through HBM as
       // tips_allreduce stages them. Both pointers of a request live on the same side. A list
@@ -562,44 +575,25 @@ class Negotiator {
     }
     thread_local NameMap name_scratch;
     thread_local HandleMap handle_scratch;
-    name_scratch.emplace(name, r);
+    name_scratch.emplace(NameKey{r->name_hash, name}, r);
     p.name_node = name_scratch.extract(name_scratch.begin());
-    handle_scratch.emplace(r->handle, r);
-    p.handle_node = handle_scratch.extract(handle_scratch.begin());
+    if (handle_entry) {  // (a request enqueued with its callback has none: nothing looks it up)
+      handle_scratch.emplace(r->handle, r);
+      p.handle_node = handle_scratch.extract(handle_scratch.begin());
+    }
     p.r = std::move(r);
     return 0;
   }
 
-  // Under m_ (held by l): the request's event, its table entries, the fresh queue. The handle, or
-  // < 0 (the event back in the pool). A new event (pool empty: the first requests of a job) is
-  // made with the lock released, on the library's device.
-  int64_t commit(Prepared& p, std::unique_lock<AdaptiveMutex>& l, PtrRanges* pr) {
+  // Under m_: the request's table entries and the fresh queue. The handle, or < 0. (Its completion
+  // event, if it ever needs one, is taken when it runs: take_event.)
+  int64_t commit(Prepared& p) {
     Req& r = *p.r;
-    if (p.need_ev) {
-      if (!ev_pool_.empty()) {
-        r.ev = ev_pool_.back();
-        ev_pool_.pop_back();
-      } else {
-        l.unlock();
-        int rc = 0;
-        if (!pr || !pr->device_set) rc = set_device(S());
-        if (pr && rc == 0) pr->device_set = true;
-        const hipError_t e = rc == 0 ? hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) : hipSuccess;
-        l.lock();
-        if (rc) return rc;
-        if (e != hipSuccess) return fail(TIPS_ERR_HIP, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
-      }
-    }
-    auto refuse = [&](int code, const std::string& msg) -> int64_t {  // the event goes back to the pool
-      if (r.ev) ev_pool_.push_back(r.ev);
-      r.ev = nullptr;
-      return fail(code, "%s", msg.c_str());
-    };
-    if (!running_) return refuse(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
+    if (!running_) return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
     if (!by_name_.insert(std::move(p.name_node)).inserted)
-      return refuse(TIPS_ERR_INVALID_ARG, "a request named " + r.name + " is already pending");
-    by_handle_.insert(std::move(p.handle_node));
-    admit(p.r);
+      return fail(TIPS_ERR_INVALID_ARG, "a request named %s is already pending", r.name.c_str());
+    if (p.handle_node) by_handle_.insert(std::move(p.handle_node));
+    admit(std::move(p.r));
     return r.handle;
   }
 
@@ -608,10 +602,12 @@ class Negotiator {
                   void* actx = nullptr, int64_t* out_rows = nullptr, std::function<int()> body = nullptr,
                   PtrRanges* pr = nullptr, tips_done_fn cb = nullptr, void* cb_ctx = nullptr) {
     Prepared p;
-    TRY(prepare(p, name, in, out, shape, ndim, dtype, s, type, root, alloc, actx, out_rows, std::move(body), pr));
+    TRY(prepare(p, name, in, out, shape, ndim, dtype, s, type, root, alloc, actx, out_rows, std::move(body), pr,
+                cb == nullptr));
     if (cb) {  // tips_enqueue_allreduce_cb: the callback travels with the request (one lock, as OpRecord)
       p.r->cb = cb;
       p.r->cb_ctx = cb_ctx;
+      p.r->cb_only = true;
     }
     // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
     if (cb && !waiter_started_.load(std::memory_order_acquire)) {
@@ -622,7 +618,7 @@ class Negotiator {
     if (!lockfree_) {  // (TIPS_ENQUEUE_LOCKFREE=0: round 4's locked commit, for A/B runs only)
       std::unique_lock<AdaptiveMutex> l(m_);
       drain_locked();
-      const int64_t h = commit(p, l, pr);
+      const int64_t h = commit(p);
       if (h > 0) {
         last_arrival_ns_.store(steady_ns(), std::memory_order_release);
         if (fresh_.size() == 1) cv_.notify_all();
@@ -633,10 +629,14 @@ class Negotiator {
       return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
     const int64_t h = p.r->handle;
     Pending* node = new Pending{std::move(p), nullptr};
-    Pending* old = pending_.load(std::memory_order_relaxed);
+    // (each thread pushes onto its own shard of the stack: drain_locked walks the shards' chains
+    // side by side, so their cache misses overlap)
+    thread_local const int tl_shard = (int)(g_next_shard.fetch_add(1, std::memory_order_relaxed) % kShards);
+    std::atomic<Pending*>& head = shards_[tl_shard].head;
+    Pending* old = head.load(std::memory_order_relaxed);
     do {
       node->next = old;
-    } while (!pending_.compare_exchange_weak(old, node, std::memory_order_seq_cst, std::memory_order_relaxed));
+    } while (!head.compare_exchange_weak(old, node, std::memory_order_seq_cst, std::memory_order_relaxed));
     // the linger's quiet time, to a few microseconds (a store per request would bounce the line)
     const int64_t now = steady_ns();
     if (now - last_arrival_ns_.load(std::memory_order_relaxed) > 2000)
@@ -653,80 +653,92 @@ class Negotiator {
     return h;
   }
 
-  // (m_ held) Admit the lock-free stack's requests to the tables, oldest first, as commit() does
-  // for a list; a request that cannot be admitted (a duplicate name, the thread stopped) fails
+  // (m_ held) Admit the lock-free stack's requests to the tables, each thread's in its order, as
+  // commit() does for a list; a request that cannot be admitted (a duplicate name, the thread stopped) fails
   // through its handle or callback instead of at its enqueue.
   int drain_locked() {
-    Pending* h = pending_.exchange(nullptr, std::memory_order_acquire);
-    if (!h) return 0;
+    Pending* heads[kShards];
+    int m = 0;
+    for (Shard& sh : shards_)
+      if (Pending* h = sh.head.exchange(nullptr, std::memory_order_acquire)) heads[m++] = h;
+    if (!m) return 0;
     int count = 0;
-    Pending* fifo = nullptr;
-    while (h) {
-      Pending* n = h->next;
-      h->next = fifo;
-      fifo = h;
-      h = n;
-    }
-    while (fifo) {
-      Pending* n = fifo->next;
-      Prepared& p = fifo->p;
-      Req& r = *p.r;
-      std::string why;
-      int code = TIPS_ERR_INVALID_ARG;
-      if (p.need_ev && !ev_pool_.empty()) {
-        r.ev = ev_pool_.back();
-        ev_pool_.pop_back();
-      } else if (p.need_ev) {
-        const int rc = set_device(S());
-        if (rc != 0 || hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
-          r.ev = nullptr;
-          why = "hipEventCreateWithFlags failed";
-          code = TIPS_ERR_HIP;
+    int64_t t = adm_prof_ ? steady_ns() : 0;
+    auto lap = [&](int k) {  // (TIPS_NEG_TRACE: where an admission's time goes)
+      if (!adm_prof_) return;
+      const int64_t u = steady_ns();
+      adm_ns_[k] += u - t;
+      t = u;
+    };
+    // Each chain reversed to its thread's order, one node of every chain per step: the nodes and
+    // requests were written by other cores, and the walks' misses overlap instead of following one
+    // another (the requests are fetched while the walk goes on, for the admissions below).
+    Pending* rev[kShards] = {};
+    for (bool more = true; more;) {
+      more = false;
+      for (int k = 0; k < m; k++)
+        if (Pending* h = heads[k]) {
+          heads[k] = h->next;
+          __builtin_prefetch(h->p.r.get(), 1);
+          h->next = rev[k];
+          rev[k] = h;
+          more = true;
         }
+    }
+    lap(0);
+    for (int k = 0; k < m; k++) {
+      for (Pending* q = rev[k]; q;) {
+        Pending* n = q->next;
+        Prepared& p = q->p;
+        Req& r = *p.r;
+        std::string why;
+        int code = TIPS_ERR_INVALID_ARG;
+        if (!running_) {
+          why = "negotiation thread is not running";
+          code = TIPS_ERR_NOT_INITIALIZED;
+        }
+        if (why.empty() && !by_name_.insert(std::move(p.name_node)).inserted)
+          why = "a request named " + r.name + " is already pending";
+        lap(1);
+        if (p.handle_node) by_handle_.insert(std::move(p.handle_node));
+        lap(2);
+        if (why.empty()) {
+          admit(std::move(p.r));
+        } else {
+          r.state = -1;
+          r.code = code;
+          r.err = why;
+          if (r.cb) queue_done(p.r);
+          cv_.notify_all();
+        }
+        lap(3);
+        delete q;
+        lap(4);
+        q = n;
+        count++;
       }
-      if (why.empty() && !running_) {
-        why = "negotiation thread is not running";
-        code = TIPS_ERR_NOT_INITIALIZED;
-      }
-      if (why.empty() && !by_name_.insert(std::move(p.name_node)).inserted)
-        why = "a request named " + r.name + " is already pending";
-      by_handle_.insert(std::move(p.handle_node));
-      if (why.empty()) {
-        admit(p.r);
-      } else {
-        if (r.ev) ev_pool_.push_back(r.ev);
-        r.ev = nullptr;
-        r.state = -1;
-        r.code = code;
-        r.err = why;
-        if (r.cb) queue_done(p.r);
-        cv_.notify_all();
-      }
-      delete fifo;
-      fifo = n;
-      count++;
     }
     return count;
   }
 
   // (m_ held) A request joins the next announce; counted when the previous batch named it
-  void admit(const std::shared_ptr<Req>& r) {
-    fresh_.push_back(r);
-    if (!expect_.empty() && expect_.count(r->name)) expect_hits_++;
+  void admit(std::shared_ptr<Req>&& r) {
+    if (!expect_.empty() && std::binary_search(expect_.begin(), expect_.end(), r->name_hash)) expect_hits_++;
+    fresh_.push_back(std::move(r));
   }
 
   // A list (tips_enqueue_*_n): every request prepared before the lock, all of them committed under
   // one hold, one wake-up. The negotiation then sees the list arrive at once instead of lingering
   // through it (1000 requests one lock each took ~0.9 ms on the GPU box). handles[i] < 0 entries
   // (refused before, or here) are skipped / set; returns the first refusal or 0.
-  int enqueue_list(std::vector<Prepared>& ps, int64_t* handles, PtrRanges* pr, std::string* first_err) {
+  int enqueue_list(std::vector<Prepared>& ps, int64_t* handles, std::string* first_err) {
     int rc = 0;
     std::unique_lock<AdaptiveMutex> l(m_);
     drain_locked();  // (earlier single enqueues first)
     bool any = false;
     for (size_t i = 0; i < ps.size(); i++) {
       if (!ps[i].r) continue;
-      handles[i] = commit(ps[i], l, pr);
+      handles[i] = commit(ps[i]);
       if (handles[i] < 0 && rc == 0) {
         rc = (int)handles[i];
         *first_err = last_error();
@@ -824,11 +836,12 @@ class Negotiator {
   }
 
   ~Negotiator() {
-    for (Pending* q = pending_.exchange(nullptr); q;) {  // (never admitted)
-      Pending* n = q->next;
-      delete q;
-      q = n;
-    }
+    for (Shard& sh : shards_)
+      for (Pending* q = sh.head.exchange(nullptr); q;) {  // (never admitted)
+        Pending* n = q->next;
+        delete q;
+        q = n;
+      }
     for (auto& kv : by_handle_)  // never polled to completion
       if (kv.second->ev) ev_pool_.push_back(kv.second->ev);
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
@@ -861,18 +874,27 @@ class Negotiator {
     // below it ended cycles no sooner (38-112 us after the latest arrival against 55-80 us waiting,
     // profiles/r05/aa_op_host_ab.txt) and keeps a core busy, so it is off.
     const bool spin_linger = env_i64("TIPS_LINGER_SPIN", 0) != 0;
-    // Once every request of the previous batch is in again (a step's gradients, same names), the
-    // linger ends after TIPS_LINGER_EXPECT_US of quiet instead of TIPS_BATCH_LINGER_US: the 30 us
-    // quiet time exists to catch the rest of a burst, and the burst is known to be complete. A step
-    // that adds requests after them goes on in the next cycle. TIPS_LINGER_EXPECT=0 turns it off.
+    // Once every name of the last two cycles is in again (a training step's gradients: the same
+    // names every step), the linger ends after TIPS_LINGER_EXPECT_US of quiet instead of
+    // TIPS_BATCH_LINGER_US: the 30 us quiet time exists to catch the rest of a burst, and the burst
+    // is known to be complete. A step that adds requests after them goes on in the next cycle. (Two
+    // cycles, not one: a step that was split over two cycles once, its executor threads issuing in
+    // another order the next step, would otherwise keep splitting.) TIPS_LINGER_EXPECT=0: off.
+    // (Delimiting steps by the thread's idle waits does not work: the next step's first requests
+    // arrive while this cycle still executes.)
     const bool expect_on = env_i64("TIPS_LINGER_EXPECT", 1) != 0;
     const int64_t expect_quiet_ns = 1000 * std::max<int64_t>(0, env_i64("TIPS_LINGER_EXPECT_US", 4));
-    // (the waits while the batch is not complete are stepped, so its completion is seen within this)
+    // (the waits while the set is not complete are stepped, so its completion is seen within this)
     const int64_t expect_step_ns = 8000;
+    std::vector<std::shared_ptr<Req>> prev;  // the previous cycle's named requests
     auto complete = [&] { return expect_on && !expect_.empty() && expect_hits_ == expect_.size(); };
     // TIPS_NEG_TRACE=1: per cycle with requests, on stderr: the batch, and how long the linger, the
     // exchange with rank 0 and the execution took (microseconds)
     const bool trace = env_i64("TIPS_NEG_TRACE", 0) != 0;
+    {
+      std::lock_guard<AdaptiveMutex> l(m_);
+      adm_prof_ = trace;
+    }
     auto us_since = [](std::chrono::steady_clock::time_point t) {
       return (long long)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t).count();
     };
@@ -897,7 +919,7 @@ class Negotiator {
         std::unique_lock<AdaptiveMutex> l(m_);
         idle_.store(true, std::memory_order_seq_cst);
         cv_.wait_for(l, cycle, [&] {
-          return !fresh_.empty() || pending_.load(std::memory_order_seq_cst) != nullptr || want_stop_;
+          return !fresh_.empty() || any_pending() || want_stop_;
         });
         idle_.store(false, std::memory_order_relaxed);
         drain_locked();
@@ -943,14 +965,20 @@ class Negotiator {
         timed_drain();
         batch.assign(fresh_.begin(), fresh_.end());
         fresh_.clear();
-        if (expect_on) {  // the next cycle expects this batch's names (kept when they are the same)
-          size_t named = 0;
-          for (auto& r : batch) named += r->name.compare(0, 6, "~sync.") != 0;
-          if (named && !(expect_hits_ == expect_.size() && named == expect_.size())) {
+        if (expect_on) {  // the next cycle expects this one's names and the previous one's
+          std::vector<std::shared_ptr<Req>> cur;  // (routed ~sync requests are named per call: never expected)
+          for (auto& r : batch)
+            if (r->name.compare(0, 6, "~sync.") != 0) cur.push_back(r);
+          // (kept as it is when this cycle named exactly the expected set: the previous one's
+          // names are in it already)
+          if (!cur.empty() && !(expect_hits_ == expect_.size() && cur.size() == expect_.size())) {
             expect_.clear();
-            for (auto& r : batch)
-              if (r->name.compare(0, 6, "~sync.") != 0) expect_.insert(r->name);
+            for (auto& r : cur) expect_.push_back(r->name_hash);
+            for (auto& r : prev) expect_.push_back(r->name_hash);
+            std::sort(expect_.begin(), expect_.end());
+            expect_.erase(std::unique(expect_.begin(), expect_.end()), expect_.end());
           }
+          if (!cur.empty()) prev.swap(cur);
           expect_hits_ = 0;
         }
         for (auto& r : batch) r->state = 1;
@@ -1011,6 +1039,13 @@ class Negotiator {
                 "ended %lld us after the latest arrival; waits %lld us, admissions %lld us, the last %d in %lld us), exchange %lld us, "
                 "execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, windows, t_tail,
                 (long long)(wait_ns / 1000), (long long)(drain_ns / 1000), last_drained, (long long)(last_drain_ns / 1000), t_exchange, us_since(t_e));
+      if (trace && (!batch.empty() || nd)) {
+        std::lock_guard<AdaptiveMutex> l(m_);
+        fprintf(stderr, "[tips neg]   admission phases (us): walk %lld, name table %lld, handle table %lld, queue %lld, "
+                "free %lld\n", (long long)(adm_ns_[0] / 1000), (long long)(adm_ns_[1] / 1000), (long long)(adm_ns_[2] / 1000),
+                (long long)(adm_ns_[3] / 1000), (long long)(adm_ns_[4] / 1000));
+        for (int64_t& x : adm_ns_) x = 0;
+      }
       if (shutdown) break;
     }
     std::lock_guard<AdaptiveMutex> l(m_);
@@ -1018,10 +1053,10 @@ class Negotiator {
     drain_locked();  // (admitted while still running: they join the unmatched below)
     running_ = false;
     std::vector<std::string> unmatched;
-    for (auto& kv : by_name_) unmatched.push_back(kv.first);
+    for (auto& kv : by_name_) unmatched.push_back(kv.first.s);
     std::sort(unmatched.begin(), unmatched.end());
     for (auto& name : unmatched) {  // never matched on every rank before the stop
-      auto& r = by_name_[name];
+      auto& r = by_name_.find(NameKey{std::hash<std::string>()(name), name})->second;
       r->state = -1;
       r->code = TIPS_ERR_MISMATCH;
       r->err = "request " + name + " was not enqueued on every rank before shutdown";
@@ -1084,7 +1119,7 @@ class Negotiator {
           if (r->ev) ev_pool_.push_back(r->ev);
           r->ev = nullptr;
           r->gev.reset();
-          gone.push_back(by_handle_.extract(r->handle));
+          if (!r->cb_only) gone.push_back(by_handle_.extract(r->handle));
         }
         cb_called_ += (int64_t)batch.size();
       }
@@ -1169,7 +1204,9 @@ class Negotiator {
     {
       std::lock_guard<AdaptiveMutex> l(m_);
       for (size_t i = 0; i < n; i++) {
-        auto it = by_name_.find(ds[i].name);
+        look_.h = std::hash<std::string>()(ds[i].name);
+        look_.s.assign(ds[i].name);  // (a kept key: no allocation per lookup)
+        auto it = by_name_.find(look_);
         if (it == by_name_.end()) continue;  // (cannot happen: every rank announced it)
         reqs[i] = it->second;
         gone.push_back(by_name_.extract(it));
@@ -1265,6 +1302,7 @@ class Negotiator {
           j = i + 1;
           auto& r = reqs[i];
           if (rc == 0) rc = allreduce_device(st, r->in, r->out, r->count, r->dtype, r->stream);
+          if (rc == 0) rc = take_event(*r);
           if (rc == 0 && hipEventRecord(r->ev, r->stream) != hipSuccess) rc = fail(TIPS_ERR_HIP, "hipEventRecord failed");
         }
         if (rc != 0)
@@ -1281,6 +1319,23 @@ class Negotiator {
         if (reqs[i]->cb) queue_done(reqs[i]);
       }
     cv_.notify_all();
+  }
+
+  // A single device request's completion event, taken when it runs (a fused batch shares one
+  // GroupEv, a host request finishes before it is reported): most requests never need one, and an
+  // admission that took one touched the pool and the request for nothing.
+  int take_event(Req& r) {
+    {
+      std::lock_guard<AdaptiveMutex> l(m_);
+      if (!ev_pool_.empty()) {
+        r.ev = ev_pool_.back();
+        ev_pool_.pop_back();
+        return 0;
+      }
+    }
+    TRY(set_device(S()));
+    HIP_TRY(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
+    return 0;
   }
 
   // PerformCollectiveOp's broadcast and allgather branches (coordinator.cc:275-336) for one
@@ -1319,7 +1374,10 @@ class Negotiator {
       if (r.out_rows) *r.out_rows = rows;
       TRY(tips_allgatherv(r.in, r.count, r.out, counts.data(), r.dtype, r.stream));
     }
-    if (!r.host) HIP_TRY(hipEventRecord(r.ev, r.stream));
+    if (!r.host) {
+      TRY(take_event(r));
+      HIP_TRY(hipEventRecord(r.ev, r.stream));
+    }
     return 0;
   }
 
@@ -1374,18 +1432,32 @@ class Negotiator {
     Prepared p;
     Pending* next = nullptr;
   };
-  std::atomic<Pending*> pending_{nullptr};
+  static constexpr int kShards = 8;
+  struct alignas(64) Shard {
+    std::atomic<Pending*> head{nullptr};
+  };
+  Shard shards_[kShards];
+  bool any_pending() {
+    for (Shard& sh : shards_)
+      if (sh.head.load(std::memory_order_seq_cst)) return true;
+    return false;
+  }
   std::atomic<bool> idle_{false};  // the background thread waits for a cycle's first request
   bool lockfree_ = true;           // (set in start(), before any enqueue)
   std::atomic<bool> waiter_started_{false};
   std::deque<std::shared_ptr<Req>> fresh_;
-  // (m_) The names the previous batch announced (routed ~sync requests aside) and how many of them
+  // (m_) The names the last two cycles announced (routed ~sync requests aside) and how many of them
   // fresh_ holds: a training step enqueues the same gradients every step, and once all of them are
   // in the linger need not wait out its quiet time (loop()).
-  std::unordered_set<std::string> expect_;
+  // (sorted name hashes, made by the enqueuing threads: admit() compares integers, and a collision
+  // only ends a linger early or late, never changes what runs)
+  std::vector<uint64_t> expect_;
+  bool adm_prof_ = false;     // (TIPS_NEG_TRACE) drain_locked's phases, per cycle in the trace
+  int64_t adm_ns_[5] = {};
   size_t expect_hits_ = 0;
   std::atomic<int64_t> last_arrival_ns_{0};  // (steady clock) the latest enqueue: the linger's clock
   NameMap by_name_;
+  NameKey look_{0, std::string()};  // (m_) execute()'s lookup key
   HandleMap by_handle_;
   std::vector<std::string> log_;
   std::vector<hipEvent_t> ev_pool_;
@@ -1448,7 +1520,7 @@ class Negotiator {
     int k = 0;
     for (auto& kv : by_name_) {
       if (k++ == 8) break;
-      out += (k == 1 ? " | waiting for other ranks: " : ", ") + kv.first + "(state " + std::to_string(kv.second->state) + ")";
+      out += (k == 1 ? " | waiting for other ranks: " : ", ") + kv.first.s + "(state " + std::to_string(kv.second->state) + ")";
     }
     if (!done_q_.empty()) out += " | next callback: " + done_q_.front()->name + "(state " + std::to_string(done_q_.front()->state) + ")";
     return out;
@@ -1645,7 +1717,7 @@ int enqueue_named_list(const char* const* names, const void* const* ins, void* c
       if (!ps[(size_t)i].r) continue;
       one[0] = std::move(ps[(size_t)i]);
       std::string err;
-      const int e = neg->enqueue_list(one, handles + i, &pr, &err);
+      const int e = neg->enqueue_list(one, handles + i, &err);
       if (e && rc == 0) {
         rc = e;
         first_err = err;
@@ -1653,7 +1725,7 @@ int enqueue_named_list(const char* const* names, const void* const* ins, void* c
     }
   } else if (neg) {
     std::string err;
-    const int e = neg->enqueue_list(ps, handles, &pr, &err);
+    const int e = neg->enqueue_list(ps, handles, &err);
     if (e && rc == 0) {
       rc = e;
       first_err = err;
@@ -1870,7 +1942,7 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
         batching = false;
         std::vector<int64_t> hs(batch.size(), 0);
         std::string err;
-        if (neg.enqueue_list(batch, hs.data(), nullptr, &err) != 0) {
+        if (neg.enqueue_list(batch, hs.data(), &err) != 0) {
           rcs[k] = TIPS_ERR_INVALID_ARG;
           return;
         }
