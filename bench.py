@@ -1750,6 +1750,15 @@ def bench_job(args):
         _RESULT["line"] = line if rank == 0 else None
     if args.workload == "auto" and not args.no_sub:
         sub_records(job, line, args.sub_steps)
+        anchor = (line.get("configs") or {}).get("config3_bucket") or {}
+        if world == 1 and anchor.get("value") is not None:
+            # the metric names two workloads (config 2's sum at N = 1, config 3's allreduce at N > 1):
+            # the same-workload point for a scaling curve is config 3 at one rank
+            line["scaling_anchor"] = {"workload": "config 3 at one rank (configs.config3_bucket)",
+                                      "value": anchor["value"], "unit": anchor.get("unit"),
+                                      "ms_per_step": anchor.get("ms_per_step"),
+                                      "note": "value(N) / (N x this) compares like with like; the N = 1 "
+                                              "headline is config 2's sum kernel, a different workload"}
         _RESULT["line"] = line if rank == 0 else None
     last_words = crash_line() if rank == 0 and not args.no_compare else None
     if w is not None and workload == "bucket" and world > 1 and not args.no_compare:
