@@ -748,6 +748,68 @@ def test_named_async_allreduce_single_rank(gpu):
     assert torch.equal(gpu.allgather_op(ts[5].view(-1, 1), name="ag"), ts[5].view(-1, 1))
 
 
+def test_named_requests_from_threads_across_a_restart():
+    """Executor threads keep a per-thread view of the negotiator (negotiate.cc cached(), refreshed
+    by a generation counter) and push onto per-thread submission shards. The same three pool
+    threads enqueue named host requests with callbacks (tips_enqueue_allreduce_cb) and device
+    requests (allreduce_async) before a shutdown and after a new init; every result is its input,
+    bit for bit, in both generations. A callback request's handle is a receipt: tips_wait refuses
+    it. Enqueueing between the shutdown and the new init is refused, never hangs. (Its own
+    process: it restarts the library.)"""
+    import subprocess
+    import sys
+    from conftest import REPO
+    code = r'''
+import ctypes, threading, numpy as np, torch
+from concurrent.futures import ThreadPoolExecutor
+import tips_amd
+from tips_amd import _lib
+L = _lib.lib()
+done, lock, ev = [], threading.Lock(), threading.Event()
+@_lib.DONE_FN
+def on_done(ctx, status, msg):
+    with lock:
+        done.append((ctx, status))
+        if len(done) == want[0]:
+            ev.set()
+want = [0]
+def host_job(gen, t):
+    outs = []
+    for i in range(30):
+        x = np.random.default_rng(gen * 1000 + t * 100 + i).random(1000 + 17 * i, dtype=np.float32)
+        y = np.empty_like(x)
+        shape = (ctypes.c_int64 * 1)(x.size)
+        h = L.tips_enqueue_allreduce_cb(("g%d.t%d.h%d" % (gen, t, i)).encode(), x.ctypes.data, y.ctypes.data,
+                                        shape, 1, _lib.FLOAT32, None, on_done, None)
+        assert h > 0, _lib.last_error()
+        outs.append((x, y, h))
+    return outs
+def dev_job(gen, t):
+    xs = [torch.randn(500 + 31 * i, device="cuda") for i in range(10)]
+    hs = [tips_amd.allreduce_async(x, "g%d.t%d.d%d" % (gen, t, i)) for i, x in enumerate(xs)]
+    return [(x, tips_amd.synchronize(h)) for x, h in zip(xs, hs)]
+pool = ThreadPoolExecutor(3)
+for gen in range(2):
+    tips_amd.init()
+    done.clear(); ev.clear(); want[0] = 90
+    hosts = [f.result() for f in [pool.submit(host_job, gen, t) for t in range(3)]]
+    devs = [f.result() for f in [pool.submit(dev_job, gen, t) for t in range(3)]]
+    assert ev.wait(120), len(done)
+    assert all(s == 0 for _, s in done)
+    assert all(np.array_equal(x, y) for outs in hosts for x, y, _ in outs)
+    assert all(torch.equal(x, y) for outs in devs for x, y in outs)
+    assert L.tips_wait(hosts[0][0][2]) < 0 and "unknown request handle" in _lib.last_error()
+    tips_amd.shutdown()
+    x = np.ones(4, dtype=np.float32); shape = (ctypes.c_int64 * 1)(4)
+    h = pool.submit(lambda: L.tips_enqueue_allreduce_cb(b"after.shutdown", x.ctypes.data, x.ctypes.data, shape, 1,
+                                                        _lib.FLOAT32, None, on_done, None)).result(60)
+    assert h < 0, h
+print("RESTART_OK")
+'''
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=REPO, timeout=300)
+    assert "RESTART_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
 def test_named_async_many_single_rank(gpu, monkeypatch):
     """allreduce_async_many / synchronize_many (tips_enqueue_allreduce_n / tips_wait_n): 500
     named tensors in one call, fused per readiness list (1 MiB threshold: some batches, some
