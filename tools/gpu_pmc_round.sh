@@ -26,6 +26,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   pass config5 $c python3 tools/pack_ceiling.py 3 --only=config5/pack
 done
 echo "[$(date +%T)] kernel trace" >> "$OUT/steps.txt"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- python3 bench.py \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py \
   --no-sub --no-cpu-baseline --no-extras --steps 200 --warmup 20 > "$OUT/trace.log" 2>&1 || exit 1
 echo "[$(date +%T)] done" >> "$OUT/steps.txt"
