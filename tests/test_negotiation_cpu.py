@@ -102,6 +102,66 @@ def test_repeated_steps_with_growing_and_shrinking_sets(expect):
     assert len(logs[0]) == want and all(l.endswith(" OK") for l in logs[0])
 
 
+def cached(log):
+    return int([l for l in log.splitlines() if l.startswith("# cached decisions")][0].split()[-1])
+
+
+@pytest.mark.parametrize("cache", ["1", "0", "mixed"])
+def test_response_cache_repeated_steps(cache):
+    """The response cache: names decided OK are announced by id from then on, and when every rank
+    announced an id by id rank 0 answers without the table. 3 ranks, 40 names, 4 steps, each rank in
+    its own order per step: every step runs every name, the same order on every rank; with the cache
+    on, steps 2-4 come back cached (one rank with it off: none are, every announce is full)."""
+    names = ["w%d" % i for i in range(40)]
+    reqs = []
+    for r in range(3):
+        body = []
+        for step in range(4):
+            order = names[(7 * r + step) % 40:] + names[:(7 * r + step) % 40]
+            if (r + step) % 2:
+                order = list(reversed(order))
+            body += ["%s 0 %d" % (n, 16 + names.index(n)) for n in order] + ["@wait"]
+        reqs.append("\n".join(body))
+    env = {r: {"TIPS_RESPONSE_CACHE": "0" if cache == "0" or (cache == "mixed" and r == 1) else "1"}
+           for r in range(3)}
+    res = run(reqs, env=env)
+    for rank, rc, log, err in res:
+        assert rc == 0, (rank, err)
+    logs = [lines(log) for _, _, log, _ in res]
+    assert logs[0] == logs[1] == logs[2]
+    assert sorted(logs[0]) == sorted(n + " OK" for n in names * 4)
+    hits = [cached(log) for _, _, log, _ in res]
+    assert len(set(hits)) == 1
+    if cache == "1":
+        assert hits[0] >= 2 * 40, hits  # (step 1 decides in full; a cycle may take a step's first names early)
+    else:
+        assert hits[0] == 0
+
+
+def test_response_cache_shape_change_fails_everywhere_then_recaches():
+    """A cached name whose shape changes on one rank travels in full from that rank; rank 0 puts
+    the other ranks' id announces of it through the table, which fails it on every rank with the
+    reference's text (coordinator.cc:134-150). The failure drops it from the cache; the next step
+    with the new shape on every rank succeeds, then comes back cached."""
+    steps = {0: [8, 8, 8, 9, 9, 9], 1: [8, 8, 9, 9, 9, 9]}
+    reqs = []
+    for r in range(2):
+        body = []
+        for k, n in enumerate(steps[r]):
+            body += ["w 0 %d" % n, "b%d 0 4" % k, "@wait"]
+        reqs.append("\n".join(body))
+    res = run(reqs)
+    for rank, rc, log, err in res:
+        assert rc == 0, (rank, err)
+    logs = [lines(log) for _, _, log, _ in res]
+    assert logs[0] == logs[1]
+    w = [l for l in logs[0] if l.startswith("w ")]
+    assert w[:2] == ["w OK", "w OK"]
+    assert w[2] == "w ERR Mismatched allreduce tensor shapes: [8] vs [9]"
+    assert w[3:] == ["w OK"] * 3
+    assert cached(res[0][2]) >= 2  # (steps 2 and 6 at least: w by id on both ranks)
+
+
 def test_list_commits_mixed_with_single_requests():
     """Lists committed under one lock hold (Negotiator::enqueue_list, as tips_enqueue_allreduce_n):
     3 ranks, each a different mix of lists and single requests in its own order, one rank's list

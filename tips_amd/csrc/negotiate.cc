@@ -830,6 +830,9 @@ class Negotiator {
   }
 
   // number of completion callbacks called so far (the selftest's log)
+  // decisions that came back as "cached OK" (the response cache; read after stop())
+  int64_t cached_decisions() const { return cached_decisions_.load(std::memory_order_relaxed); }
+
   int64_t callbacks_called() {
     std::lock_guard<AdaptiveMutex> l(m_);
     return cb_called_;
@@ -902,6 +905,12 @@ class Negotiator {
     Writer w;
     std::string resp;
     std::vector<Decision> ds;
+    std::vector<uint32_t> cids;
+    std::vector<Req*> full;
+    // TIPS_RESPONSE_CACHE=0: announce every request in full (A/B; every rank keeps the cache's
+    // bookkeeping either way, so ranks may differ in this setting). Rank 0 counts ids in a 64-bit
+    // rank mask: above 64 ranks everything travels in full.
+    const bool send_ids = env_i64("TIPS_RESPONSE_CACHE", 1) != 0 && size_ <= 64;
     while (true) {
       std::vector<std::shared_ptr<Req>> batch;
       bool stopping;
@@ -996,8 +1005,17 @@ class Negotiator {
       const auto t_x = std::chrono::steady_clock::now();
       w.b.clear();
       w.put<uint8_t>(stopping ? 1 : 0);
-      w.put<uint32_t>((uint32_t)batch.size());
+      // a request the response cache holds with the same dtype and shape travels as its cache id
+      // (4 bytes; rank 0 counts it without a name); the rest as full records
+      cids.clear();
+      full.clear();
       for (auto& r : batch) {
+        const int32_t id = send_ids ? cached_id(*r) : -1;
+        if (id >= 0) cids.push_back((uint32_t)id);
+        else full.push_back(r.get());
+      }
+      w.put<uint32_t>((uint32_t)full.size());
+      for (Req* r : full) {
         w.put<int32_t>(r->type);
         w.put<int32_t>(r->root);
         w.put<uint8_t>(r->bad.empty() ? 0 : 1);
@@ -1007,6 +1025,8 @@ class Negotiator {
         for (int64_t d : r->shape) w.put<int64_t>(d);
         w.str(r->name);
       }
+      w.put<uint32_t>((uint32_t)cids.size());
+      for (uint32_t id : cids) w.put<uint32_t>(id);
       set_phase("exchange (cycle " + std::to_string((long long)cycles_) + ", announcing " + std::to_string(batch.size()) + ")");
       if (!exchange(w.b, &resp)) break;
       {
@@ -1020,10 +1040,23 @@ class Negotiator {
       for (uint32_t i = 0; i < n && rd.ok; i++) {
         if (nd == ds.size()) ds.emplace_back();
         Decision& d = ds[nd++];  // (a kept slot: its strings keep their capacity)
-        d.ok = rd.get<uint8_t>() != 0;
+        const uint8_t tag = rd.get<uint8_t>();
+        d.sizes.clear();
+        d.err.clear();
+        if (tag == kCachedOk) {  // a cached allreduce every rank announced by id
+          const uint32_t id = rd.get<uint32_t>();
+          if (id >= cache_.size() || !cache_[id].live) {
+            rd.ok = false;
+            break;
+          }
+          d.ok = true;
+          d.name.assign(cache_[id].name);
+          cached_decisions_.fetch_add(1, std::memory_order_relaxed);
+          continue;
+        }
+        d.ok = tag != 0;
         rd.str_into(d.name);
         rd.str_into(d.err);
-        d.sizes.clear();
         const uint32_t m = rd.get<uint32_t>();
         for (uint32_t k = 0; k < m && rd.ok && k < (1u << 20); k++) d.sizes.push_back(rd.get<int64_t>());
       }
@@ -1036,9 +1069,10 @@ class Negotiator {
       execute(ds, nd);
       if (trace && (!batch.empty() || nd))
         fprintf(stderr, "[tips neg] rank %d cycle %lld: announced %zu, decided %zu; linger %lld us (%d windows, "
-                "ended %lld us after the latest arrival; waits %lld us, admissions %lld us, the last %d in %lld us), exchange %lld us, "
-                "execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, windows, t_tail,
-                (long long)(wait_ns / 1000), (long long)(drain_ns / 1000), last_drained, (long long)(last_drain_ns / 1000), t_exchange, us_since(t_e));
+                "ended %lld us after the latest arrival; waits %lld us, admissions %lld us, the last %d in %lld us), exchange %lld us "
+                "(rank 0's decision %lld us), execute %lld us\n", rank_, (long long)cycles_, batch.size(), nd, t_linger, windows,
+                t_tail, (long long)(wait_ns / 1000), (long long)(drain_ns / 1000), last_drained, (long long)(last_drain_ns / 1000),
+                t_exchange, (long long)(rank_ == 0 ? decide_ns_ / 1000 : -1), us_since(t_e));
       if (trace && (!batch.empty() || nd)) {
         std::lock_guard<AdaptiveMutex> l(m_);
         fprintf(stderr, "[tips neg]   admission phases (us): walk %lld, name table %lld, handle table %lld, queue %lld, "
@@ -1130,7 +1164,12 @@ class Negotiator {
 
   // One lockstep cycle: my announce goes up, rank 0's decision comes back.
   bool exchange(const std::string& mine, std::string* resp) {
-    if (size_ == 1) return decide({mine}, resp);
+    if (size_ == 1) {
+      const int64_t a = steady_ns();
+      const bool ok = decide({mine}, resp);
+      decide_ns_ = steady_ns() - a;
+      return ok;
+    }
     if (rank_ != 0) {
       if (!send_msg(up_, mine) || !recv_msg(up_, resp, timeout_ms_)) {
         set_loop_error("negotiation: lost rank 0");
@@ -1145,7 +1184,9 @@ class Negotiator {
         set_loop_error("negotiation: lost rank " + std::to_string(r));
         return false;
       }
+    const int64_t a = steady_ns();
     if (!decide(all, resp)) return false;
+    decide_ns_ = steady_ns() - a;
     for (int r = 1; r < size_; r++)
       if (!send_msg(peers_[r], *resp)) {
         set_loop_error("negotiation: lost rank " + std::to_string(r));
@@ -1173,12 +1214,44 @@ class Negotiator {
         if (ndim > TIPS_MAX_DIMS) rd.ok = false;
         for (uint32_t d = 0; d < ndim && rd.ok; d++) a.shape.push_back(rd.get<int64_t>());
         rd.str_into(a.name);
-        if (rd.ok) table_.announce(r, a);
+        if (!rd.ok) break;
+        // a full record of a name others announced by id this round: theirs join the table too
+        if (!cache_ids_.empty()) {
+          const int32_t id = cache_lookup(a.name, std::hash<std::string>()(a.name));
+          if (id >= 0) to_table(id);
+        }
+        table_.announce(r, a);
+      }
+      const uint32_t k = rd.get<uint32_t>();
+      for (uint32_t i = 0; i < k && rd.ok; i++) {
+        const uint32_t id = rd.get<uint32_t>();
+        if (id >= cache_.size() || !cache_[id].live) {
+          rd.ok = false;
+          break;
+        }
+        if (idst_.size() < cache_.size()) idst_.resize(cache_.size());
+        IdState& st = idst_[id];
+        const uint64_t bit = 1ull << r;
+        if (st.table || (st.mask & bit)) {  // (a rank's second announce: the table names the duplicate)
+          to_table(id);
+          table_.announce(r, expand(id));
+          continue;
+        }
+        st.mask |= bit;
+        if (++st.n == (int)all.size()) {  // every rank, every one by id: ready, valid as cached
+          st.mask = 0;
+          st.n = 0;
+          id_ready_.push_back(id);
+        }
       }
       if (!rd.ok) {
         set_loop_error("negotiation: malformed announce from rank " + std::to_string(r));
         return false;
       }
+    }
+    for (size_t q = 0; q < table_.nready; q++) {  // (decided now: later ids of these names count anew)
+      const int32_t id = idst_.empty() ? -1 : cache_lookup(table_.ready_q[q], std::hash<std::string>()(table_.ready_q[q]));
+      if (id >= 0 && (size_t)id < idst_.size()) idst_[id].table = false;
     }
     Writer w;
     w.b.swap(*resp);  // (the previous response's buffer, reused)
@@ -1186,10 +1259,85 @@ class Negotiator {
     w.put<uint8_t>(everyone_stops ? 1 : 0);
     const size_t count_at = w.b.size();
     w.put<uint32_t>(0);
-    const uint32_t n = table_.write_ready(w);
+    uint32_t n = table_.write_ready(w);
+    for (uint32_t id : id_ready_) {  // after the table's: readiness order among themselves
+      w.put<uint8_t>(kCachedOk);
+      w.put<uint32_t>(id);
+    }
+    n += (uint32_t)id_ready_.size();
+    id_ready_.clear();
     memcpy(&w.b[count_at], &n, sizeof n);
     resp->swap(w.b);
     return true;
+  }
+
+  // ---- response cache (rank-0 side and the shared bookkeeping) ----------------------------
+  // An allreduce decided OK is cached on every rank under an id: the position of its first OK
+  // decision in the response stream, which every rank reads in the same order (execute()), so the
+  // ids agree without being sent. A later request with that name, dtype and shape is announced
+  // by id; when every rank announced an id by id, rank 0 answers "cached OK" without the table:
+  // the checks ConstructResponseMessage makes (coordinator.cc:90-186) passed for exactly these
+  // parameters. Any full record of the name (changed shape, an unusable pointer, a rank with the
+  // cache off) sends the round's ids of that name through the table, which then checks and
+  // words every failure as before. A failure drops the name from the cache on every rank.
+  int32_t cache_lookup(const std::string& name, uint64_t h) {
+    cache_look_.h = h;
+    cache_look_.s.assign(name);
+    auto it = cache_ids_.find(cache_look_);
+    return it == cache_ids_.end() ? -1 : (int32_t)it->second;
+  }
+  int32_t cached_id(const Req& r) {
+    if (r.type != TIPS_REQ_ALLREDUCE || !r.bad.empty() || cache_ids_.empty()) return -1;
+    const int32_t id = cache_lookup(r.name, r.name_hash);
+    if (id < 0) return -1;
+    const CacheEntry& e = cache_[(size_t)id];
+    return e.dtype == r.dtype && e.shape == r.shape ? id : -1;
+  }
+  Announce expand(uint32_t id) {
+    const CacheEntry& e = cache_[id];
+    Announce a;
+    a.type = TIPS_REQ_ALLREDUCE;
+    a.dtype = e.dtype;
+    a.count = e.count;
+    a.shape = e.shape;
+    a.name = e.name;
+    return a;
+  }
+  // (rank 0) this round's announces of id go to the table from now on, the ones counted so far too
+  void to_table(int32_t id) {
+    if ((size_t)id >= idst_.size()) idst_.resize(cache_.size());
+    IdState& st = idst_[(size_t)id];
+    if (st.table) return;
+    st.table = true;
+    for (int q = 0; q < 64 && st.mask; q++)
+      if (st.mask & (1ull << q)) {
+        st.mask &= ~(1ull << q);
+        table_.announce(q, expand((uint32_t)id));
+      }
+    st.n = 0;
+  }
+  // (every rank, execute(), in response order) an OK allreduce joins the cache or refreshes its
+  // parameters; a failure leaves it
+  void cache_note(const Decision& d, const Req* r) {
+    if (d.name.compare(0, 6, "~sync.") == 0) return;  // (routed calls: a name per call)
+    const int32_t id = cache_lookup(d.name, std::hash<std::string>()(d.name));
+    if (!d.ok || !r || r->type != TIPS_REQ_ALLREDUCE) {
+      if (id >= 0) {
+        cache_[(size_t)id].live = false;
+        cache_ids_.erase(cache_look_);
+      }
+      return;
+    }
+    if (id >= 0) {
+      CacheEntry& e = cache_[(size_t)id];
+      e.dtype = r->dtype;
+      e.count = r->count;
+      e.shape = r->shape;
+      return;
+    }
+    if (cache_.size() >= kCacheCap) return;  // (full: later names travel in full, on every rank alike)
+    cache_ids_.emplace(NameKey{std::hash<std::string>()(d.name), d.name}, (uint32_t)cache_.size());
+    cache_.push_back(CacheEntry{d.name, r->dtype, r->count, r->shape, true});
   }
 
   // PerformCollectiveOp for one cycle's ready list, in rank 0's order. Readiness
@@ -1218,6 +1366,7 @@ class Negotiator {
       }
     }
     gone.clear();
+    for (size_t i = 0; i < n; i++) cache_note(ds[i], reqs[i].get());  // (every rank, this order)
     std::vector<int> state(n, 0), code(n, TIPS_ERR_MISMATCH);
     std::vector<std::string> msg(n);
     for (size_t i = 0; i < n; i++) {
@@ -1458,6 +1607,28 @@ class Negotiator {
   std::atomic<int64_t> last_arrival_ns_{0};  // (steady clock) the latest enqueue: the linger's clock
   NameMap by_name_;
   NameKey look_{0, std::string()};  // (m_) execute()'s lookup key
+  // the response cache (the negotiation thread's own: no lock)
+  static constexpr uint8_t kCachedOk = 2;  // a response entry: a cached name decided OK (then its id)
+  static constexpr size_t kCacheCap = 1 << 16;
+  struct CacheEntry {
+    std::string name;
+    int dtype;
+    int64_t count;
+    std::vector<int64_t> shape;
+    bool live;
+  };
+  struct IdState {  // (rank 0) this round's announces of a cached name
+    uint64_t mask = 0;   // the ranks that announced it by id
+    int n = 0;
+    bool table = false;  // a full record came: the rest of the round goes through the table
+  };
+  std::vector<CacheEntry> cache_;
+  std::unordered_map<NameKey, uint32_t, NameKeyHash> cache_ids_;
+  NameKey cache_look_{0, std::string()};
+  std::vector<IdState> idst_;
+  std::vector<uint32_t> id_ready_;
+  std::atomic<int64_t> cached_decisions_{0};
+  int64_t decide_ns_ = 0;  // (rank 0, the trace) the last cycle's decide()
   HandleMap by_handle_;
   std::vector<std::string> log_;
   std::vector<hipEvent_t> ev_pool_;
@@ -1998,7 +2169,8 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
     if (r) return r;
   std::string log;
   for (auto& l : neg.log()) log += l + "\n";
-  if (cbs) {
+  log += "# cached decisions " + std::to_string((long long)neg.cached_decisions()) + "\n";
+  if (cbs) {  // (the last line)
     int64_t n = 0;
     for (auto& c : counts) n += c.done.load();
     log += "callbacks " + std::to_string((long long)n) + "\n";

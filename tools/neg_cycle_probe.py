@@ -1,6 +1,6 @@
 """The negotiation's per-cycle cost at N ranks on the CPU (no GPU): N processes run
 tips_negotiation_selftest (dry-run executor) over 127.0.0.1, each enqueueing config 5's 214 names
-per step from T executor threads (callbacks), STEPS steps; TIPS_NEG_TRACE=1 prints each cycle's
+per step (PROBE_NAMES to change it) from T executor threads (callbacks), STEPS steps; TIPS_NEG_TRACE=1 prints each cycle's
 linger / exchange / execute. Prints the per-rank median of every part over the steady cycles.
 
   python3 tools/neg_cycle_probe.py [N=8] [STEPS=12] [THREADS=4]
@@ -13,7 +13,7 @@ import statistics
 import sys
 import tempfile
 
-NAMES = 214
+NAMES = int(os.environ.get("PROBE_NAMES", "214"))
 
 
 def _rank(rank, size, port, script, errpath, env):
@@ -58,7 +58,7 @@ def main():
         p.start()
     for p in ps:
         p.join(300)
-    pat = re.compile(r"announced (\d+), decided (\d+); linger (\d+) us .*?ended (\d+) us after .*?exchange (\d+) us, "
+    pat = re.compile(r"announced (\d+), decided (\d+); linger (\d+) us .*?ended (\d+) us after .*?exchange (\d+) us .*?"
                      r"execute (\d+) us")
     for r in range(n):
         rows = [tuple(map(int, m.groups())) for m in pat.finditer(open(os.path.join(d, "r%d.err" % r)).read())]
@@ -66,9 +66,14 @@ def main():
         med = lambda k: statistics.median(x[k] for x in steady) if steady else None  # noqa: E731
         print("rank %d: %d cycles (%d steady); median announced %s decided %s linger %s us tail %s us exchange %s us"
               % (r, len(rows), len(steady), med(0), med(1), med(2), med(3), med(4)))
-        adm = [int(x) for x in re.findall(r"admissions (\d+) us", open(os.path.join(d, "r%d.err" % r)).read())][2:]
+        txt = open(os.path.join(d, "r%d.err" % r)).read()
+        adm = [int(x) for x in re.findall(r"admissions (\d+) us", txt)][2:]
+        dec = [int(x) for x in re.findall(r"rank 0's decision (\d+) us", txt)][2:]
         if adm:
             print("rank %d: admissions per cycle, median %s us" % (r, statistics.median(adm)))
+        if r == 0 and dec:
+            print("rank 0: decision per cycle, median %s us, total %s us over %d cycles"
+                  % (statistics.median(dec), sum(dec), len(dec)))
 
 
 if __name__ == "__main__":
