@@ -1236,6 +1236,9 @@ class Workload(object):
             rec["per_tensor_us"] = round(ms * 1e3 / len(self.sizes), 2)
             rec["host_us_per_tensor"] = {k: round(v / self.steps / len(self.sizes) * 1e6, 2) for k, v in self.host_split.items()}
             rec["api"] = "tips_enqueue_allreduce_n + tips_wait_n (1000 named requests, one call each way)"
+            rec["response_cache"] = "on" if os.environ.get("TIPS_RESPONSE_CACHE", "1") != "0" else "off"
+            if world > 1 and self.job.args.workload == "auto":  # (a sub-record at N > 1: the list API only)
+                return rec
             self.per_call = True  # the same requests through one ctypes call per tensor, for comparison
             for _ in range(2):
                 self.step()
@@ -1641,15 +1644,17 @@ def comparisons(job, w, line, last_words):
 def sub_records(job, line, steps):
     """The other configs at this N, each a record of its own in line["configs"]."""
     subs = line.setdefault("configs", {})
+    # config 4 as 1000 NAMED requests last (the negotiated path: readiness batches fused, the
+    # response cache after the first step; SURVEY row a6), only while the budget lasts
     order = ([("config3_bucket", "bucket")] if job.world == 1 else []) + \
-        [("config4_fused1000", "fused1000"), ("config5_resnet50", "resnet50")]
+        [("config4_fused1000", "fused1000"), ("config5_resnet50", "resnet50"), ("config4_negotiated", "negotiated1000")]
     for key, wl in order:
         # a record costs its tuning + warm-up + steps: at N = 8 over the socket rehearsal ~20 s each
         if not job.afford(key, 30):
             subs[key] = {"skipped": "time budget (TIPS_BENCH_BUDGET_S)"}
             continue
         progress(job.rank, "sub-record %s" % key)
-        w = Workload(job, wl, steps, 5 if wl != "bucket" else 3)
+        w = Workload(job, wl, min(steps, 10) if wl == "negotiated1000" else steps, 5 if wl != "bucket" else 3)
         try:
             rec = w.run()
             if wl in SUB_WORKLOADS and job.afford("%s gradient_api legs" % key, 25):
