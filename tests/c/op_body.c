@@ -218,6 +218,18 @@ static void on_usr1(int sig) {
   backtrace_symbols_fd(fr, n, 2);
 }
 
+/* a fatal signal: the faulting thread's stack on stderr, then the default action */
+static void on_fatal(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  char hdr[96];
+  const int l = snprintf(hdr, sizeof hdr, "--- fatal signal %d in thread %ld\n", sig, (long)syscall(SYS_gettid));
+  if (write(2, hdr, (size_t)l) < 0) _exit(128 + sig);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 static void dump_stacks(void) {
   signal(SIGUSR1, on_usr1);
   const long self = (long)syscall(SYS_gettid);
@@ -257,6 +269,8 @@ int main(void) {
   const char* nt = getenv("OP_BODY_TENSORS");
   g_nonblocking = getenv("OP_BODY_NONBLOCKING") && atoi(getenv("OP_BODY_NONBLOCKING")) != 0;
   g_ntensors = nt ? atoi(nt) : 96;
+  signal(SIGSEGV, on_fatal);
+  signal(SIGABRT, on_fatal);
   tips_init();
   if (!tips_is_initialize()) {
     printf("{\"ok\": false, \"error\": \"tips_init: %s\"}\n", tips_last_error());
@@ -314,57 +328,79 @@ int main(void) {
     (void)hipFree(d);
     fprintf(stderr, "[op_body rank %d] negotiation started\n", g_rank);
   }
-  pthread_t th[THREADS + 1];
-  Job jobs[THREADS];
-  for (int k = 0; k < THREADS; k++) {
-    jobs[k].thread = k;
-    jobs[k].order = order;
-    pthread_create(&th[k], NULL, executor, &jobs[k]);
-  }
-  pthread_create(&th[THREADS], NULL, sync_caller, NULL);
-  for (int k = 0; k <= THREADS; k++) pthread_join(th[k], NULL);
-  /* every callback, bounded */
-  struct timespec dl;
-  clock_gettime(CLOCK_REALTIME, &dl);
-  dl.tv_sec += 120;
-  pthread_mutex_lock(&g_mu);
-  while (atomic_load(&g_callbacks) < g_ntensors)
-    if (pthread_cond_timedwait(&g_cv, &g_mu, &dl) != 0) break;
-  pthread_mutex_unlock(&g_mu);
-  const int callbacks = atomic_load(&g_callbacks);
-  int bad = 0;
+  /* OP_BODY_PASSES training steps (default 2) over the same names, each in this rank's order,
+   * reversed every other step: from the second step on, the names every rank announces by id
+   * (the negotiation's response cache) come back decided without rank 0's table */
+  const int passes = getenv("OP_BODY_PASSES") ? atoi(getenv("OP_BODY_PASSES")) : 2;
+  int callbacks = 0, bad = 0;
   void** all = (void**)malloc(sizeof(void*) * g_size);
-  for (int i = 0; i < g_ntensors && callbacks == g_ntensors; i++) {
-    Tensor* t = &g_t[i];
-    const size_t bytes = (size_t)t->n * 4;
-    if (atomic_load(&t->status) != 0) {
-      note("tensor failed: %s (%d); ", t->msg, i);
-      bad++;
-      continue;
+  for (int pass = 0; pass < passes && bad == 0; pass++) {
+    if (pass > 0) {
+      for (int i = 0; i < g_ntensors; i++) {  /* fresh outputs: a stale one from the last step must not pass */
+        Tensor* t = &g_t[i];
+        atomic_store(&t->done, 0);
+        atomic_store(&t->status, 0);
+        if (t->kind == KIND_HOST_F32) memset(t->out, 0xA5, (size_t)t->n * 4);
+        else if (hipMemset(t->out, 0xA5, (size_t)t->n * 4) != hipSuccess) note("%shipMemset of tensor %d; ", "", i);
+      }
+      for (int i = 0; i < g_ntensors / 2; i++) {
+        const int tmp = order[i];
+        order[i] = order[g_ntensors - 1 - i];
+        order[g_ntensors - 1 - i] = tmp;
+      }
+      atomic_store(&g_callbacks, 0);
     }
-    void* got = malloc(bytes);
-    void* exp = malloc(bytes);
-    if (t->kind == KIND_HOST_F32) memcpy(got, t->out, bytes);
-    else if (hipMemcpy(got, t->out, bytes, hipMemcpyDeviceToHost) != hipSuccess) note("%sD2H of tensor %d; ", "", i);
-    for (int r = 0; r < g_size; r++) {
-      all[r] = malloc(bytes);
-      fill(all[r], r, i, t->kind, t->n);
+    pthread_t th[THREADS + 1];
+    Job jobs[THREADS];
+    for (int k = 0; k < THREADS; k++) {
+      jobs[k].thread = k;
+      jobs[k].order = order;
+      pthread_create(&th[k], NULL, executor, &jobs[k]);
     }
-    if (t->kind == KIND_BCAST) memcpy(exp, all[1 % g_size], bytes);
-    else oracle_fold(t->kind == KIND_DEV_I32 ? ORACLE_I32 : ORACLE_F32, exp, (const void* const*)all, g_size, t->n, 1);
-    if (memcmp(got, exp, bytes) != 0) {
-      note("%stensor %d differs from the oracle; ", "", i);
-      bad++;
+    pthread_create(&th[THREADS], NULL, sync_caller, NULL);
+    for (int k = 0; k <= THREADS; k++) pthread_join(th[k], NULL);
+    /* every callback, bounded */
+    struct timespec dl;
+    clock_gettime(CLOCK_REALTIME, &dl);
+    dl.tv_sec += 120;
+    pthread_mutex_lock(&g_mu);
+    while (atomic_load(&g_callbacks) < g_ntensors)
+      if (pthread_cond_timedwait(&g_cv, &g_mu, &dl) != 0) break;
+    pthread_mutex_unlock(&g_mu);
+    callbacks = atomic_load(&g_callbacks);
+    if (callbacks != g_ntensors) break;
+    for (int i = 0; i < g_ntensors && callbacks == g_ntensors; i++) {
+      Tensor* t = &g_t[i];
+      const size_t bytes = (size_t)t->n * 4;
+      if (atomic_load(&t->status) != 0) {
+        note("tensor failed: %s (%d); ", t->msg, i);
+        bad++;
+        continue;
+      }
+      void* got = malloc(bytes);
+      void* exp = malloc(bytes);
+      if (t->kind == KIND_HOST_F32) memcpy(got, t->out, bytes);
+      else if (hipMemcpy(got, t->out, bytes, hipMemcpyDeviceToHost) != hipSuccess) note("%sD2H of tensor %d; ", "", i);
+      for (int r = 0; r < g_size; r++) {
+        all[r] = malloc(bytes);
+        fill(all[r], r, i, t->kind, t->n);
+      }
+      if (t->kind == KIND_BCAST) memcpy(exp, all[1 % g_size], bytes);
+      else oracle_fold(t->kind == KIND_DEV_I32 ? ORACLE_I32 : ORACLE_F32, exp, (const void* const*)all, g_size, t->n, 1);
+      if (memcmp(got, exp, bytes) != 0) {
+        note("%stensor %d differs from the oracle; ", "", i);
+        bad++;
+      }
+      for (int r = 0; r < g_size; r++) free(all[r]);
+      free(got);
+      free(exp);
     }
-    for (int r = 0; r < g_size; r++) free(all[r]);
-    free(got);
-    free(exp);
   }
   tips_shutdown();
   atomic_store(&g_finished, 1);
   const int ok = callbacks == g_ntensors && bad == 0 && !atomic_load(&g_sync_bad);
-  printf("{\"rank\": %d, \"ok\": %s, \"callbacks\": %d, \"tensors\": %d, \"sync_calls\": %d, \"error\": \"", g_rank,
-         ok ? "true" : "false", callbacks, g_ntensors, SYNC_CALLS);
+  printf("{\"rank\": %d, \"ok\": %s, \"callbacks\": %d, \"tensors\": %d, \"passes\": %d, \"sync_calls\": %d, "
+         "\"error\": \"", g_rank, ok ? "true" : "false", callbacks, g_ntensors, passes, SYNC_CALLS);
   for (const char* c = g_err; *c; c++) putchar(*c == '"' ? '\'' : *c);
   printf("\"}\n");
   return ok ? 0 : 3;

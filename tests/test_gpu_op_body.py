@@ -7,8 +7,10 @@ allreduces and a broadcast - each thread in its own order and each rank in a dif
 every request completing through a tips_on_done callback, while a fifth thread issues synchronous
 tips_allreduce calls that the library routes through the same negotiation. Every output is checked
 bit-exact against the oracle's rank-order fold (oracle_fold) of all ranks' regenerated inputs
-(AUTO at p = 3: one-shot and direct schedules and fused batches - all rank-order folds). The
-reference pins the same path with callbacks in coordinator_test.cc:10-45."""
+(AUTO at p = 3: one-shot and direct schedules and fused batches - all rank-order folds). Two
+training steps run over the same names, the second in the reversed order with fresh outputs: its
+allreduces go through the negotiation's response cache (announced by id, decided without rank
+0's table). The reference pins the same path with callbacks in coordinator_test.cc:10-45."""
 import json
 import os
 import socket
@@ -73,7 +75,7 @@ def _run_op_body(p, tensors, binary, extra_env=None):
     assert not bad, "\n".join("rank %d rc %s: %s %s\nstderr: %s" % b for b in bad)
     for rc, out, err in outs:
         res = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
-        assert res["callbacks"] == tensors
+        assert res["callbacks"] == tensors and res["passes"] == 2
 
 
 def test_op_host_config5_over_rccl(gpu):

@@ -1715,6 +1715,8 @@ const char* master_addr() {
 
 }  // namespace
 
+bool on_negotiation_thread() { return tl_negotiation_thread; }
+
 int negotiation_stop() {
   std::shared_ptr<Negotiator> n;
   {

@@ -322,6 +322,8 @@ int negotiation_stop();
 // run directly (no negotiation, or already on the negotiation thread).
 bool route_collective(int type, int dtype, const int64_t* shape, int ndim, int root, const std::function<int()>& body,
                       int* rc);
+// Whether the calling thread is a negotiation thread (named requests and routed calls execute there)
+bool on_negotiation_thread();
 
 // ---------------------------------------------------------------------------
 // host staging: the reference's ops work on host (TF CPU) tensors (ops.cc:88-90)

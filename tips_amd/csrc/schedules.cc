@@ -260,6 +260,12 @@ bool graphs_supported() {
 
 bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
   if ((st.graphs && st.graphs->off) || st.replays_yield) return false;
+  // Not on the negotiation thread: it executes named requests (and, once a negotiation runs, every
+  // routed collective) while the caller's threads go on calling HIP - creating streams, copying,
+  // waiting on events. A plan captured there in a C host (/opt/rocm's 7.2 runtime, RCCL 2.27) with
+  // such calls in flight crashed inside RCCL at the capture (tests/c/op_body.c's second step over
+  // the same names, 3 ranks); with graphs off the same run is bit-exact. Those plans run eagerly.
+  if (on_negotiation_thread()) return false;
   const int64_t want = env_i64("TIPS_GRAPHS", 1);
   if (want <= 0 || (want == 1 && !graphs_supported())) return false;
   int64_t cap = env_i64("TIPS_GRAPH_MAX_BYTES", 8 << 20);
