@@ -162,6 +162,52 @@ def test_response_cache_shape_change_fails_everywhere_then_recaches():
     assert cached(res[0][2]) >= 2  # (steps 2 and 6 at least: w by id on both ranks)
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_response_cache_random_steps(seed):
+    """Random training-like steps over a pool of names, 3 ranks in their own orders: each step
+    enqueues a random subset on every rank; sometimes one rank changes a name's shape, or every
+    rank issues a name as a broadcast instead. A name must come out OK in every step where all
+    ranks agreed and fail in the step where they did not, the same on every rank, whether its
+    earlier steps were decided in full or from the response cache."""
+    import random
+    rng = random.Random(seed)
+    pool = ["p%d" % i for i in range(24)]
+    steps = []
+    for s in range(6):
+        names = rng.sample(pool, rng.randint(8, 24))
+        odd = rng.choice(names) if rng.random() < 0.6 else None  # one rank's shape differs
+        bc = rng.choice([n for n in names if n != odd]) if rng.random() < 0.4 else None  # all: broadcast
+        steps.append((names, odd, bc))
+    reqs = []
+    for r in range(3):
+        body = []
+        for names, odd, bc in steps:
+            order = names[:]
+            random.Random(seed * 100 + r).shuffle(order)
+            for n in order:
+                count = 32 + pool.index(n) + (1 if (n == odd and r == 2) else 0)
+                body.append("%s 0 %d - %s" % (n, count, "bc:0" if n == bc else "ar"))
+            body.append("@wait")
+        reqs.append("\n".join(body))
+    res = run(reqs)
+    for rank, rc, log, err in res:
+        assert rc == 0, (rank, err)
+    logs = [lines(log) for _, _, log, _ in res]
+    assert logs[0] == logs[1] == logs[2]
+    got = {}
+    for l in logs[0]:
+        n, rest = l.split(" ", 1)
+        got.setdefault(n, []).append(rest)
+    want = {}
+    for names, odd, bc in steps:
+        for n in names:
+            want.setdefault(n, []).append("ERR" if n == odd else "OK")
+    assert set(got) == set(want)
+    for n in want:
+        assert [g.split(" ")[0] for g in got[n]] == want[n], (n, got[n], want[n])
+    assert cached(res[0][2]) > 0
+
+
 def test_list_commits_mixed_with_single_requests():
     """Lists committed under one lock hold (Negotiator::enqueue_list, as tips_enqueue_allreduce_n):
     3 ranks, each a different mix of lists and single requests in its own order, one rank's list
