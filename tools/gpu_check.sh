@@ -32,7 +32,7 @@ for s in ${STEPS:-pytest bench1}; do
               --timeout-method thread > "$OUT/pytest.log" 2>&1 || exit $? ;;
     bench1) run bench1 "${BENCH_TIMEOUT:-500}" python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench_n1.jsonl" \
               2> "$OUT/bench_n1.err" || exit $? ;;
-    bench1prof) run bench1prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py \
+    bench1prof) run bench1prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py \
                   --no-sub --no-cpu-baseline --no-extras --steps 200 --warmup 20 > "$OUT/bench_prof.log" 2>&1 || exit $? ;;
     rehearse2) TIPS_BENCH_FAKE_HOSTS=1 run rehearse2 "${N2_TIMEOUT:-600}" python -u bench.py --gpus 2 ${REHEARSE_ARGS:-} \
                  > "$OUT/rehearsal_n2.log" 2>&1 || exit $? ;;
