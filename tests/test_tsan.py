@@ -32,37 +32,49 @@ def _port():
     return p
 
 
-def _op_body_scripts(ranks, names, threads, seed, batch=0):
+def _op_body_scripts(ranks, names, threads, seed, batch=0, steps=1):
     """batch > 0: each thread commits its requests as lists of that many (@batch ... @endbatch,
-    Negotiator::enqueue_list) instead of one at a time."""
+    Negotiator::enqueue_list) instead of one at a time. steps > 1: the same names again after every
+    thread has seen its callbacks (from the second step on through the response cache)."""
     out = []
     for r in range(ranks):
         rnd = random.Random(seed + r)
-        order = names[:]
-        rnd.shuffle(order)
         body = []
-        per_thread = [0] * threads
-        for k, n in enumerate(order):
-            t = k % threads
-            if batch and per_thread[t] % batch == 0:
-                body.append(("t%d: @endbatch\n" % t if per_thread[t] else "") + "t%d: @batch" % t)
-            per_thread[t] += 1
-            kind = "bc:1" if names.index(n) % 7 == 3 else "ar"
-            body.append("t%d: %s %d %d - %s" % (t, n, names.index(n) % 4, 64 + names.index(n), kind))
-            if rnd.random() < 0.1 and not batch:
-                body.append("t%d: @sleep %d" % (t, rnd.randint(1, 3)))
-        if batch:
-            body += ["t%d: @endbatch" % t for t in range(threads) if per_thread[t]]
+        first = names[:]
+        rnd.shuffle(first)
+        # a name stays with one thread in every step (a thread's @wait then covers its last
+        # instance: a framework never enqueues a name again while its last request is pending)
+        owner = {n: k % threads for k, n in enumerate(first)}
+        for step in range(steps):
+            if step:
+                body += ["t%d: @wait" % t for t in range(threads)]
+            _op_body_step(body, rnd, first if step == 0 else rnd.sample(names, len(names)), owner, threads, batch)
         body.append("t1: @wait")
         out.append("\n".join(body) + "\n")
     return out
 
 
-@pytest.mark.parametrize("ranks,seed,batch", [(3, 100, 0), (2, 7, 0), (3, 11, 5)])
-def test_negotiation_threads_and_callbacks_race_free(tmp_path, ranks, seed, batch):
+def _op_body_step(body, rnd, order, owner, threads, batch):
+    per_thread = [0] * threads
+    names = sorted(owner, key=lambda n: int(n[len("layer"):].split("/")[0]))  # (the sizes' index)
+    for n in order:
+        t = owner[n]
+        if batch and per_thread[t] % batch == 0:
+            body.append(("t%d: @endbatch\n" % t if per_thread[t] else "") + "t%d: @batch" % t)
+        per_thread[t] += 1
+        kind = "bc:1" if names.index(n) % 7 == 3 else "ar"
+        body.append("t%d: %s %d %d - %s" % (t, n, names.index(n) % 4, 64 + names.index(n), kind))
+        if rnd.random() < 0.1 and not batch:
+            body.append("t%d: @sleep %d" % (t, rnd.randint(1, 3)))
+    if batch:
+        body += ["t%d: @endbatch" % t for t in range(threads) if per_thread[t]]
+
+
+@pytest.mark.parametrize("ranks,seed,batch,steps", [(3, 100, 0, 1), (2, 7, 0, 1), (3, 11, 5, 1), (3, 21, 0, 3)])
+def test_negotiation_threads_and_callbacks_race_free(tmp_path, ranks, seed, batch, steps):
     assert os.path.exists(BIN), "tools/_bin/tsan_selftest missing: run make (builds the tsan target)"
     names = ["layer%d/grad" % i for i in range(40)]
-    scripts = _op_body_scripts(ranks, names, 4, seed, batch)
+    scripts = _op_body_scripts(ranks, names, 4, seed, batch, steps)
     port = _port()
     procs = []
     for r, sc in enumerate(scripts):
@@ -82,7 +94,7 @@ def test_negotiation_threads_and_callbacks_race_free(tmp_path, ranks, seed, batc
     for rc, o, e in outs:
         assert "ThreadSanitizer" not in e, e[-4000:]
         assert rc == 0, (rc, e[-2000:])
-        assert o.strip().endswith("callbacks %d" % len(names)), o[-300:]
+        assert o.strip().endswith("callbacks %d" % (len(names) * steps)), o[-300:]
     logs = [[l for l in o.splitlines() if l and not l.startswith("#")] for _, o, _ in outs]
     assert all(lg == logs[0] for lg in logs)  # one order on every rank
 
