@@ -14,7 +14,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-gpu-flush-denormals
 
 CRASH    := tools/lib/libcrashline.so
 
-REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe tools/_bin/op_body tools/_bin/op_host tools/_bin/op_host_check
+REPRO    := tools/_bin/graph_repro tools/_bin/graph_probe tools/_bin/op_body tools/_bin/op_host tools/_bin/op_host_check \
+            tools/_bin/capture_race tools/_bin/capture_race_hip
 
 FAST     := tips_amd/_fast$(shell python3 -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
 TORCH    := $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
@@ -68,6 +69,18 @@ tools/_bin/op_body: tests/c/op_body.c $(LIB) include/tips_hip.h oracle/build/lib
 	gcc -O2 -std=gnu11 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -Ioracle -o $@ $< \
 	  -Ltips_amd/lib -ltips_hip -Loracle/build -loracle -L/opt/rocm/lib -lamdhip64 -lpthread \
 	  -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -Wl,-rpath,/opt/rocm/lib
+
+# direct tips_allreduce captures on one thread while other threads make HIP calls (tests/test_gpu_op_body.py)
+tools/_bin/capture_race: tests/c/capture_race.c $(LIB) include/tips_hip.h oracle/build/liboracle.so
+	@mkdir -p tools/_bin
+	gcc -O2 -std=gnu11 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -Ioracle -o $@ $< \
+	  -Ltips_amd/lib -ltips_hip -Loracle/build -loracle -L/opt/rocm/lib -lamdhip64 -lpthread \
+	  -Wl,-rpath,'$$ORIGIN/../../tips_amd/lib' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -Wl,-rpath,/opt/rocm/lib
+
+# the same capture pattern on the HIP runtime alone, no RCCL and no library (diagnostic)
+tools/_bin/capture_race_hip: tools/capture_race_hip.cc
+	@mkdir -p tools/_bin
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -o $@ $< -lpthread
 
 # what the HIP calls of a named-request enqueue cost (diagnostic, tools/enqueue_probe.cc)
 tools/_bin/enqueue_probe: tools/enqueue_probe.cc

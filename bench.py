@@ -549,7 +549,8 @@ SMALL_BUCKET_KIB = (16, 256, 512, 1024, 2048, 4096, 8192)
 
 def small_bucket_latency(job, torch, dist, _lib, L, rank, sp, calls=40, kibs=SMALL_BUCKET_KIB):
     """Per-call time of small allreduces, 16 KiB - 8 MiB (config 1 is a 1 MiB bucket at p = 2), for
-    the path the library ships (AUTO with its default one-shot threshold and graph-replay limit)
+    the path the library ships (AUTO with its default one-shot threshold; replays only if the job
+    opted in with TIPS_GRAPHS=1)
     and for each candidate beside it: direct eager, direct replayed as a HIP graph at any size,
     one-shot eager and one-shot replayed. The wall time of `calls` back-to-back calls on the same
     buffers (a quarter of them above 1 MiB), slowest rank; `best` names the fastest candidate and
@@ -589,7 +590,8 @@ def small_bucket_latency(job, torch, dist, _lib, L, rank, sp, calls=40, kibs=SMA
             ok = True
             use(_lib.ALGO_AUTO, {})
             shipped = L.tips_resolve_algorithm(world, n * 4)
-            graphs = n * 4 <= (8 << 20)  # (schedules.cc: TIPS_GRAPH_MAX_BYTES's default)
+            # (schedules.cc: replays are opt-in since round 6, TIPS_GRAPH_MAX_BYTES's default 8 MiB)
+            graphs = saved.get("TIPS_GRAPHS") not in (None, "", "0") and n * 4 <= (8 << 20)
             for rnd in range(2):  # two interleaved rounds, best of both: no mode always runs first
                 for mode, algo, env in (modes if rnd == 0 else modes[::-1]):
                     use(algo, env)

@@ -369,12 +369,15 @@ TIPS_API int tips_tuned_schedule(int64_t bytes, int* algo, int* depth, int* lane
  * Fills up to `cap` entries and returns how many candidates there were (0 before that class was
  * tuned; cap 0 asks the count), < 0 on error. */
 TIPS_API int tips_tuned_timings(int64_t bytes, int* algos, int* depths, int* lanes, double* ms, int cap);
-/* Replayed plans (TIPS_GRAPHS, default 1): a ring / direct / one-shot call of at most
- * TIPS_GRAPH_MAX_BYTES (1 MiB: latency-bound buckets) made again on the same buffers (same
+/* Replayed plans (TIPS_GRAPHS=1, opt-in; default 0): a ring / direct / one-shot call of at most
+ * TIPS_GRAPH_MAX_BYTES (8 MiB: latency-bound buckets) made again on the same buffers (same
  * addresses and allocations) is captured once into a HIP graph and replayed with one launch;
- * streams, events and results are those of the eager steps. On where the loaded HIP runtime and
- * RCCL are ROCm >= 7.0 / RCCL >= 2.26 (torch's bundled runtime and /opt/rocm's 7.2 are both
- * tested); TIPS_GRAPHS=0 turns it off.
+ * streams, events and results are those of the eager steps. Needs ROCm >= 7.0 / RCCL >= 2.26
+ * (torch's bundled runtime and /opt/rocm's 7.2 are both tested). Opt in only when no other thread
+ * of the process issues work on the legacy null stream (hipMemcpy, hipMemset, launches on stream
+ * 0, torch's default stream): such work invalidates a capture in progress on any stream, and RCCL
+ * crashes inside the invalidated capture. Plans executed by the negotiation thread
+ * (named requests, routed collectives) are never captured.
  * Reports this process's captures, replays and cached graphs.
  * A plan whose capture fails runs eagerly from then on; the others keep replaying.
  * Returns 0 (graphs on), 1 (3 failed captures turned them off for the job), 2 (off: not asked

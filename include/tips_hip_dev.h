@@ -41,6 +41,13 @@ TIPS_API int tips_host_pool_selftest(int nthreads, int runs, int njobs);
 TIPS_API int tips_negotiation_selftest(int rank, int size, const char* host, int port, const char* requests,
                                        char* out, int64_t cap);
 
+/* The lock-free enqueue against a stop, one rank, no GPU: `threads` threads enqueue callback
+ * requests while the caller stops the negotiation after stop_after_us, `rounds` times. result[0..3]:
+ * accepted enqueues, callbacks called, requests whose callback count was wrong (an accepted one must
+ * be called back exactly once, a refused one never), refusals. TIPS_OK when result[2] is 0. */
+TIPS_API int tips_negotiation_stop_race_selftest(int threads, int per_thread, int stop_after_us, int rounds, int port,
+                                                 int64_t* result);
+
 /* ---- single-GPU harnesses (tests and benchmarks) ---- */
 
 /* Runs the device ring schedule for p virtual ranks on this one GPU:

@@ -396,11 +396,14 @@ int main(void) {
       free(exp);
     }
   }
+  int64_t captured = 0, replayed = 0, cached = 0;
+  (void)tips_graph_stats(&captured, &replayed, &cached);
   tips_shutdown();
   atomic_store(&g_finished, 1);
   const int ok = callbacks == g_ntensors && bad == 0 && !atomic_load(&g_sync_bad);
   printf("{\"rank\": %d, \"ok\": %s, \"callbacks\": %d, \"tensors\": %d, \"passes\": %d, \"sync_calls\": %d, "
-         "\"error\": \"", g_rank, ok ? "true" : "false", callbacks, g_ntensors, passes, SYNC_CALLS);
+         "\"captured\": %lld, \"replayed\": %lld, \"error\": \"", g_rank, ok ? "true" : "false", callbacks, g_ntensors,
+         passes, SYNC_CALLS, (long long)captured, (long long)replayed);
   for (const char* c = g_err; *c; c++) putchar(*c == '"' ? '\'' : *c);
   printf("\"}\n");
   return ok ? 0 : 3;

@@ -65,7 +65,7 @@ def test_product_and_development_exports():
     assert prod == set(header_functions())
     assert not prod & dev_only
     assert dev == prod | dev_only
-    assert len(dev_only) == 13  # simulators (4), self-tests (2), sweeps (4), tips_schedule_plan, tile table,
+    assert len(dev_only) == 14  # simulators (4), self-tests (3), sweeps (4), tips_schedule_plan, tile table,
     #                             tips_tune_candidates
     from tips_amd import _lib
     D, L = _lib.dev(), _lib.lib()

@@ -108,3 +108,83 @@ def test_op_host_config5_over_rccl(gpu):
         res = json.loads(line[-1]) if line else None
         assert rc == 0 and res and res["ok"], "rank %d rc %s: %s\n%s" % (r, rc, out[-1500:], err[-3000:])
         assert res["tensors"] == 214 and res["elements"] == 25583592 and res["check"].startswith("bit-exact"), res
+
+
+def _run_capture_race(churn, graphs):
+    """tools/_bin/capture_race (tests/c/capture_race.c) over 2 RCCL ranks: one thread calls
+    tips_allreduce directly on 40 bucket sizes (4 KiB - 4 MiB) x 3 rounds x 3 buffer sets, every
+    result bit-exact against the oracle's fold, while 3 threads churn HIP calls."""
+    exe = os.path.join(REPO, "tools", "_bin", "capture_race")
+    assert os.path.exists(exe), "build it first: make tools/_bin/capture_race (part of __graft_entry__.build())"
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), TIPS_BOOTSTRAP_PORT=str(port), NCCL_HOSTID="tips-race-%d" % r,
+                   NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", CAPTURE_RACE_CHURN=churn,
+                   TIPS_FRESH_WAIT_LIMIT="1000")
+        env.pop("TIPS_GRAPHS", None)
+        if graphs:
+            env["TIPS_GRAPHS"] = "1"
+        procs.append(subprocess.Popen([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            out, err = pr.communicate(timeout=200)
+            outs.append((pr.returncode, out, err))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    res = []
+    for r, (rc, out, err) in enumerate(outs):
+        line = [l for l in out.splitlines() if l.startswith("{")]
+        d = json.loads(line[-1]) if line else None
+        assert rc == 0 and d and d["ok"], "rank %d rc %s: %s\nstderr: %s" % (r, rc, out[-1500:], err[-3000:])
+        assert d["calls"] == 3 * 3 * 40 and d["churn_ops"] > 0, d
+        res.append(d)
+    return res
+
+
+def test_direct_calls_beside_legacy_stream_threads(gpu):
+    """a C host whose other threads create and destroy blocking streams,
+    hipMalloc / hipFree and copy / memset on the legacy null stream while one thread calls
+    tips_allreduce directly, call after call on the same buffers. Replays are at their default,
+    off: nothing is captured, every result is bit-exact and no call fails. (With TIPS_GRAPHS=1 the
+    same run crashes inside RCCL: the legacy-stream calls invalidate the capture RCCL is inside,
+    profiles/r06/)"""
+    for d in _run_capture_race("all", graphs=False):
+        assert d["captured"] == 0 and d["graph_state"] == 2, d
+
+
+@pytest.mark.parametrize("churn", ["async", "streams", "free"])
+def test_replays_beside_threads_that_keep_off_the_legacy_stream(gpu, churn):
+    """Replays opted in (TIPS_GRAPHS=1) with the other threads' HIP calls on streams of their own:
+    copies and syncs on non-blocking streams, blocking streams created and destroyed, hipMalloc /
+    hipFree. Captures happen (every size's second call) and succeed, replays run, every result is
+    bit-exact: what the runtime invalidates a capture for is legacy-stream work alone."""
+    for d in _run_capture_race(churn, graphs=True):
+        assert d["graph_state"] == 0 and d["captured"] >= 40 and d["replayed"] >= 80, d
+
+
+def test_runtime_invalidates_a_capture_on_legacy_stream_work(gpu):
+    """Pins the HIP runtime behaviour the replay default rests on, with no RCCL and no library
+    (tools/_bin/capture_race_hip): while one thread captures on NON-BLOCKING streams, another
+    thread's hipMemcpy / hipMemset on the legacy null stream fails ("operation would make the legacy
+    stream depend on a capturing blocking stream") and invalidates the capture, in relaxed mode as
+    in thread-local mode; copies on the other thread's own non-blocking stream disturb nothing. If a
+    later runtime stops doing this, this test fails and TIPS_GRAPHS can default to on again."""
+    exe = os.path.join(REPO, "tools", "_bin", "capture_race_hip")
+    assert os.path.exists(exe), "build it first: make tools/_bin/capture_race_hip"
+    rows = {}
+    for churn, mode in (("async", "relaxed"), ("legacy", "relaxed"), ("legacy", "thread")):
+        p = subprocess.run([exe, churn, "3", mode], capture_output=True, text=True, timeout=60)
+        line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+        assert line, (p.returncode, p.stdout[-500:], p.stderr[-2000:])
+        rows[churn, mode] = json.loads(line[-1])
+    ok = rows["async", "relaxed"]
+    assert ok["capture_failures"] == 0 and ok["churn_errors"] == 0 and ok["captures"] > 10, ok
+    for key in (("legacy", "relaxed"), ("legacy", "thread")):
+        r = rows[key]
+        assert r["capture_failures"] > 0 and r["churn_errors"] > 0, r
+        assert "legacy stream" in r["first_churn_error"], r

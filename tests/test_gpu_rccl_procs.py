@@ -88,8 +88,9 @@ def test_fusion_buckets_mixed_with_a_replayed_list(gpu, p):
     replayed from its second call), in place, new values every round, over real RCCL ranks: every
     round bit-exact against the fold, and the replay -> eager host waits stop once the first one has
     widened the replay limit (TIPS_GRAPH_MIXED_MAX_BYTES): the fusion buckets become replays too."""
-    results = run_job(p, [{"fused": "config4", "seed": 3, "mode": "mixed", "rounds": 5}], timeout=600,
-                      **rccl_env("auto"))
+    env = rccl_env("auto")
+    env.update(TIPS_GRAPHS="1")  # (replays are opt-in since round 6)
+    results = run_job(p, [{"fused": "config4", "seed": 3, "mode": "mixed", "rounds": 5}], timeout=600, **env)
     check(results)
     for res in results:
         c = res["results"][0]

@@ -455,3 +455,38 @@ def test_debug_state_reports_the_threads():
     assert live, seen[:3]
     assert all("| negotiation: " in s and "| completion: " in s for s in live)
     assert any(" pending " in s for s in live)
+
+
+def _stop_race_worker(gap_us, q):
+    import ctypes
+    import os
+    os.environ["TIPS_TEST_ENQUEUE_GAP_US"] = str(gap_us)  # (read once, at the process's first enqueue)
+    from tips_amd import _lib
+    L = _lib.dev()
+    out = []
+    for stop_us in (0, 100, 1000, 3000):
+        res = (ctypes.c_int64 * 4)()
+        rc = L.tips_negotiation_stop_race_selftest(4, 50 if gap_us else 2000, stop_us, 3, _port(), res)
+        out.append((stop_us, rc, list(res), L.tips_last_error().decode()))
+    q.put(out)
+
+
+@pytest.mark.parametrize("gap_us", [0, 300])
+def test_enqueue_with_callbacks_races_a_stop(gap_us):
+    """the lock-free enqueue checked that the negotiation accepts requests, then pushed
+    its node; a stop() whose last drain fell between the two left the node unadmitted, and a
+    tips_enqueue_allreduce_cb caller, already holding a handle, never saw its callback. Four threads
+    enqueue callback requests while the negotiation stops; once stop() and the enqueues have
+    returned, every accepted request must have been called back exactly once and no refused one.
+    gap_us = 300 sleeps between the check and the push (TIPS_TEST_ENQUEUE_GAP_US) so that many
+    enqueues straddle the stop: without the re-check after the push, 16-20 of ~20-60 accepted
+    requests per point were never called back."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_stop_race_worker, args=(gap_us, q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(60)
+    for stop_us, rc, (accepted, called, wrong, refused), err in out:
+        assert rc == 0 and wrong == 0, (stop_us, rc, accepted, called, wrong, err)
+        assert called == accepted and accepted + refused == 4 * 3 * (50 if gap_us else 2000)

@@ -150,6 +150,8 @@ _DEV_SIGNATURES = [
     ("tips_host_pool_selftest", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tips_negotiation_selftest", ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
+    ("tips_negotiation_stop_race_selftest", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
     ("tips_ring_simulate", ctypes.c_int,
      [_c_void_pp, _c_void_pp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]),
     ("tips_oneshot_simulate", ctypes.c_int,

@@ -612,8 +612,10 @@ class Negotiator {
     // (no st.mu: the executor holds it while it reduces, and nothing here needs it)
     if (cb && !waiter_started_.load(std::memory_order_acquire)) {
       std::lock_guard<AdaptiveMutex> l(m_);
-      if (!waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
-      waiter_started_.store(true, std::memory_order_release);
+      // (only while running: a waiter started after stop() joined the last one is never joined,
+      // and the negotiator's destructor would end the process on it - ADVICE r05)
+      if (!running_ || waiter_stop_) return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
+      start_waiter_locked();
     }
     if (!lockfree_) {  // (TIPS_ENQUEUE_LOCKFREE=0: round 4's locked commit, for A/B runs only)
       std::unique_lock<AdaptiveMutex> l(m_);
@@ -628,6 +630,10 @@ class Negotiator {
     if (!accepting_.load(std::memory_order_acquire))
       return fail(TIPS_ERR_NOT_INITIALIZED, "negotiation thread is not running");
     const int64_t h = p.r->handle;
+    static std::atomic<int64_t> gap_us{-1};  // (tests: TIPS_TEST_ENQUEUE_GAP_US widens the check-to-push window)
+    int64_t gap = gap_us.load(std::memory_order_relaxed);
+    if (gap < 0) gap_us.store(gap = std::max<int64_t>(0, env_i64("TIPS_TEST_ENQUEUE_GAP_US", 0)), std::memory_order_relaxed);
+    if (gap > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap));
     Pending* node = new Pending{std::move(p), nullptr};
     // (each thread pushes onto its own shard of the stack: drain_locked walks the shards' chains
     // side by side, so their cache misses overlap)
@@ -650,17 +656,42 @@ class Negotiator {
       std::lock_guard<AdaptiveMutex> l(m_);
       cv_.notify_all();
     }
+    // A stop may have closed the door between the check above and the push, and run its last
+    // drain before the push: nobody would ever admit this node, and a callback request's done()
+    // would never fire. The push and this load are sequentially consistent, as are
+    // stop's store and its drain's exchange: either that drain saw the node, or this load sees the
+    // door closed and the node is failed here.
+    if (!accepting_.load(std::memory_order_seq_cst)) reclaim_after_stop();
     return h;
+  }
+
+  // (the lock-free enqueue, after a stop) Fail whatever is left on the submission stacks. While the
+  // completion thread still runs it calls the callbacks (drain_locked queues them); once it has
+  // ended they are called here, outside the lock, as the completion thread would.
+  void reclaim_after_stop() {
+    std::vector<std::shared_ptr<Req>> orphans;
+    {
+      std::lock_guard<AdaptiveMutex> l(m_);
+      drain_locked(waiter_stop_ ? &orphans : nullptr);
+    }
+    for (auto& r : orphans) r->cb(r->cb_ctx, r->code, r->err.c_str());
+  }
+
+  // (m_ held) the completion thread, if it is not running yet
+  void start_waiter_locked() {
+    if (!waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
+    waiter_started_.store(true, std::memory_order_release);
   }
 
   // (m_ held) Admit the lock-free stack's requests to the tables, each thread's in its order, as
   // commit() does for a list; a request that cannot be admitted (a duplicate name, the thread stopped) fails
   // through its handle or callback instead of at its enqueue.
-  int drain_locked() {
+  // orphans: the completion thread has ended; failed callback requests go there instead of to it.
+  int drain_locked(std::vector<std::shared_ptr<Req>>* orphans = nullptr) {
     Pending* heads[kShards];
     int m = 0;
-    for (Shard& sh : shards_)
-      if (Pending* h = sh.head.exchange(nullptr, std::memory_order_acquire)) heads[m++] = h;
+    for (Shard& sh : shards_)  // (seq_cst: pairs with the enqueue's push and its re-check after a stop)
+      if (Pending* h = sh.head.exchange(nullptr, std::memory_order_seq_cst)) heads[m++] = h;
     if (!m) return 0;
     int count = 0;
     int64_t t = adm_prof_ ? steady_ns() : 0;
@@ -708,7 +739,10 @@ class Negotiator {
           r.state = -1;
           r.code = code;
           r.err = why;
-          if (r.cb) queue_done(p.r);
+          if (r.cb) {
+            if (orphans) orphans->push_back(p.r);
+            else queue_done(p.r);
+          }
           cv_.notify_all();
         }
         lap(3);
@@ -799,10 +833,13 @@ class Negotiator {
     if (it == by_handle_.end()) return fail(TIPS_ERR_INVALID_ARG, "unknown request handle %lld", (long long)h);
     auto& r = it->second;
     if (r->cb) return fail(TIPS_ERR_INVALID_ARG, "request %s already has a completion callback", r->name.c_str());
+    if (waiter_stop_) {  // (after stop: no completion thread will come; the request has finished)
+      fn(ctx, r->state < 0 ? r->code : 0, r->state < 0 ? r->err.c_str() : "");
+      return 0;
+    }
     r->cb = fn;
     r->cb_ctx = ctx;
-    if (!waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
-    waiter_started_.store(true, std::memory_order_release);
+    start_waiter_locked();
     if (r->state >= 2 || r->state < 0) queue_done(r);
     return 0;
   }
@@ -818,7 +855,7 @@ class Negotiator {
     if (thread_.joinable()) thread_.join();
     {  // the completion thread drains what is queued (the loop failed every unmatched request), then ends
       std::lock_guard<AdaptiveMutex> l(m_);
-      accepting_.store(false, std::memory_order_release);
+      accepting_.store(false, std::memory_order_seq_cst);
       drain_locked();  // enqueued during the stop: failed (not running)
       waiter_stop_ = true;
       done_cv_.notify_all();
@@ -826,6 +863,7 @@ class Negotiator {
     if (waiter_.joinable()) waiter_.join();
     close_all();
     peers_.clear();
+    release_device_resources();
     return loop_err_.empty() ? 0 : fail(TIPS_ERR_BOOTSTRAP, "%s", loop_err_.c_str());
   }
 
@@ -838,13 +876,36 @@ class Negotiator {
     return cb_called_;
   }
 
+  // The negotiation's own HIP objects, released by stop() (a stopped negotiator can
+  // outlive it in a thread's cached() copy, and its destructor may then run at any time, even
+  // after tips_shutdown or during the runtime's teardown at exit). Only host memory is left to the
+  // destructor, plus the events of requests nobody polled after the stop.
+  void release_device_resources() {
+    std::vector<hipEvent_t> evs;
+    {
+      std::lock_guard<AdaptiveMutex> l(m_);
+      evs.swap(ev_pool_);
+    }
+    for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+    join_ev_.release();
+    if (neg_stream_) (void)hipStreamDestroy(neg_stream_);
+    neg_stream_ = nullptr;
+  }
+
   ~Negotiator() {
-    for (Shard& sh : shards_)
-      for (Pending* q = sh.head.exchange(nullptr); q;) {  // (never admitted)
-        Pending* n = q->next;
-        delete q;
-        q = n;
-      }
+    {  // a completion thread still running (the negotiator was never stopped): let it drain, join it
+      std::lock_guard<AdaptiveMutex> l(m_);
+      waiter_stop_ = true;
+      done_cv_.notify_all();
+    }
+    if (waiter_.joinable()) waiter_.join();
+    std::vector<std::shared_ptr<Req>> orphans;  // never admitted: failed, their callbacks called
+    {
+      std::lock_guard<AdaptiveMutex> l(m_);
+      running_ = false;
+      drain_locked(&orphans);
+    }
+    for (auto& r : orphans) r->cb(r->cb_ctx, r->code, r->err.c_str());
     for (auto& kv : by_handle_)  // never polled to completion
       if (kv.second->ev) ev_pool_.push_back(kv.second->ev);
     for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
@@ -1083,7 +1144,7 @@ class Negotiator {
       if (shutdown) break;
     }
     std::lock_guard<AdaptiveMutex> l(m_);
-    accepting_.store(false, std::memory_order_release);
+    accepting_.store(false, std::memory_order_seq_cst);
     drain_locked();  // (admitted while still running: they join the unmatched below)
     running_ = false;
     std::vector<std::string> unmatched;
@@ -2179,6 +2240,58 @@ int tips_negotiation_selftest(int rank, int size, const char* host, int port, co
   }
   snprintf(out, (size_t)cap, "%s", log.c_str());
   return rc;
+}
+
+// Enqueue-vs-stop race check, one rank, dry executor: `threads` threads enqueue
+// callback requests (tips_enqueue_allreduce_cb's path) as fast as they can while the calling thread
+// stops the negotiation after stop_after_us; `rounds` times. Every enqueue that returned a handle
+// must see its callback exactly once (OK if it ran before the stop, an error after it), and a
+// refused one never. result[0..3]: accepted, callbacks, requests whose callback count was not 1,
+// refusals. TIPS_OK when result[2] == 0 in every round.
+int tips_negotiation_stop_race_selftest(int threads, int per_thread, int stop_after_us, int rounds, int port,
+                                        int64_t* result) {
+  if (threads < 1 || per_thread < 1 || rounds < 1 || !result) return fail(TIPS_ERR_INVALID_ARG, "bad args");
+  for (int k = 0; k < 4; k++) result[k] = 0;
+  struct Slot {
+    std::atomic<int> calls{0};
+    bool accepted = false;
+  };
+  auto count_cb = [](void* ctx, int, const char*) { static_cast<Slot*>(ctx)->calls.fetch_add(1); };
+  for (int round = 0; round < rounds; round++) {
+    std::vector<Slot> slots((size_t)threads * per_thread);
+    {
+      Negotiator neg;
+      TRY(neg.start(0, 1, "127.0.0.1", port, true, 30, 0, 0));
+      std::atomic<bool> go{false};
+      std::vector<std::thread> th;
+      for (int t = 0; t < threads; t++)
+        th.emplace_back([&, t] {
+          while (!go.load()) std::this_thread::yield();
+          const int64_t shape[1] = {4};
+          for (int i = 0; i < per_thread; i++) {
+            Slot& sl = slots[(size_t)t * per_thread + i];
+            const std::string name = "r" + std::to_string(round) + "/t" + std::to_string(t) + "/" + std::to_string(i);
+            const int64_t h = neg.enqueue(name, nullptr, nullptr, shape, 1, TIPS_FLOAT32, nullptr, TIPS_REQ_ALLREDUCE, 0,
+                                          nullptr, nullptr, nullptr, nullptr, nullptr, count_cb, &sl);
+            sl.accepted = h > 0;
+          }
+        });
+      go.store(true);
+      std::this_thread::sleep_for(std::chrono::microseconds(stop_after_us));
+      (void)neg.stop();  // (its verdict is not the point: the callbacks are)
+      for (auto& x : th) x.join();
+      // counted before the destructor, which would fail and call back whatever is still stacked:
+      // once stop() has returned and the enqueues have, every callback must have been called
+      for (auto& sl : slots) {
+        const int c = sl.calls.load();
+        result[0] += sl.accepted;
+        result[1] += c;
+        result[2] += sl.accepted ? c != 1 : c != 0;
+        result[3] += !sl.accepted;
+      }
+    }
+  }
+  return result[2] == 0 ? TIPS_OK : fail(TIPS_ERR_MISMATCH, "%lld requests saw a wrong number of callbacks", (long long)result[2]);
 }
 #endif  // TIPS_DEV
 

@@ -141,7 +141,7 @@ void rccl_env_defaults() {
   // Captured plans (TIPS_GRAPHS) key their graphs by buffer address and allocation id; RCCL's
   // graph-time buffer registration would pin peers' mappings of a buffer past its free, so with
   // replays on it is off unless the user sets it (read by RCCL at its first communicator).
-  if (env_i64("TIPS_GRAPHS", 1) > 0) setenv("NCCL_GRAPH_REGISTER", "0", 0);
+  if (env_i64("TIPS_GRAPHS", 0) > 0) setenv("NCCL_GRAPH_REGISTER", "0", 0);
 }
 
 int ensure_comm(State& st) {

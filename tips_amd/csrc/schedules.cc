@@ -233,7 +233,15 @@ void destroy_exec(State& st, hipGraphExec_t e) {
   (void)hipGraphExecDestroy(e);
 }
 
-// Replays are on (TIPS_GRAPHS=1, the default) where the capture pattern (capture_plan) was seen
+// Replays are opt-in (TIPS_GRAPHS=1; round 6): while a plan is being captured, any
+// other thread's work on the legacy null stream (hipMemcpy, hipMemset, a launch on stream 0 - torch's
+// default stream) makes the HIP runtime invalidate the capture, although every stream in it is
+// non-blocking ("operation would make the legacy stream depend on a capturing blocking stream", in
+// relaxed, thread-local and global mode alike: tools/capture_race_hip.cc, profiles/r06/), and RCCL's
+// group launch does not survive a capture invalidated under it (SIGSEGV in hipGraphRetainUserObject
+// / hipLaunchHostFunc, heap corruption: the round-5 op-body crash). The library cannot see what a
+// host's other threads do, so it captures only when the host says none of them uses the legacy
+// stream. Where opted in, replays run where the capture pattern (capture_plan) was seen
 // to replay correctly: RCCL >= 2.26 on a HIP runtime >= 7.0, i.e. torch's bundled ROCm 7.0.2 (a
 // Python process) and /opt/rocm's 7.2 (a C / cgo / JNI host) - tests/test_gpu_graphs.py and
 // test_gpu_rccl_procs.py::test_replayed_plans_in_python_processes - and for buckets up to
@@ -241,7 +249,7 @@ void destroy_exec(State& st, hipGraphExec_t e) {
 // of a call drops 126 -> 22 us (one-shot p = 2, Python) (profiles/r02/graph_host_cost*.jsonl), and
 // on the p = 2 rehearsal a replayed one-shot was the fastest path at every size from 16 KiB to
 // 8 MiB, 4-30 % under the eager one (profiles/r03/small_bucket_rehearsal_n2_before.json; round 2 stopped
-// at 1 MiB). TIPS_GRAPHS=0 turns them off; 2 forces them on any runtime (probing only).
+// at 1 MiB). TIPS_GRAPHS=0 (the default) keeps them off; 2 forces them on any runtime (probing only).
 // Once an eager plan has had to wait on the host for a replay (order_after_replays: replayed and
 // eager buckets alternate, e.g. a step's buckets straddle the 8 MiB limit), plans up to
 // TIPS_GRAPH_MIXED_MAX_BYTES (1 GiB; 0 keeps the limit) are replayed as well: from their third call
@@ -265,8 +273,8 @@ bool graph_eligible(State& st, const Plan& pl, hipStream_t user) {
   // waiting on events. A plan captured there in a C host (/opt/rocm's 7.2 runtime, RCCL 2.27) with
   // such calls in flight crashed inside RCCL at the capture (tests/c/op_body.c's second step over
   // the same names, 3 ranks); with graphs off the same run is bit-exact. Those plans run eagerly.
-  if (on_negotiation_thread()) return false;
-  const int64_t want = env_i64("TIPS_GRAPHS", 1);
+  if (on_negotiation_thread() && env_i64("TIPS_GRAPHS_NEGOTIATION", 0) == 0) return false;
+  const int64_t want = env_i64("TIPS_GRAPHS", 0);
   if (want <= 0 || (want == 1 && !graphs_supported())) return false;
   int64_t cap = env_i64("TIPS_GRAPH_MAX_BYTES", 8 << 20);
   if (st.replays_mixed) cap = std::max(cap, env_i64("TIPS_GRAPH_MIXED_MAX_BYTES", int64_t(1) << 30));
@@ -893,7 +901,7 @@ int tips_graph_stats(int64_t* captured, int64_t* replayed, int64_t* cached) {
   if (st.graphs)
     for (const auto& kv : st.graphs->m) *cached += kv.second.exec != nullptr;
   if (st.graphs && st.graphs->off) return 1;
-  const int64_t want = env_i64("TIPS_GRAPHS", 1);
+  const int64_t want = env_i64("TIPS_GRAPHS", 0);
   if (want <= 0 || (want == 1 && !graphs_supported())) return 2;
   return st.replays_yield ? 3 : 0;
 }
