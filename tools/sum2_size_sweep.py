@@ -1,0 +1,58 @@
+"""The 2-input sum's HBM rate against operand size and launch shape (the p = 2
+fold of 2 x 128 MiB ran at 0.75 of HBM against 0.82 for config 2's 2 x 256 MiB).
+
+For each operand size, every variant (tips_sum_variant, the development library) runs over 4
+rotating buffer sets (so no launch finds its operands in the Infinity Cache), interleaved over
+ROUNDS rounds; one JSON line per (size, variant) with the best round's us per launch and its
+fraction of 8 TB/s (3 x size bytes per launch)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tips_amd import _lib  # noqa: E402
+
+D = _lib.dev()
+torch.cuda.set_device(0)
+s = torch.cuda.current_stream()
+SIZES = [int(x) for x in os.environ.get("SIZES_MIB", "64,128,192,256").split(",")]
+ROUNDS = int(os.environ.get("ROUNDS", "3"))
+# (name, mode, unroll, nt index, LDS bytes per workgroup, threads): mode 3 = buffer ops (nt index 1 =
+# nt loads + sc1 stores, the shipped policy); blocks = unused LDS reserved per workgroup
+VARIANTS = [("shipped", 3, 1, 1, 0, 256), ("u2", 3, 2, 1, 0, 256), ("u4", 3, 4, 1, 0, 256),
+            ("t512", 3, 1, 1, 0, 512), ("t128", 3, 1, 1, 0, 128), ("u2t512", 3, 2, 1, 0, 512),
+            ("cap8", 3, 1, 1, 20480, 256), ("cap4", 3, 1, 1, 40960, 256), ("cap3", 3, 1, 1, 53248, 256)]
+for mib in SIZES:
+    n = mib << 18
+    sets = [(torch.randn(n, device="cuda"), torch.randn(n, device="cuda"), torch.empty(n, device="cuda"))
+            for _ in range(4)]
+    best = {}
+    for rnd in range(ROUNDS):
+        for name, mode, unroll, nt, blocks, threads in (VARIANTS if rnd % 2 == 0 else VARIANTS[::-1]):
+            def launch(i):
+                a, b, c = sets[i % 4]
+                rc = D.tips_sum_variant(c.data_ptr(), a.data_ptr(), b.data_ptr(), n, _lib.FLOAT32, mode, unroll, nt,
+                                        blocks, threads, s.cuda_stream)
+                assert rc == 0, (name, rc)
+            for i in range(8):
+                launch(i)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            K = 40
+            e0.record(s)
+            for i in range(K):
+                launch(i)
+            e1.record(s)
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / K * 1e3
+            best[name] = min(us, best.get(name, us))
+    a, b, c = sets[0]
+    ok = bool(torch.equal(c, a + b))  # (the last launch of the last variant wrote set 3; set 0 earlier)
+    for name, *_ in VARIANTS:
+        us = best[name]
+        print(json.dumps({"operand_MiB": mib, "variant": name, "us_per_launch": round(us, 2),
+                          "frac_of_8TBps": round(3 * n * 4 / us / 1e6 / 8.0, 4), "check": ok}), flush=True)
+    del sets
+    torch.cuda.empty_cache()
