@@ -205,6 +205,45 @@ def cpu_ring_baseline(world, elems=16 << 20, iters=20):
                       % (elems, world, elems * 4 >> 20, iters, world)}
 
 
+def thread_placement(names=("tips-neg", "tips-done")):
+    """Where this process's main thread and the library's named threads last ran (/proc/self/task/*/stat
+    field 39), each with its L3 domain (a CCD on EPYC: the first CPU sharing its L3) and socket (VERDICT
+    r05 item 3: which placement makes the negotiated path slow)."""
+    def cpu_info(cpu):
+        base = "/sys/devices/system/cpu/cpu%d" % cpu
+        try:
+            with open(base + "/cache/index3/shared_cpu_list") as f:
+                l3 = int(f.read().split(",")[0].split("-")[0])
+        except (OSError, ValueError):
+            l3 = None
+        try:
+            with open(base + "/topology/physical_package_id") as f:
+                sock = int(f.read())
+        except (OSError, ValueError):
+            sock = None
+        return {"cpu": cpu, "l3_first_cpu": l3, "socket": sock}
+
+    out = {}
+    try:
+        for tid in os.listdir("/proc/self/task"):
+            with open("/proc/self/task/%s/comm" % tid) as f:
+                comm = f.read().strip()
+            if int(tid) != os.getpid() and comm not in names:
+                continue
+            with open("/proc/self/task/%s/stat" % tid) as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            out["caller" if int(tid) == os.getpid() else comm] = cpu_info(int(fields[36]))  # (field 39 overall)
+    except (OSError, ValueError, IndexError):
+        return None
+    if len(out) > 1:
+        l3s = {v["l3_first_cpu"] for v in out.values()}
+        socks = {v["socket"] for v in out.values()}
+        out["same_l3"] = len(l3s) == 1
+        out["same_socket"] = len(socks) == 1
+    out["bind"] = os.environ.get("TIPS_NEG_BIND") or "l3 (the default)"
+    return out
+
+
 def pmc_traffic(kernel_substr, file_pattern="*pmc*.json"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/<file_pattern>), or None."""
     import glob
@@ -381,7 +420,9 @@ def fusion_one_rank_kernels(torch, L, _lib, sizes, offs, rot_sets, cp, stream, m
     """One rank, configs 4/5: (1) the fusion's pack kernel - the launch fusion.cc issues per bucket
     (copy_segs_kernel over the bucket's tiles of the layout), through tips_fused_pack_bucket - over
     rotating gradient sets, HIP events on the launch stream: the dominant kernel's roofline (unpack
-    is the same kernel with source and destination swapped); (2) the whole fused step captured
+    is the same kernel with source and destination swapped); beside it the opt-in merged form, every
+    bucket of the step in one launch (TIPS_PACK_MERGE=1, copy_segs_groups_kernel); (2) the whole
+    fused step captured
     into one HIP graph per gradient set (torch.cuda.graph around tips_fused_allreduce) and
     replayed: the step without its host cost."""
     nb = int(_lib.check("tips_fused_pack_bucket", L.tips_fused_pack_bucket(rot_sets[0][1], cp, len(sizes),
@@ -425,16 +466,63 @@ def fusion_one_rank_kernels(torch, L, _lib, sizes, offs, rot_sets, cp, stream, m
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / (reps * nb)
     per_launch = 2 * sum(payload) / nb  # read + write of one bucket's tensors
+    per_bucket = {"us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": int(per_launch),
+                  "frac": round(per_launch / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                  "kernel": "copy_segs_kernel", "check": "bit-exact bucket bytes" if ok else "FAIL: packed bytes differ",
+                  "note": "one launch per bucket (tips_fused_pack_bucket), as fusion.cc packed a step before round 6"}
+    del dst
+    # the step's packs as fusion.cc issues them (round 6): every bucket of the step in ONE launch
+    # (copy_segs_groups_kernel, bucket 0's tiles first), timed through tips_fused_allreduce_flat at one
+    # rank with TIPS_FUSION_MEASURE_PACK=1 (pack into the flat output; the identity allreduce skipped)
+    flat_bytes = int(_lib.check("tips_fused_layout", L.tips_fused_layout(cp, len(sizes), _lib.FLOAT32, None)))
+    flat = torch.empty(flat_bytes // 4 + 64, dtype=torch.float32, device="cuda")
+
+    def merged(r):
+        rc = L.tips_fused_allreduce_flat(rot_sets[r][1], cp, len(sizes), _lib.FLOAT32, flat.data_ptr(), sp)
+        if rc < 0:
+            raise _lib.TipsError("tips_fused_allreduce_flat", int(rc), _lib.last_error())
+
+    saved = (os.environ.get("TIPS_FUSION_MEASURE_PACK"), os.environ.get("TIPS_PACK_MERGE"))
+    os.environ["TIPS_FUSION_MEASURE_PACK"] = "1"
+    os.environ["TIPS_PACK_MERGE"] = "1"
+    try:
+        for r in range(len(rot_sets)):  # (tables built and uploaded once per set)
+            merged(r)
+        torch.cuda.synchronize()
+        fv = flat.view(torch.uint8)
+        ok_m = all(torch.equal(fv[int(lo[i]):int(lo[i]) + sizes[i] * 4],
+                               rot_sets[len(rot_sets) - 1][0][offs[i]:offs[i] + sizes[i]].view(torch.uint8))
+                   for i in range(len(sizes)))
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(12_000_000)
+        e0.record(stream)
+        for k in range(reps):
+            merged(k % len(rot_sets))
+        e1.record(stream)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in zip(("TIPS_FUSION_MEASURE_PACK", "TIPS_PACK_MERGE"), saved):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    mus = e0.elapsed_time(e1) * 1e3 / reps
+    per_merged = 2 * sum(payload)  # read + write of every packed tensor of the step
     roof = {"bound": "hbm", "achieved": round(per_launch / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(per_launch / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+            "frac": per_bucket["frac"], "traffic": None,
             "kernel": "copy_segs_kernel (fusion pack; unpack is the same kernel, source and destination swapped)",
             "us_per_launch": round(us, 2), "algorithmic_bytes_per_launch": int(per_launch),
-            "launches_per_step": 2 * nb, "buckets": nb, "tile_bytes": tile,
-            "check": "bit-exact bucket bytes" if ok else "FAIL: packed bytes differ",
+            "launches_per_step": 2 * nb, "buckets": nb, "tile_bytes": tile, "check": per_bucket["check"],
+            "merged_launch": {"us_per_launch": round(mus, 2), "algorithmic_bytes_per_launch": int(per_merged),
+                              "frac": round(per_merged / (mus * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                              "kernel": "copy_segs_groups_kernel",
+                              "check": "bit-exact packed bytes (every tensor)" if ok_m else "FAIL: packed bytes differ",
+                              "note": "TIPS_PACK_MERGE=1 (opt-in): the step's %d buckets in ONE pack launch, through "
+                                      "tips_fused_allreduce_flat with TIPS_FUSION_MEASURE_PACK=1" % nb},
             "note": "per-bucket pack launches of fusion.cc's layout (tips_fused_pack_bucket), gradient set i %% %d "
                     "(HBM-only), HIP events on the launch stream; algorithmic bytes = read + write of the bucket's "
                     "tensors" % len(rot_sets)}
-    del dst
+    del flat
     # the whole step, captured once per gradient set and replayed
     side = torch.cuda.Stream()
     side.wait_stream(stream)
@@ -486,9 +574,11 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         params.append(ps)
     grads = [[p_.grad for p_ in ps] for ps in params]
     opts = [tips_amd.DistributedOptimizer(torch.optim.SGD(ps, lr=0.0)) for ps in params]
+    fp16 = tips_amd.Compression.fp16
     if world > 1:
-        calls = {"optimizer": lambda i: opts[i].synchronize(whole_groups=True), "allreduce_grads": lambda i: tips_amd.allreduce_grads(grads[i])}
-        what = "DistributedOptimizer.synchronize() / tips_amd.allreduce_grads"
+        calls = {"optimizer": lambda i: opts[i].synchronize(whole_groups=True), "allreduce_grads": lambda i: tips_amd.allreduce_grads(grads[i]),
+                 "fp16_compressed": lambda i: tips_amd.allreduce_grads(grads[i], compression=fp16)}
+        what = "DistributedOptimizer.synchronize() / tips_amd.allreduce_grads (and with Compression.fp16)"
     else:
         from tips_amd.ops import FusedList
         fls = [FusedList([p_.numel() for p_ in ps]) for ps in params]
@@ -496,12 +586,14 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         from tips_amd.optim import _allreduce_flat_
         calls = {"optimizer": lambda i: _allreduce_flat_(flats[i]),
                  "packed_separate_grads": lambda i: fls[i].allreduce_(grads[i]),
-                 "allreduce_grads": lambda i: tips_amd._reduce_grads(grads[i])}
+                 "allreduce_grads": lambda i: tips_amd._reduce_grads(grads[i]),
+                 "fp16_compressed": lambda i: tips_amd._reduce_grads(grads[i], compression=fp16)}
         what = ("one rank: both API calls are the identity (reference _allreduce_cond); timed is what each runs at "
                 "N > 1: the optimizer's in-place allreduce of the flat buffer its gradient bucket views live in "
                 "(no device work at all on one rank), FusedList.allreduce_ over separately allocated gradients "
-                "(pack + unpack), and allreduce_grads' N > 1 body (_reduce_grads: pack into one flat output, "
-                "per bucket)")
+                "(pack + unpack), allreduce_grads' N > 1 body (_reduce_grads: pack into one flat output, "
+                "per bucket), and the same with Compression.fp16 (one tips_fused_allreduce_cast: cast while packed, "
+                "cast back while unpacked; at one rank the reference's round trip f32 -> f16 -> f32)")
     import warnings  # (the optimizer leg calls synchronize() repeatedly with no backward: it warns)
     warnings.filterwarnings("ignore", message="DistributedOptimizer.synchronize")
     out = {"calls": what, "bytes_per_rank": sum(sizes) * 4, "fixed_view_ms": round(fixed_ms, 4)}
@@ -522,15 +614,23 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
         leg = {"ms_per_step": round(t * 1e3, 4), "vs_fixed_view": round(t * 1e3 / fixed_ms, 3)}
         if world == 1:
             # bucket views: nothing to pack; flat outputs: pack only; separate outputs: pack + unpack
-            moved = {"optimizer": 0, "allreduce_grads": 2 * sum(sizes) * 4}.get(name, 4 * sum(sizes) * 4)
+            # (fp16: pack reads 4 B and writes 2 B per element, unpack reads 2 B and writes 4 B)
+            moved = {"optimizer": 0, "allreduce_grads": 2 * sum(sizes) * 4,
+                     "fp16_compressed": 12 * sum(sizes)}.get(name, 4 * sum(sizes) * 4)
             leg["algorithmic_hbm_bytes"] = moved
             if moved:
                 leg["hbm_achieved_GBps"] = round(moved / t / 1e9, 1)
+                leg["frac_of_hbm"] = round(moved / t / 1e9 / HBM_PEAK_GBPS, 4)
             got = fn(0)
             torch.cuda.synchronize()
             got = {"optimizer": [flats[0]], "packed_separate_grads": grads[0]}.get(name, got)
-            leg["check"] = "identity, bit-exact" if torch.equal(torch.cat([g.reshape(-1) for g in got]), ref[0]) else "FAIL"
+            want = ref[0].half().float() if name == "fp16_compressed" else ref[0]  # (torch's cast: RNE, as the oracle's)
+            leg["check"] = ("%s, bit-exact" % ("round trip through f16" if name == "fp16_compressed" else "identity")
+                            if torch.equal(torch.cat([g.reshape(-1) for g in got]), want) else "FAIL")
         out[name] = leg
+    if "fp16_compressed" in out and "allreduce_grads" in out:
+        out["fp16_compressed"]["vs_fp32_allreduce_grads"] = round(
+            out["fp16_compressed"]["ms_per_step"] / out["allreduce_grads"]["ms_per_step"], 3)
     del params, grads, opts
     return out
 
@@ -1235,6 +1335,7 @@ class Workload(object):
                     rec["roofline"]["traffic"] = round(tr["bytes"])
                     rec["roofline"]["traffic_source"] = tr["source"]
         if self.workload == "negotiated1000":
+            rec["placement"] = thread_placement()  # (right after the timed steps: where they ran)
             rec["per_tensor_us"] = round(ms * 1e3 / len(self.sizes), 2)
             rec["host_us_per_tensor"] = {k: round(v / self.steps / len(self.sizes) * 1e6, 2) for k, v in self.host_split.items()}
             rec["api"] = "tips_enqueue_allreduce_n + tips_wait_n (1000 named requests, one call each way)"
@@ -1662,6 +1763,9 @@ def sub_records(job, line, steps):
             if wl in SUB_WORKLOADS and job.afford("%s gradient_api legs" % key, 25):
                 rec["gradient_api"] = gradient_api_legs(job.torch, job.dist, job.tips_amd, job.world, w.sizes, w.offs,
                                                         w.rot_sets, min(steps, 10), w.ms)
+                if "fp16_compressed" in rec["gradient_api"]:  # (beside the fp32 step)
+                    rec["fp16_compressed"] = dict(rec["gradient_api"]["fp16_compressed"],
+                                                  fp32_allreduce_grads_ms=rec["gradient_api"]["allreduce_grads"]["ms_per_step"])
             if wl == "resnet50" and job.afford("config5 host legs", 40):
                 host_legs(job, w, rec)
                 if job.world == 1:

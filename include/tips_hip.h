@@ -219,6 +219,19 @@ TIPS_API int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int 
  * allreduce loop returns (tips/tensorflow/__init__.py:203-222), fused. */
 TIPS_API int tips_fused_allreduce_oop(const void* const* ins, void* const* outs, const int64_t* counts, int n,
                                       int dtype, void* stream);
+
+/* Compression.fp16 fused into the buckets (tips/tensorflow/compression.py:49-66 cast per tensor
+ * before and after the allreduce, __init__.py:81-88): n f32 device tensors in[i] -> out[i]
+ * (in == out allowed) allreduced in `wire_dtype` (TIPS_FLOAT16 or TIPS_BFLOAT16). Each tensor is cast
+ * to the wire type (round to nearest even) as it is packed into a fusion bucket, every bucket is
+ * allreduced in the wire type (half the bytes on the links), and cast back to f32 as it is
+ * unpacked: one pack and one unpack launch per bucket instead of two casts per tensor. The
+ * results are those of the per-tensor compress -> allreduce -> decompress. At one rank: the round
+ * trip through the wire type. dtype must be TIPS_FLOAT32 (else TIPS_ERR_UNSUPPORTED), device memory,
+ * stream-ordered as tips_fused_allreduce; routed through the negotiation (announced with the wire
+ * type) once one runs. */
+TIPS_API int tips_fused_allreduce_cast(const void* const* ins, void* const* outs, const int64_t* counts, int n,
+                                       int dtype, int wire_dtype, void* stream);
 /* The byte offset of each tensor of a fused list in ONE flat buffer laid out as the fusion buckets
  * (offsets[i], 256-B aligned; may be NULL); returns the flat buffer's size in bytes (< 0 = error).
  * A pure host function of counts, dtype and TIPS_FUSION_THRESHOLD - the same on every rank. */

@@ -89,6 +89,20 @@ uint16_t oracle_float_to_bf16(float f) {
   return (uint16_t)((x + 0x7fffu + ((x >> 16) & 1u)) >> 16);
 }
 
+int oracle_cast_to16(int code, uint16_t* out, const float* in, int64_t n) {
+  int64_t i;
+  if (code != ORACLE_F16 && code != ORACLE_BF16) return -1;
+  for (i = 0; i < n; i++) out[i] = code == ORACLE_F16 ? oracle_float_to_half(in[i]) : oracle_float_to_bf16(in[i]);
+  return 0;
+}
+
+int oracle_cast_from16(int code, float* out, const uint16_t* in, int64_t n) {
+  int64_t i;
+  if (code != ORACLE_F16 && code != ORACLE_BF16) return -1;
+  for (i = 0; i < n; i++) out[i] = code == ORACLE_F16 ? oracle_half_to_float(in[i]) : oracle_bf16_to_float(in[i]);
+  return 0;
+}
+
 /* ---- one MPI_SUM step: out = a + b ------------------------------------- */
 
 int oracle_sum2(int dtype, void* out, const void* a, const void* b, int64_t n) {

@@ -42,6 +42,8 @@ def load():
     L.oracle_bf16_to_float.restype = ctypes.c_float
     L.oracle_float_to_bf16.argtypes = [ctypes.c_float]
     L.oracle_float_to_bf16.restype = ctypes.c_uint16
+    L.oracle_cast_to16.argtypes = [ctypes.c_int, vp, vp, i64]
+    L.oracle_cast_from16.argtypes = [ctypes.c_int, vp, vp, i64]
     _lib = L
     return L
 
@@ -81,3 +83,28 @@ def chunk_bounds(n, p, align_elems, c):
     b, e = ctypes.c_int64(), ctypes.c_int64()
     load().oracle_chunk_bounds(n, p, align_elems, c, ctypes.byref(b), ctypes.byref(e))
     return b.value, e.value
+
+
+def cast_to16(x, code):
+    """float32 array -> uint16 bits of F16 / BF16 (RNE): Compression.fp16's compress (compression.py:49-66)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.shape, dtype=np.uint16)
+    assert load().oracle_cast_to16(code, out.ctypes.data, x.ctypes.data, x.size) == 0
+    return out
+
+
+def cast_from16(h, code):
+    """uint16 bits of F16 / BF16 -> float32 (exact): the decompress."""
+    h = np.ascontiguousarray(h, dtype=np.uint16)
+    out = np.empty(h.shape, dtype=np.float32)
+    assert load().oracle_cast_from16(code, out.ctypes.data, h.ctypes.data, h.size) == 0
+    return out
+
+
+def compressed_fold(ins, code):
+    """What Compression.fp16 (code F16) or a bf16 wire gives for an allreduce of f32 inputs under a
+    rank-order schedule: each rank's tensor cast to the 16-bit type, folded in rank order in fp32
+    and rounded once (the library's f16 / bf16 fold: oracle_fold wide_acc), cast back to f32."""
+    folded = fold([cast_to16(x, code).view(np.float16 if code == F16 else np.uint16) for x in ins], code=code,
+                  wide_acc=True)
+    return cast_from16(folded.view(np.uint16), code)

@@ -581,6 +581,17 @@ def fused_case(c, rank, size, L, _lib, sp):
         L.tips_graph_stats(ctypes.byref(cap), ctypes.byref(rep), ctypes.byref(cached))
         return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": True, "error": "",
                 "waits_after_each_call": waits, "captured": cap.value, "replayed": rep.value}
+    elif mode in ("fp16", "fp16_fresh_outputs"):
+        # Compression.fp16 fused into the buckets (allreduce_grads -> tips_fused_allreduce_cast): f32
+        # in, f32 out, f16 on the wire; the second form releases the outputs and calls again, so the
+        # flat output set is reused (and the layout and tables found)
+        got = tips_amd.allreduce_grads(views, compression=tips_amd.Compression.fp16)
+        if mode == "fp16_fresh_outputs":
+            torch.cuda.synchronize()
+            del got
+            got = tips_amd.allreduce_grads(views, compression=tips_amd.Compression.fp16)
+    elif mode == "bf16_wire":
+        got = tips_amd.fused_allreduce_cast(views, "bfloat16")
     elif mode == "host_grads":
         # the reference's op is a CPU op (ops.cc:118): host gradients (numpy), fused into page-locked
         # pieces (tips_fused_allreduce_host) by allreduce_grads
@@ -598,7 +609,13 @@ def fused_case(c, rank, size, L, _lib, sp):
         got = [0.0 - p.detach() for p in params]  # p = 0 - 1.0 * sum exactly (0 - p: no -0.0 where sum == +0)
     torch.cuda.synchronize()
     allin = np.stack([inputs(r).cpu().numpy() for r in range(size)])
-    exp = oracle_bind.fold([allin[r] for r in range(size)], code=0, wide_acc=True)
+    if mode in ("fp16", "fp16_fresh_outputs", "bf16_wire"):  # cast -> rank-order 16-bit fold -> cast back
+        exp = oracle_bind.compressed_fold([allin[r] for r in range(size)],
+                                          oracle_bind.BF16 if mode == "bf16_wire" else oracle_bind.F16)
+        if not all(t.dtype == torch.float32 for t in got):
+            return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": False, "error": "outputs not float32"}
+    else:
+        exp = oracle_bind.fold([allin[r] for r in range(size)], code=0, wide_acc=True)
     got_flat = torch.cat([t.reshape(-1) for t in got]).cpu().numpy()
     bad = []
     if not np.array_equal(got_flat.view(np.uint32), exp.view(np.uint32)):
@@ -612,7 +629,7 @@ def fused_case(c, rank, size, L, _lib, sp):
                     i, k, d.size, int(d[0]), int(d[-1]), float(got_flat[j]), float(exp[j]), own))
             off += k
         bad.append("%d of %d tensors differ: %s" % (len(wrong), len(sizes), "; ".join(wrong[:3])))
-    if mode in ("oop", "grads") and not torch.equal(mine, before):
+    if mode in ("oop", "grads", "fp16", "fp16_fresh_outputs", "bf16_wire") and not torch.equal(mine, before):
         bad.append("inputs modified by an out-of-place call")
     return {"case": {"fused": c["fused"], "mode": mode}, "rc": 0, "ok": not bad, "error": "; ".join(bad)}
 

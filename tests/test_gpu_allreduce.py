@@ -198,6 +198,55 @@ def test_rccl_allreduce_single_rank(gpu):
         gpu.set_algorithm(prev)
 
 
+@pytest.mark.parametrize("wire", ["float16", "bfloat16"])
+@pytest.mark.parametrize("threshold", [4096, 64 << 20])
+def test_fused_cast_round_trip(gpu, monkeypatch, threshold, wire):
+    """One rank: tips_fused_allreduce_cast is the round trip f32 -> wire -> f32 (the reference's
+    compress -> allreduce -> decompress at one rank, compression.py:49-66), bit-exact against the
+    oracle's casts (RNE): 300 odd-sized misaligned views (ragged ends: the kernel's per-element
+    path), a tensor above the threshold at 4096 (the range-cast path through the scratch buffer),
+    values that round to f16 subnormals and overflow to inf; out of place through
+    tips_amd.fused_allreduce_cast and in place through the C-ABI; the inputs of the out-of-place
+    call unchanged."""
+    import torch
+    import oracle_bind
+    from tips_amd import _lib
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", str(threshold))
+    code = oracle_bind.F16 if wire == "float16" else oracle_bind.BF16
+    rng = np.random.default_rng(7)
+    sizes = [int(round(2 ** rng.uniform(0, 14))) for _ in range(300)] + [5000, 1, 70001]
+    vals = rng.standard_normal(sum(sizes) + len(sizes) + 1).astype(np.float32)
+    vals[::97] *= 1e-6   # f16 subnormals
+    vals[::211] *= 1e5   # beyond f16's range: inf
+    base = torch.from_numpy(vals).cuda()
+    views, off = [], 1  # offset 1: misaligned views (4-B aligned f32 sides), a gap after each
+    for k in sizes:
+        views.append(base[off:off + k])
+        off += k + 1
+    before = base.clone()
+    exp = [oracle_bind.cast_from16(oracle_bind.cast_to16(v.cpu().numpy(), code), code) for v in views]
+    for _ in range(2):  # (the second call finds the layout and the table)
+        outs = gpu.fused_allreduce_cast(views, wire)
+        torch.cuda.synchronize()
+        for o, e in zip(outs, exp):
+            assert o.dtype == torch.float32
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), e.view(np.uint32))
+        del outs
+    assert torch.equal(base, before)
+    # in place through the C-ABI (in == out)
+    pp, _k = _lib.ptr_array([v.data_ptr() for v in views])
+    cp, _k2 = _lib.i64_array(sizes)
+    wcode = _lib.FLOAT16 if wire == "float16" else _lib.BFLOAT16
+    _lib.call("tips_fused_allreduce_cast", pp, pp, cp, len(sizes), _lib.FLOAT32, wcode,
+              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for v, e in zip(views, exp):
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), e.view(np.uint32))
+    # only f32 tensors, only 16-bit wires
+    assert _lib.lib().tips_fused_allreduce_cast(pp, pp, cp, len(sizes), _lib.FLOAT64, wcode, None) == -5
+    assert _lib.lib().tips_fused_allreduce_cast(pp, pp, cp, len(sizes), _lib.FLOAT32, _lib.FLOAT32, None) == -5
+
+
 @pytest.mark.parametrize("measure_pack", ["1", "0"])
 @pytest.mark.parametrize("threshold", [4096, 64 << 20])
 def test_fused_pack_unpack_round_trip(gpu, monkeypatch, threshold, measure_pack):

@@ -82,6 +82,37 @@ def test_fusion_workloads_over_rccl(gpu, workload, p):
     check(run_job(p, cases, timeout=600, **rccl_env("auto")))
 
 
+@pytest.mark.parametrize("workload,p", [("config4", 3), ("config5", 3), ("config4", 8), ("config5", 8)])
+def test_fp16_compression_fused_over_rccl(gpu, workload, p):
+    """Compression.fp16 fused into the bucket path. allreduce_grads(...,
+    compression=Compression.fp16) issues ONE tips_fused_allreduce_cast per list: every f32 gradient
+    cast to f16 (RNE) as it is packed, each bucket allreduced in f16 (half the bytes on the links),
+    cast back as it is unpacked - no per-tensor cast launches. Bit-exact against the oracle's
+    cast -> rank-order f16 fold (fp32 accumulate, one rounding) -> cast back, over 3 and 8 RCCL
+    ranks, configs 4 and 5; also with the outputs released and the call repeated (flat outputs
+    reused), and with a bf16 wire (tips_amd.fused_allreduce_cast(..., "bfloat16")). The reference
+    casts per tensor (tips/tensorflow/compression.py:49-66); its op has no 16-bit allreduce
+    (ops.cc:121), so the 16-bit fold itself is parity-unpinned."""
+    cases = [{"fused": workload, "seed": 12, "mode": m} for m in ("fp16", "fp16_fresh_outputs", "bf16_wire")]
+    check(run_job(p, cases, timeout=600, **rccl_env("auto")))
+
+
+@pytest.mark.parametrize("variant", ["merged_signals", "merged_no_signals"])
+def test_fusion_pack_launch_variants_over_rccl(gpu, variant):
+    """VERDICT r05 item 4, opt-in (TIPS_PACK_MERGE=1): a step's first two pack launches (the slot
+    path) and all of the flat path's are one launch (copy_segs_groups_kernel). With signals (the
+    default when merged) the bucket stream waits on the device for each bucket (hipStreamWaitValue64
+    on a signal word the bucket's last workgroup raises); without (TIPS_PACK_SIGNALS=0) for the
+    launch as a whole. Both bit-exact over 3 RCCL ranks, configs 4 and 5, in place, out of place and
+    through allreduce_grads (the flat path). Per-bucket launches (the default) are covered above."""
+    env = rccl_env("auto")
+    env.update(TIPS_PACK_MERGE="1")
+    if variant == "merged_no_signals":
+        env.update(TIPS_PACK_SIGNALS="0")
+    cases = [{"fused": w, "seed": 6, "mode": m} for w in ("config4", "config5") for m in ("inplace", "oop", "grads")]
+    check(run_job(3, cases, timeout=600, **env))
+
+
 @pytest.mark.parametrize("p", [2, 3])
 def test_fusion_buckets_mixed_with_a_replayed_list(gpu, p):
     """Config 4's fusion buckets (two of ~41 MB: eager) alternating with a 2.5 MiB list (one bucket,

@@ -180,3 +180,25 @@ def test_reference_kat_binary():
     exe = os.path.join(REPO, "oracle", "_ref", "mpi_allreduce_test")
     r = subprocess.run(["/opt/conda/bin/mpirun", "-np", "3", exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_compression_casts_match_numpy_and_rne():
+    """The oracle's Compression.fp16 casts (oracle_cast_to16 / oracle_cast_from16, the checker of
+    tips_fused_allreduce_cast): f32 -> f16 equals numpy's IEEE cast (RNE, subnormals, overflow to
+    inf) on every value class; f32 -> bf16 -> f32 rounds to nearest even on the 16 dropped bits."""
+    import numpy as np
+    import oracle_bind as ob
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.standard_normal(200000).astype(np.float32),
+                        (rng.standard_normal(20000) * 1e-6).astype(np.float32),   # f16 subnormals
+                        (rng.standard_normal(20000) * 1e5).astype(np.float32),    # f16 overflow
+                        np.array([0.0, -0.0, np.inf, -np.inf, 65504.0, 65520.0, 65519.99, 2 ** -24, 2 ** -25],
+                                 dtype=np.float32)])
+    h = ob.cast_to16(x, ob.F16)
+    assert np.array_equal(h, x.astype(np.float16).view(np.uint16))
+    assert np.array_equal(ob.cast_from16(h, ob.F16), x.astype(np.float16).astype(np.float32))
+    b = ob.cast_to16(x, ob.BF16).astype(np.uint32)
+    u = x.view(np.uint32).astype(np.uint64)
+    exp = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint32)
+    assert np.array_equal(b, exp)
+    assert np.array_equal(ob.cast_from16(b.astype(np.uint16), ob.BF16).view(np.uint32), b << 16)

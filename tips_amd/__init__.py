@@ -10,7 +10,7 @@ from .basics import TipsBasics, init, is_initialized, rank, shutdown, size
 from .compression import Compression, Compressor, FP16Compressor, NoneCompressor
 from .ops import (Handle, allgather_async, allgather_op, allreduce_async, broadcast_async, allreduce_async_many, synchronize_many, allreduce_op, broadcast_op, poll, synchronize, broadcast_variables, bucket_sum, fused_allreduce,
                   fused_allreduce_, rank_op, registered_host_buffer, set_algorithm, set_consistency_check, size_op)
-from .ops import fused_allreduce_flat, fused_allreduce_host, fused_allreduce_host_flat, fusion_stats
+from .ops import fused_allreduce_cast, fused_allreduce_flat, fused_allreduce_host, fused_allreduce_host_flat, fusion_stats
 from ._lib import TipsError, TipsLibraryError
 from . import ops as _ops
 from . import tensors as _tensors
@@ -35,7 +35,7 @@ __all__ = [
     "shutdown",
     "is_initialized", "size", "rank", "size_op", "rank_op", "set_algorithm", "Compression", "Compressor",
     "NoneCompressor", "FP16Compressor", "Average", "Sum", "TipsBasics", "TipsError", "TipsLibraryError",
-    "DistributedOptimizer", "DistributedGradientTape", "fused_allreduce_flat", "fused_allreduce_host", "fused_allreduce_host_flat", "fusion_stats",
+    "DistributedOptimizer", "DistributedGradientTape", "fused_allreduce_cast", "fused_allreduce_flat", "fused_allreduce_host", "fused_allreduce_host_flat", "fusion_stats",
 ]
 
 
@@ -143,6 +143,10 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
     if _DATA_PTR is None:
         import torch
         _DATA_PTR = torch.Tensor.data_ptr
+    if fused and grads and compression is FP16Compressor:  # (one list of dense f32 device tensors)
+        res = _ops._dev_list_cast(grads)
+        if res is not None:
+            return res
     if fused and none and grads:
         res = _ops._dev_list_flat(grads)  # (one dtype of dense device tensors: the common case)
         if res is not None:
@@ -154,8 +158,9 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
                 return res
             _PLANS.remove(plan)
     out = list(grads)
-    dev, host = {}, {}
+    dev, host, cast = {}, {}, {}
     simple = fused and none  # only dense, contiguous device tensors: the split can be remembered
+    fp16 = fused and compression is FP16Compressor
     for i, g in enumerate(grads):
         if g is None:
             continue
@@ -166,6 +171,11 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
         if kind is None:
             out[i] = allreduce(g, compression=compression, op=op)
             simple = False
+            continue
+        if fp16 and kind == "dev" and g.dtype == _torch().float32:
+            # Compression.fp16 fused into the buckets: cast while packed, fp16 on the wire, cast back
+            # while unpacked (tips_fused_allreduce_cast) - no per-tensor cast launches
+            cast.setdefault(g.device, []).append((i, g if g.is_contiguous() else g.contiguous()))
             continue
         c, ctx = (g, None) if none else compression.compress(g)
         if kind == "dev":
@@ -184,6 +194,9 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
         for (i, _, ctx), s in zip(members, sums):
             out[i] = s if none else compression.decompress(s, ctx)
         plan_groups.append(([i for i, _, _ in members], None, None))
+    for members in cast.values():
+        for (i, _), s in zip(members, _ops.fused_allreduce_cast([c for _, c in members], "float16")):
+            out[i] = s
     for members in host.values():
         ts = [c for _, c, _ in members]
         sums = _ops.fused_allreduce_host_flat(ts)
@@ -205,6 +218,11 @@ def _reduce_grads(grads, compression=Compression.none, op=None, fused=True):
 
 
 _DATA_PTR = None  # torch.Tensor.data_ptr, bound on first use
+
+
+def _torch():
+    import torch
+    return torch
 _PLANS = []       # recent _GradPlans, most recent first
 
 

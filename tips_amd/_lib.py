@@ -90,6 +90,8 @@ _SIGNATURES = [
     ("tips_fused_allreduce", ctypes.c_int, [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_fused_allreduce_oop", ctypes.c_int,
      [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    ("tips_fused_allreduce_cast", ctypes.c_int,
+     [_c_void_pp, _c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     ("tips_fused_layout", ctypes.c_int64, [_c_i64_p, ctypes.c_int, ctypes.c_int, _c_i64_p]),
     ("tips_fused_allreduce_flat", ctypes.c_int,
      [_c_void_pp, _c_i64_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),

@@ -56,7 +56,8 @@ int64_t copy_tile_bytes() {
 // sum kernels' stores), 1 = nt, 0 = plain (TIPS_COPY_STORE_POLICY, the tuning sweep's knob)
 int copy_store_policy() { return (int)std::min<int64_t>(2, std::max<int64_t>(0, env_i64("TIPS_COPY_STORE_POLICY", 2))); }
 
-enum Mode { kSlot = 0, kCopy = 1, kFlat = 2 };
+enum Mode { kSlot = 0, kCopy = 1, kFlat = 2, kSlotCast = 3 };  // kSlotCast: kSlot with f32 tensors, wire-type slots
+inline int tables_of(int mode) { return mode == kSlot || mode == kSlotCast ? 2 : 1; }
 
 struct Bucket {
   int64_t off;    // byte offset in the flat space (tile-aligned, so no tile straddles two buckets)
@@ -338,7 +339,7 @@ std::vector<int> tile_order(const Layout& L) {
 // tests' interpreter of copy_segs_kernel.
 void fill_records(const Layout& L, int mode, const BatchItem* items, const void* base, std::vector<CopySeg>* dst) {
   const int nseg = (int)L.seg_tensor.size();
-  const int ntab = mode == kSlot ? 2 : 1;
+  const int ntab = tables_of(mode);
   const size_t per = 2 * (size_t)L.ntiles + nseg;
   const int64_t es = tips::dtype_size(L.dtype);
   std::vector<CopySeg>& rec = *dst;
@@ -348,12 +349,15 @@ void fill_records(const Layout& L, int mode, const BatchItem* items, const void*
     const int64_t b = L.off[i], e = b + L.counts[i] * es;
     const int64_t in = (int64_t)(uintptr_t)items[i].in - b, out = (int64_t)(uintptr_t)items[i].out - b;
     CopySeg* r = rec.data() + 2 * L.ntiles + k;
-    if (mode == kSlot) {
+    if (mode == kSlot || mode == kSlotCast) {
       const int bk = L.bucket[i];
       // bucket bk lives in slot bk % 2: virtual byte v of it at slot + (v - bucket offset)
       const int64_t slot = bk < 0 ? 0 : (int64_t)(uintptr_t)base + (int64_t)(bk % 2) * L.threshold - L.buckets[bk].off;
-      r[0] = CopySeg{in, slot, b, e};    // pack
-      r[per] = CopySeg{slot, out, b, e};  // unpack
+      // kSlotCast: the tensors are f32 and the space the wire type's, so the f32 side of virtual
+      // byte v is at base + 2 v (cast_segs_kernel)
+      const int64_t win = (int64_t)(uintptr_t)items[i].in - 2 * b, wout = (int64_t)(uintptr_t)items[i].out - 2 * b;
+      r[0] = mode == kSlot ? CopySeg{in, slot, b, e} : CopySeg{win, slot, b, e};       // pack
+      r[per] = mode == kSlot ? CopySeg{slot, out, b, e} : CopySeg{slot, wout, b, e};   // unpack
     } else if (mode == kCopy) {
       r[0] = CopySeg{in, out, b, e};
     } else {  // kFlat: straight into the flat output
@@ -413,7 +417,7 @@ Table* find_table(State& st, FusionCache& fc, Layout& L, int mode, const BatchIt
     }
   }
   const int nseg = (int)L.seg_tensor.size();
-  const int ntab = mode == kSlot ? 2 : 1;
+  const int ntab = tables_of(mode);
   const size_t per = 2 * (size_t)L.ntiles + nseg;  // one table: [2 records per tile | segment records]
   if (!t) {
     t = new Table();
@@ -490,6 +494,70 @@ int copy_tiles(const Layout& L, const Table& t, int table, int tile0, int ntiles
   return 0;
 }
 
+// One pack launch for a step's buckets: TIPS_PACK_MERGE=1, opt-in. The idea was
+// that each launch pays ~1.7 us of ramp and drain, so a step of two ~41-51 MB buckets
+// paid it twice. Measured (profiles/r06/pack_merged.jsonl): back-to-back launches on one stream do not
+// pay it - config 4's two packs take 28.56 us merged against 2 x 14.11 us, config 5's 33.14 against
+// 2 x 16.56 - so per-bucket launches stay the default; the merged form (bit-exact, with device-side
+// per-bucket completion signals) is kept for the N = 8 node to A/B.
+bool pack_merge(const State& st) { return !st.fuse_capturing && env_i64("TIPS_PACK_MERGE", 0) != 0; }
+
+// Whether the bucket stream can wait on the device for one bucket of a merged pack launch
+// (hipStreamWaitValue64 on signal memory, raised by the bucket's last workgroup); sets up the
+// counters and the signal words once. Without it a merged launch is waited for as a whole.
+bool pack_signals_ready(State& st, hipStream_t ws) {
+  if (st.pack_signals >= 0) return st.pack_signals == 1;
+  st.pack_signals = 0;
+  if (env_i64("TIPS_PACK_SIGNALS", 1) == 0) return false;
+  int can = 0;
+  if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, st.device) != hipSuccess || !can) {
+    (void)hipGetLastError();
+    return false;
+  }
+  bool ok = hipMalloc((void**)&st.pack_counters, tips::kMaxPackGroups * sizeof(unsigned)) == hipSuccess &&
+            hipMemsetAsync(st.pack_counters, 0, tips::kMaxPackGroups * sizeof(unsigned), ws) == hipSuccess;
+  for (int k = 0; k < tips::kMaxPackGroups && ok; k++) {
+    ok = hipExtMallocWithFlags(&st.pack_done[k], sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess &&
+         hipMemsetAsync(st.pack_done[k], 0, sizeof(uint64_t), ws) == hipSuccess;
+    st.pack_done_value[k] = 0;
+  }
+  if (!ok) {
+    (void)hipGetLastError();
+    pack_signals_release(st);
+    return false;
+  }
+  st.pack_signals = 1;
+  return true;
+}
+
+// Buckets [b0, b0 + nb) of table `table` in one launch, nb <= kMaxPackGroups, in bucket order.
+// signal: bucket b0 + k's completion raises signal word k to values[k] (wait_packed).
+int pack_buckets(State& st, const Layout& L, const Table& t, int table, int b0, int nb, bool signal, uint64_t* values,
+                 hipStream_t s) {
+  tips::PackGroups g{};
+  g.n = nb;
+  g.counters = signal ? st.pack_counters : nullptr;
+  for (int k = 0; k < nb; k++) {
+    g.tile0[k] = L.buckets[b0 + k].tile0;
+    g.ntiles[k] = L.buckets[b0 + k].ntiles;
+    if (signal) {
+      g.done[k] = static_cast<unsigned long long*>(st.pack_done[k]);
+      g.sig_value[k] = st.pack_done_value[k] + 1;
+    }
+  }
+  const CopySeg* base = t.dev + (size_t)table * (2 * (size_t)L.ntiles + L.seg_tensor.size());
+  HIP_TRY(tips::launch_copy_segs_groups(base, base + 2 * L.ntiles, g, L.tile, copy_store_policy(), s));
+  if (signal)
+    for (int k = 0; k < nb; k++) values[k] = ++st.pack_done_value[k];
+  return 0;
+}
+
+// The bucket stream waits until signal word k has reached value (its bucket is packed).
+int wait_packed(State& st, int k, uint64_t value) {
+  HIP_TRY(hipStreamWaitValue64(st.bucket_stream, st.pack_done[k], value, hipStreamWaitValueGte, ~0ull));
+  return 0;
+}
+
 // A fused call's entry: the work stream (the caller's, or fuse_stream under
 // TIPS_FUSION_CALLER_STREAM=0) after the chain's previous call and after the caller's own work.
 // A call captured into a graph (torch.cuda.graph around it) stays out of the chain: the capture
@@ -553,6 +621,16 @@ int64_t fusion_threshold_bytes() {
   return round_up(std::max<int64_t>(kAlignBytes, env_i64("TIPS_FUSION_THRESHOLD", 64 << 20)), kAlignBytes);
 }
 
+void pack_signals_release(State& st) {
+  if (st.pack_counters) (void)hipFree(st.pack_counters);
+  st.pack_counters = nullptr;
+  for (void*& p : st.pack_done) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+  }
+  st.pack_signals = -1;
+}
+
 void fusion_release(State& st) {
   FusionCache* fc = st.fusion_cache;
   if (st.ev_fuse_chain) {
@@ -568,6 +646,11 @@ void fusion_release(State& st) {
     st.ev_fuse_chain = nullptr;
     st.fuse_chain_valid = false;
   }
+  if (st.pack_counters || st.pack_signals == 1) {  // (no launch may still raise them)
+    (void)hipDeviceSynchronize();
+    pack_signals_release(st);
+  }
+  st.pack_signals = -1;
   if (!fc) return;
   for (Layout* L : fc->layouts) free_layout(st, L);
   if (st.fuse_stream) (void)hipStreamSynchronize(st.fuse_stream);
@@ -638,10 +721,16 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
     auto pack = [&](int b) { return copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, ws); };
     auto unpack = [&](int b) { return copy_tiles(*L, *t, 1, L->buckets[b].tile0, L->buckets[b].ntiles, ws); };
     auto slot = [&](int b) { return (char*)st.fusion.p + (int64_t)(b % 2) * threshold; };
-    if (st.size == 1) {  // TIPS_FUSION_MEASURE_PACK: pack, (identity), unpack, in stream order
+    // pack(0) and pack(1) (both slots) go first: one launch when merged, bucket 0's tiles first
+    const int first = std::min(B, 2);
+    const bool merge = first > 1 && pack_merge(st);
+    if (st.size == 1) {  // TIPS_FUSION_MEASURE_PACK: the N > 1 step's launches, the allreduces left out
+      if (merge) TRY(pack_buckets(st, *L, *t, 0, 0, first, false, nullptr, ws));
+      else
+        for (int b = 0; b < first; b++) TRY(pack(b));
       for (int b = 0; b < B; b++) {
-        TRY(pack(b));
         TRY(unpack(b));
+        if (b + 2 < B) TRY(pack(b + 2));
       }
       for (int i : L->direct) TRY(allreduce_device(st, items[i].in, items[i].out, items[i].count, dtype, ws));
       return 0;
@@ -654,12 +743,22 @@ int fused_allreduce(State& st, const BatchItem* items, int n, int dtype, hipStre
     TRY(st.fuse_ev.ensure(2 * (size_t)B));
     hipEvent_t* packed = st.fuse_ev.ev.data();
     hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
-    for (int b = 0; b < std::min(B, 2); b++) {
-      TRY(pack(b));
-      HIP_TRY(hipEventRecord(packed[b], ws));
+    // merged: the bucket stream waits for each bucket's signal word (or, without signals, for the
+    // whole launch)
+    const bool signal = merge && pack_signals_ready(st, ws);
+    uint64_t sigv[2] = {};
+    if (merge) {
+      TRY(pack_buckets(st, *L, *t, 0, 0, first, signal, sigv, ws));
+      HIP_TRY(hipEventRecord(packed[0], ws));  // (read when !signal: the launch as a whole)
+    } else {
+      for (int b = 0; b < first; b++) {
+        TRY(pack(b));
+        HIP_TRY(hipEventRecord(packed[b], ws));
+      }
     }
     for (int b = 0; b < B; b++) {
-      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[b], 0));
+      if (signal && b < first) TRY(wait_packed(st, b, sigv[b]));
+      else HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[merge && b < first ? 0 : b], 0));
       TRY(allreduce_device(st, slot(b), slot(b), L->buckets[b].bytes / es, dtype, st.bucket_stream));
       HIP_TRY(hipEventRecord(reduced[b], st.bucket_stream));
       HIP_TRY(hipStreamWaitEvent(ws, reduced[b], 0));
@@ -702,17 +801,100 @@ int fused_allreduce_flat(State& st, const BatchItem* items, int n, int dtype, vo
     for (int i : L->direct)
       TRY(allreduce_device(st, items[i].in, (char*)flat + L->off[i], items[i].count, dtype, red));
     TRY(st.fuse_ev.ensure((size_t)B));
-    for (int b = 0; b < B; b++) {
-      TRY(copy_tiles(*L, *t, 0, L->buckets[b].tile0, L->buckets[b].ntiles, ws));
+    // merged: every bucket's pack in launches of up to kMaxPackGroups buckets, bucket order, each
+    // bucket's allreduce behind its signal word (or, without signals, behind its launch)
+    const bool merge = B > 1 && pack_merge(st);
+    const bool signal = merge && st.size > 1 && pack_signals_ready(st, ws);
+    for (int b0 = 0; b0 < B;) {
+      const int nb = merge ? std::min(B - b0, tips::kMaxPackGroups) : 1;
+      uint64_t sigv[tips::kMaxPackGroups] = {};
+      if (merge) TRY(pack_buckets(st, *L, *t, 0, b0, nb, signal, sigv, ws));
+      else TRY(copy_tiles(*L, *t, 0, L->buckets[b0].tile0, L->buckets[b0].ntiles, ws));
       if (st.size > 1) {
-        HIP_TRY(hipEventRecord(st.fuse_ev.ev[b], ws));
-        HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.fuse_ev.ev[b], 0));
-        char* p = (char*)flat + L->buckets[b].off;
-        TRY(allreduce_device(st, p, p, L->buckets[b].bytes / es, dtype, st.bucket_stream));
+        if (!signal) {
+          HIP_TRY(hipEventRecord(st.fuse_ev.ev[b0], ws));
+          HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.fuse_ev.ev[b0], 0));
+        }
+        for (int k = 0; k < nb; k++) {
+          if (signal) TRY(wait_packed(st, k, sigv[k]));
+          char* p = (char*)flat + L->buckets[b0 + k].off;
+          TRY(allreduce_device(st, p, p, L->buckets[b0 + k].bytes / es, dtype, st.bucket_stream));
+        }
       }
+      b0 += nb;
     }
     if (st.size > 1) TRY(join(ws, st.bucket_stream, st.ev_comp_done));
     return 0;
+  });
+}
+
+int fused_allreduce_cast(State& st, const BatchItem* items, int n, int wire, hipStream_t user) {
+  if (n <= 0) return 0;
+  FusionCache& fc = cache(st);
+  const int64_t threshold = fusion_threshold_bytes();
+  TRY(ensure_slots(st, fc, threshold));
+  std::vector<int64_t> counts((size_t)n);
+  for (int i = 0; i < n; i++) counts[i] = items[i].count;
+  return in_fusion(st, user, [&](hipStream_t ws) -> int {
+    if (st.size > 1) {  // inputs ready for the bucket stream too (the large tensors start at once)
+      HIP_TRY(hipEventRecord(st.ev_start, ws));
+      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
+    }
+    // the layout of the WIRE type's bytes: buckets of at most the threshold in wire bytes
+    Layout* L = find_layout(st, fc, counts.data(), n, wire, threshold, copy_tile_bytes(),
+                            env_i64("TIPS_FUSION_BALANCE", 1) != 0);
+    if (!L) return TIPS_ERR_HIP;
+    if (L->seg_tensor.empty()) return 0;
+    const int64_t es = tips::dtype_size(wire);
+    const int B = (int)L->buckets.size();
+    Table* t = B ? find_table(st, fc, *L, kSlotCast, items, n, st.fusion.p) : nullptr;
+    if (B && !t) return TIPS_ERR_HIP;
+    const size_t per = 2 * (size_t)L->ntiles + L->seg_tensor.size();
+    auto cast = [&](int dir, int b) -> int {
+      const CopySeg* base = t->dev + (size_t)dir * per;
+      HIP_TRY(tips::launch_cast_segs(base, base + 2 * L->ntiles, L->buckets[b].tile0, L->buckets[b].ntiles, L->tile, dir,
+                                     wire, ws));
+      return 0;
+    };
+    auto slot = [&](int b) { return (char*)st.fusion.p + (int64_t)(b % 2) * threshold; };
+    // tensors of at least the threshold (in wire bytes): one at a time through a scratch buffer of
+    // the wire type - cast in, allreduce in place, cast out - on the bucket stream (their exchange
+    // starts at once) or, at one rank, on the work stream (the round trip)
+    hipStream_t big = st.size > 1 ? st.bucket_stream : ws;
+    for (int i : L->direct) {
+      TRY(st.cast_scratch.ensure((size_t)(items[i].count * es)));
+      HIP_TRY(tips::launch_cast_range(st.cast_scratch.p, items[i].in, items[i].count, 0, wire, big));
+      if (st.size > 1) TRY(allreduce_device(st, st.cast_scratch.p, st.cast_scratch.p, items[i].count, wire, big));
+      HIP_TRY(tips::launch_cast_range(items[i].out, st.cast_scratch.p, items[i].count, 1, wire, big));
+    }
+    if (st.size == 1) {  // one rank: the allreduce is the identity; the casts are the reference's
+      for (int b = 0; b < B; b++) {
+        TRY(cast(0, b));
+        TRY(cast(1, b));
+      }
+      return 0;
+    }
+    // as fused_allreduce: pack(0) pack(1) | unpack(0) pack(2) | ..., allreduce(b) on the bucket
+    // stream between pack(b) and unpack(b), in the wire type
+    TRY(st.fuse_ev.ensure(2 * (size_t)B));
+    hipEvent_t* packed = st.fuse_ev.ev.data();
+    hipEvent_t* reduced = st.fuse_ev.ev.data() + B;
+    for (int b = 0; b < std::min(B, 2); b++) {
+      TRY(cast(0, b));
+      HIP_TRY(hipEventRecord(packed[b], ws));
+    }
+    for (int b = 0; b < B; b++) {
+      HIP_TRY(hipStreamWaitEvent(st.bucket_stream, packed[b], 0));
+      TRY(allreduce_device(st, slot(b), slot(b), L->buckets[b].bytes / es, wire, st.bucket_stream));
+      HIP_TRY(hipEventRecord(reduced[b], st.bucket_stream));
+      HIP_TRY(hipStreamWaitEvent(ws, reduced[b], 0));
+      TRY(cast(1, b));
+      if (b + 2 < B) {
+        TRY(cast(0, b + 2));
+        HIP_TRY(hipEventRecord(packed[b + 2], ws));
+      }
+    }
+    return join(ws, st.bucket_stream, st.ev_comp_done);  // (the large tensors' work too)
   });
 }
 
@@ -772,6 +954,32 @@ int tips_fused_allreduce(void* const* ptrs, const int64_t* counts, int n, int dt
 int tips_fused_allreduce_oop(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype,
                              void* stream) {
   return fused_entry(ins, outs, counts, n, dtype, stream);
+}
+
+int tips_fused_allreduce_cast(const void* const* ins, void* const* outs, const int64_t* counts, int n, int dtype,
+                              int wire_dtype, void* stream) {
+  if (dtype != TIPS_FLOAT32)
+    return fail(TIPS_ERR_UNSUPPORTED, "tips_fused_allreduce_cast: the tensors must be TIPS_FLOAT32 (got dtype %d)", dtype);
+  if (wire_dtype != TIPS_FLOAT16 && wire_dtype != TIPS_BFLOAT16)
+    return fail(TIPS_ERR_UNSUPPORTED, "tips_fused_allreduce_cast: the wire type must be TIPS_FLOAT16 or TIPS_BFLOAT16 "
+                                      "(got %d)", wire_dtype);
+  if (!outs && n > 0) return fail(TIPS_ERR_INVALID_ARG, "bad tensor list");
+  std::vector<BatchItem> items;
+  TRY(check_list(ins, counts, n, dtype, &items, outs));
+  int routed_rc;
+  int64_t shape[2];
+  list_shape(counts, n, shape);
+  // (announced with the wire type: a rank compressing to f16 and one to bf16 fail as mismatched dtypes)
+  if (route_collective(TIPS_REQ_ALLREDUCE, wire_dtype, shape, 2, 0,
+                       [&] { return tips_fused_allreduce_cast(ins, outs, counts, n, dtype, wire_dtype, stream); },
+                       &routed_rc))
+    return routed_rc;
+  State& st = S();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (!st.initialized) return fail(TIPS_ERR_NOT_INITIALIZED, "tips_init has not been called");
+  if (n == 0) return 0;
+  TRY(set_device(st));
+  return fused_allreduce_cast(st, items.data(), n, wire_dtype, (hipStream_t)stream);
 }
 
 #ifdef TIPS_DEV  // (development surface: libtips_hip_dev.so only, include/tips_hip_dev.h)

@@ -53,6 +53,30 @@ struct CopySeg {
 hipError_t launch_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int64_t tile_bytes,
                             int pol, hipStream_t s);
 
+// Several tile groups (a step's fusion buckets) in one launch: group k copies record slots
+// [tile0[k], tile0[k] + ntiles[k]) with workgroups [blk0[k], blk0[k + 1]) (the launcher fills blk0).
+// done[k] != null: when group k is complete its last workgroup stores sig_value[k] into *done[k]
+// (signal memory: another stream waits for it with hipStreamWaitValue64); counters[k] (device
+// memory, zero before the first launch) count the group's workgroups and are left at zero.
+constexpr int kMaxPackGroups = 8;
+struct PackGroups {
+  int n;
+  int tile0[kMaxPackGroups], ntiles[kMaxPackGroups];
+  unsigned blk0[kMaxPackGroups + 1];
+  unsigned* counters;
+  unsigned long long* done[kMaxPackGroups];
+  unsigned long long sig_value[kMaxPackGroups];
+};
+hipError_t launch_copy_segs_groups(const CopySeg* tiles, const CopySeg* segs, PackGroups g, int64_t tile_bytes, int pol,
+                                   hipStream_t s);
+
+// The segment copy with a cast (fused Compression.fp16): the byte space is the wire type's (wire =
+// f16 or bf16 dtype code); the f32 side of a segment is at its record's address + 2 v. dir 0: pack
+// (f32 -> wire, round to nearest even), dir 1: unpack (wire -> f32). And one contiguous range cast.
+hipError_t launch_cast_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int64_t tile_bytes,
+                            int dir, int wire, hipStream_t s);
+hipError_t launch_cast_range(void* dst, const void* src, int64_t n, int dir, int wire, hipStream_t s);
+
 // One contiguous device-to-device copy of `bytes` (tips_allreduce / tips_broadcast at one rank, out
 // of place): copy_buf_kernel when both pointers are 16-B aligned, else hipMemcpyAsync.
 hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_t s);

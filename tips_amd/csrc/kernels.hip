@@ -801,15 +801,18 @@ __device__ __forceinline__ void small_store(int64_t s, int64_t d, int len, const
 // first): the tile's segment and {0, 0, tile byte, 0}; or its two segments (the tensor ending in
 // it, the tensor starting in it); or {first segment, count, -, -1} and {0, 0, tile byte, 0} when
 // it meets more than two (then staged from segs[] in LDS).
+template <int U>
+struct SegStage {  // a multi-segment tile's records, staged in LDS
+  CopySeg L[(int)((int64_t)kBlock * 16 * U / 256) + 1];
+};
+
+// One tile of the segment copy: record slot t. Called by whole workgroups (the multi-segment
+// branch has a barrier; every branch to it is workgroup-uniform).
 template <int U, int POL>
-__global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __restrict__ tiles,
-                                                          const CopySeg* __restrict__ segs, int tile0, int ntiles) {
+__device__ __forceinline__ void copy_seg_tile(const CopySeg* __restrict__ tiles, const CopySeg* __restrict__ segs,
+                                              int t, CopySeg* L) {
   constexpr int64_t kTileBytes = (int64_t)kBlock * 16 * U;
   constexpr int kMaxSeg = (int)(kTileBytes / 256) + 1;
-  __shared__ CopySeg L[kMaxSeg];
-  const int64_t tt = xcd_tile(blockIdx.x, gridDim.x);
-  if (tt >= ntiles) return;  // (whole workgroup: before any barrier)
-  const int t = tile0 + (int)tt;  // the record slot (fusion.cc may order a group's tiles: slow ones first)
   // One (scalar) load of both records before the first data load. (A tile -> segment index
   // followed by the segment's record puts two dependent loads there: 17.5 against 14.1 us per
   // config-4 bucket, measured.)
@@ -885,6 +888,183 @@ __global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __rest
   for (int u = 0; u < U; u++) {
     if (full[u]) store16_pol<POL>(dp[u], x[u]);
     else if (len[u] > 0) small_store(sp[u], dp[u], len[u], m[u]);
+  }
+}
+
+template <int U, int POL>
+__global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __restrict__ tiles,
+                                                          const CopySeg* __restrict__ segs, int tile0, int ntiles) {
+  __shared__ SegStage<U> st;
+  const int64_t tt = xcd_tile(blockIdx.x, gridDim.x);
+  if (tt >= ntiles) return;  // (whole workgroup: before any barrier)
+  copy_seg_tile<U, POL>(tiles, segs, tile0 + (int)tt, st.L);  // (fusion.cc may order a group's tiles: slow ones first)
+}
+
+// ---------------------------------------------------------------------------
+// Fusion pack / unpack with a cast (Compression.fp16 fused into the buckets):
+// the layout's byte space is the WIRE type's (f16 or bf16, 2 B per element); the f32 side of a
+// segment lives at base + 2 v for virtual byte v (fusion.cc's kSlotCast records). DIR 0 (pack):
+// f32 source -> wire destination, RNE as oracle_float_to_half / oracle_float_to_bf16 (the
+// reference's tf.cast, compression.py:49-66); DIR 1 (unpack): wire source -> f32 destination, exact.
+// A lane moves one 16-B wire vector = 8 elements = 32 B of f32 (two 16-B accesses).
+
+template <int WT>
+__device__ __forceinline__ u32x4 narrow8(f32x4 a, f32x4 b) {
+  if constexpr (WT == kF16) {
+    const f32x8 w = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(u32x4, __builtin_convertvector(w, f16x8));
+  } else {  // bf16: word i = elements 2i (low half) and 2i + 1 (high half)
+    const u32x4 x = __builtin_bit_cast(u32x4, a), y = __builtin_bit_cast(u32x4, b);
+    return u32x4{bf16_round_bits(x[0]) | (bf16_round_bits(x[1]) << 16), bf16_round_bits(x[2]) | (bf16_round_bits(x[3]) << 16),
+                 bf16_round_bits(y[0]) | (bf16_round_bits(y[1]) << 16), bf16_round_bits(y[2]) | (bf16_round_bits(y[3]) << 16)};
+  }
+}
+
+template <int WT>
+__device__ __forceinline__ void widen8(u32x4 v, f32x4& a, f32x4& b) {
+  if constexpr (WT == kF16) {
+    const f32x8 w = __builtin_convertvector(__builtin_bit_cast(f16x8, v), f32x8);
+    a = f32x4{w[0], w[1], w[2], w[3]};
+    b = f32x4{w[4], w[5], w[6], w[7]};
+  } else {
+    a = __builtin_bit_cast(f32x4, u32x4{v[0] << 16, v[0] & 0xffff0000u, v[1] << 16, v[1] & 0xffff0000u});
+    b = __builtin_bit_cast(f32x4, u32x4{v[2] << 16, v[2] & 0xffff0000u, v[3] << 16, v[3] & 0xffff0000u});
+  }
+}
+
+template <int WT>
+__device__ __forceinline__ unsigned short narrow1(float f) {
+  if constexpr (WT == kF16) return __builtin_bit_cast(unsigned short, (_Float16)f);
+  else return (unsigned short)bf16_round_bits(__builtin_bit_cast(unsigned, f));
+}
+
+template <int WT>
+__device__ __forceinline__ float widen1(unsigned short h) {
+  if constexpr (WT == kF16) return (float)__builtin_bit_cast(_Float16, h);
+  else return __builtin_bit_cast(float, (unsigned)h << 16);
+}
+
+typedef __attribute__((address_space(1))) f32x4 g_f32x4;
+typedef __attribute__((address_space(1))) float g_f32;
+
+template <int U, int DIR, int WT>
+__global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __restrict__ tiles,
+                                                          const CopySeg* __restrict__ segs, int tile0, int ntiles) {
+  constexpr int64_t kTileBytes = (int64_t)kBlock * 16 * U;  // wire bytes
+  constexpr int kMaxSeg = (int)(kTileBytes / 256) + 1;
+  __shared__ CopySeg L[kMaxSeg];
+  const int64_t tt = xcd_tile(blockIdx.x, gridDim.x);
+  if (tt >= ntiles) return;  // (whole workgroup: before any barrier)
+  const int64_t* tr = reinterpret_cast<const int64_t*>(tiles + 2 * (int64_t)(tile0 + tt));
+  const int64_t a_src = tr[0], a_dst = tr[1], a_beg = tr[2], a_end = tr[3];
+  const int64_t b_src = tr[4], b_dst = tr[5], b_beg = tr[6], b_end = tr[7];
+  const int tid = threadIdx.x;
+  const bool multi = a_end < 0, two = b_end > 0;
+  const int64_t tb = two ? (b_beg & ~(kTileBytes - 1)) : b_beg;
+  int cnt = 1;
+  if (multi) {  // workgroup-uniform branch
+    cnt = min((int)a_dst, kMaxSeg);
+    if (cnt <= 0) return;
+    if (tid < cnt) L[tid] = segs[(int)a_src + tid];
+    __syncthreads();
+  }
+  int64_t sp[U], dp[U];
+  int len[U];
+  bool full[U];
+  u32x4 nv[U];      // pack: the narrowed vector; unpack: the loaded wire vector
+  f32x4 wa[U], wb[U];  // pack: the loaded f32 pair
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int64_t v = tb + (int64_t)u * (kBlock * 16) + (int64_t)tid * 16;
+    int64_t g_src, g_dst, g_beg, g_end;
+    if (multi) {
+      int lo = 0, hi = cnt - 1;  // the last segment beginning at or before v
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (L[mid].begin <= v) lo = mid;
+        else hi = mid - 1;
+      }
+      g_src = L[lo].src;
+      g_dst = L[lo].dst;
+      g_beg = L[lo].begin;
+      g_end = L[lo].end;
+    } else {
+      const bool b = two && v >= b_beg;
+      g_src = b ? b_src : a_src;
+      g_dst = b ? b_dst : a_dst;
+      g_beg = b ? b_beg : a_beg;
+      g_end = b ? b_end : a_end;
+    }
+    const int64_t left = g_end - v;
+    len[u] = (v >= g_beg && left > 0) ? (int)(left < 16 ? left : 16) : 0;
+    sp[u] = g_src + (DIR == 0 ? 2 * v : v);  // the f32 side at base + 2 v
+    dp[u] = g_dst + (DIR == 0 ? v : 2 * v);
+    full[u] = len[u] == 16 && ((sp[u] | dp[u]) & 15) == 0;
+    if (full[u]) {
+      if constexpr (DIR == 0) {
+        wa[u] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(sp[u]));
+        wb[u] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(sp[u] + 16));
+      } else {
+        nv[u] = __builtin_nontemporal_load(reinterpret_cast<const g_u32x4*>(sp[u]));
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (full[u]) {
+      if constexpr (DIR == 0) {
+        store16_pol<2>(dp[u], narrow8<WT>(wa[u], wb[u]));
+      } else {
+        f32x4 a, b;
+        widen8<WT>(nv[u], a, b);
+        store16_pol<2>(dp[u], __builtin_bit_cast(u32x4, a));
+        store16_pol<2>(dp[u] + 16, __builtin_bit_cast(u32x4, b));
+      }
+    } else {
+      for (int e = 0; 2 * e < len[u]; e++) {  // a tensor's ragged end, or an f32 side not 16-B aligned
+        if constexpr (DIR == 0)
+          *reinterpret_cast<g_u16*>(dp[u] + 2 * e) = narrow1<WT>(*reinterpret_cast<const g_f32*>(sp[u] + 4 * e));
+        else
+          *reinterpret_cast<g_f32*>(dp[u] + 4 * e) = widen1<WT>(*reinterpret_cast<const g_u16*>(sp[u] + 2 * e));
+      }
+    }
+  }
+}
+
+// Elementwise cast of one contiguous range (a fused list's tensors of at least the threshold, which
+// travel through a scratch buffer of the wire type): DIR 0 f32 -> wire, 1 wire -> f32.
+template <int DIR, int WT>
+__global__ __launch_bounds__(kBlock) void cast_range_kernel(void* __restrict__ dst, const void* __restrict__ src,
+                                                           int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    if constexpr (DIR == 0) static_cast<unsigned short*>(dst)[i] = narrow1<WT>(static_cast<const float*>(src)[i]);
+    else static_cast<float*>(dst)[i] = widen1<WT>(static_cast<const unsigned short*>(src)[i]);
+  }
+}
+
+// Several groups of tiles (a step's fusion buckets) in one launch, each group a contiguous range of
+// workgroups in group order, XCD-contiguous inside it: the dispatcher hands out workgroups in
+// order, so group 0 is done first and its allreduce can start while the later groups are still
+// being packed. The launch pays one ramp and drain instead of one per bucket.
+// With done[k] set, the last workgroup of group k (a device counter per group, reset by that
+// workgroup for the next launch) stores sig_value[k] into *done[k] with a system-scope release, which
+// the bucket stream waits on (hipStreamWaitValue64 on signal memory, fusion.cc).
+template <int U, int POL>
+__global__ __launch_bounds__(kBlock) void copy_segs_groups_kernel(const CopySeg* __restrict__ tiles,
+                                                                 const CopySeg* __restrict__ segs, PackGroups g) {
+  __shared__ SegStage<U> st;
+  int k = 0;
+  while (k + 1 < g.n && blockIdx.x >= g.blk0[k + 1]) k++;
+  const unsigned local = blockIdx.x - g.blk0[k], gk = g.blk0[k + 1] - g.blk0[k];
+  const int64_t tt = xcd_tile(local, gk);
+  if (tt < g.ntiles[k]) copy_seg_tile<U, POL>(tiles, segs, g.tile0[k] + (int)tt, st.L);
+  if (g.done[k]) {
+    __syncthreads();  // (every wave's copies before the workgroup's count)
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&g.counters[k], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gk - 1) {
+      __hip_atomic_store(&g.counters[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g.done[k], g.sig_value[k], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -1477,6 +1657,18 @@ hipError_t launch_pack_tiles(const CopyTile* tiles_dev, int ntiles, int64_t max_
 namespace {
 
 template <int U>
+hipError_t run_copy_segs_groups(const CopySeg* tiles, const CopySeg* segs, const PackGroups& g, int pol, hipStream_t s) {
+  const unsigned grid = g.blk0[g.n];
+  switch (pol) {
+    case 0: hipLaunchKernelGGL((copy_segs_groups_kernel<U, 0>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, g); break;
+    case 1: hipLaunchKernelGGL((copy_segs_groups_kernel<U, 1>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, g); break;
+    case 2: hipLaunchKernelGGL((copy_segs_groups_kernel<U, 2>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, g); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int U>
 hipError_t run_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int pol, hipStream_t s) {
   const unsigned grid = (unsigned)std::max<int64_t>(8, ((int64_t)ntiles + 7) / 8 * 8);
   switch (pol) {
@@ -1499,6 +1691,67 @@ hipError_t launch_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0
     case 16384: return run_copy_segs<4>(tiles, segs, tile0, ntiles, pol, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_copy_segs_groups(const CopySeg* tiles, const CopySeg* segs, PackGroups g, int64_t tile_bytes, int pol,
+                                   hipStream_t s) {
+  if (g.n < 1 || g.n > kMaxPackGroups) return hipErrorInvalidValue;
+  for (int k = 0; k < g.n; k++)
+    if (g.done[k] && !g.counters) return hipErrorInvalidValue;
+  int64_t blk = 0;
+  for (int k = 0; k < g.n; k++) {  // each group's workgroups: whole XCD rounds (xcd_tile), at least 8
+    if (g.ntiles[k] < 0) return hipErrorInvalidValue;
+    g.blk0[k] = (unsigned)blk;
+    blk += std::max<int64_t>(8, ((int64_t)g.ntiles[k] + 7) / 8 * 8);
+  }
+  if (blk > 0x7fffffff) return hipErrorInvalidValue;
+  g.blk0[g.n] = (unsigned)blk;
+  switch (tile_bytes) {
+    case 4096: return run_copy_segs_groups<1>(tiles, segs, g, pol, s);
+    case 8192: return run_copy_segs_groups<2>(tiles, segs, g, pol, s);
+    case 16384: return run_copy_segs_groups<4>(tiles, segs, g, pol, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+namespace {
+template <int U, int DIR>
+hipError_t run_cast_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int wire, hipStream_t s) {
+  const unsigned grid = (unsigned)std::max<int64_t>(8, ((int64_t)ntiles + 7) / 8 * 8);
+  if (wire == kF16)
+    hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles);
+  else if (wire == kBF16)
+    hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kBF16>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+template <int DIR>
+hipError_t run_cast_range(void* dst, const void* src, int64_t n, int wire, hipStream_t s) {
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, (int64_t)kNumCUs * 16));
+  if (wire == kF16) hipLaunchKernelGGL((cast_range_kernel<DIR, kF16>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, src, n);
+  else if (wire == kBF16) hipLaunchKernelGGL((cast_range_kernel<DIR, kBF16>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, src, n);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_cast_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int64_t tile_bytes,
+                            int dir, int wire, hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  if (dir != 0 && dir != 1) return hipErrorInvalidValue;
+  switch (tile_bytes) {
+    case 4096: return dir ? run_cast_segs<1, 1>(tiles, segs, tile0, ntiles, wire, s) : run_cast_segs<1, 0>(tiles, segs, tile0, ntiles, wire, s);
+    case 8192: return dir ? run_cast_segs<2, 1>(tiles, segs, tile0, ntiles, wire, s) : run_cast_segs<2, 0>(tiles, segs, tile0, ntiles, wire, s);
+    case 16384: return dir ? run_cast_segs<4, 1>(tiles, segs, tile0, ntiles, wire, s) : run_cast_segs<4, 0>(tiles, segs, tile0, ntiles, wire, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_cast_range(void* dst, const void* src, int64_t n, int dir, int wire, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  return dir ? run_cast_range<1>(dst, src, n, wire, s) : run_cast_range<0>(dst, src, n, wire, s);
 }
 
 hipError_t launch_xfer(const XferSeg* segs, int nseg, hipStream_t s) {

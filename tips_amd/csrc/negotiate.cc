@@ -23,6 +23,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <pthread.h>
+#include <sched.h>
 #include <sys/prctl.h>
 #include <deque>
 #include <memory>
@@ -354,6 +355,66 @@ struct NameKeyHash {
 using NameMap = std::unordered_map<NameKey, std::shared_ptr<Req>, NameKeyHash>;
 using HandleMap = std::unordered_map<int64_t, std::shared_ptr<Req>>;
 
+
+// Where the negotiation's threads run (1000 named requests at one rank took
+// 0.40 or 0.87-1.85 us per tensor, bimodal across processes on one box). The caller, the negotiation
+// thread and the completion thread hand every request over through shared cache lines; on the GPU
+// box's 2-socket EPYC 9575F (16 CCDs of one L3 each) the scheduler put the negotiation thread on
+// another CCD than the caller in every slow process and on the same one in every fast process:
+// unbound 1.01-1.60 us per tensor with the threads on different L3s (4 of 4 runs), bound to the
+// caller's L3 or core 0.39-0.41 (8 of 8; profiles/r06/neg_placement/). So TIPS_NEG_BIND=l3, the
+// default, pins both threads to the CPUs that share an L3 with the thread that started the
+// negotiation; =core to that thread's SMT siblings; =0 leaves them free. The threads are named
+// (tips-neg, tips-done: /proc/<pid>/task/*/comm), so bench.py records where each last ran.
+bool cpu_list(const std::string& path, cpu_set_t* set) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  char buf[4096] = {};
+  const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+  fclose(f);
+  if (!ok) return false;
+  CPU_ZERO(set);
+  int n = 0;
+  for (char* q = buf; *q && *q != '\n';) {
+    char* e = nullptr;
+    const long a = strtol(q, &e, 10);
+    if (e == q) break;
+    long b = a;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; c++) CPU_SET((int)c, set), n++;
+    q = *e == ',' ? e + 1 : e;
+  }
+  return n > 0;
+}
+
+// The CPU set TIPS_NEG_BIND asks for around `cpu` (the starting thread's), within the process's
+// affinity; false: leave the thread unbound.
+bool neg_bind_set(int cpu, cpu_set_t* out) {
+  const char* v = getenv("TIPS_NEG_BIND");
+  if (!v || !*v) v = "l3";
+  if (!strcmp(v, "0") || !strcmp(v, "off") || cpu < 0) return false;
+  const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(cpu);
+  cpu_set_t want;
+  if (!strcmp(v, "l3")) {
+    if (!cpu_list(base + "/cache/index3/shared_cpu_list", &want)) return false;
+  } else if (!strcmp(v, "core")) {
+    if (!cpu_list(base + "/topology/thread_siblings_list", &want)) return false;
+  } else {
+    return false;
+  }
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
+  CPU_AND(out, &want, &allowed);
+  return CPU_COUNT(out) > 0;
+}
+
+// At the top of a negotiation thread: its name, and its CPUs when TIPS_NEG_BIND asks.
+void neg_thread_setup(const char* name, int start_cpu) {
+  (void)pthread_setname_np(pthread_self(), name);
+  cpu_set_t set;
+  if (neg_bind_set(start_cpu, &set)) (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+}
+
 class Negotiator {
  public:
   // Rank 0 listens on the first free port of [port, port + kPortTries); every other rank connects
@@ -496,8 +557,10 @@ class Negotiator {
     lockfree_ = env_i64("TIPS_ENQUEUE_LOCKFREE", 1) != 0;
     running_ = true;
     accepting_.store(true, std::memory_order_release);
+    start_cpu_ = sched_getcpu();  // (the starting thread's CPU: TIPS_NEG_BIND's anchor)
     thread_ = std::thread([this] {
       tl_negotiation_thread = true;
+      neg_thread_setup("tips-neg", start_cpu_);
       loop();
     });
     return 0;
@@ -679,7 +742,11 @@ class Negotiator {
 
   // (m_ held) the completion thread, if it is not running yet
   void start_waiter_locked() {
-    if (!waiter_.joinable()) waiter_ = std::thread([this] { waiter_loop(); });
+    if (!waiter_.joinable())
+      waiter_ = std::thread([this] {
+        neg_thread_setup("tips-done", start_cpu_);
+        waiter_loop();
+      });
     waiter_started_.store(true, std::memory_order_release);
   }
 
@@ -1696,6 +1763,7 @@ class Negotiator {
   std::string loop_err_;
   hipStream_t neg_stream_ = nullptr;  // fused batches whose requests came on several streams
   std::thread waiter_;                // completion callbacks (started by the first tips_on_done)
+  int start_cpu_ = -1;                // the CPU of the thread that started the negotiation (TIPS_NEG_BIND)
   std::deque<std::shared_ptr<Req>> done_q_;
   std::condition_variable_any done_cv_;
   bool waiter_stop_ = false;

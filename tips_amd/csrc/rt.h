@@ -206,9 +206,17 @@ struct State {
   bool fuse_in_call = false;     // fuse_ws is set (it may be the legacy null stream, i.e. nullptr)
   int64_t fusion_threshold = 0;  // the fusion slots' size (2 slots of it in `fusion`)
   std::vector<void*> fusion_retired;  // earlier slots a captured graph may still pack into (freed at shutdown)
+  // fusion.cc, one pack launch for a step's buckets: per bucket of the launch a workgroup counter
+  // (device memory, reset by the kernel) and a signal word (hipMallocSignalMemory) its last workgroup
+  // raises to the next value, which the bucket stream waits for (hipStreamWaitValue64)
+  unsigned* pack_counters = nullptr;
+  void* pack_done[8] = {};
+  uint64_t pack_done_value[8] = {};
+  int pack_signals = -1;  // -1 not tried yet, 0 unavailable (events per bucket), 1 ready
   hipEvent_t ev_start = nullptr, ev_done = nullptr, ev_comp_done = nullptr, ev_comp_prev = nullptr;
   EventPool recv_ev, sum_ev;
   DevBuf staging, host_in, host_out, fusion, small;
+  DevBuf cast_scratch;  // fusion.cc, fused casts: a list's tensors of at least the threshold, in the wire type
   void* bounce_in = nullptr;  // page-locked kBounceBytes each (hipHostMalloc), for small pageable host tensors
   void* bounce_out = nullptr;
   HostPool* host_pool = nullptr;  // fused host tensors: pack / unpack threads
@@ -310,7 +318,12 @@ int fused_allreduce_flat(State& st, const BatchItem* items, int n, int dtype, vo
 int64_t fused_layout(const int64_t* counts, int n, int dtype, int64_t* offsets);  // flat bytes; pure host
 int fusion_stats(State& st, int64_t* v);  // layouts built, layout hits, tables built, table hits
 int64_t fusion_threshold_bytes();
+// fusion.cc: Compression.fp16 fused into the buckets - n f32 device tensors in[i] -> out[i]
+// (in == out allowed) reduced in `wire` (TIPS_FLOAT16 / TIPS_BFLOAT16): cast while packed (RNE),
+// each bucket allreduced in the wire type, cast back while unpacked. One rank: the round trip.
+int fused_allreduce_cast(State& st, const BatchItem* items, int n, int wire, hipStream_t stream);
 void fusion_release(State& st);  // (shutdown)
+void pack_signals_release(State& st);  // fusion.cc: the merged pack's counters and signal words
 // control.cc: ConstructResponseMessage's rules over p request records (TIPS_REQUEST_WORDS each)
 int check_records(const int64_t* t, int p);
 // negotiate.cc: stop the negotiation thread (collective; call without holding st.mu)

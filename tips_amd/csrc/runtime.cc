@@ -125,6 +125,7 @@ void tips_shutdown(void) {
     }
   st.fusion.release();
   st.small.release();
+  st.cast_scratch.release();
   st.tuned.clear();
   st.recv_ev.release();
   st.sum_ev.release();

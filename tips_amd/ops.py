@@ -236,6 +236,36 @@ def fused_allreduce(tensor_list, out_list=None):
     return outs
 
 
+_WIRE_CODES = {"float16": _lib.FLOAT16, "bfloat16": _lib.BFLOAT16}
+
+
+def fused_allreduce_cast(tensor_list, wire="float16"):
+    """SUM of a list of float32 device tensors reduced in a 16-bit wire type
+    (tips_fused_allreduce_cast): each tensor is cast to `wire` (round to nearest even) as it is
+    packed into a fusion bucket, every bucket is allreduced in the wire type, and the sums are cast
+    back to float32 as they are unpacked - Compression.fp16's compress -> allreduce -> decompress
+    (tips/tensorflow/compression.py:49-66) with one pack and one unpack launch per bucket instead of
+    two casts per tensor. Returns float32 views of one flat buffer (reused, as fused_allreduce_flat's,
+    once every view is released); inputs unchanged."""
+    basics.init()
+    if not tensor_list:
+        return []
+    code = _check_fusable(tensor_list, "fused_allreduce_cast")
+    if code != _lib.FLOAT32:
+        raise TypeError("fused_allreduce_cast: float32 tensors only (got dtype code %d)" % code)
+    if wire not in _WIRE_CODES:
+        raise ValueError("fused_allreduce_cast: wire must be one of %s" % sorted(_WIRE_CODES))
+    res = _dev_list_cast(tensor_list, _WIRE_CODES[wire])  # (dense, contiguous, one device: C++ reads the list)
+    if res is not None:
+        return res
+    fo = _flat_outputs(tensor_list, code)
+    flat, views = fo.take()
+    pi, _keep1 = _lib.ptr_array([t.data_ptr() for t in tensor_list])
+    _lib.call("tips_fused_allreduce_cast", pi, _out_ptrs(fo, flat), fo.cp[0], len(tensor_list), code, _WIRE_CODES[wire],
+              tensors.stream_of(tensor_list[0]))
+    return views
+
+
 class _FlatOutputs(object):
     """Output sets of fused_allreduce_flat for one list signature (dtype, device, shapes): the
     layout's byte offsets (tips_fused_layout: a function of the counts alone) and a few sets of
@@ -390,6 +420,60 @@ def _dev_list_flat(tensor_list):
     _lib.call("tips_fused_allreduce_flat", bufs[0], fo.cp[0], n, fo.code, flat.data_ptr(),
               _CUR_STREAM(tensor_list[0].device).cuda_stream)
     return views
+
+
+def _dev_list_cast(tensor_list, wire=_lib.FLOAT16):
+    """fused_allreduce_cast of a list of dense, contiguous float32 device tensors on one device,
+    with the per-tensor host work in C++ as _dev_list_flat's (Compression.fp16's fast path in
+    allreduce_grads); the float32 outputs, or None when the list is not such a list."""
+    global _CUR_STREAM
+    n = len(tensor_list)
+    mine = getattr(_LIST_BUFS, "d", None)
+    if mine is None:
+        mine = _LIST_BUFS.d = {}
+    bufs = mine.get(n)
+    if bufs is None:
+        import ctypes
+        pa, na = (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
+        if len(mine) >= 16:
+            mine.pop(next(iter(mine)))
+        bufs = mine[n] = (pa, na, ctypes.addressof(pa), ctypes.addressof(na))
+    r = _fast.dev_list(tensor_list, bufs[2], bufs[3], 1, n)
+    if r is None or _ST_CODES.get(r[0]) != _lib.FLOAT32:
+        return None
+    import ctypes
+    key = (r[0], r[1], n, r[2], _layout_settings())
+    hit = _FAST_FLAT.get(key)
+    counts = ctypes.string_at(bufs[3], 8 * n)
+    if hit is None or hit[1] != counts:
+        fo = _flat_outputs(tensor_list, _lib.FLOAT32)
+        if len(_FAST_FLAT) >= 16:
+            _FAST_FLAT.pop(next(iter(_FAST_FLAT)))
+        _FAST_FLAT[key] = hit = (fo, counts)
+    fo = hit[0]
+    flat, views = fo.take()
+    if _CUR_STREAM is None:
+        import torch
+        _CUR_STREAM = torch.cuda.current_stream
+    _lib.call("tips_fused_allreduce_cast", bufs[0], _out_ptrs(fo, flat), fo.cp[0], n, _lib.FLOAT32, wire,
+              _CUR_STREAM(tensor_list[0].device).cuda_stream)
+    return views
+
+
+def _out_ptrs(fo, flat):
+    """The data pointers of an output set's views (flat buffer + each view's offset), as a void**,
+    cached per flat buffer."""
+    cache = fo.__dict__.setdefault("out_ptrs", {})
+    base = flat.data_ptr()
+    hit = cache.get(base)
+    if hit is None:
+        import ctypes
+        import numpy as np
+        arr = np.asarray(fo.offs, dtype=np.uint64) * np.uint64(fo.es) + np.uint64(base)
+        if len(cache) >= 2 * _FlatOutputs.MAX_SETS:
+            cache.pop(next(iter(cache)))
+        hit = cache[base] = (arr, ctypes.cast(arr.ctypes.data, ctypes.POINTER(ctypes.c_void_p)))
+    return hit[1]
 
 
 def _flat_call(tensor_list, code, ptrs):

@@ -4,7 +4,8 @@ The fusion pack kernel (copy_segs_kernel) moves one bucket per launch: 39.5 MiB 
 ~46-52 MiB (config 5). This probe separates what the segment logic costs from what the launch
 size costs, all with HIP events on one stream, 4 rotating source sets (HBM-only), launches queued
 behind a spin so they run back to back, median of interleaved rounds:
-  pack      tips_fused_pack_bucket over the config's own layout (what bench.py reports)
+  pack      tips_fused_pack_bucket over the config's own layout, one launch per bucket (what bench.py reports)
+  merged    every bucket of the step in one launch (TIPS_PACK_MERGE=1, opt-in since round 6)
   contig    the same kernel on a list of ONE tensor of the bucket's byte count (every tile on the
             one-segment fast path: no segment search, no ragged ends)
   memcpy    hipMemcpyAsync D2D of the same bytes (the copy engine path torch uses for copy_)
@@ -97,6 +98,21 @@ def main():
                 if rc < 0:
                     raise _lib.TipsError("tips_fused_pack_bucket", int(rc), _lib.last_error())
         cases[wname + "/pack"] = (pack, nb, sum(payload) / nb)
+        if want(wname + "/merged"):
+            # the step's packs as fusion.cc issues them since round 6: every bucket in ONE launch
+            # (copy_segs_groups_kernel), through tips_fused_allreduce_flat at one rank with
+            # TIPS_FUSION_MEASURE_PACK=1 (pack into the flat buffer, the identity allreduce skipped)
+            os.environ["TIPS_FUSION_MEASURE_PACK"] = "1"
+            os.environ["TIPS_PACK_MERGE"] = "1"
+            fb = int(_lib.check("tips_fused_layout", L.tips_fused_layout(cp, len(sizes), _lib.FLOAT32, None)))
+            flat = torch.empty(fb // 4 + 64, dtype=torch.float32, device="cuda")
+
+            def merged(k, ptrs=ptrs, cp=cp, n=len(sizes), flat=flat):
+                rc = L.tips_fused_allreduce_flat(ptrs[k % 4][0], cp, n, _lib.FLOAT32, flat.data_ptr(), sp)
+                if rc < 0:
+                    raise _lib.TipsError("tips_fused_allreduce_flat", int(rc), _lib.last_error())
+            merged(0)
+            cases[wname + "/merged"] = (merged, 1, sum(payload))
         for b, pb in enumerate(payload):
             if not want("%s/contig_b%d" % (wname, b)) and not want("%s/memcpy_b%d" % (wname, b)):
                 continue
