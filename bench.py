@@ -783,14 +783,42 @@ def overlap_probe(torch, dist, tips_amd, _lib, algo_code, job, steps=10):
     return out
 
 
-def env_variant_jobs(args, dist, rank, world, timeout_s=240):
-    """Rank 0 reruns the bucket allreduce with the direct schedule as a child job of `world` ranks
-    (torch.distributed.run, the same GPUs) per RCCL setting in ENV_VARIANTS, while every rank of
-    this job waits at a gloo barrier, idle on the GPU. A child that fails or outlasts `timeout_s`
-    is killed (its own process group) and reported; the main line is never at stake."""
+def run_child(cmd, env, budget):
+    """One child job (its own process group), killed with its group if it outlasts `budget` s: the
+    parsed last JSON line's fields and an "error" when it failed. Never raises: a child never costs
+    the main line (a hang costs its own entry, tests/test_distributed_cpu.py pins that)."""
+    res = {}
+    try:
+        if os.environ.get("TIPS_BENCH_CHILD_TEST") == "hang":  # (tests: a child that never ends)
+            cmd = [sys.executable, "-c", "import time; time.sleep(100000)"]
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+        _RESULT["child_pgid"] = p.pid
+        try:
+            o, e = p.communicate(timeout=budget)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            o, e = p.communicate()
+            res["error"] = "timed out after %d s (killed with its process group)" % budget
+        _RESULT["child_pgid"] = None
+        lines = [ln for ln in (o or "").splitlines() if ln.startswith("{")]
+        if lines:
+            res["line"] = json.loads(lines[-1])
+        elif "error" not in res:
+            res["error"] = "no result line (exit %s): %s" % (p.returncode, (e or "")[-400:])
+    except Exception as ex:  # noqa: BLE001
+        res["error"] = "%s: %s" % (type(ex).__name__, ex)
+    return res
+
+
+def child_bucket_jobs(args, dist, rank, world, specs, timeout_s=240):
+    """Rank 0 reruns the bucket allreduce as a child job of `world` ranks (torch.distributed.run, the
+    same GPUs) per (name, algo, env) in `specs`, while every rank of this job waits at a gloo barrier,
+    idle on the GPU. A child that fails or outlasts its budget is killed (its own process group) and
+    reported; the main line is never at stake. Returns name -> the child's result."""
     import socket
     out = {}
-    for name, env in ENV_VARIANTS:
+    for name, algo, env in specs:
         dist.barrier()
         if rank == 0:
             s_ = socket.socket()
@@ -799,49 +827,47 @@ def env_variant_jobs(args, dist, rank, world, timeout_s=240):
             s_.close()
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
                    "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
-                   "--gpus", str(world), "--steps", "10", "--warmup", "2", "--algo", "direct", "--no-compare",
+                   "--gpus", str(world), "--steps", "10", "--warmup", "2", "--algo", algo, "--no-compare",
                    "--no-sub", "--no-cpu-baseline", "--no-env-variants"] + \
                 (["--bucket-mib", str(args.bucket_mib)] if args.bucket_mib else [])
             cenv = {k: v for k, v in os.environ.items()
                     if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                                  "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TIPS_BOOTSTRAP_PORT")}
             cenv.update(env)
-            res = {"env": env}
+            res = {"env": env, "algorithm": algo}
             # within this job's watchdog, with a margin for the line and teardown
             budget = min(timeout_s, int(_RESULT.get("deadline", time.time() + timeout_s) - time.time()) - 40)
-            if budget < 60:
+            if budget < min(30, timeout_s):
                 out[name] = dict(res, error="skipped: %d s left before the watchdog" % (budget + 40))
                 dist.barrier()
                 continue
-            cenv["TIPS_BENCH_WATCHDOG"] = str(budget - 15)
-            try:
-                p = subprocess.Popen(cmd, env=cenv, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                                     start_new_session=True)
-                _RESULT["child_pgid"] = p.pid
-                try:
-                    o, e = p.communicate(timeout=budget)
-                except subprocess.TimeoutExpired:
-                    os.killpg(p.pid, signal.SIGKILL)
-                    o, e = p.communicate()
-                    res["error"] = "timed out after %d s" % budget
-                _RESULT["child_pgid"] = None
-                lines = [ln for ln in (o or "").splitlines() if ln.startswith("{")]
-                if lines:
-                    d = json.loads(lines[-1])
-                    res.update({k: d.get(k) for k in ("value", "ms_per_step", "check", "error")})
-                    res["algbw_gib_s"] = d.get("algbw_gib_s")
-                    ring = (d.get("configs") or {}).get("config3_ring") or {}
-                    if ring:  # the north star's ring under this setting (more channels per xGMI link)
-                        res["config3_ring"] = {k: ring.get(k) for k in ("ms_per_step", "busbw_GBps", "pipeline_depth",
-                                                                        "check")}
-                        res["config3_ring"]["frac_of_one_link"] = (ring.get("roofline") or {}).get("frac_of_one_link")
-                elif "error" not in res:
-                    res["error"] = "no result line (exit %s): %s" % (p.returncode, (e or "")[-400:])
-            except Exception as ex:  # noqa: BLE001 - a variant never costs the main line
-                res["error"] = "%s: %s" % (type(ex).__name__, ex)
+            cenv["TIPS_BENCH_WATCHDOG"] = str(max(15, budget - 15))
+            r = run_child(cmd, cenv, budget)
+            d = r.pop("line", None)
+            res.update(r)
+            if d:
+                res.update({k: d.get(k) for k in ("value", "ms_per_step", "check", "error") if d.get(k) is not None})
+                res["algbw_gib_s"] = d.get("algbw_gib_s")
+                ring = (d.get("configs") or {}).get("config3_ring") or {}
+                if ring:  # the north star's ring under this setting (more channels per xGMI link)
+                    res["config3_ring"] = {k: ring.get(k) for k in ("ms_per_step", "busbw_GBps", "pipeline_depth",
+                                                                    "check")}
+                    res["config3_ring"]["frac_of_one_link"] = (ring.get("roofline") or {}).get("frac_of_one_link")
             out[name] = res
         dist.barrier()
     return out
+
+
+def env_variant_jobs(args, dist, rank, world, timeout_s=240):
+    """The direct schedule under each RCCL setting of ENV_VARIANTS, as child jobs."""
+    return child_bucket_jobs(args, dist, rank, world, [(n, "direct", env) for n, env in ENV_VARIANTS], timeout_s)
+
+
+# The MI355X-native peer schedules (peer.cc: our own kernels over IPC-mapped peer memory, xGMI), as
+# child jobs on every N > 1 line (VERDICT r05 item 2): the push form and the fused pull-fold, whose
+# reduce-scatter is one kernel per rank reading every peer's slice over its xGMI link.
+PEER_CHILDREN = [("peer", "peer", {"TIPS_BENCH_CHILD_NO_RING": "1"}),
+                 ("peer_pullfold", "peer", {"TIPS_PEER_RS": "pullfold", "TIPS_BENCH_CHILD_NO_RING": "1"})]
 
 
 _RESULT = {}  # rank 0's finished result line, if the main measurement completed
@@ -1690,6 +1716,18 @@ def comparisons(job, w, line, last_words):
                   ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
                   # the same plan captured once and replayed as a HIP graph (TIPS_GRAPHS)
                   ("direct_graphs", "direct", {"TIPS_GRAPHS": "1", "TIPS_GRAPH_MAX_BYTES": str(1 << 40)})])
+    # The peer schedules as child jobs (TIPS_BENCH_PEER_CHILD=0 turns them off; TIPS_BENCH_PEER=1 ran
+    # them in this process above instead): a child that hangs or faults costs only its own entry.
+    if job.world > 1 and w.workload == "bucket" and os.environ.get("TIPS_BENCH_PEER") != "1" and \
+            os.environ.get("TIPS_BENCH_PEER_CHILD", "1") != "0" and not job.args.no_env_variants and \
+            job.afford("the peer-schedule child jobs", 120):
+        note_progress("the peer-schedule child jobs")
+        kids = child_bucket_jobs(job.args, job.dist, job.rank, job.world, PEER_CHILDREN,
+                                 timeout_s=int(os.environ.get("TIPS_BENCH_PEER_CHILD_TIMEOUT_S", "150")))
+        line["peer_children"] = kids
+        for name, r in kids.items():
+            compare[name] = r.get("algbw_gib_s") if not r.get("error") else None
+            compare_check[name] = r.get("check") or ("error: %s" % r.get("error"))
     if job.world > 1 and not os.environ.get("TIPS_NO_RCCL") and job.afford("the xGMI link probe", 30):
         note_progress("the xGMI link probe")
         try:
@@ -1715,8 +1753,8 @@ def comparisons(job, w, line, last_words):
                       # the fused pull-fold reduce-scatter: one kernel per rank reads its chunk's slices
                       # from every peer's workspace over xGMI and folds them (peer.cc peer_piece_pullfold)
                       ("peer_pullfold", "peer", {"TIPS_PEER_RS": "pullfold"})])
-    elif job.world > 1:
-        compare_check["peer"] = "opt-in: TIPS_BENCH_PEER=1 (not yet run across real GPUs)"
+    elif job.world > 1 and "peer" not in compare_check:
+        compare_check["peer"] = "not run (peer_children: TIPS_BENCH_PEER_CHILD=0, --no-env-variants or the budget)"
     # Opt-in (TIPS_BENCH_LANES=1): transfer lanes split communicators that live to the end of
     # the job; on the socket rehearsal they ran 10x slower and slowed every later call.
     if os.environ.get("TIPS_BENCH_LANES") == "1":
@@ -1856,7 +1894,8 @@ def bench_job(args):
             line["gpu_topology"] = topo
     _RESULT["line"] = line if rank == 0 else None
     _RESULT["done"] = True
-    if w is not None and workload == "bucket" and world > 1:
+    # (mandatory on every N > 1 line; a peer-schedule child job skips it: its parent line has it)
+    if w is not None and workload == "bucket" and world > 1 and os.environ.get("TIPS_BENCH_CHILD_NO_RING") != "1":
         north_star_ring(job, w, line)  # mandatory, before every sub-record and budgeted leg
         _RESULT["line"] = line if rank == 0 else None
     if args.workload == "auto" and not args.no_sub:

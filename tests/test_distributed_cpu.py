@@ -316,3 +316,51 @@ def test_bench_budget_is_decided_together():
     for rank, got, skipped in res:
         assert got == [True, False, True], (rank, got)
         assert skipped == ["b"]
+
+
+def _child_hang_worker(rank, world, port, q):
+    import time
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TIPS_BENCH_CHILD_TEST="hang")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    class Args:
+        bucket_mib = None
+    line = {"metric": "m", "value": 1.0, "compare_algbw_gib_s": {}, "compare_check": {}}
+    t0 = time.time()
+    bench._RESULT["deadline"] = t0 + 600  # (the job's watchdog, far away)
+    kids = bench.child_bucket_jobs(Args(), dist, rank, world, bench.PEER_CHILDREN, timeout_s=4)
+    line["peer_children"] = kids
+    for name, r in kids.items():
+        line["compare_algbw_gib_s"][name] = r.get("algbw_gib_s") if not r.get("error") else None
+        line["compare_check"][name] = r.get("check") or ("error: %s" % r.get("error"))
+    dt = time.time() - t0
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, line, dt))
+
+
+def test_peer_child_that_hangs_costs_only_its_entry():
+    """bench.py runs the peer schedules (push and the fused pull-fold) as child
+    jobs on every N > 1 line, after the main line is measured. A child that never ends
+    (TIPS_BENCH_CHILD_TEST=hang replaces it with a sleeping process) is killed with its process group
+    at its budget; every rank of the parent job leaves the barrier, and the line keeps its measured
+    value with the child's entry reporting the time-out."""
+    import torch.multiprocessing as tmp
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_child_hang_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+    line0, dt0 = res[0][1], res[0][2]
+    assert line0["value"] == 1.0 and dt0 < 30
+    for name in ("peer", "peer_pullfold"):
+        assert "timed out" in line0["peer_children"][name]["error"], line0
+        assert line0["compare_algbw_gib_s"][name] is None and line0["compare_check"][name].startswith("error: timed out")
+    assert res[1][1]["peer_children"] == {}  # (the other ranks only wait)
