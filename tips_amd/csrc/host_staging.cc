@@ -13,6 +13,8 @@
 #include <condition_variable>
 #include <thread>
 
+#include <pthread.h>
+
 #include "rt.h"
 
 namespace tips {
@@ -132,8 +134,42 @@ inline int64_t now_ns() {
 }  // namespace
 
 HostPool::HostPool(int nthreads) : spin_ns_(std::max<int64_t>(0, env_i64("TIPS_HOST_SPIN_US", 300)) * 1000) {
-  for (int i = 1; i < nthreads; i++) th_.emplace_back([this] { worker(); });
+  for (int i = 1; i < nthreads; i++)
+    th_.emplace_back([this, i] {
+      (void)pthread_setname_np(pthread_self(), "tips-host");  // (/proc/<pid>/task/*/comm: placement records)
+      worker(i - 1);
+    });
 }
+
+namespace {
+bool read_cpulist(const std::string& path, cpu_set_t* set);  // (below)
+
+// Worker k's share of a pool mask (TIPS_HOST_SPREAD, default 1): the CPUs of the mask that share an
+// L3 (one CCD on EPYC) with the mask's (k mod domains)-th L3 domain. Left to the scheduler, the
+// workers woken by one thread gather on its CCD, and one CCD's link to the I/O die caps what its
+// cores copy: config 5 as named host requests took 3.2-4.7 ms per step with the pool gathered on the
+// pinned negotiation thread's CCD (profiles/r06/op_host_bind_ab_r6q/r6r/r6s.txt) and 2.89-3.22 with
+// the workers spread, against 3.00-3.12 unpinned (op_host_bind_ab_r6t.txt).
+bool l3_share(const cpu_set_t& mask, int k, cpu_set_t* out) {
+  std::vector<cpu_set_t> groups;
+  std::vector<int> firsts;
+  for (int c = 0; c < CPU_SETSIZE; c++) {
+    if (!CPU_ISSET(c, &mask)) continue;
+    bool known = false;
+    for (const cpu_set_t& g : groups) known = known || CPU_ISSET(c, &g);
+    if (known) continue;
+    cpu_set_t g;
+    if (!read_cpulist("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/shared_cpu_list", &g))
+      return false;
+    CPU_AND(&g, &g, &mask);
+    if (CPU_COUNT(&g) == 0) return false;
+    groups.push_back(g);
+  }
+  if (groups.size() < 2) return false;
+  *out = groups[(size_t)k % groups.size()];
+  return true;
+}
+}  // namespace
 
 HostPool::~HostPool() {
   {
@@ -160,10 +196,13 @@ void HostPool::grab(uint64_t gen) {  // claim jobs of run `gen` until none is le
   }
 }
 
-void HostPool::worker() {
+void HostPool::worker(int k) {
   uint64_t seen = 0, mask_seen = 0;
-  cpu_set_t start;
-  const bool have_start = sched_getaffinity(0, sizeof start, &start) == 0;
+  // unbound, a worker may run anywhere the process may - not only where the thread that started the
+  // pool may (the negotiation thread that runs named host requests is pinned to one L3)
+  cpu_set_t start = process_cpus();
+  const bool have_start = true;
+  (void)sched_setaffinity(0, sizeof start, &start);
   while (true) {
     uint64_t gen;
     std::vector<unsigned char> want;
@@ -186,8 +225,14 @@ void HostPool::worker() {
       }
     }
     if (remask) {  // (best effort: a refused mask leaves the thread where it was)
-      if (want.size() == sizeof(cpu_set_t)) (void)sched_setaffinity(0, sizeof(cpu_set_t), (const cpu_set_t*)want.data());
-      else if (have_start) (void)sched_setaffinity(0, sizeof start, &start);
+      if (want.size() == sizeof(cpu_set_t)) {
+        const cpu_set_t* m = (const cpu_set_t*)want.data();
+        cpu_set_t share;
+        if (env_i64("TIPS_HOST_SPREAD", 1) != 0 && l3_share(*m, k, &share)) m = &share;
+        (void)sched_setaffinity(0, sizeof(cpu_set_t), m);
+      } else if (have_start) {
+        (void)sched_setaffinity(0, sizeof start, &start);
+      }
     }
     grab(gen);
   }
@@ -303,9 +348,8 @@ bool gpu_local_cpus(int device, cpu_set_t* out) {
   const int got = fscanf(f, "%d", &node);
   fclose(f);
   if (got != 1 || node < 0) return false;
-  cpu_set_t local, allowed;
+  cpu_set_t local, allowed = process_cpus();  // (not this thread's mask: it may be the pinned negotiation thread)
   if (!read_cpulist("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", &local)) return false;
-  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
   CPU_AND(out, &local, &allowed);
   return CPU_COUNT(out) > 0;
 }
@@ -407,18 +451,35 @@ int fused_allreduce_host(State& st, const BatchItem* items, int n, int dtype, ch
     delete st.host_pool;
     st.host_pool = new HostPool(nthreads);
   }
-  {  // TIPS_HOST_BIND (default 1): the pool's threads on the GPU's NUMA node, as RCCL places its own
-     // threads (the caller's thread stays put). Config 5 host -> host: 0.5-1.5 % faster in each of 3
-     // interleaved rounds on a box whose process may run on both nodes (profiles/r03/p_numa_probe.jsonl)
-    static int local_ok = -1;
-    static cpu_set_t local;
-    if (env_i64("TIPS_HOST_BIND", 1) != 0) {
-      if (local_ok < 0) local_ok = gpu_local_cpus(st.device, &local) ? 1 : 0;
-      st.host_pool->set_affinity(local_ok == 1 ? &local : nullptr);
-    } else {
-      st.host_pool->set_affinity(nullptr);
-    }
+  // TIPS_HOST_BIND (default 1): the pool's threads on the GPU's NUMA node, as RCCL places its own
+  // threads (the caller's thread stays put). Config 5 host -> host: 0.5-1.5 % faster in each of 3
+  // interleaved rounds on a box whose process may run on both nodes (profiles/r03/p_numa_probe.jsonl)
+  static int local_ok = -1;
+  static cpu_set_t local;
+  const bool host_bind = env_i64("TIPS_HOST_BIND", 1) != 0;
+  if (host_bind) {
+    if (local_ok < 0) local_ok = gpu_local_cpus(st.device, &local) ? 1 : 0;
+    st.host_pool->set_affinity(local_ok == 1 ? &local : nullptr);
+  } else {
+    st.host_pool->set_affinity(nullptr);
   }
+  // The negotiation thread runs named host requests' fused calls, and it is pinned to its caller's
+  // L3 (TIPS_NEG_BIND): for the call it moves to the GPU's node, where the pool and the DMA engines
+  // are (it packs and unpacks a share and issues every copy), and back after it. A user's thread is
+  // never moved. Config 5 as named host requests: 3.37-3.47 ms per step with the thread left on the
+  // caller's L3 on the other socket, 3.08-3.22 unbound (profiles/r06/op_host_bind_ab_r6r.txt).
+  struct Near {
+    bool moved = false;
+    cpu_set_t saved;
+    Near(bool want, const cpu_set_t* to) {
+      if (want && to && pthread_getaffinity_np(pthread_self(), sizeof saved, &saved) == 0 &&
+          pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), to) == 0)
+        moved = true;
+    }
+    ~Near() {
+      if (moved) (void)pthread_setaffinity_np(pthread_self(), sizeof saved, &saved);
+    }
+  } near(host_bind && local_ok == 1 && on_negotiation_thread(), &local);
   if (st.hpin_bytes < (size_t)(R * piece)) {
     for (void*& p : st.hpin)
       if (p) (void)hipHostFree(p), p = nullptr;

@@ -402,8 +402,7 @@ bool neg_bind_set(int cpu, cpu_set_t* out) {
   } else {
     return false;
   }
-  cpu_set_t allowed;
-  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
+  cpu_set_t allowed = process_cpus();
   CPU_AND(out, &want, &allowed);
   return CPU_COUNT(out) > 0;
 }

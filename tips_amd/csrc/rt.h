@@ -3,6 +3,8 @@
 // simulators; fusion.cc; host_staging.cc; control.cc). Not part of the C-ABI.
 #pragma once
 
+#include <sched.h>
+
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
@@ -164,7 +166,7 @@ class HostPool {
   void set_affinity(const void* cpus);
 
  private:
-  void worker();
+  void worker(int k);  // k: the worker's index (its L3 share of the mask, TIPS_HOST_SPREAD)
   void grab(uint64_t gen);
   std::vector<unsigned char> mask_;  // guarded by m_: the wanted cpu_set_t bytes (empty: the start mask)
   std::atomic<uint64_t> mask_gen_{0};
@@ -323,6 +325,10 @@ int64_t fusion_threshold_bytes();
 // each bucket allreduced in the wire type, cast back while unpacked. One rank: the round trip.
 int fused_allreduce_cast(State& st, const BatchItem* items, int n, int wire, hipStream_t stream);
 void fusion_release(State& st);  // (shutdown)
+// The CPUs this process may run on, as the thread that loaded the library saw them: the base of
+// every binding the library makes. (A thread's own mask is not: the negotiation thread is pinned to
+// one L3, and a pool it starts, or a mask computed on it, would inherit that.)
+const cpu_set_t& process_cpus();
 void pack_signals_release(State& st);  // fusion.cc: the merged pack's counters and signal words
 // control.cc: ConstructResponseMessage's rules over p request records (TIPS_REQUEST_WORDS each)
 int check_records(const int64_t* t, int p);

@@ -137,6 +137,23 @@ int resolve_algo(int algo, int p, int64_t bytes) {
   return (p <= 2 || p > tips::kMaxSrcs) ? TIPS_ALGO_RING : TIPS_ALGO_DIRECT;
 }
 
+const cpu_set_t& process_cpus() {
+  static const cpu_set_t set = [] {
+    cpu_set_t s;
+    if (sched_getaffinity(0, sizeof s, &s) != 0) {
+      CPU_ZERO(&s);
+      for (int i = 0; i < CPU_SETSIZE; i++) CPU_SET(i, &s);
+    }
+    return s;
+  }();
+  return set;
+}
+
+namespace {
+// captured when the library is loaded, on the loading thread (before any thread of ours is pinned)
+__attribute__((constructor)) void capture_process_cpus() { (void)process_cpus(); }
+}  // namespace
+
 void rccl_env_defaults() {
   // Captured plans (TIPS_GRAPHS) key their graphs by buffer address and allocation id; RCCL's
   // graph-time buffer registration would pin peers' mappings of a buffer past its free, so with

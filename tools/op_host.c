@@ -22,6 +22,7 @@
  *                             (oracle_fold) of all ranks' regenerated inputs (test infrastructure).
  * Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (tips_init); OP_HOST_STEPS (20), OP_HOST_WARMUP (3),
  * OP_HOST_THREADS (4). Prints one JSON line. */
+#include <dirent.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdint.h>
@@ -227,6 +228,58 @@ static int env_int(const char* k, int d) {
   return v && *v ? atoi(v) : d;
 }
 
+/* where the main thread and the library's named threads (tips-neg, tips-done, tips-host) last ran:
+ * "name:cpu/first CPU of its L3/socket ..." (/proc/self/task/ * /stat field 39; sysfs topology) */
+static int read_first_int(const char* path) {
+  FILE* f = fopen(path, "r");
+  int v = -1;
+  if (f) {
+    if (fscanf(f, "%d", &v) != 1) v = -1;
+    fclose(f);
+  }
+  return v;
+}
+
+static void thread_placement(char* out, size_t cap) {
+  size_t l = 0;
+  out[0] = 0;
+  DIR* d = opendir("/proc/self/task");
+  if (!d) return;
+  struct dirent* e;
+  while ((e = readdir(d)) != NULL && l + 64 < cap) {
+    const long tid = atol(e->d_name);
+    if (tid <= 0) continue;
+    char path[128], comm[64] = "", stat[1024];
+    snprintf(path, sizeof path, "/proc/self/task/%ld/comm", tid);
+    FILE* f = fopen(path, "r");
+    if (!f) continue;
+    if (!fgets(comm, sizeof comm, f)) comm[0] = 0;
+    fclose(f);
+    comm[strcspn(comm, "\n")] = 0;
+    const int is_main = tid == (long)getpid();
+    if (!is_main && strncmp(comm, "tips-", 5) != 0) continue;
+    snprintf(path, sizeof path, "/proc/self/task/%ld/stat", tid);
+    f = fopen(path, "r");
+    if (!f) continue;
+    const size_t n = fread(stat, 1, sizeof stat - 1, f);
+    fclose(f);
+    stat[n] = 0;
+    char* q = strrchr(stat, ')');
+    int cpu = -1, field = 2;
+    for (char* t = q ? strtok(q + 1, " ") : NULL; t; t = strtok(NULL, " "))
+      if (++field == 39) {
+        cpu = atoi(t);
+        break;
+      }
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+    const int l3 = read_first_int(path);
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/physical_package_id", cpu);
+    const int sock = read_first_int(path);
+    l += (size_t)snprintf(out + l, cap - l, "%s%s:%d/%d/%d", l ? " " : "", is_main ? "main" : comm, cpu, l3, sock);
+  }
+  closedir(d);
+}
+
 int main(void) {
   const int steps = env_int("OP_HOST_STEPS", 20), warmup = env_int("OP_HOST_WARMUP", 3);
   g_threads = env_int("OP_HOST_THREADS", 4);
@@ -310,14 +363,16 @@ int main(void) {
     check = bad ? "FAIL vs oracle_fold" : "bit-exact vs oracle_fold of all ranks' inputs";
   }
 #endif
+  char placement[1024];
+  thread_placement(placement, sizeof placement);
   tips_shutdown();
   const int ok = rc == 0 && bad == 0;
   const double bytes = (double)total * 4;
   printf("{\"rank\": %d, \"ok\": %s, \"ranks\": %d, \"tensors\": %d, \"elements\": %lld, \"threads\": %d, \"steps\": %d, "
          "\"warmup\": %d, \"ms_per_step\": %.4f, \"ms_mean\": %.4f, \"ms_best\": %.4f, \"algbw_gib_s\": %.3f, "
-         "\"check\": \"%s\", \"error\": \"",
+         "\"check\": \"%s\", \"placement\": \"%s\", \"error\": \"",
          g_rank, ok ? "true" : "false", g_size, g_n, (long long)total, g_threads, steps, warmup, med * 1e3,
-         sum / steps * 1e3, best * 1e3, bytes / med / (double)(1ull << 30), check);
+         sum / steps * 1e3, best * 1e3, bytes / med / (double)(1ull << 30), check, placement);
   for (const char* c = g_err; *c; c++) putchar(*c == '"' ? '\'' : *c);
   printf("\"}\n");
   free(per);
