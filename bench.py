@@ -1709,15 +1709,9 @@ def comparisons(job, w, line, last_words):
     # (oneshot targets small buckets only.) The _k entries re-run a schedule at another sub-chunk
     # pipeline depth (read per call). Order: RCCL's allreduce and the other schedules, the link probe,
     # the probes; then the opt-in legs (IPC peer schedules, transfer lanes).
-    # (ring at its best depth and ncclAllReduce are the mandatory configs.config3_ring / _rccl records)
-    run_variants([("direct", "direct", {}),
-                  ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
-                  ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
-                  ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
-                  # the same plan captured once and replayed as a HIP graph (TIPS_GRAPHS)
-                  ("direct_graphs", "direct", {"TIPS_GRAPHS": "1", "TIPS_GRAPH_MAX_BYTES": str(1 << 40)})])
-    # The peer schedules as child jobs (TIPS_BENCH_PEER_CHILD=0 turns them off; TIPS_BENCH_PEER=1 ran
-    # them in this process above instead): a child that hangs or faults costs only its own entry.
+    # First, the peer schedules as child jobs (the MI355X-native exchange: our kernels over IPC-mapped
+    # peer memory; TIPS_BENCH_PEER_CHILD=0 turns them off; TIPS_BENCH_PEER=1 runs them in this
+    # process instead, below): a child that hangs or faults costs only its own entry.
     if job.world > 1 and w.workload == "bucket" and os.environ.get("TIPS_BENCH_PEER") != "1" and \
             os.environ.get("TIPS_BENCH_PEER_CHILD", "1") != "0" and not job.args.no_env_variants and \
             job.afford("the peer-schedule child jobs", 120):
@@ -1728,6 +1722,13 @@ def comparisons(job, w, line, last_words):
         for name, r in kids.items():
             compare[name] = r.get("algbw_gib_s") if not r.get("error") else None
             compare_check[name] = r.get("check") or ("error: %s" % r.get("error"))
+    # (ring at its best depth and ncclAllReduce are the mandatory configs.config3_ring / _rccl records)
+    run_variants([("direct", "direct", {}),
+                  ("direct_k1", "direct", {"TIPS_PIPELINE_DEPTH": "1"}),
+                  ("direct_k8", "direct", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
+                  ("ring_k8", "ring", {"TIPS_PIPELINE_DEPTH": "8", "TIPS_MIN_SUBCHUNK_BYTES": str(2 << 20)}),
+                  # the same plan captured once and replayed as a HIP graph (TIPS_GRAPHS)
+                  ("direct_graphs", "direct", {"TIPS_GRAPHS": "1", "TIPS_GRAPH_MAX_BYTES": str(1 << 40)})])
     if job.world > 1 and not os.environ.get("TIPS_NO_RCCL") and job.afford("the xGMI link probe", 30):
         note_progress("the xGMI link probe")
         try:

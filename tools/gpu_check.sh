@@ -6,7 +6,9 @@
 #   bench1      python bench.py (N = 1, the driver's default command)        -> bench_n1.jsonl
 #   bench1prof  rocprofv3 --kernel-trace --stats of bench.py --no-sub          -> prof/
 #   rehearse2   bench.py --gpus 2 over the socket transport (TIPS_BENCH_FAKE_HOSTS=1)  -> rehearsal_n2.log
-#   rehearse8   the same at N = 8                                             -> rehearsal_n8.log
+#   rehearse4   the same at N = 4 (with its peer-schedule child jobs: 4 + 4 processes on the GPU)
+#   rehearse8   the same at N = 8 (its child jobs would put 16+ processes on the one GPU: the box's
+#               process guard allows 16, so run it with TIPS_BENCH_PEER_CHILD=0 or --no-env-variants)                                             -> rehearsal_n8.log
 #   smoke       __graft_entry__.smoke()
 #   custom      bash -c "$CUSTOM"
 set -u
@@ -36,6 +38,8 @@ for s in ${STEPS:-pytest bench1}; do
                   --no-sub --no-cpu-baseline --no-extras --steps 200 --warmup 20 > "$OUT/bench_prof.log" 2>&1 || exit $? ;;
     rehearse2) TIPS_BENCH_FAKE_HOSTS=1 run rehearse2 "${N2_TIMEOUT:-600}" python -u bench.py --gpus 2 ${REHEARSE_ARGS:-} \
                  > "$OUT/rehearsal_n2.log" 2>&1 || exit $? ;;
+    rehearse4) TIPS_BENCH_FAKE_HOSTS=1 run rehearse4 "${N4_TIMEOUT:-700}" python -u bench.py --gpus 4 ${REHEARSE_ARGS:-} \
+                 > "$OUT/rehearsal_n4.log" 2>&1 || exit $? ;;
     rehearse8) TIPS_BENCH_FAKE_HOSTS=1 run rehearse8 "${N8_TIMEOUT:-700}" python -u bench.py --gpus 8 ${REHEARSE_ARGS:-} \
                  > "$OUT/rehearsal_n8.log" 2>&1 || exit $? ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit $? ;;
