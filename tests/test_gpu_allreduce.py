@@ -198,16 +198,18 @@ def test_rccl_allreduce_single_rank(gpu):
         gpu.set_algorithm(prev)
 
 
+@pytest.mark.parametrize("aligned", [False, True])
 @pytest.mark.parametrize("wire", ["float16", "bfloat16"])
 @pytest.mark.parametrize("threshold", [4096, 64 << 20])
-def test_fused_cast_round_trip(gpu, monkeypatch, threshold, wire):
+def test_fused_cast_round_trip(gpu, monkeypatch, threshold, wire, aligned):
     """One rank: tips_fused_allreduce_cast is the round trip f32 -> wire -> f32 (the reference's
     compress -> allreduce -> decompress at one rank, compression.py:49-66), bit-exact against the
     oracle's casts (RNE): 300 odd-sized misaligned views (ragged ends: the kernel's per-element
     path), a tensor above the threshold at 4096 (the range-cast path through the scratch buffer),
     values that round to f16 subnormals and overflow to inf; out of place through
     tips_amd.fused_allreduce_cast and in place through the C-ABI; the inputs of the out-of-place
-    call unchanged."""
+    call unchanged. aligned=True starts every view on 16 B (the kernels' quad path: 16 B of f32 and
+    8 B of wire per lane, the odd sizes' last n % 4 elements one at a time)."""
     import torch
     import oracle_bind
     from tips_amd import _lib
@@ -215,14 +217,16 @@ def test_fused_cast_round_trip(gpu, monkeypatch, threshold, wire):
     code = oracle_bind.F16 if wire == "float16" else oracle_bind.BF16
     rng = np.random.default_rng(7)
     sizes = [int(round(2 ** rng.uniform(0, 14))) for _ in range(300)] + [5000, 1, 70001]
-    vals = rng.standard_normal(sum(sizes) + len(sizes) + 1).astype(np.float32)
+    vals = rng.standard_normal(sum(sizes) + 4 * len(sizes) + 4).astype(np.float32)
     vals[::97] *= 1e-6   # f16 subnormals
     vals[::211] *= 1e5   # beyond f16's range: inf
     base = torch.from_numpy(vals).cuda()
-    views, off = [], 1  # offset 1: misaligned views (4-B aligned f32 sides), a gap after each
+    views, off = [], 0 if aligned else 1  # offset 1: misaligned views (4-B aligned f32 sides), a gap after each
     for k in sizes:
         views.append(base[off:off + k])
         off += k + 1
+        if aligned:
+            off = (off + 3) // 4 * 4
     before = base.clone()
     exp = [oracle_bind.cast_from16(oracle_bind.cast_to16(v.cpu().numpy(), code), code) for v in views]
     for _ in range(2):  # (the second call finds the layout and the table)

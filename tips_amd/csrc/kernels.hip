@@ -31,6 +31,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 enum { kF32 = 0, kF64 = 1, kI32 = 2, kI64 = 3, kF16 = 4, kBF16 = 5 };
 constexpr int kBlock = 256;  // 4 waves of 64
@@ -765,6 +766,15 @@ __device__ __forceinline__ void store16_pol(int64_t d, u32x4 x) {
   }
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u32x2 g_u32x2;
+
+// the 8-B form (the wire side of the cast kernels: 4 half-width elements per lane)
+__device__ __forceinline__ void store8_sc1(int64_t d, u32x2 x) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" ::"v"(reinterpret_cast<g_u32x2*>(d)), "v"(x)
+               : "memory");
+}
+
 // The < 16 bytes of a vector at a tensor's ragged end, or a whole vector of a tensor that is not
 // 16-B aligned: loaded as dwords (shorts when the tensor's offset or length is only 2-B aligned,
 // 16-bit types) - phase 1 issues the loads, phase 2 the stores, so a lane waits for memory once.
@@ -906,30 +916,26 @@ __global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __rest
 // segment lives at base + 2 v for virtual byte v (fusion.cc's kSlotCast records). DIR 0 (pack):
 // f32 source -> wire destination, RNE as oracle_float_to_half / oracle_float_to_bf16 (the
 // reference's tf.cast, compression.py:49-66); DIR 1 (unpack): wire source -> f32 destination, exact.
-// A lane moves one 16-B wire vector = 8 elements = 32 B of f32 (two 16-B accesses).
+// A lane moves quads: 4 elements = 16 B of f32 and 8 B of the wire type, so every access of a
+// wave is one contiguous run (1 KiB of f32, 512 B of wire). (Round 6's first form moved 8 elements
+// per lane as one 16-B wire vector and two 16-B f32 accesses 32 B apart: each f32 instruction then
+// touched every other 16 B of a 2 KiB span, and config 5's round trip ran at 0.44 of HBM, the
+// unpack at 0.37; profiles/r06/cast_probe_*.)
 
 template <int WT>
-__device__ __forceinline__ u32x4 narrow8(f32x4 a, f32x4 b) {
+__device__ __forceinline__ u32x2 narrow4(f32x4 a) {
   if constexpr (WT == kF16) {
-    const f32x8 w = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    return __builtin_bit_cast(u32x4, __builtin_convertvector(w, f16x8));
+    return __builtin_bit_cast(u32x2, __builtin_convertvector(a, f16x4));
   } else {  // bf16: word i = elements 2i (low half) and 2i + 1 (high half)
-    const u32x4 x = __builtin_bit_cast(u32x4, a), y = __builtin_bit_cast(u32x4, b);
-    return u32x4{bf16_round_bits(x[0]) | (bf16_round_bits(x[1]) << 16), bf16_round_bits(x[2]) | (bf16_round_bits(x[3]) << 16),
-                 bf16_round_bits(y[0]) | (bf16_round_bits(y[1]) << 16), bf16_round_bits(y[2]) | (bf16_round_bits(y[3]) << 16)};
+    const u32x4 x = __builtin_bit_cast(u32x4, a);
+    return u32x2{bf16_round_bits(x[0]) | (bf16_round_bits(x[1]) << 16), bf16_round_bits(x[2]) | (bf16_round_bits(x[3]) << 16)};
   }
 }
 
 template <int WT>
-__device__ __forceinline__ void widen8(u32x4 v, f32x4& a, f32x4& b) {
-  if constexpr (WT == kF16) {
-    const f32x8 w = __builtin_convertvector(__builtin_bit_cast(f16x8, v), f32x8);
-    a = f32x4{w[0], w[1], w[2], w[3]};
-    b = f32x4{w[4], w[5], w[6], w[7]};
-  } else {
-    a = __builtin_bit_cast(f32x4, u32x4{v[0] << 16, v[0] & 0xffff0000u, v[1] << 16, v[1] & 0xffff0000u});
-    b = __builtin_bit_cast(f32x4, u32x4{v[2] << 16, v[2] & 0xffff0000u, v[3] << 16, v[3] & 0xffff0000u});
-  }
+__device__ __forceinline__ f32x4 widen4(u32x2 v) {
+  if constexpr (WT == kF16) return __builtin_convertvector(__builtin_bit_cast(f16x4, v), f32x4);
+  else return __builtin_bit_cast(f32x4, u32x4{v[0] << 16, v[0] & 0xffff0000u, v[1] << 16, v[1] & 0xffff0000u});
 }
 
 template <int WT>
@@ -947,11 +953,14 @@ __device__ __forceinline__ float widen1(unsigned short h) {
 typedef __attribute__((address_space(1))) f32x4 g_f32x4;
 typedef __attribute__((address_space(1))) float g_f32;
 
-template <int U, int DIR, int WT>
+// VAR (sweeps, TIPS_CAST_VARIANT): bit 0 plain loads instead of nt; bits 1-2 the store policy
+// (0 = sc1, the default; 1 = plain; 2 = nt)
+template <int U, int DIR, int WT, int VAR = 0>
 __global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __restrict__ tiles,
                                                           const CopySeg* __restrict__ segs, int tile0, int ntiles) {
   constexpr int64_t kTileBytes = (int64_t)kBlock * 16 * U;  // wire bytes
   constexpr int kMaxSeg = (int)(kTileBytes / 256) + 1;
+  constexpr int Q = 2 * U;  // quads per lane
   __shared__ CopySeg L[kMaxSeg];
   const int64_t tt = xcd_tile(blockIdx.x, gridDim.x);
   if (tt >= ntiles) return;  // (whole workgroup: before any barrier)
@@ -968,14 +977,14 @@ __global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __rest
     if (tid < cnt) L[tid] = segs[(int)a_src + tid];
     __syncthreads();
   }
-  int64_t sp[U], dp[U];
-  int len[U];
-  bool full[U];
-  u32x4 nv[U];      // pack: the narrowed vector; unpack: the loaded wire vector
-  f32x4 wa[U], wb[U];  // pack: the loaded f32 pair
+  int64_t sp[Q], dp[Q];
+  int len[Q];  // wire bytes of this quad inside its segment (8 = all four elements)
+  bool full[Q];
+  u32x2 nv[Q];  // unpack: the loaded wire quad
+  f32x4 wa[Q];  // pack: the loaded f32 quad
 #pragma unroll
-  for (int u = 0; u < U; u++) {
-    const int64_t v = tb + (int64_t)u * (kBlock * 16) + (int64_t)tid * 16;
+  for (int u = 0; u < Q; u++) {
+    const int64_t v = tb + (int64_t)u * (kBlock * 8) + (int64_t)tid * 8;
     int64_t g_src, g_dst, g_beg, g_end;
     if (multi) {
       int lo = 0, hi = cnt - 1;  // the last segment beginning at or before v
@@ -996,32 +1005,32 @@ __global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __rest
       g_end = b ? b_end : a_end;
     }
     const int64_t left = g_end - v;
-    len[u] = (v >= g_beg && left > 0) ? (int)(left < 16 ? left : 16) : 0;
+    len[u] = (v >= g_beg && left > 0) ? (int)(left < 8 ? left : 8) : 0;
     sp[u] = g_src + (DIR == 0 ? 2 * v : v);  // the f32 side at base + 2 v
     dp[u] = g_dst + (DIR == 0 ? v : 2 * v);
-    full[u] = len[u] == 16 && ((sp[u] | dp[u]) & 15) == 0;
+    const int64_t f32_side = DIR == 0 ? sp[u] : dp[u], wire_side = DIR == 0 ? dp[u] : sp[u];
+    full[u] = len[u] == 8 && (f32_side & 15) == 0 && (wire_side & 7) == 0;
     if (full[u]) {
-      if constexpr (DIR == 0) {
-        wa[u] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(sp[u]));
-        wb[u] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(sp[u] + 16));
-      } else {
-        nv[u] = __builtin_nontemporal_load(reinterpret_cast<const g_u32x4*>(sp[u]));
-      }
+      if constexpr (DIR == 0) wa[u] = (VAR & 1) ? *reinterpret_cast<const g_f32x4*>(sp[u])
+                                                : __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(sp[u]));
+      else nv[u] = (VAR & 1) ? *reinterpret_cast<const g_u32x2*>(sp[u])
+                             : __builtin_nontemporal_load(reinterpret_cast<const g_u32x2*>(sp[u]));
     }
   }
+  constexpr int kStore = (VAR >> 1) & 3;
 #pragma unroll
-  for (int u = 0; u < U; u++) {
+  for (int u = 0; u < Q; u++) {
     if (full[u]) {
       if constexpr (DIR == 0) {
-        store16_pol<2>(dp[u], narrow8<WT>(wa[u], wb[u]));
+        const u32x2 w = narrow4<WT>(wa[u]);
+        if constexpr (kStore == 0) store8_sc1(dp[u], w);
+        else if constexpr (kStore == 1) *reinterpret_cast<g_u32x2*>(dp[u]) = w;
+        else __builtin_nontemporal_store(w, reinterpret_cast<g_u32x2*>(dp[u]));
       } else {
-        f32x4 a, b;
-        widen8<WT>(nv[u], a, b);
-        store16_pol<2>(dp[u], __builtin_bit_cast(u32x4, a));
-        store16_pol<2>(dp[u] + 16, __builtin_bit_cast(u32x4, b));
+        store16_pol<kStore == 0 ? 2 : kStore == 1 ? 0 : 1>(dp[u], __builtin_bit_cast(u32x4, widen4<WT>(nv[u])));
       }
     } else {
-      for (int e = 0; 2 * e < len[u]; e++) {  // a tensor's ragged end, or an f32 side not 16-B aligned
+      for (int e = 0; 2 * e < len[u]; e++) {  // a tensor's ragged end, or a side not aligned
         if constexpr (DIR == 0)
           *reinterpret_cast<g_u16*>(dp[u] + 2 * e) = narrow1<WT>(*reinterpret_cast<const g_f32*>(sp[u] + 4 * e));
         else
@@ -1032,11 +1041,28 @@ __global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __rest
 }
 
 // Elementwise cast of one contiguous range (a fused list's tensors of at least the threshold, which
-// travel through a scratch buffer of the wire type): DIR 0 f32 -> wire, 1 wire -> f32.
+// travel through a scratch buffer of the wire type): DIR 0 f32 -> wire, 1 wire -> f32. Quads as in
+// cast_segs_kernel (16 B of f32, 8 B of wire per lane per access) when both sides allow it (the
+// caller's f32 pointer 16-B aligned, the wire side 8-B aligned); the last n % 4 elements, or every
+// element of a misaligned range, one at a time.
 template <int DIR, int WT>
 __global__ __launch_bounds__(kBlock) void cast_range_kernel(void* __restrict__ dst, const void* __restrict__ src,
                                                            int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t f32_side = (int64_t)(DIR == 0 ? src : dst), wire_side = (int64_t)(DIR == 0 ? dst : src);
+  int64_t head = 0;
+  if ((f32_side & 15) == 0 && (wire_side & 7) == 0) {
+    const int64_t nq = n / 4;
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += stride) {
+      if constexpr (DIR == 0)
+        store8_sc1(wire_side + 8 * q, narrow4<WT>(__builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(f32_side + 16 * q))));
+      else
+        store16_pol<2>(f32_side + 16 * q, __builtin_bit_cast(u32x4, widen4<WT>(
+                                              __builtin_nontemporal_load(reinterpret_cast<const g_u32x2*>(wire_side + 8 * q)))));
+    }
+    head = 4 * nq;
+  }
+  for (int64_t i = head + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     if constexpr (DIR == 0) static_cast<unsigned short*>(dst)[i] = narrow1<WT>(static_cast<const float*>(src)[i]);
     else static_cast<float*>(dst)[i] = widen1<WT>(static_cast<const unsigned short*>(src)[i]);
   }
@@ -1715,13 +1741,33 @@ hipError_t launch_copy_segs_groups(const CopySeg* tiles, const CopySeg* segs, Pa
 }
 
 namespace {
+// dynamic LDS per cast workgroup (an occupancy cap: 160 KiB / bytes workgroups per CU), per
+// direction; TIPS_CAST_LDS_PACK / TIPS_CAST_LDS_UNPACK (bytes) for sweeps
+int cast_lds_bytes(int dir) {
+  static const int v[2] = {(int)std::min<long>(65536, std::max<long>(0, getenv("TIPS_CAST_LDS_PACK") ? atol(getenv("TIPS_CAST_LDS_PACK")) : 0)),
+                           (int)std::min<long>(65536, std::max<long>(0, getenv("TIPS_CAST_LDS_UNPACK") ? atol(getenv("TIPS_CAST_LDS_UNPACK")) : 0))};
+  return v[dir];
+}
+
 template <int U, int DIR>
 hipError_t run_cast_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int wire, hipStream_t s) {
   const unsigned grid = (unsigned)std::max<int64_t>(8, ((int64_t)ntiles + 7) / 8 * 8);
+  const int lds = cast_lds_bytes(DIR);
+  static const int var = getenv("TIPS_CAST_VARIANT") ? atoi(getenv("TIPS_CAST_VARIANT")) : 0;
+  if (U == 2 && wire == kF16 && var > 0) {  // (the load / store policy sweep, f16 wire, 8 KiB tiles)
+    switch (var) {
+      case 1: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 1>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
+      case 2: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 2>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
+      case 3: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 3>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
+      case 4: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 4>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
+      default: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 5>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
+    }
+    return hipGetLastError();
+  }
   if (wire == kF16)
-    hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles);
+    hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles);
   else if (wire == kBF16)
-    hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kBF16>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles);
+    hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kBF16>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
