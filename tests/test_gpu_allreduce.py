@@ -594,6 +594,25 @@ def test_allreduce_grads_identity_single_rank(gpu):
 
 # ------------------------------------------------------------------ the rest of the op surface (one rank)
 
+@pytest.mark.parametrize("wire", ["float16", "bfloat16"])
+def test_fused_cast_range_many_tiles(gpu, monkeypatch, wire):
+    """A tensor above the threshold goes through the range cast (cast_range_kernel): 20,971,523
+    elements = 5,120 whole 8 KiB wire tiles (more than the launch's 4,096 workgroups, so workgroups
+    loop over tiles and reuse their LDS) plus 3 elements one at a time; a second, 1-element-offset
+    view takes the misaligned path. Bit-exact against torch's RNE casts (as the oracle's)."""
+    import torch
+    monkeypatch.setenv("TIPS_FUSION_THRESHOLD", "4096")
+    n = 4096 * 5120 + 3
+    g = torch.Generator(device="cuda").manual_seed(11)
+    base = torch.randn(n + 1, device="cuda", generator=g) * 3
+    tdt = torch.float16 if wire == "float16" else torch.bfloat16
+    for view in (base[:n], base[1:]):
+        want = view.to(tdt).float()
+        (out,) = gpu.fused_allreduce_cast([view], wire)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), want.view(torch.int32))
+
+
 def test_broadcast_allgather_checked_single_rank(gpu, monkeypatch):
     import torch
     from tips_amd import _lib, ops

@@ -953,9 +953,42 @@ __device__ __forceinline__ float widen1(unsigned short h) {
 typedef __attribute__((address_space(1))) f32x4 g_f32x4;
 typedef __attribute__((address_space(1))) float g_f32;
 
+// One whole tile of kBlock * 16 * U wire bytes, both sides 16-B aligned, moved 16 B per lane on
+// both sides: the quads (16 B of f32 = 8 B of wire) are reordered through LDS, so the wire side is
+// read or written as 16-B vectors too (8-B-per-lane wire accesses ran the round trip 10 % slower:
+// profiles/r06/cast/). Called by whole workgroups; W holds 2 U quads per lane.
+template <int U, int DIR, int WT>
+__device__ __forceinline__ void cast_tile_staged(int64_t f32_base, int64_t wire_base, u32x2* W) {
+  const int tid = threadIdx.x;
+  if constexpr (DIR == 0) {
+    f32x4 x[2 * U];
+#pragma unroll
+    for (int u = 0; u < 2 * U; u++)
+      x[u] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(f32_base + 16 * (int64_t)(u * kBlock + tid)));
+#pragma unroll
+    for (int u = 0; u < 2 * U; u++) W[u * kBlock + tid] = narrow4<WT>(x[u]);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      store16_pol<2>(wire_base + 16 * (int64_t)(u * kBlock + tid), reinterpret_cast<const u32x4*>(W)[u * kBlock + tid]);
+  } else {
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      x[u] = __builtin_nontemporal_load(reinterpret_cast<const g_u32x4*>(wire_base + 16 * (int64_t)(u * kBlock + tid)));
+#pragma unroll
+    for (int u = 0; u < U; u++) reinterpret_cast<u32x4*>(W)[u * kBlock + tid] = x[u];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2 * U; u++)
+      store16_pol<2>(f32_base + 16 * (int64_t)(u * kBlock + tid), __builtin_bit_cast(u32x4, widen4<WT>(W[u * kBlock + tid])));
+  }
+}
+
 // VAR (sweeps, TIPS_CAST_VARIANT): bit 0 plain loads instead of nt; bits 1-2 the store policy
-// (0 = sc1, the default; 1 = plain; 2 = nt)
-template <int U, int DIR, int WT, int VAR = 0>
+// (0 = sc1, the default; 1 = plain; 2 = nt); bit 3 (the default) one-segment tiles staged in LDS
+// (cast_tile_staged); the other tiles move quads
+template <int U, int DIR, int WT, int VAR = 8>
 __global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __restrict__ tiles,
                                                           const CopySeg* __restrict__ segs, int tile0, int ntiles) {
   constexpr int64_t kTileBytes = (int64_t)kBlock * 16 * U;  // wire bytes
@@ -970,6 +1003,15 @@ __global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __rest
   const int tid = threadIdx.x;
   const bool multi = a_end < 0, two = b_end > 0;
   const int64_t tb = two ? (b_beg & ~(kTileBytes - 1)) : b_beg;
+  if constexpr ((VAR & 8) != 0) {
+    // (bit 3, the default) a tile inside one segment with both sides 16-B aligned (workgroup-uniform)
+    __shared__ u32x2 W[kBlock * Q];
+    if (!multi && !two && a_beg <= tb && a_end >= tb + kTileBytes && ((a_src | a_dst) & 15) == 0) {
+      if constexpr (DIR == 0) cast_tile_staged<U, 0, WT>(a_src + 2 * tb, a_dst + tb, W);
+      else cast_tile_staged<U, 1, WT>(a_dst + 2 * tb, a_src + tb, W);
+      return;
+    }
+  }
   int cnt = 1;
   if (multi) {  // workgroup-uniform branch
     cnt = min((int)a_dst, kMaxSeg);
@@ -1040,20 +1082,31 @@ __global__ __launch_bounds__(kBlock) void cast_segs_kernel(const CopySeg* __rest
   }
 }
 
-// Elementwise cast of one contiguous range (a fused list's tensors of at least the threshold, which
-// travel through a scratch buffer of the wire type): DIR 0 f32 -> wire, 1 wire -> f32. Quads as in
-// cast_segs_kernel (16 B of f32, 8 B of wire per lane per access) when both sides allow it (the
-// caller's f32 pointer 16-B aligned, the wire side 8-B aligned); the last n % 4 elements, or every
-// element of a misaligned range, one at a time.
+// Cast of one contiguous range (a fused list's tensors of at least the threshold, which travel
+// through a scratch buffer of the wire type): DIR 0 f32 -> wire, 1 wire -> f32. With both sides
+// 16-B aligned, whole 8 KiB wire tiles go through cast_tile_staged (grid-stride over tiles), the
+// rest in quads (16 B of f32, 8 B of wire per lane) and the last n % 4 elements one at a time; a
+// misaligned range element by element.
 template <int DIR, int WT>
 __global__ __launch_bounds__(kBlock) void cast_range_kernel(void* __restrict__ dst, const void* __restrict__ src,
                                                            int64_t n) {
+  constexpr int U = 2;
+  constexpr int64_t kTileElems = (int64_t)kBlock * 8 * U;
+  __shared__ u32x2 W[kBlock * 2 * U];
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   const int64_t f32_side = (int64_t)(DIR == 0 ? src : dst), wire_side = (int64_t)(DIR == 0 ? dst : src);
   int64_t head = 0;
+  if (((f32_side | wire_side) & 15) == 0) {
+    const int64_t nt = n / kTileElems;
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {  // (workgroup-uniform trip count)
+      cast_tile_staged<U, DIR, WT>(f32_side + 4 * t * kTileElems, wire_side + 2 * t * kTileElems, W);
+      __syncthreads();  // (every lane's LDS reads before the next tile's writes)
+    }
+    head = nt * kTileElems;
+  }
   if ((f32_side & 15) == 0 && (wire_side & 7) == 0) {
     const int64_t nq = n / 4;
-    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += stride) {
+    for (int64_t q = head / 4 + (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += stride) {
       if constexpr (DIR == 0)
         store8_sc1(wire_side + 8 * q, narrow4<WT>(__builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(f32_side + 16 * q))));
       else
@@ -1753,9 +1806,10 @@ template <int U, int DIR>
 hipError_t run_cast_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int wire, hipStream_t s) {
   const unsigned grid = (unsigned)std::max<int64_t>(8, ((int64_t)ntiles + 7) / 8 * 8);
   const int lds = cast_lds_bytes(DIR);
-  static const int var = getenv("TIPS_CAST_VARIANT") ? atoi(getenv("TIPS_CAST_VARIANT")) : 0;
-  if (U == 2 && wire == kF16 && var > 0) {  // (the load / store policy sweep, f16 wire, 8 KiB tiles)
+  static const int var = getenv("TIPS_CAST_VARIANT") ? atoi(getenv("TIPS_CAST_VARIANT")) : 8;
+  if (U == 2 && wire == kF16 && var != 8) {  // (the load / store policy sweep, f16 wire, 8 KiB tiles)
     switch (var) {
+      case 0: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 0>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
       case 1: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 1>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
       case 2: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 2>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;
       case 3: hipLaunchKernelGGL((cast_segs_kernel<U, DIR, kF16, 3>), dim3(grid), dim3(kBlock), lds, s, tiles, segs, tile0, ntiles); break;

@@ -19,7 +19,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CAPS = {"none": 0, "7/CU": 22272, "6/CU": 26112, "5/CU": 31488, "4/CU": 39680, "3/CU": 53504}
 TILES = {"4KiB": 4096, "8KiB": 8192, "16KiB": 16384}  # the cast layout's tile (wire bytes)
 # TIPS_CAST_VARIANT: bit 0 plain loads (else nt), bits 1-2 the store (0 sc1, 1 plain, 2 nt)
-VARIANTS = {"nt/sc1": 0, "plain/sc1": 1, "nt/plain": 2, "plain/plain": 3, "nt/nt": 4, "plain/nt": 5}
+VARIANTS = {"nt/sc1": 0, "plain/sc1": 1, "nt/plain": 2, "plain/plain": 3, "nt/nt": 4, "plain/nt": 5,
+            "nt/sc1+lds16": 8}
+if os.environ.get("CAST_SWEEP_VARIANTS"):  # e.g. "0,8": a subset
+    VARIANTS = {k: v for k, v in VARIANTS.items() if str(v) in os.environ["CAST_SWEEP_VARIANTS"].split(",")}
 
 
 def main():
