@@ -10,7 +10,8 @@ one flat output). This probe times the same call three ways, one JSON line each:
             waiting for the host: the device-side cost alone
 Run it under `rocprofv3 --kernel-trace --stats` to split the device span per kernel.
 
-usage: python3 tools/cast_probe.py [steps]
+usage: python3 tools/cast_probe.py [steps] [--config4]   (--config4: config 4's 1000 gradients instead;
+       the host lines then also give tips_fusion_stats' deltas and the fp32 allreduce_grads body's time)
 """
 import json
 import os
@@ -21,14 +22,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    steps = int(args[0]) if args else 40
+    config4 = "--config4" in sys.argv
     import torch
 
     import bench
     import tips_amd
     torch.cuda.set_device(0)
     tips_amd.init()
-    sizes = bench.resnet50_grad_sizes()
+    sizes = bench.fused1000_sizes() if config4 else bench.resnet50_grad_sizes()
     rot = 4
     gens = [torch.Generator(device="cuda").manual_seed(5000 + k) for k in range(rot)]
     grads = [[torch.rand(n, device="cuda", generator=gens[k]) + 0.5 for n in sizes] for k in range(rot)]
@@ -46,11 +49,35 @@ def main():
         print(json.dumps({"mode": mode, "us_per_call": round(us, 2), "algorithmic_bytes": moved,
                           "GBps": round(moved / us / 1e3, 1), "frac": round(moved / us / 1e3 / 8000.0, 4)}), flush=True)
 
+    st0 = tips_amd.fusion_stats()
     t0 = time.perf_counter()
     for i in range(steps):
         call(i)
     torch.cuda.synchronize()
     line("host", (time.perf_counter() - t0) * 1e6 / steps)
+    if config4:
+        print(json.dumps({"fusion_stats_before": st0, "after": tips_amd.fusion_stats()}), flush=True)
+        for name, fn in (("fp32_reduce_grads", lambda i: tips_amd._reduce_grads(grads[i % rot])),):
+            try:
+                for i in range(rot):
+                    fn(i)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(steps):
+                    fn(i)
+                torch.cuda.synchronize()
+                print(json.dumps({"mode": "host", "call": name, "us_per_call": round((time.perf_counter() - t0) * 1e6 / steps, 2)}), flush=True)
+            except Exception as e:  # noqa: BLE001
+                print(json.dumps({"call": name, "error": str(e)}), flush=True)
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for i in range(steps):
+            call(i)
+        pr.disable()
+        torch.cuda.synchronize()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(12)
 
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
