@@ -37,7 +37,8 @@ def main():
         order = names[r % len(names):] + names[:r % len(names)]
         for n in order:
             env = dict(os.environ, **{var: str(CAPS[n])})
-            p = subprocess.run([sys.executable, os.path.join(HERE, "cast_probe.py"), "40"], env=env,
+            p = subprocess.run([sys.executable, os.path.join(HERE, "cast_probe.py"), "40"]
+                               + os.environ.get("CAST_PROBE_ARGS", "").split(), env=env,
                                capture_output=True, text=True, timeout=180)
             if p.returncode != 0:
                 print(json.dumps({"cap": n, "error": p.stderr[-400:]}), flush=True)
@@ -51,7 +52,7 @@ def main():
     for n in names:
         m = statistics.median(res[n])
         print(json.dumps({"summary": which, "cap": n, "lds": CAPS[n], "us_median": m, "runs": res[n],
-                          "frac": round(307003104 / m / 1e3 / 8000.0, 4)}), flush=True)
+                          "probe_args": os.environ.get("CAST_PROBE_ARGS", "")}), flush=True)
 
 
 if __name__ == "__main__":
