@@ -642,10 +642,18 @@ def gradient_api_legs(torch, dist, tips_amd, world, sizes, offs, rot_sets, steps
                     torch.cuda.synchronize()
                     t_ = e0.elapsed_time(e1) * 1e3 / 20
                     dus = t_ if dus is None else min(dus, t_)
+                # PMC: the pack and unpack launches' HBM bytes (mean per launch, one of each per bucket)
+                tp, tu = pmc_traffic("cast_segs_kernel<2, 0", "*pmc_cast_pack*.json"), \
+                    pmc_traffic("cast_segs_kernel<2, 1", "*pmc_cast_unpack*.json")
+                traffic = None
+                if tp and tu and sizes == resnet50_grad_sizes():  # (measured on config 5's layout)
+                    traffic = round(2 * (tp["bytes"] + tu["bytes"]))
                 leg["roofline"] = {"bound": "hbm", "achieved": round(moved / dus / 1e3, 1), "peak": HBM_PEAK_GBPS,
-                                   "unit": "GB/s", "frac": round(moved / dus / 1e3 / HBM_PEAK_GBPS, 4),
+                                   "unit": "GB/s", "frac": round(moved / dus / 1e3 / HBM_PEAK_GBPS, 4), "traffic": traffic,
                                    "us_per_step": round(dus, 2), "kernel": "cast_segs_kernel (pack f32 -> f16, unpack "
                                    "f16 -> f32; one of each per bucket), HIP events around 20 back-to-back calls, best of 3"}
+                if traffic:
+                    leg["roofline"]["traffic_source"] = "%s + %s" % (tp["source"], tu["source"])
         out[name] = leg
     if "fp16_compressed" in out and "allreduce_grads" in out:
         out["fp16_compressed"]["vs_fp32_allreduce_grads"] = round(
