@@ -52,6 +52,15 @@ int64_t copy_tile_bytes() {
   return t <= 4096 ? 4096 : t <= 8192 ? 8192 : 16384;
 }
 
+// the fused cast's tile (wire bytes; TIPS_CAST_TILE_BYTES): 4 KiB, against the copy's 8 KiB. A
+// cast launch moves 3 wire bytes per wire byte of tile, so at the copy's tile config 4's 20 MB
+// buckets were 2,500 workgroups (1.2 x what the chip holds at once) and the round trip took
+// 49.7 us; at 4 KiB, 46.1 us (profiles/r06/cast/sweep_cast_tile_*.jsonl)
+int64_t cast_tile_bytes() {
+  const int64_t t = env_i64("TIPS_CAST_TILE_BYTES", 4096);
+  return t <= 4096 ? 4096 : t <= 8192 ? 8192 : 16384;
+}
+
 // store cache policy of the segment copy: 2 = sc1 (default: the line leaves the XCD's L2, as the
 // sum kernels' stores), 1 = nt, 0 = plain (TIPS_COPY_STORE_POLICY, the tuning sweep's knob)
 int copy_store_policy() { return (int)std::min<int64_t>(2, std::max<int64_t>(0, env_i64("TIPS_COPY_STORE_POLICY", 2))); }
@@ -841,7 +850,7 @@ int fused_allreduce_cast(State& st, const BatchItem* items, int n, int wire, hip
       HIP_TRY(hipStreamWaitEvent(st.bucket_stream, st.ev_start, 0));
     }
     // the layout of the WIRE type's bytes: buckets of at most the threshold in wire bytes
-    Layout* L = find_layout(st, fc, counts.data(), n, wire, threshold, copy_tile_bytes(),
+    Layout* L = find_layout(st, fc, counts.data(), n, wire, threshold, cast_tile_bytes(),
                             env_i64("TIPS_FUSION_BALANCE", 1) != 0);
     if (!L) return TIPS_ERR_HIP;
     if (L->seg_tensor.empty()) return 0;

@@ -6,8 +6,8 @@ so at most 160 KiB / (bytes + the kernel's own ~1 KiB) workgroups share a CU. Ea
 every setting once, in a rotated order; one JSON line per run (the probe's gated device time per
 config-5 round trip), then one summary line per setting (median over rounds).
 
-usage: python3 tools/cast_sweep.py [rounds] [pack|unpack|tile|variant]
-  (tile: TIPS_COPY_TILE_BYTES 4/8/16 KiB; variant: TIPS_CAST_VARIANT, load / store policies)
+usage: python3 tools/cast_sweep.py [rounds] [pack|unpack|tile|cast_tile|variant]
+  (tile: TIPS_COPY_TILE_BYTES 4/8/16 KiB, before the cast had its own; cast_tile: TIPS_CAST_TILE_BYTES; variant: TIPS_CAST_VARIANT, load / store policies)
 """
 import json
 import os
@@ -29,8 +29,9 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     which = sys.argv[2] if len(sys.argv) > 2 else "pack"
     var = {"pack": "TIPS_CAST_LDS_PACK", "unpack": "TIPS_CAST_LDS_UNPACK", "tile": "TIPS_COPY_TILE_BYTES",
+           "cast_tile": "TIPS_CAST_TILE_BYTES",
            "variant": "TIPS_CAST_VARIANT"}[which]
-    CAPS = {"tile": TILES, "variant": VARIANTS}.get(which, globals()["CAPS"])
+    CAPS = {"tile": TILES, "cast_tile": TILES, "variant": VARIANTS}.get(which, globals()["CAPS"])
     names = list(CAPS)
     res = {n: [] for n in names}
     for r in range(rounds):
