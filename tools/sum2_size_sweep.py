@@ -4,7 +4,8 @@ fold of 2 x 128 MiB ran at 0.75 of HBM against 0.82 for config 2's 2 x 256 MiB).
 For each operand size, every variant (tips_sum_variant, the development library) runs over 4
 rotating buffer sets (so no launch finds its operands in the Infinity Cache), interleaved over
 ROUNDS rounds; one JSON line per (size, variant) with the best round's us per launch and its
-fraction of 8 TB/s (3 x size bytes per launch)."""
+fraction of 8 TB/s (3 x size bytes per launch). VARIANT_SET=policy sweeps cache policies instead of
+launch shapes."""
 import json
 import os
 import sys
@@ -24,6 +25,13 @@ ROUNDS = int(os.environ.get("ROUNDS", "3"))
 VARIANTS = [("shipped", 3, 1, 1, 0, 256), ("u2", 3, 2, 1, 0, 256), ("u4", 3, 4, 1, 0, 256),
             ("t512", 3, 1, 1, 0, 512), ("t128", 3, 1, 1, 0, 128), ("u2t512", 3, 2, 1, 0, 512),
             ("cap8", 3, 1, 1, 20480, 256), ("cap4", 3, 1, 1, 40960, 256), ("cap3", 3, 1, 1, 53248, 256)]
+if os.environ.get("VARIANT_SET") == "policy":
+    # cache policies (nt index into the (load aux, store aux) pairs of sum2_dispatch's mode 3):
+    # does the best store / load policy depend on the operand size?
+    VARIANTS = [("shipped", 3, 1, 1, 0, 256), ("st_plain", 3, 1, 0, 0, 256), ("st_nt", 3, 1, 7, 0, 256),
+                ("st_sc1glc", 3, 1, 2, 0, 256), ("st_ntsc1", 3, 1, 10, 0, 256), ("st_sc0ntsc1", 3, 1, 11, 0, 256),
+                ("st_sc0", 3, 1, 12, 0, 256), ("st_sc0nt", 3, 1, 13, 0, 256), ("ld_plain", 3, 1, 8, 0, 256),
+                ("ld_nt2_st_sc1", 3, 1, 6, 0, 256)]
 for mib in SIZES:
     n = mib << 18
     sets = [(torch.randn(n, device="cuda"), torch.randn(n, device="cuda"), torch.empty(n, device="cuda"))
