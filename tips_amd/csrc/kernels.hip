@@ -156,6 +156,20 @@ __device__ __forceinline__ int64_t xcd_tile(unsigned b, unsigned grid) {
   return (int64_t)(b & 7u) * (grid >> 3) + (b >> 3);
 }
 
+// XCD stripes (round 6): the tiles cut into stripes of C tiles (1 MiB of each operand), stripe s
+// on XCD s % 8, and workgroup j of an XCD takes the j-th tile of that XCD's stripes. With one
+// contiguous eighth per XCD (xcd_tile) the 8 XCDs' streams sit at the same offset of their
+// eighths, all 3 operands' alike; at 128 MiB operands that cost the 2-input sum 6 % (0.774 against
+// 0.820 in 1 MiB stripes, profiles/r06/stripes/sum2_map_sweep.jsonl), at 256 MiB it ties. C <= 0, or one
+// stripe per XCD or fewer (the grid's eighth R <= C), is xcd_tile. The grid must then cover whole
+// rounds of 8 stripes (stripe_grid): R a multiple of C, so the map is a bijection onto [0, grid).
+__device__ __forceinline__ int64_t stripe_tile(unsigned b, unsigned grid, int64_t C) {
+  const int64_t R = grid >> 3;
+  if (C <= 0 || R <= C) return xcd_tile(b, grid);
+  const int64_t j = b >> 3;
+  return ((j / C) * 8 + (b & 7u)) * C + j % C;
+}
+
 // ---------------------------------------------------------------------------
 // 2-input sum: dst = a + b
 
@@ -202,9 +216,9 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
 template <int DT, int LAUX, int SAUX, int U = 1, int BLOCK = 256>
 __global__ __launch_bounds__(BLOCK) void sum2_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
                                                         const u32x4* __restrict__ b, int64_t nvec,
-                                                        int64_t tail_begin, int64_t n) {
+                                                        int64_t tail_begin, int64_t n, int64_t stripe) {
   constexpr int64_t kTile = (int64_t)BLOCK * U;
-  const int64_t t = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t t = stripe_tile(blockIdx.x, gridDim.x, stripe);
   const int64_t first = t * kTile;
   if (first < nvec) {
     const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
@@ -222,6 +236,32 @@ __global__ __launch_bounds__(BLOCK) void sum2_buf_kernel(u32x4* __restrict__ dst
   }
   if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<DT>(dst, a, b, tail_begin + threadIdx.x);
 }
+
+// The shipped sum with other workgroup -> tile maps (tuning sweep only, f32; the 128 MiB dip,
+// DESIGN.md §3): stripe = 0 address order; else the tiles cut into stripes of `stripe` tiles dealt
+// round-robin over the 8 XCDs (stripe s to XCD s % 8; the shipped map is one stripe per XCD), and
+// workgroup j of XCD x takes the j-th tile of that XCD's stripes. The grid covers whole rounds of
+// 8 stripes (the workgroups past the last tile exit at once).
+#ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
+__global__ __launch_bounds__(256) void sum2_map_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
+                                                       const u32x4* __restrict__ b, int64_t nvec, int64_t tail_begin,
+                                                       int64_t n, int64_t stripe) {
+  constexpr int64_t kTile = 256;
+  const int64_t bx = blockIdx.x, x = bx & 7, j = bx >> 3;
+  const int64_t t = stripe == 0 ? bx : (x + 8 * (j / stripe)) * stripe + j % stripe;
+  const int64_t first = t * kTile;
+  if (first < nvec) {
+    const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
+    __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)(a + first), (short)0, rec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(b + first), (short)0, rec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
+    const u32x4 xv = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)threadIdx.x * 16, 0, 2);
+    const u32x4 yv = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)threadIdx.x * 16, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(add16<kF32>(xv, yv), rd, (int)threadIdx.x * 16, 0, 16);
+  }
+  if (blockIdx.x == 0 && tail_begin + (int64_t)threadIdx.x < n) add_elem<kF32>(dst, a, b, tail_begin + threadIdx.x);
+}
+#endif  // TIPS_DEV
 
 // LDS-staged 2-input sum (tuning sweep only, f32): both operand tiles go global -> LDS with
 // gfx950's direct-to-LDS loads (global_load_lds_dwordx4 nt: no VGPR destination, each
@@ -451,11 +491,11 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
 // every source's vectors in flight before the fold (as sum2_buf_kernel).
 template <int DT, int NSRC, int U, int LAUX, int BLOCK = kBlock>
 __global__ __launch_bounds__(BLOCK) void multi_sum_buf_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
-                                                             int64_t tail_begin, int64_t n) {
+                                                             int64_t tail_begin, int64_t n, int64_t stripe) {
   using W = Wide<DT>;
   constexpr int64_t kTile = (int64_t)BLOCK * U;
   const int tid = threadIdx.x;
-  const int64_t first = xcd_tile(blockIdx.x, gridDim.x) * kTile;
+  const int64_t first = stripe_tile(blockIdx.x, gridDim.x, stripe) * kTile;
   if (first < nvec) {
     const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
     u32x4 v[U][NSRC];
@@ -687,9 +727,9 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __
 // moved config 3's 1 GiB at 0.62 of HBM, profiles/r04/n_bench_n1.jsonl.)
 template <int U, int SAUX = 16>
 __global__ __launch_bounds__(kBlock) void copy_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
-                                                         int64_t nvec, int64_t tail_begin, int64_t bytes) {
+                                                         int64_t nvec, int64_t tail_begin, int64_t bytes, int64_t stripe) {
   constexpr int64_t kTile = (int64_t)kBlock * U;
-  const int64_t first = xcd_tile(blockIdx.x, gridDim.x) * kTile;
+  const int64_t first = stripe_tile(blockIdx.x, gridDim.x, stripe) * kTile;
   const int tid = threadIdx.x;
   if (first < nvec) {
     const int rec = (int)(((nvec - first) < kTile ? (nvec - first) : kTile) * 16);
@@ -703,6 +743,25 @@ __global__ __launch_bounds__(kBlock) void copy_buf_kernel(u32x4* __restrict__ ds
   }
   if (blockIdx.x == 0 && tail_begin + tid < bytes)
     reinterpret_cast<char*>(dst)[tail_begin + tid] = reinterpret_cast<const char*>(src)[tail_begin + tid];
+}
+
+// Stripe size for stripe_tile, in 16-B vectors of one operand (TIPS_STRIPE_KIB, default 1 MiB;
+// 0: xcd_tile's contiguous eighths), and the grid that covers `tiles` tiles of `tile` vectors:
+// whole rounds of 8 stripes once there are more than 8 stripes' worth of tiles.
+int64_t stripe_vecs() {
+  static const int64_t v = [] {
+    const char* e = getenv("TIPS_STRIPE_KIB");
+    const long kib = e && *e ? atol(e) : 1024;
+    return (int64_t)std::max<long>(0, kib) * 1024 / 16;
+  }();
+  return v;
+}
+
+int64_t stripe_of(int64_t tile) { return stripe_vecs() / std::max<int64_t>(1, tile); }
+
+int64_t stripe_grid(int64_t tiles, int64_t C) {
+  if (C <= 0 || tiles <= 8 * C) return std::max<int64_t>(8, (tiles + 7) / 8 * 8);
+  return (tiles + 8 * C - 1) / (8 * C) * (8 * C);
 }
 
 hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_t s) {
@@ -720,18 +779,18 @@ hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_
   if (variant == 4) return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
   const int U = variant == 1 ? 2 : variant == 2 ? 4 : 1;
   const int64_t nvec = bytes / 16;
-  int64_t grid = (nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U);
-  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
+  const int64_t stripe = stripe_of((int64_t)kBlock * U);
+  const int64_t grid = stripe_grid((nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U), stripe);
   if (grid > 0x7fffffff) return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
   const dim3 g((unsigned)grid), b(kBlock);
   if (variant == 1)
-    hipLaunchKernelGGL((copy_buf_kernel<2>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
+    hipLaunchKernelGGL((copy_buf_kernel<2>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);
   else if (variant == 2)
-    hipLaunchKernelGGL((copy_buf_kernel<4>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
+    hipLaunchKernelGGL((copy_buf_kernel<4>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);
   else if (variant == 3)
-    hipLaunchKernelGGL((copy_buf_kernel<1, 2>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
+    hipLaunchKernelGGL((copy_buf_kernel<1, 2>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);
   else
-    hipLaunchKernelGGL((copy_buf_kernel<1>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes);
+    hipLaunchKernelGGL((copy_buf_kernel<1>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);
   return hipGetLastError();
 }
 
@@ -1233,6 +1292,18 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     }
     return hipErrorInvalidValue;
   }
+  if (mode == 6) {  // other tile maps, f32, 256 threads; unroll = stripe in KiB of one operand (0: address order)
+    if constexpr (DT == kF32) {
+      const int64_t nvec = n / 4, T = (nvec + 255) / 256;
+      const int64_t stripe = (int64_t)unroll * 1024 / 4096;  // tiles of 4 KiB
+      if (unroll < 0 || (unroll > 0 && stripe < 1)) return hipErrorInvalidValue;
+      const int64_t grid = stripe == 0 ? std::max<int64_t>(1, T) : ((T + stripe - 1) / stripe + 7) / 8 * 8 * stripe;
+      hipLaunchKernelGGL(sum2_map_kernel, dim3((unsigned)grid), dim3(256), 0, s, (u32x4*)dst, (const u32x4*)a,
+                         (const u32x4*)b, nvec, nvec * 4, n, stripe);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (mode == 4) {  // LDS-staged (direct-to-LDS loads), f32, 256 threads; unroll = 16-B vectors per lane
     if constexpr (DT == kF32) {
       const int64_t nvec = n / 4;
@@ -1269,8 +1340,9 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
     const unsigned shmem = (unsigned)blocks;
 #define TIPS_BUF_CASE(I, L, S_, U, B)                                                                          \
   if (nt == I && unroll == U && threads == B) {                                                            \
-    hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_, U, B>), dim3(grid_for((int64_t)U * B)), dim3(B), shmem, s, \
-                       (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n);                 \
+    hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_, U, B>),                                                    \
+                       dim3((unsigned)stripe_grid((nvec + U * B - 1) / (U * B), stripe_of(U * B))), dim3(B), shmem, s, \
+                       (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n, stripe_of(U * B));          \
     return hipGetLastError();                                                                              \
   }
     TIPS_BUF_CASE(1, 2, 16, 1, 256)  // the product default: nt loads, sc1 stores, 1 x 16 B per lane, 256 lanes
@@ -1391,18 +1463,18 @@ hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
   constexpr int kCapBlock = 128;
   const int block = capped ? kCapBlock : kBlock;
   const int64_t per = (int64_t)block * (u4 ? 4 : 1);
-  int64_t grid = (nvec + per - 1) / per;
-  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // xcd_tile order; surplus workgroups fall off the bounds check
+  const int64_t stripe = stripe_of(per);
+  const int64_t grid = stripe_grid((nvec + per - 1) / per, stripe);  // surplus workgroups fall off the bounds check
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   if (capped)
     hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX, kCapBlock>), dim3((unsigned)grid), dim3(kCapBlock),
-                       NSRC >= 6 ? kFoldLdsCap5 : kFoldLdsCap8, s, (u32x4*)dst, sl, nvec, nvec * ve, n);
+                       NSRC >= 6 ? kFoldLdsCap5 : kFoldLdsCap8, s, (u32x4*)dst, sl, nvec, nvec * ve, n, stripe);
   else if (u4)
     hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 4, LAUX>), dim3((unsigned)grid), dim3(kBlock), 0, s,
-                       (u32x4*)dst, sl, nvec, nvec * ve, n);
+                       (u32x4*)dst, sl, nvec, nvec * ve, n, stripe);
   else
     hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX>), dim3((unsigned)grid), dim3(kBlock), 0, s,
-                       (u32x4*)dst, sl, nvec, nvec * ve, n);
+                       (u32x4*)dst, sl, nvec, nvec * ve, n, stripe);
   return hipGetLastError();
 }
 
@@ -1513,31 +1585,31 @@ hipError_t run_multi_variant(void* dst, const SrcList& sl, int64_t n, int varian
     }
     case 1:
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 2>), dim3(grid_for(1)), dim3(kBlock), 0, s,
-                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+                         (u32x4*)dst, sl, nvec, nvec * 4, n, (int64_t)0);
       break;
     case 2:
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 2, 2>), dim3(grid_for(2)), dim3(kBlock), 0, s,
-                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+                         (u32x4*)dst, sl, nvec, nvec * 4, n, (int64_t)0);
       break;
     case 3:
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 0>), dim3(grid_for(1)), dim3(kBlock), 0, s,
-                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+                         (u32x4*)dst, sl, nvec, nvec * 4, n, (int64_t)0);
       break;
     case 4:
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 4, 2>), dim3(grid_for(4)), dim3(kBlock), 0, s,
-                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+                         (u32x4*)dst, sl, nvec, nvec * 4, n, (int64_t)0);
       break;
     case 5:  // sc0 loads
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 1>), dim3(grid_for(1)), dim3(kBlock), 0, s,
-                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+                         (u32x4*)dst, sl, nvec, nvec * 4, n, (int64_t)0);
       break;
     case 6:  // sc1 loads
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 1, 16>), dim3(grid_for(1)), dim3(kBlock), 0, s,
-                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+                         (u32x4*)dst, sl, nvec, nvec * 4, n, (int64_t)0);
       break;
     case 7:  // plain loads, 2 vectors per lane
       hipLaunchKernelGGL((multi_sum_buf_kernel<kF32, NSRC, 2, 0>), dim3(grid_for(2)), dim3(kBlock), 0, s,
-                         (u32x4*)dst, sl, nvec, nvec * 4, n);
+                         (u32x4*)dst, sl, nvec, nvec * 4, n, (int64_t)0);
       break;
     default:
       return run_multi_x<NSRC>(dst, sl, n, variant, s);
@@ -1552,10 +1624,10 @@ hipError_t run_multi_remote(void* dst, const SrcList& sl, int64_t n, hipStream_t
   const int64_t ve = 16 / (int64_t)dtype_size(DT);
   const int64_t nvec = n / ve;
   int64_t grid = (nvec + 4 * kBlock - 1) / (4 * kBlock);
-  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);
+  grid = std::max<int64_t>(8, (grid + 7) / 8 * 8);  // (xcd_tile: remote sources, not measured with stripes)
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 4, 2>), dim3((unsigned)grid), dim3(kBlock), 0, s, (u32x4*)dst, sl,
-                     nvec, nvec * ve, n);
+                     nvec, nvec * ve, n, (int64_t)0);
   return hipGetLastError();
 }
 

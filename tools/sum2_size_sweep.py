@@ -5,7 +5,7 @@ For each operand size, every variant (tips_sum_variant, the development library)
 rotating buffer sets (so no launch finds its operands in the Infinity Cache), interleaved over
 ROUNDS rounds; one JSON line per (size, variant) with the best round's us per launch and its
 fraction of 8 TB/s (3 x size bytes per launch). VARIANT_SET=policy sweeps cache policies instead of
-launch shapes."""
+launch shapes, VARIANT_SET=map workgroup -> tile maps."""
 import json
 import os
 import sys
@@ -32,6 +32,12 @@ if os.environ.get("VARIANT_SET") == "policy":
                 ("st_sc1glc", 3, 1, 2, 0, 256), ("st_ntsc1", 3, 1, 10, 0, 256), ("st_sc0ntsc1", 3, 1, 11, 0, 256),
                 ("st_sc0", 3, 1, 12, 0, 256), ("st_sc0nt", 3, 1, 13, 0, 256), ("ld_plain", 3, 1, 8, 0, 256),
                 ("ld_nt2_st_sc1", 3, 1, 6, 0, 256)]
+if os.environ.get("VARIANT_SET") == "map":
+    # workgroup -> tile maps (sum2_map_kernel, mode 6; unroll = stripe KiB per operand, 0 = address
+    # order): stripes dealt round-robin over the XCDs, against the shipped XCD-contiguous eighths
+    VARIANTS = [("shipped", 3, 1, 1, 0, 256), ("map_address", 6, 0, 0, 0, 256)] + [
+        ("stripe%dK" % kib, 6, kib, 0, 0, 256) for kib in
+        [int(x) for x in os.environ.get("STRIPES_KIB", "256,1024,2048,4096,8192").split(",")]]
 for mib in SIZES:
     n = mib << 18
     sets = [(torch.randn(n, device="cuda"), torch.randn(n, device="cuda"), torch.empty(n, device="cuda"))
