@@ -1120,7 +1120,7 @@ def sum_record(args, cpu):
         "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
                    "bucket_bytes": n * 4, "elements": n, "rotating_sets": ROTATING_SETS,
                    "timing": "HIP events over the timed launches; launch i sums triple i %% %d (HBM-only: no launch "
-                             "finds its operands in the 256 MiB Infinity Cache)" % ROTATING_SETS, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, XCD-contiguous order, buffer_load/store_dwordx4)",
+                             "finds its operands in the 256 MiB Infinity Cache)" % ROTATING_SETS, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, 1 MiB stripes dealt round-robin over the 8 XCDs, buffer_load/store_dwordx4)",
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),

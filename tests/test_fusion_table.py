@@ -162,3 +162,32 @@ def test_boundary_tiles_come_first_in_each_group(monkeypatch):
     # no slow tile of the same bucket follows (buckets are the contiguous tile ranges of tips_fused_layout)
     assert any(slow) and not all(slow)
     assert slow[0]
+
+
+def _striped_tables_child():
+    """(run in a child process: TIPS_PACK_STRIPE_KIB is read once per process)"""
+    from tips_amd import _lib
+    threshold = 1 << 20
+    os.environ["TIPS_FUSION_THRESHOLD"] = str(threshold)
+    rng = random.Random(11)
+    for dtype, es in ((_lib.FLOAT32, 4), (_lib.FLOAT16, 2)):
+        counts, ins, outs = random_list(rng, 160, es, threshold)
+        rec, ntiles, T = table(counts, ins, outs, dtype)
+        check(counts, ins, outs, es, run_table(rec, ntiles, T))
+    print("striped tables ok")
+
+
+@pytest.mark.parametrize("stripe_kib", ["16", "64"])
+def test_striped_pack_tables_copy_every_byte_once(stripe_kib):
+    """TIPS_PACK_STRIPE_KIB (opt-in): the pack launch deals stripes of slots round-robin over the
+    XCDs and fusion.cc's tile_order places each XCD's boundary tiles by that map. The records stay
+    a permutation of the layout's tiles: every byte copied exactly once (stripes small enough that
+    1 MiB buckets hold several rounds of 8)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, TIPS_PACK_STRIPE_KIB=stripe_kib)
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = "import sys; sys.path[:0] = [%r, %r]; import test_fusion_table as t; t._striped_tables_child()" % (
+        os.path.dirname(here), here)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "striped tables ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

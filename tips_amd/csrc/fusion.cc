@@ -324,6 +324,30 @@ std::vector<int> tile_order(const Layout& L) {
     // range gets an equal share of them, first in the range, then interior tiles.
     const int n = g1 - g0, R = (int)(std::max<int64_t>(8, ((int64_t)n + 7) / 8 * 8) / 8);
     std::vector<int> slow(order.begin() + g0, mid), fast(mid, order.begin() + g1);
+    const int64_t C = tips::pack_stripe_vecs() * 16 / std::max<int64_t>(1, L.tile);
+    if (C > 0 && (int64_t)n > 8 * C) {
+      // Striped launch (TIPS_PACK_STRIPE_KIB): XCD x issues its slots in stripe order. Each XCD's
+      // first-issued slots get an equal share of the boundary tiles; the interior tiles keep
+      // address order over the slots left, so every stripe still streams one run of the bucket.
+      std::vector<int> sx;
+      std::vector<int64_t> sp;
+      tips::stripe_slots(n, C, &sx, &sp);
+      std::vector<std::vector<int>> by(8);
+      for (int t = 0; t < n; t++) by[sx[t]].push_back(t);
+      for (auto& v : by) std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return sp[a] < sp[b]; });
+      std::vector<char> taken(n, 0);
+      size_t si = 0;
+      for (int x = 0; x < 8 && si < slow.size(); x++) {
+        const size_t share = std::min(by[x].size(), (slow.size() - si + (7 - x)) / (8 - x));
+        for (size_t k = 0; k < share; k++) order[g0 + by[x][k]] = slow[si++], taken[by[x][k]] = 1;
+      }
+      size_t fi = 0;
+      for (int t = 0; t < n; t++) {
+        if (taken[t]) continue;
+        order[g0 + t] = si < slow.size() ? slow[si++] : fast[fi++];
+      }
+      continue;
+    }
     std::vector<std::vector<int>> xcd(8);
     size_t si = 0, fi = 0;
     for (int x = 0; x < 8; x++) {

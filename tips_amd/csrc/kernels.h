@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace tips {
 
 int dtype_size(int dtype);  // 0 for unknown dtypes
@@ -52,6 +54,11 @@ struct CopySeg {
 };
 hipError_t launch_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int64_t tile_bytes,
                             int pol, hipStream_t s);
+// The pack launch's workgroup -> slot map: 1 MiB-style XCD stripes of this many 16-B vectors
+// (TIPS_PACK_STRIPE_KIB; 0, the default, = one contiguous eighth of the slots per XCD), and the
+// XCD / issue position of every slot under it (fusion.cc's tile_order places boundary tiles by it).
+int64_t pack_stripe_vecs();
+void stripe_slots(int64_t nslots, int64_t C, std::vector<int>* xcd, std::vector<int64_t>* pos);
 
 // Several tile groups (a step's fusion buckets) in one launch: group k copies record slots
 // [tile0[k], tile0[k] + ntiles[k]) with workgroups [blk0[k], blk0[k + 1]) (the launcher fills blk0).

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
 }
 
 // The shipped 2-input sum (and, with other CPol bits, the cache-policy sweep
-// variants): one 4 KiB tile per operand per workgroup in XCD-contiguous order,
+// variants): one 4 KiB tile per operand per workgroup, placed by stripe_tile (1 MiB XCD stripes),
 // through buffer_load/store_dwordx4 with explicit CPol bits (aux: 1 = sc0,
 // 2 = nt, 16 = sc1). Default LAUX = 2 (nt loads), SAUX = 16 (sc1 stores: the
 // written line leaves the XCD's L2 instead of occupying it — 7.46 vs 7.10 TB/s
@@ -757,11 +757,33 @@ int64_t stripe_vecs() {
   return v;
 }
 
+// The fusion pack's stripe (TIPS_PACK_STRIPE_KIB, default 0 = xcd_tile), in 16-B vectors; the
+// layout's tile order (fusion.cc tile_order) places boundary tiles by the same map.
+int64_t pack_stripe_vecs() {
+  static const int64_t v = [] {
+    const char* e = getenv("TIPS_PACK_STRIPE_KIB");
+    const long kib = e && *e ? atol(e) : 0;
+    return (int64_t)std::max<long>(0, kib) * 1024 / 16;
+  }();
+  return v;
+}
+
 int64_t stripe_of(int64_t tile) { return stripe_vecs() / std::max<int64_t>(1, tile); }
 
 int64_t stripe_grid(int64_t tiles, int64_t C) {
   if (C <= 0 || tiles <= 8 * C) return std::max<int64_t>(8, (tiles + 7) / 8 * 8);
   return (tiles + 8 * C - 1) / (8 * C) * (8 * C);
+}
+
+void stripe_slots(int64_t nslots, int64_t C, std::vector<int>* xcd, std::vector<int64_t>* pos) {
+  xcd->assign((size_t)nslots, 0);
+  pos->assign((size_t)nslots, 0);
+  const int64_t grid = stripe_grid(nslots, C), R = grid >> 3;
+  for (int64_t b = 0; b < grid; b++) {  // (host restatement of stripe_tile)
+    const int64_t j = b >> 3;
+    const int64_t t = (C <= 0 || R <= C) ? (b & 7) * R + j : ((j / C) * 8 + (b & 7)) * C + j % C;
+    if (t < nslots) (*xcd)[t] = (int)(b & 7), (*pos)[t] = j;
+  }
 }
 
 hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_t s) {
@@ -962,9 +984,10 @@ __device__ __forceinline__ void copy_seg_tile(const CopySeg* __restrict__ tiles,
 
 template <int U, int POL>
 __global__ __launch_bounds__(kBlock) void copy_segs_kernel(const CopySeg* __restrict__ tiles,
-                                                          const CopySeg* __restrict__ segs, int tile0, int ntiles) {
+                                                          const CopySeg* __restrict__ segs, int tile0, int ntiles,
+                                                          int64_t stripe) {
   __shared__ SegStage<U> st;
-  const int64_t tt = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t tt = stripe_tile(blockIdx.x, gridDim.x, stripe);
   if (tt >= ntiles) return;  // (whole workgroup: before any barrier)
   copy_seg_tile<U, POL>(tiles, segs, tile0 + (int)tt, st.L);  // (fusion.cc may order a group's tiles: slow ones first)
 }
@@ -1333,7 +1356,6 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
   if (mode == 3) {  // buffer-op variants: nt = index into (load aux, store aux); unroll x threads = tile
     const int64_t ve = 16 / (int64_t)dtype_size(DT);
     const int64_t nvec = n / ve;
-    auto grid_for = [&](int64_t tile) { return (unsigned)std::max<int64_t>(8, ((nvec + tile - 1) / tile + 7) / 8 * 8); };
     // blocks > 0: that many bytes of (unused) LDS reserved per workgroup, capping workgroups per CU
     // at 160 KiB / blocks (the occupancy sweep); 0 = no cap
     if (blocks < 0 || blocks > 65536) return hipErrorInvalidValue;
@@ -1822,11 +1844,12 @@ hipError_t run_copy_segs_groups(const CopySeg* tiles, const CopySeg* segs, const
 
 template <int U>
 hipError_t run_copy_segs(const CopySeg* tiles, const CopySeg* segs, int tile0, int ntiles, int pol, hipStream_t s) {
-  const unsigned grid = (unsigned)std::max<int64_t>(8, ((int64_t)ntiles + 7) / 8 * 8);
+  const int64_t C = pack_stripe_vecs() / ((int64_t)kBlock * U);  // tiles per stripe (0: xcd_tile)
+  const unsigned grid = (unsigned)stripe_grid(ntiles, C);
   switch (pol) {
-    case 0: hipLaunchKernelGGL((copy_segs_kernel<U, 0>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles); break;
-    case 1: hipLaunchKernelGGL((copy_segs_kernel<U, 1>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles); break;
-    case 2: hipLaunchKernelGGL((copy_segs_kernel<U, 2>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles); break;
+    case 0: hipLaunchKernelGGL((copy_segs_kernel<U, 0>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles, C); break;
+    case 1: hipLaunchKernelGGL((copy_segs_kernel<U, 1>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles, C); break;
+    case 2: hipLaunchKernelGGL((copy_segs_kernel<U, 2>), dim3(grid), dim3(kBlock), 0, s, tiles, segs, tile0, ntiles, C); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
