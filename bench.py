@@ -50,7 +50,7 @@ XGMI_LINK_GBPS = 153.0   # per link per direction (task / SURVEY §8d)
 GIB = float(1 << 30)
 # the exact instantiation tips_bucket_sum launches for f32 (kernels.hip kDef*): PMC traffic is only
 # reported from a profile of this kernel
-DEFAULT_SUM_KERNEL = "sum2_buf_kernel<0, 2, 16, 1, 256>"
+DEFAULT_SUM_KERNEL = "sum2_buf_kernel<0, 2, 2, 1, 128>"
 # N == 1 cycles over this many (a, b, c) triples of config 2's size (3 GiB at 4): see sum_record
 ROTATING_SETS = 4
 SUB_WORKLOADS = ("fused1000", "resnet50")
@@ -1120,7 +1120,7 @@ def sum_record(args, cpu):
         "config": {"workload": "config 2: c = a + b, two 256 MiB fp32 gradient buffers on one MI355X",
                    "bucket_bytes": n * 4, "elements": n, "rotating_sets": ROTATING_SETS,
                    "timing": "HIP events over the timed launches; launch i sums triple i %% %d (HBM-only: no launch "
-                             "finds its operands in the 256 MiB Infinity Cache)" % ROTATING_SETS, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, sc1 stores>: one 4 KiB tile per operand per 256-lane workgroup, 1 MiB stripes dealt round-robin over the 8 XCDs, buffer_load/store_dwordx4)",
+                             "finds its operands in the 256 MiB Infinity Cache)" % ROTATING_SETS, "kernel": "tips_bucket_sum (sum2_buf_kernel<f32, nt loads, nt stores>: one 2 KiB tile per operand per 128-lane workgroup, tiles dealt to the 8 XCDs in stripes of TIPS_STRIPE_KIB, buffer_load/store_dwordx4)",
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),

@@ -770,6 +770,19 @@ int64_t pack_stripe_vecs() {
 
 int64_t stripe_of(int64_t tile) { return stripe_vecs() / std::max<int64_t>(1, tile); }
 
+// The 2-input sum's own stripe (TIPS_SUM_STRIPE_KIB, default 512 KiB; 0: eighths): with its
+// 128-lane launch, 512 KiB stripes ran config 2 0.6-0.8 % faster than 1 MiB, while the copy
+// kept 1 MiB (profiles/r06/sum2_focus/, stripe512/). Unset, TIPS_STRIPE_KIB=0 also turns it off.
+int64_t sum_stripe_of(int64_t tile) {
+  static const int64_t v = [] {
+    const char* e = getenv("TIPS_SUM_STRIPE_KIB");
+    const char* g = getenv("TIPS_STRIPE_KIB");
+    const long kib = e && *e ? atol(e) : (g && *g && atol(g) == 0 ? 0 : 512);
+    return (int64_t)std::max<long>(0, kib) * 1024 / 16;
+  }();
+  return v / std::max<int64_t>(1, tile);
+}
+
 int64_t stripe_grid(int64_t tiles, int64_t C) {
   if (C <= 0 || tiles <= 8 * C) return std::max<int64_t>(8, (tiles + 7) / 8 * 8);
   return (tiles + 8 * C - 1) / (8 * C) * (8 * C);
@@ -1363,11 +1376,12 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
 #define TIPS_BUF_CASE(I, L, S_, U, B)                                                                          \
   if (nt == I && unroll == U && threads == B) {                                                            \
     hipLaunchKernelGGL((sum2_buf_kernel<DT, L, S_, U, B>),                                                    \
-                       dim3((unsigned)stripe_grid((nvec + U * B - 1) / (U * B), stripe_of(U * B))), dim3(B), shmem, s, \
-                       (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n, stripe_of(U * B));          \
+                       dim3((unsigned)stripe_grid((nvec + U * B - 1) / (U * B), sum_stripe_of(U * B))), dim3(B), shmem, s, \
+                       (u32x4*)dst, (const u32x4*)a, (const u32x4*)b, nvec, nvec * ve, n, sum_stripe_of(U * B));      \
     return hipGetLastError();                                                                              \
   }
-    TIPS_BUF_CASE(1, 2, 16, 1, 256)  // the product default: nt loads, sc1 stores, 1 x 16 B per lane, 256 lanes
+    TIPS_BUF_CASE(7, 2, 2, 1, 128)   // the product default (round 6): nt loads, nt stores, 1 x 16 B per lane, 128 lanes
+    TIPS_BUF_CASE(1, 2, 16, 1, 256)  // rounds 2-5's default: nt loads, sc1 stores, 256 lanes
 #ifdef TIPS_DEV  // (tuning sweeps: libtips_hip_dev.so only)
     if constexpr (DT == kF32) {
       TIPS_BUF_CASE(0, 2, 0, 1, 256)
@@ -1453,9 +1467,11 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
   return hipErrorInvalidValue;
 }
 
-// Default variant for the product path (chosen from the gfx950 sweep,
-// profiles/ + DESIGN.md §Kernels).
-constexpr int kDefMode = 3, kDefUnroll = 1, kDefNT = 1, kDefThreads = 256;
+// Default variant for the product path (chosen from the gfx950 sweeps): buffer ops,
+// one 16-B vector per lane, 128-lane workgroups (a 2 KiB tile of each operand), nt loads and nt
+// stores. Rounds 2-5 shipped 256 lanes with sc1 stores (nt index 1); under XCD stripes the
+// 128-lane nt form is 1-3 % faster (profiles/r06/sum2_focus/).
+constexpr int kDefMode = 3, kDefUnroll = 1, kDefNT = 7, kDefThreads = 128;
 
 // Bytes the fold keeps in flight per CU (round 5, profiles/r05/): every wave-source pair has one
 // 1 KiB wave-load outstanding, and with 9 streams the DRAM efficiency falls once a CU holds much more
@@ -1668,8 +1684,8 @@ hipError_t multi_dispatch(void* dst, const void* const* srcs, int nsrc, int64_t 
     hipLaunchKernelGGL((multi_sum_scalar_kernel<DT>), dim3((unsigned)grid), dim3(kBlock), 0, s, dst, sl, nsrc, n);
     return hipGetLastError();
   }
-  // Two sources: the fold is one add, i.e. the 2-input sum, whose launch (one 4 KiB tile per operand
-  // per workgroup, 256 lanes) runs 2 x 128 MiB at the sum's rate instead of the fold's 0.75 of HBM
+  // Two sources: the fold is one add, i.e. the 2-input sum, whose launch (one 16-B vector per lane
+  // per operand, buffer ops) runs 2 x 128 MiB at the sum's rate instead of the fold's 0.75 of HBM
   // (VERDICT r05 item 6). Storage-type arithmetic for these four types: bit-identical to the fold.
   if (!remote && nsrc == 2 && (DT == kF32 || DT == kF64 || DT == kI32 || DT == kI64))
     return sum2_dispatch<DT>(dst, srcs[0], srcs[1], n, kDefMode, kDefUnroll, kDefNT, 0, kDefThreads, s);

@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT="$PWD/gpurun_out/${TAG:-stripe_ab}"
 mkdir -p "$OUT"
 for r in ${ROUNDS:-1 2}; do
-  for k in 0 1024; do
+  for k in ${STRIPES:-0 1024}; do
     echo "[$(date +%T)] round $r stripe $k" >> "$OUT/steps.txt"
     TIPS_STRIPE_KIB=$k timeout -k 10 120 python3 bench.py --no-sub --no-cpu-baseline --no-extras --steps 200 --warmup 20 \
       > "$OUT/config2_s${k}_r$r.jsonl" 2> "$OUT/config2_s${k}_r$r.err" || exit 1

@@ -38,6 +38,11 @@ if os.environ.get("VARIANT_SET") == "map":
     VARIANTS = [("shipped", 3, 1, 1, 0, 256), ("map_address", 6, 0, 0, 0, 256)] + [
         ("stripe%dK" % kib, 6, kib, 0, 0, 256) for kib in
         [int(x) for x in os.environ.get("STRIPES_KIB", "256,1024,2048,4096,8192").split(",")]]
+if os.environ.get("VARIANT_SET") == "focus":
+    # round 6, under XCD stripes: the shapes / policies that led the wider sweeps, side by side
+    # (the stripe size itself is TIPS_STRIPE_KIB, one value per process)
+    VARIANTS = [("shipped", 3, 1, 1, 0, 256), ("t128", 3, 1, 1, 0, 128), ("t128_nt", 3, 1, 7, 0, 128), ("st_nt", 3, 1, 7, 0, 256),
+                ("st_sc0nt", 3, 1, 13, 0, 256), ("cap8", 3, 1, 1, 20480, 256)]
 for mib in SIZES:
     n = mib << 18
     sets = [(torch.randn(n, device="cuda"), torch.randn(n, device="cuda"), torch.empty(n, device="cuda"))
