@@ -207,12 +207,12 @@ __global__ __launch_bounds__(BLOCK) void sum2_kernel(u32x4* __restrict__ dst, co
 }
 
 // The shipped 2-input sum (and, with other CPol bits, the cache-policy sweep
-// variants): one 4 KiB tile per operand per workgroup, placed by stripe_tile (1 MiB XCD stripes),
+// variants): one tile of U x BLOCK vectors per operand per workgroup, placed by stripe_tile,
 // through buffer_load/store_dwordx4 with explicit CPol bits (aux: 1 = sc0,
-// 2 = nt, 16 = sc1). Default LAUX = 2 (nt loads), SAUX = 16 (sc1 stores: the
-// written line leaves the XCD's L2 instead of occupying it — 7.46 vs 7.10 TB/s
-// on config 2, profiles/r01_sum_sweep_f.jsonl). Each workgroup's descriptors
-// cover exactly its tile, so the hardware range check drops lanes past the end.
+// 2 = nt, 16 = sc1). The product launch (kDef* below): BLOCK = 128, nt loads and nt stores,
+// 512 KiB stripes (round 6; rounds 2-5: 256 lanes with sc1 stores, which won when one buffer
+// triple was re-read, 7.46 vs 7.10 TB/s, profiles/r01_sum_sweep_f.jsonl). Each workgroup's
+// descriptors cover exactly its tile, so the hardware range check drops lanes past the end.
 template <int DT, int LAUX, int SAUX, int U = 1, int BLOCK = 256>
 __global__ __launch_bounds__(BLOCK) void sum2_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ a,
                                                         const u32x4* __restrict__ b, int64_t nvec,
