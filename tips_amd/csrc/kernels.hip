@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void multi_sum_kernel(u32x4* __restrict__ d
 // Buffer-op form of the multi-input sum: one descriptor per source covering
 // this workgroup's tile, cache-policy bits on the loads (LAUX) and sc1 stores,
 // every source's vectors in flight before the fold (as sum2_buf_kernel).
-template <int DT, int NSRC, int U, int LAUX, int BLOCK = kBlock>
+template <int DT, int NSRC, int U, int LAUX, int BLOCK = kBlock, int SAUX = 16>
 __global__ __launch_bounds__(BLOCK) void multi_sum_buf_kernel(u32x4* __restrict__ dst, SrcList srcs, int64_t nvec,
                                                              int64_t tail_begin, int64_t n, int64_t stripe) {
   using W = Wide<DT>;
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(BLOCK) void multi_sum_buf_kernel(u32x4* __restrict_
       typename W::A acc = W::load(v[u][0]);
 #pragma unroll
       for (int j = 1; j < NSRC; j++) acc = acc + W::load(v[u][j]);
-      __builtin_amdgcn_raw_buffer_store_b128(W::store(acc), rd, (u * BLOCK + tid) * 16, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(W::store(acc), rd, (u * BLOCK + tid) * 16, 0, SAUX);
     }
   }
   if (blockIdx.x == 0 && NSRC > 1 && tail_begin + tid < n) {
@@ -1484,6 +1484,17 @@ constexpr int kDefMode = 3, kDefUnroll = 1, kDefNT = 7, kDefThreads = 128;
 constexpr int kFoldLdsCap5 = 27648;  // floor(160 KiB / 27648) = 5, 25 KiB left
 constexpr int kFoldLdsCap8 = 20480;  // 8
 
+// The capped fold's store policy (TIPS_FOLD_STORE: sc1, the default, or nt; read once). The
+// round-5 sweep under eighths found nt stores slower (0.72-0.74 vs 0.78-0.80); an A/B knob for
+// the stripe map.
+inline bool fold_store_nt() {
+  static const bool v = [] {
+    const char* e = getenv("TIPS_FOLD_STORE");
+    return e && e[0] == 'n' && e[1] == 't' && e[2] == 0;
+  }();
+  return v;
+}
+
 template <int DT, int NSRC>
 hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
   // buffer loads, non-temporal for every source count. Round 1 kept plain loads beyond 4 sources
@@ -1504,7 +1515,10 @@ hipError_t run_multi(void* dst, const SrcList& sl, int64_t n, hipStream_t s) {
   const int64_t stripe = stripe_of(per);
   const int64_t grid = stripe_grid((nvec + per - 1) / per, stripe);  // surplus workgroups fall off the bounds check
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  if (capped)
+  if (capped && fold_store_nt())
+    hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX, kCapBlock, 2>), dim3((unsigned)grid), dim3(kCapBlock),
+                       NSRC >= 6 ? kFoldLdsCap5 : kFoldLdsCap8, s, (u32x4*)dst, sl, nvec, nvec * ve, n, stripe);
+  else if (capped)
     hipLaunchKernelGGL((multi_sum_buf_kernel<DT, NSRC, 1, LAUX, kCapBlock>), dim3((unsigned)grid), dim3(kCapBlock),
                        NSRC >= 6 ? kFoldLdsCap5 : kFoldLdsCap8, s, (u32x4*)dst, sl, nvec, nvec * ve, n, stripe);
   else if (u4)
