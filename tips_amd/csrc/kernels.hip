@@ -725,10 +725,10 @@ __global__ __launch_bounds__(kBlock) void copy_tiles_g_kernel(const CopyTile* __
 // order, buffer loads nt, buffer stores sc1 (the line leaves the XCD's L2), descriptors covering
 // exactly the tile; the < 16 trailing bytes go bytewise in workgroup 0. (hipMemcpyAsync's D2D blit
 // moved config 3's 1 GiB at 0.62 of HBM, profiles/r04/n_bench_n1.jsonl.)
-template <int U, int SAUX = 16>
-__global__ __launch_bounds__(kBlock) void copy_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
+template <int U, int SAUX = 16, int BLOCK = kBlock>
+__global__ __launch_bounds__(BLOCK) void copy_buf_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
                                                          int64_t nvec, int64_t tail_begin, int64_t bytes, int64_t stripe) {
-  constexpr int64_t kTile = (int64_t)kBlock * U;
+  constexpr int64_t kTile = (int64_t)BLOCK * U;
   const int64_t first = stripe_tile(blockIdx.x, gridDim.x, stripe) * kTile;
   const int tid = threadIdx.x;
   if (first < nvec) {
@@ -737,9 +737,9 @@ __global__ __launch_bounds__(kBlock) void copy_buf_kernel(u32x4* __restrict__ ds
     __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + first), (short)0, rec, 0x00020000);
     u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * kBlock + tid) * 16, 0, 2);
+    for (int u = 0; u < U; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (u * BLOCK + tid) * 16, 0, 2);
 #pragma unroll
-    for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (u * kBlock + tid) * 16, 0, SAUX);
+    for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (u * BLOCK + tid) * 16, 0, SAUX);
   }
   if (blockIdx.x == 0 && tail_begin + tid < bytes)
     reinterpret_cast<char*>(dst)[tail_begin + tid] = reinterpret_cast<const char*>(src)[tail_begin + tid];
@@ -806,19 +806,25 @@ hipError_t launch_copy_buf(void* dst, const void* src, int64_t bytes, hipStream_
   // TIPS_COPY_BUF_VARIANT (a sweep knob, read once; tools/copy_buf_sweep.sh): 0 = 4 KiB tiles, sc1
   // stores (shipped: 0.81-0.83 of HBM on config 3's 1 GiB, profiles/r04/z_copy_buf_sweep.txt);
   // 1 = 8 KiB tiles (0.71-0.75); 2 = 16 KiB tiles (0.73); 3 = 4 KiB tiles, nt stores;
-  // 4 = hipMemcpyAsync (0.59-0.65)
+  // 4 = hipMemcpyAsync (0.59-0.65); 5 / 6 = 128-lane workgroups (2 KiB tiles), sc1 / nt stores
+  // (round 6: the 2-input sum's shipped shape)
   static const int variant = [] {
     const char* v = getenv("TIPS_COPY_BUF_VARIANT");
     return v && *v ? atoi(v) : 0;
   }();
   if (variant == 4) return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
   const int U = variant == 1 ? 2 : variant == 2 ? 4 : 1;
+  const int64_t B = (variant == 5 || variant == 6) ? 128 : kBlock;
   const int64_t nvec = bytes / 16;
-  const int64_t stripe = stripe_of((int64_t)kBlock * U);
-  const int64_t grid = stripe_grid((nvec + (int64_t)kBlock * U - 1) / ((int64_t)kBlock * U), stripe);
+  const int64_t stripe = stripe_of(B * U);
+  const int64_t grid = stripe_grid((nvec + B * U - 1) / (B * U), stripe);
   if (grid > 0x7fffffff) return hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s);
-  const dim3 g((unsigned)grid), b(kBlock);
-  if (variant == 1)
+  const dim3 g((unsigned)grid), b((unsigned)B);
+  if (variant == 5)
+    hipLaunchKernelGGL((copy_buf_kernel<1, 16, 128>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);
+  else if (variant == 6)
+    hipLaunchKernelGGL((copy_buf_kernel<1, 2, 128>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);
+  else if (variant == 1)
     hipLaunchKernelGGL((copy_buf_kernel<2>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);
   else if (variant == 2)
     hipLaunchKernelGGL((copy_buf_kernel<4>), g, b, 0, s, (u32x4*)dst, (const u32x4*)src, nvec, nvec * 16, bytes, stripe);

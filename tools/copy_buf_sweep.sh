@@ -6,7 +6,7 @@ set -e
 OUT=gpurun_out/${TAG:-copybuf}
 mkdir -p "$OUT"
 for round in 1 2 3; do
-  for v in 0 1 2 3 4; do
+  for v in ${VARIANTS:-0 1 2 3 4 5 6}; do
     printf 'variant %s ' "$v" >> "$OUT/copy_buf_sweep.txt"
     TIPS_COPY_BUF_VARIANT=$v timeout -k 5 120 python bench.py --workload bucket --no-sub --no-cpu-baseline \
       --steps 20 --warmup 3 2>/dev/null | grep '^{' >> "$OUT/copy_buf_sweep.txt"
