@@ -67,7 +67,7 @@ SWEEP_VARIANTS = ([(m, u, t, 256) for m in (0, 1) for u in (1, 2, 4, 8) for t in
                      (0, 4, 2, 256), (2, 1, 2, 256), (2, 2, 2, 256), (2, 1, 2, 512), (2, 4, 1, 256)]
                   + [(3, 1, i, 256) for i in range(14)]
                   + [(3, u, 1, t) for u, t in ((2, 256), (4, 256), (1, 512), (2, 128), (1, 1024), (1, 128), (2, 512))]
-                  + [(3, 1, 7, 128)]  # the product default since round 6 (128 lanes, nt stores)
+                  + [(3, 1, 7, 128), (3, 1, 7, 64), (3, 2, 7, 128)]  # the product default since round 6 (128 lanes, nt stores) and its neighbours
                   + [(4, u, 0, 256) for u in (1, 2, 4)]
                   + [(5, w, 0, 256) for w in (1, 2, 4, 8)]
                   + [(3, u, 7, t) for u, t in ((1, 512), (1, 1024), (2, 256), (4, 256), (2, 512))])

@@ -1405,6 +1405,8 @@ hipError_t sum2_dispatch(void* dst, const void* a, const void* b, int64_t n, int
       TIPS_BUF_CASE(1, 2, 16, 2, 128)
       TIPS_BUF_CASE(1, 2, 16, 1, 1024)
       TIPS_BUF_CASE(1, 2, 16, 1, 128)
+      TIPS_BUF_CASE(7, 2, 2, 1, 64)   // (round 6: one wave per workgroup, nt stores)
+      TIPS_BUF_CASE(7, 2, 2, 2, 128)  // (round 6: 128 lanes, 2 vectors per lane, nt stores)
       TIPS_BUF_CASE(1, 2, 16, 2, 512)
       TIPS_BUF_CASE(7, 2, 2, 1, 512)  // nt loads + nt stores, other tile shapes (rotating-buffer sweep)
       TIPS_BUF_CASE(7, 2, 2, 1, 1024)

@@ -42,7 +42,8 @@ if os.environ.get("VARIANT_SET") == "focus":
     # round 6, under XCD stripes: the shapes / policies that led the wider sweeps, side by side
     # (the stripe size itself is TIPS_STRIPE_KIB, one value per process)
     VARIANTS = [("shipped", 3, 1, 1, 0, 256), ("t128", 3, 1, 1, 0, 128), ("t128_nt", 3, 1, 7, 0, 128), ("st_nt", 3, 1, 7, 0, 256),
-                ("st_sc0nt", 3, 1, 13, 0, 256), ("cap8", 3, 1, 1, 20480, 256)]
+                ("st_sc0nt", 3, 1, 13, 0, 256), ("cap8", 3, 1, 1, 20480, 256), ("t64_nt", 3, 1, 7, 0, 64),
+                ("u2t128_nt", 3, 2, 7, 0, 128)]
 for mib in SIZES:
     n = mib << 18
     sets = [(torch.randn(n, device="cuda"), torch.randn(n, device="cuda"), torch.empty(n, device="cuda"))
